@@ -1,0 +1,85 @@
+# Build for gfx950 (MI355X / CDNA4) only.  `make -j16` builds:
+#   mpi_cuda_cnn_amd/_C*.so   python module (kernels + engine + CPU oracle)
+#   build/bin/cnn             serial CPU trainer (reference cnn.c CLI)
+#   build/bin/cnn_hip         single-GPU trainer (same CLI)
+#   build/bin/cnn_dist        multi-GPU data-parallel trainer (RCCL, one process per GPU)
+#   build/bin/cnnmpi          CPU data-parallel trainer over MPI (if mpicxx exists)
+ROCM      ?= /opt/rocm
+HIPCC     ?= $(ROCM)/bin/hipcc
+CXX       ?= g++
+ARCH      ?= gfx950
+PYTHON    ?= python3
+MPICXX    ?= $(shell command -v mpicxx 2>/dev/null || ls /opt/conda/bin/mpicxx 2>/dev/null)
+
+PY_INC    := $(shell $(PYTHON) -c "import sysconfig;print(sysconfig.get_paths()['include'])")
+PYBIND_INC:= $(shell $(PYTHON) -c "import pybind11;print(pybind11.get_include())")
+EXT       := $(shell $(PYTHON) -c "import sysconfig;print(sysconfig.get_config_var('EXT_SUFFIX'))")
+
+OPT       ?= -O3
+INC       := -Icsrc/include -Icsrc/kernels
+HIPFLAGS  := --offload-arch=$(ARCH) $(OPT) -std=c++20 -fPIC $(INC) -Wall -Wno-unused-result
+CXXFLAGS  := $(OPT) -std=c++17 -fPIC $(INC) -Wall -Wno-unused-result
+HOSTHIP   := -D__HIP_PLATFORM_AMD__ -I$(ROCM)/include
+LDHIP     := -L$(ROCM)/lib -lamdhip64 -Wl,-rpath,$(ROCM)/lib
+
+OBJ       := build/obj
+CORE_SRC  := csrc/core/model.cpp csrc/core/cpu_net.cpp csrc/core/io.cpp
+CORE_OBJ  := $(patsubst csrc/core/%.cpp,$(OBJ)/core/%.o,$(CORE_SRC))
+KERN_SRC  := $(wildcard csrc/kernels/*.hip)
+KERN_OBJ  := $(patsubst csrc/kernels/%.hip,$(OBJ)/kernels/%.o,$(KERN_SRC))
+ENG_SRC   := $(wildcard csrc/engine/*.cpp)
+ENG_OBJ   := $(patsubst csrc/engine/%.cpp,$(OBJ)/engine/%.o,$(ENG_SRC))
+HDRS      := $(wildcard csrc/include/mcc/*.h csrc/kernels/*.h)
+
+MODULE    := mpi_cuda_cnn_amd/_C$(EXT)
+BINS      := build/bin/cnn
+ifneq ($(MPICXX),)
+BINS      += 
+endif
+
+.PHONY: all module bins clean
+all: module bins
+module: $(MODULE)
+bins: $(BINS)
+
+$(OBJ)/core/%.o: csrc/core/%.cpp $(HDRS)
+	@mkdir -p $(dir $@)
+	$(CXX) $(CXXFLAGS) -c $< -o $@
+
+$(OBJ)/kernels/%.o: csrc/kernels/%.hip $(HDRS)
+	@mkdir -p $(dir $@)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(OBJ)/engine/%.o: csrc/engine/%.cpp $(HDRS)
+	@mkdir -p $(dir $@)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(OBJ)/bindings/module.o: csrc/bindings/module.cpp $(HDRS)
+	@mkdir -p $(dir $@)
+	$(CXX) $(CXXFLAGS) $(HOSTHIP) -I$(PY_INC) -I$(PYBIND_INC) -fvisibility=hidden -c $< -o $@
+
+$(MODULE): $(OBJ)/bindings/module.o $(CORE_OBJ) $(KERN_OBJ) $(ENG_OBJ)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $^ $(LDHIP)
+
+build/bin/cnn: csrc/apps/cnn.cpp $(CORE_OBJ) $(HDRS)
+	@mkdir -p $(dir $@)
+	$(CXX) $(CXXFLAGS) -o $@ csrc/apps/cnn.cpp $(CORE_OBJ) -lm
+
+build/bin/cnnmpi: csrc/apps/cnnmpi.cpp $(CORE_OBJ) $(HDRS)
+	@mkdir -p $(dir $@)
+	MPICH_CXX=$(CXX) $(MPICXX) $(CXXFLAGS) -o $@ csrc/apps/cnnmpi.cpp $(CORE_OBJ) -lm
+
+$(OBJ)/apps/%.o: csrc/apps/%.cpp $(HDRS)
+	@mkdir -p $(dir $@)
+	$(HIPCC) $(HIPFLAGS) -I$(ROCM)/include/rccl -c $< -o $@
+
+build/bin/cnn_hip: $(OBJ)/apps/cnn_hip.o $(OBJ)/apps/trainer.o $(CORE_OBJ) $(KERN_OBJ) $(ENG_OBJ)
+	@mkdir -p $(dir $@)
+	$(HIPCC) --offload-arch=$(ARCH) -o $@ $^ $(LDHIP)
+
+build/bin/cnn_dist: $(OBJ)/apps/cnn_dist.o $(OBJ)/apps/trainer.o $(CORE_OBJ) $(KERN_OBJ) $(ENG_OBJ)
+	@mkdir -p $(dir $@)
+	$(HIPCC) --offload-arch=$(ARCH) -o $@ $^ $(LDHIP) -lrccl
+
+clean:
+	rm -rf build $(MODULE)

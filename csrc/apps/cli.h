@@ -1,0 +1,88 @@
+// Shared command-line handling for the native drivers.
+//
+// Contract kept from the reference (cnn.c:406-531): four positional IDX paths
+//   prog train-images train-labels test-images test-labels
+// exit 100 on too few arguments (guard fixed to argc < 5, defect D8), exit 111
+// on any file open / parse failure, log lines on stderr.  Everything else is an
+// optional flag whose default reproduces the reference hyper-parameters
+// (lr 0.1, 10 epochs, batch 32, seed 0 — cnn.c:413,446-449).
+#pragma once
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+namespace mcc {
+
+struct CliArgs {
+  std::string train_images, train_labels, test_images, test_labels;
+  std::string model = "ref";
+  std::string dtype = "bf16";
+  std::string save, load;
+  std::string log_json;     // machine-readable summary (stdout if "-")
+  int epochs = 10;
+  int batch = 32;           // global batch (divided across ranks in DP)
+  double lr = 0.1;
+  double momentum = 0.0;
+  double weight_decay = 0.0;
+  unsigned seed = 0;
+  int log_every = 1000;
+  bool ref_compat = false;  // CPU: reference D1 indexing + per-sample loop
+  bool fp32 = false;        // CPU: fp32 instead of fp64
+  int64_t max_train = -1;   // limit training samples
+  int64_t bucket_mb = 4;    // DP gradient bucket size
+  bool profile = false;     // per-phase timers
+  bool quiet = false;
+};
+
+inline void usage(const char* prog) {
+  std::fprintf(stderr,
+               "usage: %s train-images train-labels test-images test-labels\n"
+               "  [--model ref|lenet5|cifar3|vgg11] [--epochs N] [--batch B] [--lr X]\n"
+               "  [--momentum X] [--weight-decay X] [--seed S] [--dtype bf16|fp32]\n"
+               "  [--ref-compat] [--fp32] [--save W] [--load W] [--max-train N]\n"
+               "  [--bucket-mb MB] [--log-every N] [--profile] [--json PATH|-]\n",
+               prog);
+}
+
+// Returns 0 on success, 100 for too few positional args (reference exit code).
+inline int parse_cli(int argc, char** argv, CliArgs& a) {
+  std::vector<std::string> pos;
+  for (int i = 1; i < argc; ++i) {
+    std::string s = argv[i];
+    auto next = [&]() -> std::string {
+      if (i + 1 >= argc) { usage(argv[0]); std::exit(100); }
+      return argv[++i];
+    };
+    if (s == "--model") a.model = next();
+    else if (s == "--epochs") a.epochs = std::atoi(next().c_str());
+    else if (s == "--batch") a.batch = std::atoi(next().c_str());
+    else if (s == "--lr") a.lr = std::atof(next().c_str());
+    else if (s == "--momentum") a.momentum = std::atof(next().c_str());
+    else if (s == "--weight-decay") a.weight_decay = std::atof(next().c_str());
+    else if (s == "--seed") a.seed = (unsigned)std::strtoul(next().c_str(), nullptr, 10);
+    else if (s == "--dtype") a.dtype = next();
+    else if (s == "--save") a.save = next();
+    else if (s == "--load") a.load = next();
+    else if (s == "--max-train") a.max_train = std::atoll(next().c_str());
+    else if (s == "--bucket-mb") a.bucket_mb = std::atoll(next().c_str());
+    else if (s == "--log-every") a.log_every = std::atoi(next().c_str());
+    else if (s == "--json") a.log_json = next();
+    else if (s == "--ref-compat") a.ref_compat = true;
+    else if (s == "--fp32") a.fp32 = true;
+    else if (s == "--profile") a.profile = true;
+    else if (s == "--quiet") a.quiet = true;
+    else if (s == "-h" || s == "--help") { usage(argv[0]); std::exit(0); }
+    else if (s.size() > 2 && s[0] == '-' && s[1] == '-') { usage(argv[0]); std::exit(100); }
+    else pos.push_back(s);
+  }
+  if (pos.size() < 4) return 100;
+  a.train_images = pos[0]; a.train_labels = pos[1]; a.test_images = pos[2]; a.test_labels = pos[3];
+  if (a.batch < 1) a.batch = 1;
+  if (a.log_every < 1) a.log_every = 1000;
+  return 0;
+}
+
+}  // namespace mcc

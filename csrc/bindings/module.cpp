@@ -1,0 +1,316 @@
+// Python bindings (pybind11) for the native core.  Tensors cross the boundary
+// as raw device pointers + HIP stream handles (torch's data_ptr() and
+// current_stream().cuda_stream), so this translation unit needs no torch
+// headers and the same engine serves the native drivers and Python.
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <hip/hip_runtime_api.h>
+
+#include "kernels.h"
+#include "mcc/cpu_net.h"
+#include "mcc/engine.h"
+#include "mcc/io.h"
+#include "mcc/model.h"
+
+namespace py = pybind11;
+using namespace mcc;
+
+namespace {
+
+template <typename T>
+T* ptr(uintptr_t p) { return reinterpret_cast<T*>(p); }
+hipStream_t stream_of(uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }
+
+py::dict layer_dict(const LayerSpec& L) {
+  py::dict d;
+  d["kind"] = layer_kind_name(L.kind);
+  d["C"] = L.C; d["H"] = L.H; d["W"] = L.W;
+  d["inC"] = L.inC; d["inH"] = L.inH; d["inW"] = L.inW;
+  d["ks"] = L.ks; d["stride"] = L.stride; d["pad"] = L.pad;
+  d["act"] = act_name(L.act);
+  d["init_std"] = L.init_std;
+  d["w_off"] = L.w_off; d["b_off"] = L.b_off; d["nweights"] = L.nweights; d["nbiases"] = L.nbiases;
+  return d;
+}
+
+DType parse_dtype(const std::string& s) {
+  if (s == "bf16" || s == "bfloat16") return DType::BF16;
+  if (s == "fp32" || s == "float32" || s == "f32") return DType::F32;
+  if (s == "fp64" || s == "float64" || s == "f64") return DType::F64;
+  throw Error("unknown dtype '" + s + "'");
+}
+
+template <typename T>
+void bind_cpu_net(py::module_& m, const char* name) {
+  using Net = CpuNet<T>;
+  py::class_<Net>(m, name)
+      .def(py::init<const ModelSpec&, bool>(), py::arg("spec"), py::arg("ref_compat") = false)
+      .def_property_readonly("nparams", &Net::nparams)
+      .def_property_readonly("ref_compat", &Net::ref_compat)
+      .def("get_params", [](const Net& n) { return py::array_t<T>(n.params.size(), n.params.data()); })
+      .def("get_grads", [](const Net& n) { return py::array_t<T>(n.grads.size(), n.grads.data()); })
+      .def("set_params",
+           [](Net& n, py::array_t<T, py::array::c_style | py::array::forcecast> a) {
+             MCC_CHECK((int64_t)a.size() == n.nparams(), "set_params: size mismatch");
+             std::copy(a.data(), a.data() + a.size(), n.params.begin());
+           })
+      .def("set_grads",
+           [](Net& n, py::array_t<T, py::array::c_style | py::array::forcecast> a) {
+             MCC_CHECK((int64_t)a.size() == n.nparams(), "set_grads: size mismatch");
+             std::copy(a.data(), a.data() + a.size(), n.grads.begin());
+           })
+      .def("forward",
+           [](Net& n, py::array_t<T, py::array::c_style | py::array::forcecast> x) {
+             const int64_t in = n.spec().input_nodes();
+             MCC_CHECK(x.size() % in == 0, "forward: input size not a multiple of the input shape");
+             const int B = (int)(x.size() / in);
+             {
+               py::gil_scoped_release rel;
+               n.forward(x.data(), B);
+             }
+             const int nc = n.spec().num_classes();
+             return py::array_t<T>({B, nc}, n.probs());
+           })
+      .def("backward",
+           [](Net& n, py::array_t<int, py::array::c_style | py::array::forcecast> labels, double scale) {
+             StepStats s;
+             {
+               py::gil_scoped_release rel;
+               s = n.backward(labels.data(), (T)scale);
+             }
+             py::dict d;
+             d["loss_sum"] = s.loss_sum; d["mse_sum"] = s.mse_sum; d["correct"] = s.correct; d["count"] = s.count;
+             return d;
+           },
+           py::arg("labels"), py::arg("scale") = 1.0)
+      .def("evaluate",
+           [](const Net& n, py::array_t<int, py::array::c_style | py::array::forcecast> labels) {
+             StepStats s = n.evaluate(labels.data());
+             py::dict d;
+             d["loss_sum"] = s.loss_sum; d["mse_sum"] = s.mse_sum; d["correct"] = s.correct; d["count"] = s.count;
+             return d;
+           })
+      .def("sgd", [](Net& n, double lr) { n.sgd((T)lr); })
+      .def("zero_grads", &Net::zero_grads);
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_C, m) {
+  m.doc() = "MI355X-native CNN framework core (HIP/CDNA4 kernels + C++ runtime)";
+  py::register_exception<Error>(m, "MccError", PyExc_RuntimeError);
+
+  // ---------------------------------------------------------------- model
+  py::class_<ModelSpec>(m, "ModelSpec")
+      .def_readonly("name", &ModelSpec::name)
+      .def_readonly("nparams", &ModelSpec::nparams)
+      .def("describe", &ModelSpec::describe)
+      .def("macs_per_sample", &ModelSpec::macs_per_sample)
+      .def("num_classes", &ModelSpec::num_classes)
+      .def("input_shape", [](const ModelSpec& s) {
+        return py::make_tuple(s.input().C, s.input().H, s.input().W);
+      })
+      .def("layers", [](const ModelSpec& s) {
+        py::list l;
+        for (const auto& L : s.layers) l.append(layer_dict(L));
+        return l;
+      });
+  m.def("make_model", &make_model, py::arg("name"));
+  m.def("model_names", &model_names);
+  m.def("parse_model_spec", &parse_model_spec, py::arg("text"), py::arg("name") = "custom");
+  m.def("init_params",
+        [](const ModelSpec& s, uint64_t seed, const std::string& mode) {
+          py::array_t<double> out(s.nparams);
+          init_params(s, out.mutable_data(), seed, mode == "fast" ? InitMode::Fast : InitMode::GlibcRef);
+          return out;
+        },
+        py::arg("spec"), py::arg("seed") = 0, py::arg("mode") = "glibc");
+
+  // ------------------------------------------------------------------- io
+  m.def("idx_read", [](const std::string& path) {
+    IdxFile f = idx_read(path);
+    std::vector<py::ssize_t> shape(f.dims.begin(), f.dims.end());
+    py::array_t<uint8_t> a(shape);
+    std::copy(f.data.begin(), f.data.end(), a.mutable_data());
+    return a;
+  });
+  m.def("idx_write", [](const std::string& path, py::array_t<uint8_t, py::array::c_style | py::array::forcecast> a) {
+    std::vector<uint32_t> dims;
+    for (py::ssize_t i = 0; i < a.ndim(); ++i) dims.push_back((uint32_t)a.shape(i));
+    idx_write(path, dims, a.data());
+  });
+  m.def("synth_dataset",
+        [](int64_t N, int C, int H, int W, int classes, uint64_t seed) {
+          std::vector<uint8_t> img, lab;
+          {
+            py::gil_scoped_release rel;
+            synth_dataset(N, C, H, W, classes, seed, img, lab);
+          }
+          py::array_t<uint8_t> a({(py::ssize_t)N, (py::ssize_t)H, (py::ssize_t)W, (py::ssize_t)C});
+          std::copy(img.begin(), img.end(), a.mutable_data());
+          py::array_t<uint8_t> b((py::ssize_t)N);
+          std::copy(lab.begin(), lab.end(), b.mutable_data());
+          return py::make_tuple(a, b);
+        },
+        py::arg("n"), py::arg("c"), py::arg("h"), py::arg("w"), py::arg("classes") = 10, py::arg("seed") = 0);
+  m.def("save_weights", [](const std::string& path, const ModelSpec& s,
+                           py::array_t<double, py::array::c_style | py::array::forcecast> p) {
+    MCC_CHECK((int64_t)p.size() == s.nparams, "save_weights: size mismatch");
+    save_weights(path, s, p.data());
+  });
+  m.def("load_weights", [](const std::string& path) {
+    std::vector<double> p;
+    ModelSpec s = load_weights(path, p);
+    return py::make_tuple(s, py::array_t<double>(p.size(), p.data()));
+  });
+
+  bind_cpu_net<double>(m, "CpuNet64");
+  bind_cpu_net<float>(m, "CpuNet32");
+
+  // --------------------------------------------------------------- engine
+  py::class_<GpuNet>(m, "GpuNet")
+      .def(py::init([](const ModelSpec& s, const std::string& dtype, int max_batch, int device) {
+             return new GpuNet(s, parse_dtype(dtype), max_batch, device);
+           }),
+           py::arg("spec"), py::arg("dtype") = "bf16", py::arg("max_batch") = 1024, py::arg("device") = -1)
+      .def("plan", &GpuNet::plan)
+      .def_property_readonly("nparams", &GpuNet::nparams)
+      .def_property_readonly("num_stages", &GpuNet::num_stages)
+      .def_property_readonly("max_batch", &GpuNet::max_batch)
+      .def_property_readonly("arena_bytes", &GpuNet::arena_bytes)
+      .def_property_readonly("params_ptr", [](const GpuNet& n) { return (uintptr_t)n.params(); })
+      .def_property_readonly("grads_ptr", [](const GpuNet& n) { return (uintptr_t)n.grads(); })
+      .def_property_readonly("stats_ptr", [](const GpuNet& n) { return (uintptr_t)n.stats(); })
+      .def_property_readonly("logits_ptr", [](const GpuNet& n) { return (uintptr_t)n.logits(); })
+      .def_property_readonly("logits_ld", &GpuNet::logits_ld)
+      .def("set_params",
+           [](GpuNet& n, py::array_t<float, py::array::c_style | py::array::forcecast> a) {
+             MCC_CHECK((int64_t)a.size() == n.nparams(), "set_params: size mismatch");
+             n.set_params(a.data());
+           })
+      .def("get_params",
+           [](const GpuNet& n) {
+             py::array_t<float> a(n.nparams());
+             n.get_params(a.mutable_data());
+             return a;
+           })
+      .def("get_grads",
+           [](const GpuNet& n) {
+             py::array_t<float> a(n.nparams());
+             n.get_grads(a.mutable_data());
+             return a;
+           })
+      .def("get_logits",
+           [](const GpuNet& n, int B) {
+             MCC_CHECK(B > 0 && B <= n.max_batch(), "get_logits: bad batch");
+             const int nc = n.spec().num_classes(), ld = n.logits_ld();
+             std::vector<float> tmp((size_t)B * ld);
+             if (hipDeviceSynchronize() != hipSuccess) throw Error("hipDeviceSynchronize failed");
+             if (hipMemcpy(tmp.data(), n.logits(), 4 * tmp.size(), hipMemcpyDeviceToHost) != hipSuccess)
+               throw Error("hipMemcpy failed");
+             py::array_t<float> a({B, nc});
+             for (int b = 0; b < B; ++b)
+               for (int j = 0; j < nc; ++j) a.mutable_at(b, j) = tmp[(size_t)b * ld + j];
+             return a;
+           })
+      .def("get_stats",
+           [](const GpuNet& n) {
+             float h[4];
+             if (hipDeviceSynchronize() != hipSuccess) throw Error("hipDeviceSynchronize failed");
+             if (hipMemcpy(h, n.stats(), 16, hipMemcpyDeviceToHost) != hipSuccess) throw Error("hipMemcpy failed");
+             py::dict d;
+             d["loss_sum"] = h[0]; d["mse_sum"] = h[1]; d["correct"] = h[2];
+             return d;
+           })
+      .def("forward",
+           [](GpuNet& n, uintptr_t images, uintptr_t idx, int B, uintptr_t s) {
+             n.forward(ptr<const uint8_t>(images), ptr<const int32_t>(idx), B, stream_of(s));
+           },
+           py::arg("images"), py::arg("idx"), py::arg("batch"), py::arg("stream") = 0)
+      .def("loss",
+           [](GpuNet& n, uintptr_t labels, uintptr_t idx, float scale, bool backward, uintptr_t s, uintptr_t pred) {
+             n.loss(ptr<const uint8_t>(labels), ptr<const int32_t>(idx), scale, backward, stream_of(s),
+                    ptr<int32_t>(pred));
+           },
+           py::arg("labels"), py::arg("idx"), py::arg("scale"), py::arg("backward") = true, py::arg("stream") = 0,
+           py::arg("pred") = 0)
+      .def("zero_stats", [](GpuNet& n, uintptr_t s) { n.zero_stats(stream_of(s)); }, py::arg("stream") = 0)
+      .def("backward", [](GpuNet& n, int hi, int lo, uintptr_t s) { n.backward(hi, lo, stream_of(s)); },
+           py::arg("stage_hi"), py::arg("stage_lo"), py::arg("stream") = 0)
+      .def("backward_all", [](GpuNet& n, uintptr_t s) { n.backward_all(stream_of(s)); }, py::arg("stream") = 0)
+      .def("sgd",
+           [](GpuNet& n, float lr, float mu, float wd, uintptr_t s) { n.sgd(lr, mu, wd, stream_of(s)); },
+           py::arg("lr"), py::arg("momentum") = 0.f, py::arg("weight_decay") = 0.f, py::arg("stream") = 0)
+      .def("pack", [](GpuNet& n, uintptr_t s) { n.pack(stream_of(s)); }, py::arg("stream") = 0)
+      .def("stage_param_range",
+           [](const GpuNet& n, int s) {
+             int64_t off, cnt;
+             n.stage_param_range(s, off, cnt);
+             return py::make_tuple(off, cnt);
+           })
+      .def("buckets", [](const GpuNet& n, int64_t bytes) {
+        py::list l;
+        for (const auto& b : n.buckets(bytes)) l.append(py::make_tuple(b.stage_hi, b.stage_lo, b.off, b.count));
+        return l;
+      });
+
+  // ------------------------------------------------- raw kernels (tests)
+  py::module_ k = m.def_submodule("kernels", "raw gfx950 kernel entry points (device pointers)");
+  k.def("gemm",
+        [](const std::string& dt, int M, int N, int K, uintptr_t A, int lda, bool ta, uintptr_t B, int ldb, bool tb,
+           int ones_col, int epi, int act, uintptr_t bias, uintptr_t aux, int ldaux, uintptr_t C, int ldc,
+           uintptr_t Cf, int splitk, int64_t pstride, uintptr_t s) {
+          gpu::GemmParams p;
+          p.M = M; p.N = N; p.K = K;
+          p.A = ptr<void>(A); p.lda = lda; p.ta = ta;
+          p.B = ptr<void>(B); p.ldb = ldb; p.tb = tb;
+          p.ones_col = ones_col; p.epi = epi; p.act = act;
+          p.bias = ptr<float>(bias); p.aux = ptr<void>(aux); p.ldaux = ldaux;
+          p.C = ptr<void>(C); p.ldc = ldc; p.Cf = ptr<float>(Cf);
+          p.splitk = splitk; p.partial_stride = pstride;
+          gpu::gemm(parse_dtype(dt), p, stream_of(s));
+        },
+        py::arg("dtype"), py::arg("M"), py::arg("N"), py::arg("K"), py::arg("A"), py::arg("lda"), py::arg("ta"),
+        py::arg("B"), py::arg("ldb"), py::arg("tb"), py::arg("ones_col") = -1, py::arg("epi") = 0,
+        py::arg("act") = 0, py::arg("bias") = 0, py::arg("aux") = 0, py::arg("ldaux") = 0, py::arg("C") = 0,
+        py::arg("ldc") = 0, py::arg("Cf") = 0, py::arg("splitk") = 1, py::arg("pstride") = 0,
+        py::arg("stream") = 0);
+  k.def("sgd_update",
+        [](uintptr_t p, uintptr_t g, uintptr_t v, int64_t n, float lr, float mu, float wd, uintptr_t s) {
+          gpu::sgd_update(ptr<float>(p), ptr<const float>(g), ptr<float>(v), n, lr, mu, wd, stream_of(s));
+        },
+        py::arg("params"), py::arg("grads"), py::arg("mom"), py::arg("n"), py::arg("lr"), py::arg("momentum") = 0.f,
+        py::arg("weight_decay") = 0.f, py::arg("stream") = 0);
+  k.def("softmax_xent",
+        [](const std::string& dt, int M, int N, uintptr_t logits, int ldl, uintptr_t labels, uintptr_t idx,
+           uintptr_t dlogits, int ldd, float scale, uintptr_t stats, uintptr_t probs, uintptr_t pred, uintptr_t s) {
+          gpu::XentParams p;
+          p.M = M; p.N = N; p.logits = ptr<const float>(logits); p.ldl = ldl;
+          p.labels = ptr<const uint8_t>(labels); p.labels_idx = ptr<const int32_t>(idx);
+          p.dlogits = ptr<void>(dlogits); p.ldd = ldd; p.scale = scale;
+          p.stats = ptr<float>(stats); p.probs = ptr<float>(probs); p.pred = ptr<int32_t>(pred);
+          gpu::softmax_xent(parse_dtype(dt), p, stream_of(s));
+        },
+        py::arg("dtype"), py::arg("M"), py::arg("N"), py::arg("logits"), py::arg("ldl"), py::arg("labels"),
+        py::arg("idx") = 0, py::arg("dlogits") = 0, py::arg("ldd") = 0, py::arg("scale") = 1.f, py::arg("stats") = 0,
+        py::arg("probs") = 0, py::arg("pred") = 0, py::arg("stream") = 0);
+  k.attr("EPI_BIAS_ACT") = (int)gpu::EPI_BIAS_ACT;
+  k.attr("EPI_LOGITS") = (int)gpu::EPI_LOGITS;
+  k.attr("EPI_DACT") = (int)gpu::EPI_DACT;
+  k.attr("EPI_PARTIAL") = (int)gpu::EPI_PARTIAL;
+  k.attr("ACT_NONE") = (int)gpu::ACT_NONE;
+  k.attr("ACT_RELU") = (int)gpu::ACT_RELU;
+  k.attr("ACT_TANH") = (int)gpu::ACT_TANH;
+
+  m.def("device_count", []() {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+  });
+  m.def("synchronize", []() {
+    hipError_t e = hipDeviceSynchronize();
+    if (e != hipSuccess) throw Error(std::string("HIP error: ") + hipGetErrorString(e));
+  });
+}

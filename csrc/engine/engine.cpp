@@ -1,0 +1,474 @@
+// GpuNet implementation: model lowering, arena, packing tables, schedule.
+#include "mcc/engine.h"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <sstream>
+
+#include "kernels.h"
+
+namespace mcc {
+
+#define HIP_OK(expr)                                                                                    \
+  do {                                                                                                  \
+    hipError_t _e = (expr);                                                                             \
+    if (_e != hipSuccess)                                                                               \
+      throw Error(std::string("HIP error: ") + hipGetErrorString(_e) + " at " + __FILE__ + ":" +        \
+                  std::to_string(__LINE__));                                                            \
+  } while (0)
+
+struct GpuNet::Stage {
+  enum Kind { CONV, FC } kind = CONV;
+  int li = 0;            // spec layer index of the conv / fc layer
+  bool pooled = false;   // fused 2x2/2 maxpool
+  int act = gpu::ACT_NONE;
+  bool last = false;
+  bool cvec = true;      // conv input gathered in 8-channel vectors
+  int inC = 0, inH = 1, inW = 1;
+  int C = 0, OH = 1, OW = 1;   // conv grid (pre-pool)
+  int outH = 1, outW = 1;      // stage output spatial (pooled)
+  int64_t in_elems = 0, out_elems = 0;  // per-sample NHWC elements
+  int in_ld = 0, out_ld = 0;   // FC row strides (elements)
+  int KS = 1, stride = 1, pad = 0;
+  int64_t w_off = 0, b_off = 0, nw = 0, nb = 0;
+  // buffers
+  void* act_buf = nullptr;
+  uint8_t* arg_buf = nullptr;
+  void* grad_buf = nullptr;
+  // packed weight offsets (elements into packed_)
+  int64_t pk_fwd = -1, pk_dx = -1;
+  // conv geometry
+  int CL = 0, nchunks = 0, kpad = 0;        // forward
+  int CLd = 0, nchunks_d = 0, kpad_d = 0;   // data-gradient (transposed) form
+  bool cvec_d = true;
+  int imgs_fwd = 1, imgs_dx = 1, imgs_dw = 1, ppad = 32, kbias = 0, ncols_pad = 16, cout_pad = 16;
+  // fc geometry
+  int Kin = 0, Nout = 0, permC = 0, permHW = 0, ldp = 0;
+};
+
+static inline int r8(int x) { return (x + 7) & ~7; }
+static inline int r16(int x) { return (x + 15) & ~15; }
+static inline int r32(int x) { return (x + 31) & ~31; }
+static inline int act_kind(Act a) {
+  switch (a) {
+    case Act::ReLU: return gpu::ACT_RELU;
+    case Act::Tanh: return gpu::ACT_TANH;
+    default: return gpu::ACT_NONE;
+  }
+}
+
+GpuNet::GpuNet(const ModelSpec& spec, DType dtype, int max_batch, int device)
+    : spec_(spec), dtype_(dtype), max_batch_(max_batch), device_(device) {
+  MCC_CHECK(dtype == DType::BF16 || dtype == DType::F32, "GpuNet: dtype must be bf16 or fp32");
+  MCC_CHECK(max_batch > 0, "GpuNet: max_batch > 0");
+  if (device_ >= 0) HIP_OK(hipSetDevice(device_));
+  else HIP_OK(hipGetDevice(&device_));
+  build();
+}
+
+GpuNet::~GpuNet() {
+  for (Stage* st : stages_) delete st;
+  if (arena_) (void)hipFree(arena_);
+  if (mom_) (void)hipFree(mom_);
+}
+
+void* GpuNet::arena_alloc(size_t bytes) {
+  const size_t a = (arena_used_ + 255) & ~size_t(255);
+  arena_used_ = a + bytes;
+  return arena_ ? arena_ + a : reinterpret_cast<void*>(a + 1);  // sizing pass returns dummies
+}
+
+void GpuNet::build() {
+  const size_t es = dtype_size(dtype_);
+  // ---- lower the layer list into fused stages ----
+  const auto& L = spec_.layers;
+  for (size_t i = 1; i < L.size(); ++i) {
+    const LayerSpec& l = L[i];
+    Stage* st = new Stage();
+    st->li = (int)i;
+    st->act = act_kind(l.act);
+    st->inC = l.inC; st->inH = l.inH; st->inW = l.inW;
+    st->w_off = l.w_off; st->b_off = l.b_off; st->nw = l.nweights; st->nb = l.nbiases;
+    if (l.kind == LayerKind::Conv) {
+      st->kind = Stage::CONV;
+      st->C = l.C; st->OH = l.H; st->OW = l.W;
+      st->KS = l.ks; st->stride = l.stride; st->pad = l.pad;
+      st->outH = l.H; st->outW = l.W;
+      MCC_CHECK(l.act == Act::ReLU || l.act == Act::None, "GPU conv supports relu/none activations");
+      if (i + 1 < L.size() && L[i + 1].kind == LayerKind::MaxPool) {
+        const LayerSpec& pl = L[i + 1];
+        MCC_CHECK(pl.ks == 2 && pl.stride == 2, "GPU engine fuses only 2x2/2 max-pools");
+        MCC_CHECK(l.act == Act::ReLU, "fused max-pool needs a ReLU conv");
+        st->pooled = true;
+        st->outH = pl.H; st->outW = pl.W;
+        ++i;
+      }
+      MCC_CHECK(st->OH * st->OW <= 4096, "conv_small path: conv output larger than 64x64 per image");
+    } else if (l.kind == LayerKind::FC) {
+      st->kind = Stage::FC;
+      st->C = l.C;
+      st->Nout = l.C;
+      st->Kin = (int)l.in_nodes();
+      if (l.inH * l.inW > 1) { st->permC = l.inC; st->permHW = l.inH * l.inW; }
+    } else {
+      delete st;
+      throw Error("GPU engine: max-pool must directly follow a ReLU conv");
+    }
+    stages_.push_back(st);
+  }
+  MCC_CHECK(!stages_.empty() && stages_[0]->kind == Stage::CONV, "GPU engine: first layer must be a conv");
+  stages_.back()->last = true;
+  MCC_CHECK(stages_.back()->kind == Stage::FC, "GPU engine: last stage must be fc+softmax");
+
+  // ---- per-stage geometry ----
+  for (size_t s = 0; s < stages_.size(); ++s) {
+    Stage& st = *stages_[s];
+    st.in_elems = (int64_t)st.inC * st.inH * st.inW;
+    if (st.kind == Stage::CONV) {
+      st.out_elems = (int64_t)st.C * st.outH * st.outW;
+      st.cvec = st.inC >= 4;
+      st.CL = st.cvec ? r8(st.inC) : st.inC;
+      const int KK = st.KS * st.KS;
+      st.nchunks = st.cvec ? (int)ceil_div((int64_t)KK * (st.CL / 8), 4) : (int)ceil_div((int64_t)KK * st.inC, 32);
+      st.kpad = st.nchunks * 32;
+      st.cvec_d = st.C >= 4;
+      st.CLd = st.cvec_d ? r8(st.C) : st.C;
+      st.nchunks_d = st.cvec_d ? (int)ceil_div((int64_t)KK * (st.CLd / 8), 4) : (int)ceil_div((int64_t)KK * st.C, 32);
+      st.kpad_d = st.nchunks_d * 32;
+      const int LH = (st.OH - 1) * st.stride + st.KS, LW = (st.OW - 1) * st.stride + st.KS;
+      const int img_b = LH * LW * st.CL * (int)es;
+      st.imgs_fwd = std::max(1, std::min(16, 40960 / img_b));
+      const int LHd = st.inH + st.KS - 1, LWd = st.inW + st.KS - 1;
+      st.imgs_dx = std::max(1, std::min(16, 40960 / (LHd * LWd * st.CLd * (int)es)));
+      st.cout_pad = r16(st.C);
+      st.kbias = st.cvec ? KK * st.CL : KK * st.inC;
+      st.ncols_pad = r16(st.kbias + 1);
+      const int dw_img_b = img_b + st.cout_pad * st.OH * st.OW * (int)es;
+      st.imgs_dw = std::max(1, std::min(16, 49152 / dw_img_b));
+      st.ppad = r32(st.imgs_dw * st.OH * st.OW);
+      MCC_CHECK(st.cout_pad <= 128, "conv_small path: Cout > 128");
+    } else {
+      st.out_elems = st.Nout;
+      st.out_ld = r8(st.Nout);
+      st.ldp = r8(st.Kin + 1);
+    }
+    if (s > 0) {
+      const Stage& pv = *stages_[s - 1];
+      MCC_CHECK(pv.out_elems == st.in_elems, "stage shape mismatch");
+      if (st.kind == Stage::FC) st.in_ld = pv.kind == Stage::FC ? pv.out_ld : (int)pv.out_elems;
+    }
+    if (st.kind == Stage::FC) MCC_CHECK(st.in_ld % 8 == 0, "fc input leading dim must be a multiple of 8");
+  }
+
+  // ---- packed weight table ----
+  std::vector<int32_t> idx;
+  auto reserve = [&](int64_t n) {
+    int64_t off = (int64_t)idx.size();
+    idx.resize(off + ((n + 15) & ~int64_t(15)), -1);
+    return off;
+  };
+  for (Stage* sp : stages_) {
+    Stage& st = *sp;
+    if (st.kind == Stage::CONV) {
+      const int KK = st.KS * st.KS;
+      // forward: [r16(C)][kpad], k = (kp, cgroup, c8) or (kp, c)
+      st.pk_fwd = reserve((int64_t)r16(st.C) * st.kpad);
+      for (int n = 0; n < st.C; ++n)
+        for (int k = 0; k < st.kpad; ++k) {
+          int kp, c;
+          if (st.cvec) { const int G = k >> 3, CG = st.CL / 8; kp = G / CG; c = (G % CG) * 8 + (k & 7); }
+          else { kp = k / st.inC; c = k % st.inC; }
+          if (kp >= KK || c >= st.inC) continue;
+          const int kh = kp / st.KS, kw = kp % st.KS;
+          idx[st.pk_fwd + (int64_t)n * st.kpad + k] = (int32_t)(st.w_off + (((int64_t)n * st.inC + c) * st.KS + kh) * st.KS + kw);
+        }
+      if (&st != stages_[0]) {
+        // data gradient: [r16(inC)][kpad_d], input channels = conv outputs, flipped taps
+        st.pk_dx = reserve((int64_t)r16(st.inC) * st.kpad_d);
+        for (int ci = 0; ci < st.inC; ++ci)
+          for (int k = 0; k < st.kpad_d; ++k) {
+            int kp, co;
+            if (st.cvec_d) { const int G = k >> 3, CG = st.CLd / 8; kp = G / CG; co = (G % CG) * 8 + (k & 7); }
+            else { kp = k / st.C; co = k % st.C; }
+            if (kp >= KK || co >= st.C) continue;
+            const int kh = st.KS - 1 - kp / st.KS, kw = st.KS - 1 - kp % st.KS;
+            idx[st.pk_dx + (int64_t)ci * st.kpad_d + k] =
+                (int32_t)(st.w_off + (((int64_t)co * st.inC + ci) * st.KS + kh) * st.KS + kw);
+          }
+      }
+    } else {
+      auto perm = [&](int k) {
+        if (st.permC <= 0) return k;
+        const int hw = k / st.permC, c = k % st.permC;
+        return c * st.permHW + hw;
+      };
+      const int ldk = r8(st.Kin);
+      st.pk_fwd = reserve((int64_t)st.Nout * ldk);
+      for (int n = 0; n < st.Nout; ++n)
+        for (int k = 0; k < st.Kin; ++k)
+          idx[st.pk_fwd + (int64_t)n * ldk + k] = (int32_t)(st.w_off + (int64_t)n * st.Kin + perm(k));
+      if (&st != stages_[0]) {
+        st.pk_dx = reserve((int64_t)st.Kin * st.out_ld);
+        for (int k = 0; k < st.Kin; ++k)
+          for (int n = 0; n < st.Nout; ++n)
+            idx[st.pk_dx + (int64_t)k * st.out_ld + n] = (int32_t)(st.w_off + (int64_t)n * st.Kin + perm(k));
+      }
+    }
+  }
+  packed_count_ = (int64_t)idx.size();
+
+  // ---- arena: sizing pass then real pass ----
+  const int Bm = max_batch_;
+  size_t scratch = 0;
+  for (Stage* sp : stages_) {
+    const Stage& st = *sp;
+    if (st.kind == Stage::CONV) {
+      const int64_t groups = ceil_div(Bm, st.imgs_dw);
+      const int64_t nx = std::min<int64_t>(groups, 512);
+      scratch = std::max(scratch, (size_t)nx * st.cout_pad * st.ncols_pad * 4);
+    } else {
+      scratch = std::max(scratch, (size_t)64 * st.Nout * st.ldp * 4);  // up to 64 split-K partials
+    }
+  }
+  scratch_bytes_ = scratch;
+  for (int pass = 0; pass < 2; ++pass) {
+    arena_used_ = 0;
+    params_ = static_cast<float*>(arena_alloc(4 * (size_t)spec_.nparams));
+    grads_ = static_cast<float*>(arena_alloc(4 * (size_t)spec_.nparams));
+    stats_ = static_cast<float*>(arena_alloc(64));
+    logits_ld_ = r8(spec_.num_classes());
+    logits_ = static_cast<float*>(arena_alloc(4 * (size_t)Bm * logits_ld_));
+    packed_ = arena_alloc(es * (size_t)packed_count_);
+    pack_idx_ = static_cast<int32_t*>(arena_alloc(4 * (size_t)packed_count_));
+    scratch_ = static_cast<float*>(arena_alloc(scratch_bytes_));
+    for (Stage* sp : stages_) {
+      Stage& st = *sp;
+      const int64_t per = st.kind == Stage::FC ? st.out_ld : st.out_elems;
+      st.act_buf = arena_alloc(es * (size_t)Bm * per);
+      st.grad_buf = arena_alloc(es * (size_t)Bm * per);
+      st.arg_buf = st.pooled ? static_cast<uint8_t*>(arena_alloc((size_t)Bm * per)) : nullptr;
+    }
+    if (pass == 0) {
+      arena_bytes_ = arena_used_ + 256;
+      HIP_OK(hipMalloc(reinterpret_cast<void**>(&arena_), arena_bytes_));
+      HIP_OK(hipMemset(arena_, 0, arena_bytes_));
+    }
+  }
+  HIP_OK(hipMemcpy(pack_idx_, idx.data(), 4 * idx.size(), hipMemcpyHostToDevice));
+}
+
+std::string GpuNet::plan() const {
+  std::ostringstream os;
+  os << "GpuNet(" << spec_.name << ", " << dtype_name(dtype_) << ", max_batch=" << max_batch_
+     << ", arena=" << (arena_bytes_ >> 20) << " MiB)\n";
+  for (size_t s = 0; s < stages_.size(); ++s) {
+    const Stage& st = *stages_[s];
+    if (st.kind == Stage::CONV) {
+      os << "  [" << s << "] conv " << st.inC << "x" << st.inH << "x" << st.inW << " -> " << st.C << "x" << st.OH << "x"
+         << st.OW << (st.pooled ? " +maxpool" : "") << " k" << st.KS << "s" << st.stride << "p" << st.pad
+         << (st.cvec ? " cvec" : " scalar") << " chunks=" << st.nchunks << " imgs=" << st.imgs_fwd << "/"
+         << st.imgs_dx << "/" << st.imgs_dw << "\n";
+    } else {
+      os << "  [" << s << "] fc " << st.Kin << " -> " << st.Nout << (st.last ? " (logits)" : "")
+         << (st.permC ? " nhwc-flatten" : "") << "\n";
+    }
+  }
+  return os.str();
+}
+
+void GpuNet::set_params(const float* host) {
+  HIP_OK(hipMemcpy(params_, host, 4 * (size_t)spec_.nparams, hipMemcpyHostToDevice));
+  pack(nullptr);
+  HIP_OK(hipDeviceSynchronize());
+}
+
+void GpuNet::get_params(float* host) const {
+  HIP_OK(hipDeviceSynchronize());
+  HIP_OK(hipMemcpy(host, params_, 4 * (size_t)spec_.nparams, hipMemcpyDeviceToHost));
+}
+
+void GpuNet::get_grads(float* host) const {
+  HIP_OK(hipDeviceSynchronize());
+  HIP_OK(hipMemcpy(host, grads_, 4 * (size_t)spec_.nparams, hipMemcpyDeviceToHost));
+}
+
+void GpuNet::pack(hipStream_t s) {
+  gpu::pack_gather(dtype_, packed_, params_, pack_idx_, packed_count_, s);
+}
+
+void GpuNet::zero_stats(hipStream_t s) { HIP_OK(hipMemsetAsync(stats_, 0, 16, s)); }
+
+void GpuNet::forward(const uint8_t* images, const int32_t* idx, int B, hipStream_t s) {
+  MCC_CHECK(B > 0 && B <= max_batch_, "forward: batch exceeds max_batch");
+  B_ = B;
+  images_ = images;
+  idx_ = idx;
+  const size_t es = dtype_size(dtype_);
+  for (size_t si = 0; si < stages_.size(); ++si) {
+    Stage& st = *stages_[si];
+    if (st.kind == Stage::CONV) {
+      gpu::ConvParams p;
+      p.N = B; p.imgs = st.imgs_fwd;
+      p.Cin = st.inC; p.CL = st.CL; p.cvec = st.cvec;
+      p.LH = (st.OH - 1) * st.stride + st.KS; p.LW = (st.OW - 1) * st.stride + st.KS;
+      p.OH = st.OH; p.OW = st.OW; p.cs = st.stride; p.KS = st.KS;
+      p.Cout = st.C; p.nchunks = st.nchunks; p.kpad = st.kpad;
+      p.pool = st.pooled ? 2 : 1; p.act = st.act; p.bias_act = true;
+      p.in.SH = st.inH; p.in.SW = st.inW; p.in.SC = st.inC; p.in.off = st.pad; p.in.up = 1;
+      if (si == 0) { p.in.mode = gpu::IN_U8; p.in.src = images; p.in.idx = idx; }
+      else { p.in.mode = gpu::IN_PLAIN; p.in.src = stages_[si - 1]->act_buf; }
+      p.wpk = static_cast<const char*>(packed_) + es * st.pk_fwd;
+      p.bias = params_ + st.b_off;
+      p.out = st.act_buf; p.out_arg = st.arg_buf;
+      gpu::conv_forward(dtype_, p, s);
+    } else {
+      const Stage& pv = *stages_[si - 1];
+      gpu::GemmParams p;
+      p.M = B; p.N = st.Nout; p.K = st.Kin;
+      p.A = pv.act_buf; p.lda = st.in_ld;
+      p.B = static_cast<const char*>(packed_) + es * st.pk_fwd; p.ldb = r8(st.Kin);
+      p.bias = params_ + st.b_off;
+      if (st.last) { p.epi = gpu::EPI_LOGITS; p.Cf = logits_; p.ldc = logits_ld_; }
+      else { p.epi = gpu::EPI_BIAS_ACT; p.act = st.act; p.C = st.act_buf; p.ldc = st.out_ld; }
+      gpu::gemm(dtype_, p, s);
+    }
+  }
+}
+
+void GpuNet::loss(const uint8_t* labels, const int32_t* idx, float grad_scale, bool backward, hipStream_t s,
+                  int32_t* pred) {
+  MCC_CHECK(B_ > 0, "loss: call forward first");
+  const Stage& last = *stages_.back();
+  gpu::XentParams p;
+  p.M = B_; p.N = spec_.num_classes();
+  p.logits = logits_; p.ldl = logits_ld_;
+  p.labels_idx = idx; p.labels = labels;
+  p.dlogits = backward ? last.grad_buf : nullptr; p.ldd = last.out_ld;
+  p.scale = grad_scale;
+  p.stats = stats_;
+  p.pred = pred;
+  gpu::softmax_xent(dtype_, p, s);
+}
+
+void GpuNet::backward(int hi, int lo, hipStream_t s) {
+  MCC_CHECK(B_ > 0, "backward: call forward + loss first");
+  MCC_CHECK(hi >= lo && lo >= 0 && hi < (int)stages_.size(), "backward: bad stage range");
+  const int B = B_;
+  const size_t es = dtype_size(dtype_);
+  for (int si = hi; si >= lo; --si) {
+    Stage& st = *stages_[si];
+    if (st.kind == Stage::CONV) {
+      gpu::StageSrc dy;
+      dy.mode = st.pooled ? gpu::IN_UNPOOL : (st.act == gpu::ACT_RELU ? gpu::IN_RELU : gpu::IN_PLAIN);
+      dy.src = st.grad_buf; dy.aux_y = st.act_buf; dy.aux_arg = st.arg_buf;
+      dy.SH = st.OH; dy.SW = st.OW; dy.SC = st.C; dy.PH = st.outH; dy.PW = st.outW;
+      // weight gradient
+      gpu::ConvDwParams w;
+      w.N = B; w.imgs = st.imgs_dw;
+      w.nx = (int)std::min<int64_t>(ceil_div(B, st.imgs_dw), 512);
+      w.Cin = st.inC; w.CL = st.CL; w.cvec = st.cvec;
+      w.LH = (st.OH - 1) * st.stride + st.KS; w.LW = (st.OW - 1) * st.stride + st.KS;
+      w.OH = st.OH; w.OW = st.OW; w.cs = st.stride; w.KS = st.KS; w.Cout = st.C;
+      w.kbias = st.kbias; w.ncols_pad = st.ncols_pad; w.cout_pad = st.cout_pad; w.ppad = st.ppad;
+      w.x.SH = st.inH; w.x.SW = st.inW; w.x.SC = st.inC; w.x.off = st.pad; w.x.up = 1;
+      if (si == 0) { w.x.mode = gpu::IN_U8; w.x.src = images_; w.x.idx = idx_; }
+      else { w.x.mode = gpu::IN_PLAIN; w.x.src = stages_[si - 1]->act_buf; }
+      w.dy = dy;
+      w.slab = scratch_;
+      MCC_CHECK((size_t)w.nx * w.cout_pad * w.ncols_pad * 4 <= scratch_bytes_, "conv dW scratch too small");
+      gpu::conv_dw(dtype_, w, s);
+      gpu::ConvDwReduceParams r;
+      r.nx = w.nx; r.Cout = st.C; r.Cin = st.inC; r.KS = st.KS; r.CG = st.CL / 8; r.cvec = st.cvec;
+      r.cout_pad = st.cout_pad; r.ncols_pad = st.ncols_pad; r.kbias = st.kbias;
+      r.slab = scratch_; r.gw = grads_ + st.w_off; r.gb = grads_ + st.b_off;
+      gpu::conv_dw_reduce(r, s);
+      // data gradient into the previous stage's output gradient
+      if (si > 0) {
+        gpu::ConvParams p;
+        p.N = B; p.imgs = st.imgs_dx;
+        p.Cin = st.C; p.CL = st.CLd; p.cvec = st.cvec_d;
+        p.LH = st.inH + st.KS - 1; p.LW = st.inW + st.KS - 1;
+        p.OH = st.inH; p.OW = st.inW; p.cs = 1; p.KS = st.KS;
+        p.Cout = st.inC; p.nchunks = st.nchunks_d; p.kpad = st.kpad_d;
+        p.pool = 1; p.bias_act = false;
+        p.in = dy;
+        p.in.off = st.KS - 1 - st.pad; p.in.up = st.stride;
+        p.wpk = static_cast<const char*>(packed_) + es * st.pk_dx;
+        p.out = stages_[si - 1]->grad_buf;
+        gpu::conv_forward(dtype_, p, s);
+      }
+    } else {
+      const Stage& pv = *stages_[si - 1];
+      // weight + bias gradient: [Nout][Kin+1] = dZ^T [X | 1], split-K over the batch
+      gpu::GemmParams w;
+      w.M = st.Nout; w.N = st.Kin + 1; w.K = B;
+      w.A = st.grad_buf; w.lda = st.out_ld; w.ta = true;
+      w.B = pv.act_buf; w.ldb = st.in_ld; w.tb = true; w.ones_col = st.Kin;
+      w.epi = gpu::EPI_PARTIAL; w.Cf = scratch_; w.ldc = st.ldp;
+      const int tiles = (int)(ceil_div(st.Nout, 64) * ceil_div(st.Kin + 1, 64));
+      int sk = std::max(1, std::min(512 / std::max(1, tiles), B / 128));
+      sk = std::min(sk, 64);
+      w.splitk = sk;
+      w.partial_stride = (int64_t)st.Nout * st.ldp;
+      gpu::gemm(dtype_, w, s);
+      gpu::DwReduceParams r;
+      r.S = sk; r.Nout = st.Nout; r.kfeat = st.Kin; r.ldp = st.ldp; r.part = scratch_;
+      r.partial_stride = w.partial_stride;
+      r.gw = grads_ + st.w_off; r.gb = grads_ + st.b_off;
+      r.permC = st.permC; r.permHW = st.permHW;
+      gpu::dw_reduce(r, s);
+      // data gradient
+      if (si > 0) {
+        gpu::GemmParams d;
+        d.M = B; d.N = st.Kin; d.K = st.Nout;
+        d.A = st.grad_buf; d.lda = st.out_ld;
+        d.B = static_cast<const char*>(packed_) + es * st.pk_dx; d.ldb = st.out_ld;
+        d.epi = gpu::EPI_DACT;
+        d.act = pv.kind == Stage::FC ? pv.act : gpu::ACT_NONE;  // conv masks are applied by its staging
+        d.aux = pv.act_buf; d.ldaux = st.in_ld;
+        d.C = pv.grad_buf; d.ldc = st.in_ld;
+        gpu::gemm(dtype_, d, s);
+      }
+    }
+  }
+}
+
+void GpuNet::sgd(float lr, float momentum, float weight_decay, hipStream_t s) {
+  if (momentum != 0.f && !mom_) {
+    HIP_OK(hipMalloc(reinterpret_cast<void**>(&mom_), 4 * (size_t)spec_.nparams));
+    HIP_OK(hipMemset(mom_, 0, 4 * (size_t)spec_.nparams));
+  }
+  gpu::sgd_update(params_, grads_, momentum != 0.f ? mom_ : nullptr, spec_.nparams, lr, momentum, weight_decay, s);
+  pack(s);
+}
+
+void GpuNet::stage_param_range(int stage, int64_t& off, int64_t& count) const {
+  const Stage& st = *stages_.at(stage);
+  off = st.w_off;
+  count = st.nw + st.nb;
+}
+
+std::vector<GpuBucket> GpuNet::buckets(int64_t bucket_bytes) const {
+  // Walk stages from the last (first to finish in backward) to the first and
+  // cut a bucket whenever the accumulated gradient bytes reach bucket_bytes.
+  std::vector<GpuBucket> out;
+  GpuBucket cur;
+  bool open = false;
+  for (int s = (int)stages_.size() - 1; s >= 0; --s) {
+    int64_t off, cnt;
+    stage_param_range(s, off, cnt);
+    if (!open) { cur = GpuBucket(); cur.stage_hi = s; cur.off = off + cnt; open = true; }
+    cur.stage_lo = s;
+    cur.count += cnt;
+    cur.off = off;
+    if (cur.count * 4 >= bucket_bytes || s == 0) {
+      out.push_back(cur);
+      open = false;
+    }
+  }
+  return out;
+}
+
+}  // namespace mcc

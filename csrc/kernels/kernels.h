@@ -1,0 +1,167 @@
+// Host-visible launch API of the gfx950 kernels.  Pure C++ (no device code)
+// so the engine, the pybind module and the native drivers can call into the
+// kernels without being compiled as HIP translation units.
+//
+// Activation layout on the GPU is NHWC ("channels-last"): the MFMA epilogue
+// of a 16x16 tile holds 16 consecutive output channels per pixel, so NHWC
+// makes every store a contiguous run, and 8-channel groups become single
+// 16-byte LDS reads in the implicit-GEMM gather.
+#pragma once
+
+#include <hip/hip_runtime_api.h>
+
+#include <cstdint>
+
+#include "mcc/common.h"
+
+namespace mcc {
+namespace gpu {
+
+enum InMode : int {
+  IN_PLAIN = 0,   // src is T NHWC
+  IN_U8 = 1,      // src is u8 NHWC images (optionally gathered by idx), scaled 1/255
+  IN_RELU = 2,    // value = (aux_y > 0) ? src : 0          (ReLU backward, no pool)
+  IN_UNPOOL = 3,  // value = (argmax == pos && aux_y > 0) ? src_pooled : 0  (2x2 maxpool + ReLU backward)
+};
+
+enum ActKind : int { ACT_NONE = 0, ACT_RELU = 1, ACT_TANH = 2 };
+
+// Source description for staging an NHWC tile into LDS.  The LDS tile
+// coordinate j maps to source coordinate (j - off) / up when that is an
+// integer in range, else zero: forward conv uses off = pad, up = 1; the
+// data-gradient of a strided conv uses off = KS-1-pad, up = stride (zero
+// insertion) and runs as a stride-1 conv with flipped weights.
+struct StageSrc {
+  int mode = IN_PLAIN;
+  const void* src = nullptr;     // T* or uint8_t*
+  const int32_t* idx = nullptr;  // IN_U8: optional per-image index
+  const void* aux_y = nullptr;   // IN_RELU/IN_UNPOOL: layer output (T)
+  const uint8_t* aux_arg = nullptr;  // IN_UNPOOL: argmax (pos in 2x2 window)
+  int SH = 0, SW = 0, SC = 0;    // conv-grid dims of the source (pre-pool for UNPOOL)
+  int PH = 0, PW = 0;            // IN_UNPOOL: pooled dims of src/aux tensors
+  int off = 0, up = 1;
+};
+
+// Implicit-GEMM conv over small images staged whole in LDS ("conv_small").
+// Rows = output pixels (pool-window ordered when pool==2), cols = output
+// channels, K = (kernel position, input channel) in the packed order.
+struct ConvParams {
+  int N = 0;          // images in the batch
+  int imgs = 1;       // images per workgroup
+  int Cin = 0;        // staged channels (real)
+  int CL = 0;         // LDS channel stride: round_up(Cin, 8) (cvec) or Cin (scalar)
+  bool cvec = true;   // 8-channel vector gather (else scalar gather)
+  int LH = 0, LW = 0; // LDS tile dims per image
+  int OH = 0, OW = 0; // conv output dims
+  int cs = 1;         // conv stride (in LDS coordinates)
+  int KS = 1;
+  int Cout = 0;
+  int nchunks = 0;    // K chunks of 32
+  int kpad = 0;       // packed K row length = nchunks*32
+  int pool = 1;       // 1 or 2 (fused 2x2/2 maxpool)
+  int act = ACT_RELU;
+  bool bias_act = true;  // false: plain store (data-gradient form)
+  StageSrc in;
+  const void* wpk = nullptr;    // packed weights [round_up(Cout,16)][kpad], T
+  const float* bias = nullptr;  // fp32 canonical bias [Cout]
+  void* out = nullptr;          // T NHWC [N][OH'][OW'][Cout]
+  uint8_t* out_arg = nullptr;   // pool argmax [N][PH][PW][Cout]
+};
+
+// Weight gradient of a conv_small layer: slab[x][co][col] partial sums over
+// the images of workgroup column x; col < kbias are packed K entries and
+// col == kbias is the bias gradient (a ones-column in the im2col operand).
+struct ConvDwParams {
+  int N = 0, imgs = 1, nx = 1;
+  int Cin = 0, CL = 0;
+  bool cvec = true;
+  int LH = 0, LW = 0, OH = 0, OW = 0, cs = 1, KS = 1, Cout = 0;
+  int kbias = 0;       // first column after the packed K entries
+  int ncols_pad = 0;   // round_up(kbias + 1, 16)
+  int cout_pad = 0;    // round_up(Cout, 16)
+  int ppad = 0;        // pixels per stage, padded to 32
+  StageSrc x;          // forward input of the layer
+  StageSrc dy;         // gradient w.r.t. the conv output (via RELU/UNPOOL)
+  float* slab = nullptr;  // [nx][cout_pad][ncols_pad]
+};
+
+// Sum the dW slabs over x and scatter into the canonical fp32 gradient.
+struct ConvDwReduceParams {
+  int nx = 0, Cout = 0, Cin = 0, KS = 1, CG = 1;
+  bool cvec = true;
+  int cout_pad = 0, ncols_pad = 0, kbias = 0;
+  const float* slab = nullptr;
+  float* gw = nullptr;  // canonical [Cout][Cin][KS][KS]
+  float* gb = nullptr;  // [Cout]
+  float beta = 0.f;     // grad = beta*grad + sum (0 overwrites)
+};
+
+enum GemmEpi : int {
+  EPI_BIAS_ACT = 0,  // C = act(acc + bias[n])  (T)
+  EPI_LOGITS = 1,    // Cf = acc + bias[n]      (fp32)
+  EPI_DACT = 2,      // C = acc * act'(aux[m][n]) (T), or plain when act == ACT_NONE
+  EPI_PARTIAL = 3,   // Cf[z][m][n] = acc       (fp32 split-K partial)
+};
+
+// C[M][N] = A[M][K] * B[N][K]^T; ta: A stored [K][M]; tb: B stored [K][N].
+struct GemmParams {
+  int M = 0, N = 0, K = 0;
+  const void* A = nullptr; int lda = 0; bool ta = false;
+  const void* B = nullptr; int ldb = 0; bool tb = false;
+  int ones_col = -1;        // B row n == ones_col reads 1.0 (bias-grad column)
+  int epi = EPI_BIAS_ACT;
+  int act = ACT_NONE;
+  const float* bias = nullptr;
+  const void* aux = nullptr; int ldaux = 0;
+  void* C = nullptr; int ldc = 0;   // T output
+  float* Cf = nullptr;              // fp32 output (logits / partials)
+  int splitk = 1;                   // gridDim.z
+  int64_t partial_stride = 0;       // elements between split-K partials
+};
+
+// Reduce split-K partials of a weight gradient into the canonical grad:
+// gw[n*Kc + perm(k)] (k < kfeat), gb[n] (k == kfeat).
+struct DwReduceParams {
+  int S = 1, Nout = 0, kfeat = 0, ldp = 0;
+  const float* part = nullptr;  // [S][Nout][ldp]
+  int64_t partial_stride = 0;
+  float* gw = nullptr;
+  float* gb = nullptr;
+  int permC = 0, permHW = 0;    // k = hw*C + c  ->  c*HW + hw   (0: identity)
+  float beta = 0.f;
+};
+
+struct XentParams {
+  int M = 0, N = 0;
+  const float* logits = nullptr; int ldl = 0;
+  const int32_t* labels_idx = nullptr;  // per-sample dataset index (nullable)
+  const uint8_t* labels = nullptr;      // dataset labels (gathered by idx)
+  void* dlogits = nullptr; int ldd = 0; // T
+  float scale = 1.f;                    // dlogits = (p - y) * scale
+  float* stats = nullptr;               // [0]=loss sum [1]=mse sum [2]=correct
+  float* probs = nullptr;               // optional fp32 probs [M][N] (eval)
+  int32_t* pred = nullptr;              // optional argmax per sample
+};
+
+void conv_forward(DType t, const ConvParams& p, hipStream_t s);
+size_t conv_forward_lds_bytes(DType t, const ConvParams& p);
+void conv_dw(DType t, const ConvDwParams& p, hipStream_t s);
+size_t conv_dw_lds_bytes(DType t, const ConvDwParams& p);
+void conv_dw_reduce(const ConvDwReduceParams& p, hipStream_t s);
+
+void gemm(DType t, const GemmParams& p, hipStream_t s);
+void dw_reduce(const DwReduceParams& p, hipStream_t s);
+
+void softmax_xent(DType t, const XentParams& p, hipStream_t s);
+
+// params -= lr * (grad + wd * params) [momentum: v = mu*v + g; p -= lr*v]
+void sgd_update(float* params, const float* grads, float* mom, int64_t n, float lr, float mu, float wd,
+                hipStream_t s);
+// dst[i] = idx[i] >= 0 ? T(src[idx[i]]) : 0
+void pack_gather(DType t, void* dst, const float* src, const int32_t* idx, int64_t n, hipStream_t s);
+void fill_f32(float* dst, float v, int64_t n, hipStream_t s);
+void cast_f32(DType t, void* dst, const float* src, int64_t n, hipStream_t s);
+void to_f32(DType t, float* dst, const void* src, int64_t n, hipStream_t s);
+
+}  // namespace gpu
+}  // namespace mcc

@@ -1,0 +1,72 @@
+// Device-side helpers shared by the gfx950 kernels: 64-lane wave MFMA
+// fragments, bf16 <-> f32, 16-byte vector moves.
+//
+// Operand maps (cdna_hip_programming.md §3), lane l, g = l >> 4, r = l & 15:
+//   v_mfma_f32_16x16x32_bf16 : A[r][8g+j], B[8g+j][r], j = 0..7
+//   C/D                      : C[4g+i][r], i = 0..3
+// The f32 path runs the same 32-deep K chunk as eight v_mfma_f32_16x16x4_f32
+// with element j of every lane fragment in instruction j; that permutes K
+// identically for A and B, so the sum is the same and both dtypes share one
+// fragment layout (8 consecutive K per lane).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace mcc {
+namespace gpu {
+
+typedef __bf16 bf16;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x8 __attribute__((ext_vector_type(8)));
+
+template <typename T> struct Vec8;
+template <> struct Vec8<bf16> { typedef bf16x8 type; };
+template <> struct Vec8<float> { typedef f32x8 type; };
+
+__device__ __forceinline__ float to_f(float x) { return x; }
+__device__ __forceinline__ float to_f(bf16 x) { return (float)x; }
+template <typename T> __device__ __forceinline__ T from_f(float x) { return (T)x; }
+
+// 8 consecutive elements, 16-byte aligned for bf16, 32-byte for f32.
+__device__ __forceinline__ bf16x8 load8(const bf16* p) { return *reinterpret_cast<const bf16x8*>(p); }
+__device__ __forceinline__ void store8(bf16* p, const bf16x8& v) { *reinterpret_cast<bf16x8*>(p) = v; }
+// f32: two 16-byte moves (only 16-byte alignment is guaranteed).
+__device__ __forceinline__ f32x8 load8(const float* p) {
+  const f32x4 a = *reinterpret_cast<const f32x4*>(p);
+  const f32x4 b = *reinterpret_cast<const f32x4*>(p + 4);
+  return __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+__device__ __forceinline__ void store8(float* p, const f32x8& v) {
+  *reinterpret_cast<f32x4*>(p) = __builtin_shufflevector(v, v, 0, 1, 2, 3);
+  *reinterpret_cast<f32x4*>(p + 4) = __builtin_shufflevector(v, v, 4, 5, 6, 7);
+}
+
+__device__ __forceinline__ f32x4 mma(f32x4 acc, const bf16x8& a, const bf16x8& b) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc, 0, 0, 0);
+}
+__device__ __forceinline__ f32x4 mma(f32x4 acc, const f32x8& a, const f32x8& b) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j], b[j], acc, 0, 0, 0);
+  return acc;
+}
+
+__device__ __forceinline__ float act_apply(int act, float v) {
+  if (act == 1) return v > 0.f ? v : 0.f;
+  if (act == 2) return tanhf(v);
+  return v;
+}
+// derivative expressed in the activation output y
+__device__ __forceinline__ float act_grad_y(int act, float y) {
+  if (act == 1) return y > 0.f ? 1.f : 0.f;
+  if (act == 2) return 1.f - y * y;
+  return 1.f;
+}
+
+__host__ __device__ __forceinline__ int cdiv(int a, int b) { return (a + b - 1) / b; }
+
+}  // namespace gpu
+}  // namespace mcc

@@ -1,0 +1,166 @@
+// Loss, optimizer and layout kernels.
+//
+//  softmax_xent : fused softmax + cross-entropy forward+backward + the
+//                 reference's logged metrics, replacing the softmax in
+//                 Layer_feedForw_full (cnn.c:125-143), the output error
+//                 (cnn.c:285-286), Layer_getErrorTotal (cnn.c:275-282) and the
+//                 argmax of the test loop (cnn.c:506-515).
+//  sgd_update   : one multi-tensor pass over the flat fp32 parameter buffer
+//                 (Layer_update, cnn.c:303-314, recursive over every layer).
+//  pack_gather  : refresh the packed bf16/fp32 compute copies (MFMA order,
+//                 transposed shadows) from the fp32 master after the update.
+#include "kernels.h"
+#include "mfma.h"
+
+namespace mcc {
+namespace gpu {
+
+namespace {
+
+template <typename T>
+__global__ void __launch_bounds__(256) softmax_xent_kernel(XentParams p) {
+  const int row = blockIdx.x * blockDim.x + threadIdx.x;
+  float loss = 0.f, mse = 0.f, correct = 0.f;
+  if (row < p.M) {
+    const float* l = p.logits + (size_t)row * p.ldl;
+    const int sample = p.labels_idx ? p.labels_idx[row] : row;
+    const int label = p.labels[sample];
+    float m = l[0];
+    int am = 0;
+    for (int j = 1; j < p.N; ++j)
+      if (l[j] > m) { m = l[j]; am = j; }  // first max wins (cnn.c:510)
+    float s = 0.f;
+    for (int j = 0; j < p.N; ++j) s += __expf(l[j] - m);
+    const float inv = 1.f / s;
+    loss = __logf(s) - (l[label] - m);
+    correct = (am == label) ? 1.f : 0.f;
+    T* d = static_cast<T*>(p.dlogits);
+    for (int j = 0; j < p.N; ++j) {
+      const float pj = __expf(l[j] - m) * inv;
+      const float e = pj - (j == label ? 1.f : 0.f);
+      mse += e * e;
+      if (d) d[(size_t)row * p.ldd + j] = from_f<T>(e * p.scale);
+      if (p.probs) p.probs[(size_t)row * p.N + j] = pj;
+    }
+    mse /= (float)p.N;
+    if (p.pred) p.pred[row] = am;
+  }
+  // wave reduce (64 lanes) then one atomic per wave
+  for (int o = 32; o > 0; o >>= 1) {
+    loss += __shfl_xor(loss, o);
+    mse += __shfl_xor(mse, o);
+    correct += __shfl_xor(correct, o);
+  }
+  if ((threadIdx.x & 63) == 0 && p.stats) {
+    atomicAdd(p.stats + 0, loss);
+    atomicAdd(p.stats + 1, mse);
+    atomicAdd(p.stats + 2, correct);
+  }
+}
+
+__global__ void sgd_kernel(float* __restrict__ w, const float* __restrict__ g, float* __restrict__ v, int64_t n,
+                           float lr, float mu, float wd) {
+  const int64_t n4 = n >> 2;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    f32x4 wv = reinterpret_cast<f32x4*>(w)[i];
+    f32x4 gv = reinterpret_cast<const f32x4*>(g)[i];
+    if (wd != 0.f) gv += wd * wv;
+    if (v) {
+      f32x4 vv = reinterpret_cast<f32x4*>(v)[i];
+      vv = mu * vv + gv;
+      reinterpret_cast<f32x4*>(v)[i] = vv;
+      gv = vv;
+    }
+    reinterpret_cast<f32x4*>(w)[i] = wv - lr * gv;
+  }
+  for (int64_t i = (n4 << 2) + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    float gi = g[i] + wd * w[i];
+    if (v) { v[i] = mu * v[i] + gi; gi = v[i]; }
+    w[i] -= lr * gi;
+  }
+}
+
+template <typename T>
+__global__ void pack_kernel(T* __restrict__ dst, const float* __restrict__ src, const int32_t* __restrict__ idx,
+                            int64_t n) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const int32_t j = idx[i];
+    dst[i] = j >= 0 ? from_f<T>(src[j]) : T(0);
+  }
+}
+
+__global__ void fill_kernel(float* dst, float v, int64_t n) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) dst[i] = v;
+}
+
+template <typename T>
+__global__ void cast_kernel(T* dst, const float* src, int64_t n) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) dst[i] = from_f<T>(src[i]);
+}
+
+template <typename T>
+__global__ void to_f32_kernel(float* dst, const T* src, int64_t n) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) dst[i] = to_f(src[i]);
+}
+
+inline unsigned grid_for(int64_t n, int per_thread = 1) {
+  int64_t b = (n / per_thread + 255) / 256;
+  if (b < 1) b = 1;
+  if (b > 4096) b = 4096;
+  return (unsigned)b;
+}
+
+}  // namespace
+
+void softmax_xent(DType t, const XentParams& p, hipStream_t s) {
+  MCC_CHECK(p.M > 0 && p.N > 0, "softmax_xent: empty");
+  const dim3 grid((unsigned)cdiv(p.M, 256)), block(256);
+  if (t == DType::BF16) hipLaunchKernelGGL(softmax_xent_kernel<bf16>, grid, block, 0, s, p);
+  else hipLaunchKernelGGL(softmax_xent_kernel<float>, grid, block, 0, s, p);
+}
+
+void sgd_update(float* params, const float* grads, float* mom, int64_t n, float lr, float mu, float wd,
+                hipStream_t s) {
+  MCC_CHECK((reinterpret_cast<uintptr_t>(params) & 15) == 0 && (reinterpret_cast<uintptr_t>(grads) & 15) == 0,
+            "sgd_update: buffers must be 16-byte aligned");
+  hipLaunchKernelGGL(sgd_kernel, dim3(grid_for(n, 4)), dim3(256), 0, s, params, grads, mom, n, lr, mu, wd);
+}
+
+void pack_gather(DType t, void* dst, const float* src, const int32_t* idx, int64_t n, hipStream_t s) {
+  if (n <= 0) return;
+  if (t == DType::BF16)
+    hipLaunchKernelGGL(pack_kernel<bf16>, dim3(grid_for(n)), dim3(256), 0, s, static_cast<bf16*>(dst), src, idx, n);
+  else
+    hipLaunchKernelGGL(pack_kernel<float>, dim3(grid_for(n)), dim3(256), 0, s, static_cast<float*>(dst), src, idx,
+                       n);
+}
+
+void fill_f32(float* dst, float v, int64_t n, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(fill_kernel, dim3(grid_for(n)), dim3(256), 0, s, dst, v, n);
+}
+
+void cast_f32(DType t, void* dst, const float* src, int64_t n, hipStream_t s) {
+  if (n <= 0) return;
+  if (t == DType::BF16)
+    hipLaunchKernelGGL(cast_kernel<bf16>, dim3(grid_for(n)), dim3(256), 0, s, static_cast<bf16*>(dst), src, n);
+  else
+    hipLaunchKernelGGL(cast_kernel<float>, dim3(grid_for(n)), dim3(256), 0, s, static_cast<float*>(dst), src, n);
+}
+
+void to_f32(DType t, float* dst, const void* src, int64_t n, hipStream_t s) {
+  if (n <= 0) return;
+  if (t == DType::BF16)
+    hipLaunchKernelGGL(to_f32_kernel<bf16>, dim3(grid_for(n)), dim3(256), 0, s, dst, static_cast<const bf16*>(src), n);
+  else
+    hipLaunchKernelGGL(to_f32_kernel<float>, dim3(grid_for(n)), dim3(256), 0, s, dst, static_cast<const float*>(src),
+                       n);
+}
+
+}  // namespace gpu
+}  // namespace mcc
