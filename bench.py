@@ -1,0 +1,138 @@
+#!/usr/bin/env python3
+"""Headline benchmark: LeNet-5 training throughput on MNIST-shaped data.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch-per-gpu B]
+    torchrun --nproc-per-node N bench.py --gpus N ...   (driver, N > 1)
+
+Metric (BASELINE.json): images/sec for the whole node, LeNet-5, 28x28x1
+input, synchronous data-parallel SGD over RCCL (weak scaling: fixed per-GPU
+batch).  Synthetic data of the MNIST shape, random-init weights; every step
+does the full work: device-side sampling, forward, softmax-CE, backward, the
+bucketed gradient all-reduce and the SGD update.  The timed region is K
+steps bracketed by barrier + device synchronize on both sides; the reported
+time is the max over ranks.
+"""
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+BASELINE_IMG_S = 2510.0  # best reference number (8-rank MPI CPU)
+METRIC = "images/sec (whole node), LeNet-5 MNIST-shaped, at 1/2/4/8 MI355X"
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--model", default="lenet5")
+    ap.add_argument("--batch-per-gpu", type=int, default=16384)
+    ap.add_argument("--dtype", default="bf16")
+    ap.add_argument("--dataset", type=int, default=65536, help="synthetic samples resident per GPU")
+    ap.add_argument("--bucket-mb", type=float, default=4.0)
+    ap.add_argument("--lr", type=float, default=0.05)
+    ap.add_argument("--momentum", type=float, default=0.9)
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and rank == 0:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    import mpi_cuda_cnn_amd as mcc
+    from mpi_cuda_cnn_amd.trainer import GpuTrainer
+
+    spec = mcc.make_model(args.model)
+    C, H, W = spec.input_shape()
+    B = args.batch_per_gpu
+    imgs, labels = mcc.synth_dataset(args.dataset, C, H, W, spec.num_classes(), seed=1234 + rank)
+    d_img = torch.from_numpy(imgs).to(dev)
+    d_lab = torch.from_numpy(labels).to(dev)
+    tr = GpuTrainer(
+        spec,
+        dtype=args.dtype,
+        batch=B,
+        device=local_rank,
+        seed=0,
+        lr=args.lr,
+        momentum=args.momentum,
+        init="fast",
+        bucket_bytes=int(args.bucket_mb * (1 << 20)),
+    )
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(rank)
+
+    def step():
+        idx = torch.randint(0, args.dataset, (B,), device=dev, dtype=torch.int32, generator=gen)
+        tr.step(d_img, d_lab, idx)
+
+    tr.zero_stats()
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    tr.zero_stats()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    st = tr.net.get_stats()
+    if rank == 0:
+        total_imgs = B * world * args.steps
+        value = total_imgs / elapsed
+        out = {
+            "metric": METRIC,
+            "value": round(value, 1),
+            "unit": "images/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(1000.0 * elapsed / args.steps, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": round(value / BASELINE_IMG_S, 2),
+            "dtype": args.dtype,
+            "data": "synthetic (MNIST-shaped 28x28x1 u8, device-resident, random-init weights)",
+            "config": {
+                "model": args.model,
+                "global_batch": B * world,
+                "seq_len": H * W,
+                "parallelism": f"dp{world}",
+                "batch_per_gpu": B,
+                "input_shape": f"{C}x{H}x{W}",
+                "optimizer": f"sgd lr={args.lr} momentum={args.momentum}",
+                "allreduce": f"rccl bucketed {args.bucket_mb} MiB, overlapped",
+                "train_loss_last": round(st["loss_sum"] / (B * args.steps), 4),
+            },
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -96,6 +96,46 @@ void bind_cpu_net(py::module_& m, const char* name) {
       .def("zero_grads", &Net::zero_grads);
 }
 
+// Minimal DLPack (v0.8 ABI) so torch can alias engine-owned device buffers
+// (torch.utils.dlpack.from_dlpack) — e.g. the flat gradient buffer that
+// torch.distributed all-reduces in place.  The capsule does not own memory.
+struct DLDevice { int32_t device_type; int32_t device_id; };
+struct DLDataType { uint8_t code; uint8_t bits; uint16_t lanes; };
+struct DLTensor {
+  void* data; DLDevice device; int32_t ndim; DLDataType dtype;
+  int64_t* shape; int64_t* strides; uint64_t byte_offset;
+};
+struct DLManagedTensor { DLTensor dl_tensor; void* manager_ctx; void (*deleter)(DLManagedTensor*); };
+struct DLHolder { DLManagedTensor t; int64_t shape[1]; int64_t strides[1]; };
+
+void dl_deleter(DLManagedTensor* t) { delete reinterpret_cast<DLHolder*>(t->manager_ctx); }
+
+py::capsule dlpack_wrap(uintptr_t p, int64_t numel, const std::string& dtype, int device) {
+  auto* h = new DLHolder();
+  h->shape[0] = numel;
+  h->strides[0] = 1;
+  h->t.dl_tensor.data = reinterpret_cast<void*>(p);
+  h->t.dl_tensor.device = DLDevice{10 /* kDLROCM */, device};
+  h->t.dl_tensor.ndim = 1;
+  if (dtype == "float32") h->t.dl_tensor.dtype = DLDataType{2, 32, 1};
+  else if (dtype == "bfloat16") h->t.dl_tensor.dtype = DLDataType{4, 16, 1};
+  else if (dtype == "uint8") h->t.dl_tensor.dtype = DLDataType{1, 8, 1};
+  else if (dtype == "int32") h->t.dl_tensor.dtype = DLDataType{0, 32, 1};
+  else { delete h; throw Error("dlpack_wrap: unsupported dtype " + dtype); }
+  h->t.dl_tensor.shape = h->shape;
+  h->t.dl_tensor.strides = h->strides;
+  h->t.dl_tensor.byte_offset = 0;
+  h->t.manager_ctx = h;
+  h->t.deleter = dl_deleter;
+  return py::capsule(&h->t, "dltensor", [](PyObject* cap) {
+    // Only free if torch never consumed it (consumed capsules are renamed).
+    if (PyCapsule_IsValid(cap, "dltensor")) {
+      auto* t = static_cast<DLManagedTensor*>(PyCapsule_GetPointer(cap, "dltensor"));
+      if (t && t->deleter) t->deleter(t);
+    }
+  });
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_C, m) {
@@ -120,6 +160,13 @@ PYBIND11_MODULE(_C, m) {
   m.def("make_model", &make_model, py::arg("name"));
   m.def("model_names", &model_names);
   m.def("parse_model_spec", &parse_model_spec, py::arg("text"), py::arg("name") = "custom");
+  m.def("plan_buckets",
+        [](const ModelSpec& s, int64_t bytes) {
+          py::list l;
+          for (const auto& b : plan_buckets(s, bytes)) l.append(py::make_tuple(b.stage_hi, b.stage_lo, b.off, b.count));
+          return l;
+        },
+        py::arg("spec"), py::arg("bucket_bytes"));
   m.def("init_params",
         [](const ModelSpec& s, uint64_t seed, const std::string& mode) {
           py::array_t<double> out(s.nparams);
@@ -304,6 +351,7 @@ PYBIND11_MODULE(_C, m) {
   k.attr("ACT_RELU") = (int)gpu::ACT_RELU;
   k.attr("ACT_TANH") = (int)gpu::ACT_TANH;
 
+  m.def("dlpack_wrap", &dlpack_wrap, py::arg("ptr"), py::arg("numel"), py::arg("dtype"), py::arg("device"));
   m.def("device_count", []() {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess) return 0;

@@ -105,6 +105,27 @@ int64_t ModelSpec::macs_per_sample() const {
   return macs;
 }
 
+std::vector<Bucket> plan_buckets(const ModelSpec& spec, int64_t bucket_bytes) {
+  std::vector<const LayerSpec*> stages;
+  for (const auto& L : spec.layers)
+    if (L.nweights > 0) stages.push_back(&L);
+  std::vector<Bucket> out;
+  Bucket cur;
+  bool open = false;
+  for (int s = (int)stages.size() - 1; s >= 0; --s) {
+    const LayerSpec& L = *stages[s];
+    if (!open) { cur = Bucket(); cur.stage_hi = s; open = true; }
+    cur.stage_lo = s;
+    cur.count += L.nweights + L.nbiases;
+    cur.off = L.w_off;
+    if (cur.count * 4 >= bucket_bytes || s == 0) {
+      out.push_back(cur);
+      open = false;
+    }
+  }
+  return out;
+}
+
 ModelBuilder::ModelBuilder(std::string name, int C, int H, int W) {
   m.name = std::move(name);
   LayerSpec in;

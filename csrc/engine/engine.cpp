@@ -146,7 +146,7 @@ void GpuNet::build() {
       st.kbias = st.cvec ? KK * st.CL : KK * st.inC;
       st.ncols_pad = r16(st.kbias + 1);
       const int dw_img_b = img_b + st.cout_pad * st.OH * st.OW * (int)es;
-      st.imgs_dw = std::max(1, std::min(16, 49152 / dw_img_b));
+      st.imgs_dw = std::max(1, std::min(16, 65536 / dw_img_b));
       st.ppad = r32(st.imgs_dw * st.OH * st.OW);
       MCC_CHECK(st.cout_pad <= 128, "conv_small path: Cout > 128");
     } else {
@@ -451,22 +451,11 @@ void GpuNet::stage_param_range(int stage, int64_t& off, int64_t& count) const {
 }
 
 std::vector<GpuBucket> GpuNet::buckets(int64_t bucket_bytes) const {
-  // Walk stages from the last (first to finish in backward) to the first and
-  // cut a bucket whenever the accumulated gradient bytes reach bucket_bytes.
   std::vector<GpuBucket> out;
-  GpuBucket cur;
-  bool open = false;
-  for (int s = (int)stages_.size() - 1; s >= 0; --s) {
-    int64_t off, cnt;
-    stage_param_range(s, off, cnt);
-    if (!open) { cur = GpuBucket(); cur.stage_hi = s; cur.off = off + cnt; open = true; }
-    cur.stage_lo = s;
-    cur.count += cnt;
-    cur.off = off;
-    if (cur.count * 4 >= bucket_bytes || s == 0) {
-      out.push_back(cur);
-      open = false;
-    }
+  for (const Bucket& b : plan_buckets(spec_, bucket_bytes)) {
+    GpuBucket g;
+    g.stage_hi = b.stage_hi; g.stage_lo = b.stage_lo; g.off = b.off; g.count = b.count;
+    out.push_back(g);
   }
   return out;
 }

@@ -62,6 +62,17 @@ struct ModelSpec {
   int64_t macs_per_sample() const;
 };
 
+// Data-parallel gradient buckets.  "Stages" are the parameterised layers in
+// order (exactly the GPU engine's fused stages: a max-pool has no parameters
+// and is fused into the conv before it).  Buckets walk the stages from the
+// LAST one (first to finish in backward) and cut whenever the gradient bytes
+// reach `bucket_bytes`; each bucket is a contiguous range of the flat buffer.
+struct Bucket {
+  int stage_hi = 0, stage_lo = 0;  // inclusive, stage_hi >= stage_lo
+  int64_t off = 0, count = 0;      // elements of the flat fp32 gradient
+};
+std::vector<Bucket> plan_buckets(const ModelSpec& spec, int64_t bucket_bytes);
+
 // Builders used by the model zoo and by the text spec parser.
 struct ModelBuilder {
   ModelSpec m;

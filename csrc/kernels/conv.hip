@@ -7,19 +7,24 @@
 // Design (gfx950):
 //  * A workgroup stages `imgs` whole input images (with the zero halo) into
 //    LDS once, channels padded to 8 ("cvec") so one (kernel-position,
-//    8-channel group) im2col fragment is a single 16-byte ds_read.
+//    8-channel group) im2col fragment is a single 16-byte ds_read.  Staging is
+//    vectorised per 8-channel group for every input transform.
 //  * GEMM rows are output pixels, ordered by 2x2 pooling window when a max-
 //    pool is fused: the 16x16 MFMA C-fragment then gives each lane exactly one
 //    window (4 consecutive rows) of one channel, so bias + ReLU + maxpool +
 //    argmax is an in-register epilogue (no pre-pool tensor ever hits HBM).
+//  * Row -> LDS-offset math is table driven (per-image pixel table in LDS,
+//    reciprocal-multiply division) so the MFMA loop is not VALU-bound on
+//    index arithmetic.
 //  * Backward-data is the same kernel run as a stride-1 conv over the
 //    zero-inserted output gradient with flipped/transposed packed weights; the
 //    ReLU mask and the max-pool routing are applied while staging (IN_RELU /
 //    IN_UNPOOL), so no separate unpool/activation-grad pass exists.
 //  * Weight gradient: MFMA with the pixel dimension as the reduction axis,
 //    the output-gradient tile staged transposed ([co][pixel]), a ones-column
-//    appended to im2col so the bias gradient falls out of the same MFMAs,
-//    per-workgroup fp32 slabs reduced deterministically afterwards.
+//    appended to im2col so the bias gradient falls out of the same MFMAs; the
+//    four waves split the pixel chunks and are combined in LDS in a fixed
+//    order; per-workgroup fp32 slabs are reduced deterministically afterwards.
 #include "kernels.h"
 #include "mfma.h"
 
@@ -30,74 +35,305 @@ namespace {
 
 __device__ __forceinline__ int align16(int bytes) { return (bytes + 15) & ~15; }
 
+// Exact n / d for n < 2^24, d <= 2^16 via one 64-bit multiply-high:
+// m = ceil(2^40 / d); the error term n*(m - 2^40/d)/2^40 < 2^-16 <= 1/d.
+struct Div {
+  uint64_t m;
+  __device__ __forceinline__ explicit Div(int d) : m(((1ull << 40) + (uint64_t)d - 1) / (uint64_t)d) {}
+  __device__ __forceinline__ int div(int n) const { return (int)(((uint64_t)(uint32_t)n * m) >> 40); }
+};
+
+// ---------------------------------------------------------------------------
+// Staging.  Every tile is staged in two passes: a vectorised zero fill of the
+// whole LDS image (halo, channel padding, images past N), a barrier, then a
+// scatter pass over the SOURCE elements only.  The scatter moves channel runs
+// with the widest aligned access (16 B / 4 B / 2 B), and each thread issues
+// U independent loads before its first LDS store so the global-load latency
+// of the (L2-resident) activations overlaps instead of serialising.
+
+constexpr int U = 4;  // loads in flight per thread in the scatter passes
+
 template <typename T>
-__device__ __forceinline__ float stage_value(const StageSrc& s, int n, int sy, int sx, int c) {
-  switch (s.mode) {
-    case IN_U8: {
-      const int img = s.idx ? s.idx[n] : n;
-      const uint8_t* u = static_cast<const uint8_t*>(s.src);
-      return (float)u[(((size_t)img * s.SH + sy) * s.SW + sx) * s.SC + c] * (1.0f / 255.0f);
+__device__ __forceinline__ void lds_zero(T* p, int n) {
+  typedef typename Vec8<T>::type V8;
+  V8 z;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) z[j] = T(0);
+  for (int i = threadIdx.x * 8; i < n; i += blockDim.x * 8) store8(p + i, z);
+}
+
+__host__ __device__ __forceinline__ int round8(int n) { return (n + 7) & ~7; }
+
+__device__ __forceinline__ int chan_vw(int SC) { return (SC & 7) == 0 ? 8 : ((SC & 1) == 0 ? 2 : 1); }
+
+template <typename T, int VW>
+__device__ __forceinline__ void ld_run(const T* p, T (&v)[VW]) {
+  if constexpr (VW == 8) {
+    const auto x = load8(p);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = x[j];
+  } else if constexpr (VW == 2) {
+    if constexpr (sizeof(T) == 2) {
+      const uint32_t w = *reinterpret_cast<const uint32_t*>(p);
+      v[0] = __builtin_bit_cast(T, (unsigned short)(w & 0xffffu));
+      v[1] = __builtin_bit_cast(T, (unsigned short)(w >> 16));
+    } else {
+      const float2 w = *reinterpret_cast<const float2*>(p);
+      v[0] = w.x;
+      v[1] = w.y;
     }
-    case IN_RELU: {
-      const size_t i = (((size_t)n * s.SH + sy) * s.SW + sx) * s.SC + c;
-      const float y = to_f(static_cast<const T*>(s.aux_y)[i]);
-      return y > 0.f ? to_f(static_cast<const T*>(s.src)[i]) : 0.f;
-    }
-    case IN_UNPOOL: {
-      const int py = sy >> 1, px = sx >> 1;
-      if (py >= s.PH || px >= s.PW) return 0.f;
-      const size_t i = (((size_t)n * s.PH + py) * s.PW + px) * s.SC + c;
-      const int pos = ((sy & 1) << 1) | (sx & 1);
-      if (s.aux_arg[i] != pos) return 0.f;
-      const float y = to_f(static_cast<const T*>(s.aux_y)[i]);
-      return y > 0.f ? to_f(static_cast<const T*>(s.src)[i]) : 0.f;
-    }
-    default:
-      return to_f(static_cast<const T*>(s.src)[(((size_t)n * s.SH + sy) * s.SW + sx) * s.SC + c]);
+  } else {
+    v[0] = *p;
   }
 }
 
-// Stage `imgs` images starting at img0 into lds[img][LH][LW][CL] (zero halo,
-// zero channel padding, zero rows past N).
-template <typename T>
-__device__ void stage_tile(const StageSrc& s, T* lds, int img0, int N, int imgs, int LH, int LW, int CL,
-                           bool cvec) {
-  const int per_img = LH * LW;
-  const int total = imgs * per_img;
-  const bool vec_plain = cvec && s.mode == IN_PLAIN && (s.SC & 7) == 0;
-  for (int e = threadIdx.x; e < total; e += blockDim.x) {
-    const int img = e / per_img;
-    const int rem = e - img * per_img;
-    const int ly = rem / LW;
-    const int lx = rem - ly * LW;
-    const int n = img0 + img;
-    const int ty = ly - s.off, tx = lx - s.off;
-    bool valid = n < N && ty >= 0 && tx >= 0;
-    int sy = ty, sx = tx;
-    if (s.up != 1) {
-      valid = valid && (ty % s.up) == 0 && (tx % s.up) == 0;
-      sy = ty / s.up;
-      sx = tx / s.up;
-    }
-    valid = valid && sy < s.SH && sx < s.SW;
-    T* dst = lds + (size_t)e * CL;
-    if (cvec) {
-      for (int cg = 0; cg < (CL >> 3); ++cg) {
-        typename Vec8<T>::type v;
-        if (vec_plain && valid) {
-          v = load8(static_cast<const T*>(s.src) + (((size_t)n * s.SH + sy) * s.SW + sx) * s.SC + cg * 8);
-        } else {
+template <typename T, int VW>
+__device__ __forceinline__ void st_run(T* p, const T (&v)[VW]) {
+  if constexpr (VW == 8) {
+    typename Vec8<T>::type x;
 #pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const int c = cg * 8 + j;
-            v[j] = (valid && c < s.SC) ? from_f<T>(stage_value<T>(s, n, sy, sx, c)) : T(0);
-          }
-        }
-        store8(dst + cg * 8, v);
-      }
+    for (int j = 0; j < 8; ++j) x[j] = v[j];
+    store8(p, x);
+  } else if constexpr (VW == 2) {
+    if constexpr (sizeof(T) == 2) {
+      const uint32_t w = (uint32_t)__builtin_bit_cast(unsigned short, v[0]) |
+                         ((uint32_t)__builtin_bit_cast(unsigned short, v[1]) << 16);
+      *reinterpret_cast<uint32_t*>(p) = w;
     } else {
-      for (int c = 0; c < CL; ++c) dst[c] = valid ? from_f<T>(stage_value<T>(s, n, sy, sx, c)) : T(0);
+      *reinterpret_cast<float2*>(p) = make_float2(v[0], v[1]);
     }
+  } else {
+    *p = v[0];
+  }
+}
+
+template <int VW>
+__device__ __forceinline__ void ld_arg(const uint8_t* p, uint32_t (&a)[VW]) {
+  if constexpr (VW == 8) {
+    const uint2 w = *reinterpret_cast<const uint2*>(p);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) a[j] = ((j < 4 ? w.x : w.y) >> (8 * (j & 3))) & 0xffu;
+  } else if constexpr (VW == 2) {
+    const uint32_t w = *reinterpret_cast<const unsigned short*>(p);
+    a[0] = w & 0xffu;
+    a[1] = w >> 8;
+  } else {
+    a[0] = *p;
+  }
+}
+
+// Tile coordinate of a source element (zero insertion: s*up + off), -1 if outside.
+__device__ __forceinline__ int tile_coord(int sc, const StageSrc& s, int L) {
+  const int l = sc * s.up + s.off;
+  return (l >= 0 && l < L) ? l : -1;
+}
+
+// Where one channel-run of source pixel (sy, sx) lands.  DY=false: the
+// NHWC image lds[img][LH][LW][CL]; DY=true: the transposed conv-output
+// gradient dys[c][img*OH*OW + y*OW + x] (LH = OH, LW = OW, CL = row stride).
+template <bool DY>
+__device__ __forceinline__ int dst_index(int img, int ly, int lx, int c, int LH, int LW, int CL) {
+  if (DY) return c * CL + (img * LH + ly) * LW + lx;
+  return ((img * LH + ly) * LW + lx) * CL + c;
+}
+
+template <typename T, int VW, bool RELU, bool DY>
+__device__ void scatter_dense(const StageSrc& s, T* lds, int img0, int nimg, int LH, int LW, int CL) {
+  const T* src = static_cast<const T*>(s.src);
+  const T* ay = static_cast<const T*>(s.aux_y);
+  const int CV = s.SC / VW;
+  const int spix = s.SH * s.SW;
+  const int total = nimg * spix * CV;
+  const Div dcv(CV), dsw(s.SW), dsp(spix);
+  for (int e0 = threadIdx.x; e0 < total; e0 += U * blockDim.x) {
+    T v[U][VW], y[U][VW];
+    int img[U], ly[U], lx[U], c0[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int e = e0 + u * blockDim.x;
+      ly[u] = -1;
+      if (e < total) {
+        const int pix = dcv.div(e), cv = e - pix * CV;
+        const int im = dsp.div(pix), rem = pix - im * spix;
+        const int sy = dsw.div(rem), sx = rem - sy * s.SW;
+        const size_t gi = ((size_t)(img0 + im) * spix + rem) * s.SC + cv * VW;
+        ld_run<T, VW>(src + gi, v[u]);
+        if (RELU) ld_run<T, VW>(ay + gi, y[u]);
+        img[u] = im;
+        c0[u] = cv * VW;
+        lx[u] = tile_coord(sx, s, LW);
+        ly[u] = lx[u] < 0 ? -1 : tile_coord(sy, s, LH);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (ly[u] < 0) continue;
+      if (RELU) {
+#pragma unroll
+        for (int j = 0; j < VW; ++j) v[u][j] = to_f(y[u][j]) > 0.f ? v[u][j] : T(0);
+      }
+      if (DY) {
+#pragma unroll
+        for (int j = 0; j < VW; ++j) lds[dst_index<true>(img[u], ly[u], lx[u], c0[u] + j, LH, LW, CL)] = v[u][j];
+      } else {
+        st_run<T, VW>(lds + dst_index<false>(img[u], ly[u], lx[u], c0[u], LH, LW, CL), v[u]);
+      }
+    }
+  }
+}
+
+// Max-pool + ReLU backward folded into staging: one item per POOLED element
+// run; the gradient goes to the argmax position of its 2x2 window when the
+// pooled (= post-ReLU) output is positive.  Everything else stays zero.
+template <typename T, int VW, bool DY>
+__device__ void scatter_unpool(const StageSrc& s, T* lds, int img0, int nimg, int LH, int LW, int CL) {
+  const T* src = static_cast<const T*>(s.src);
+  const T* ay = static_cast<const T*>(s.aux_y);
+  const int CV = s.SC / VW;
+  const int ppix = s.PH * s.PW;
+  const int total = nimg * ppix * CV;
+  const Div dcv(CV), dpw(s.PW), dpp(ppix);
+  for (int e0 = threadIdx.x; e0 < total; e0 += U * blockDim.x) {
+    T d[U][VW], y[U][VW];
+    uint32_t a[U][VW];
+    int img[U], py[U], px[U], c0[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int e = e0 + u * blockDim.x;
+      py[u] = -1;
+      if (e < total) {
+        const int pix = dcv.div(e), cv = e - pix * CV;
+        const int im = dpp.div(pix), rem = pix - im * ppix;
+        const size_t gi = ((size_t)(img0 + im) * ppix + rem) * s.SC + cv * VW;
+        ld_run<T, VW>(src + gi, d[u]);
+        ld_run<T, VW>(ay + gi, y[u]);
+        ld_arg<VW>(s.aux_arg + gi, a[u]);
+        img[u] = im;
+        c0[u] = cv * VW;
+        py[u] = dpw.div(rem);
+        px[u] = rem - py[u] * s.PW;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (py[u] < 0) continue;
+#pragma unroll
+      for (int j = 0; j < VW; ++j) {
+        if (!(to_f(y[u][j]) > 0.f)) continue;
+        const int oy = 2 * py[u] + (int)(a[u][j] >> 1), ox = 2 * px[u] + (int)(a[u][j] & 1);
+        const int lx = tile_coord(ox, s, LW), ly = tile_coord(oy, s, LH);
+        if (lx < 0 || ly < 0) continue;
+        lds[dst_index<DY>(img[u], ly, lx, c0[u] + j, LH, LW, CL)] = d[u][j];
+      }
+    }
+  }
+}
+
+// u8 images (optionally gathered through idx), scaled by 1/255 (cnn.c:457).
+// Rows are moved as 32-bit words when a row is a whole number of words.
+template <typename T>
+__device__ void scatter_u8(const StageSrc& s, T* lds, int img0, int nimg, int LH, int LW, int CL) {
+  const uint8_t* src = static_cast<const uint8_t*>(s.src);
+  const int row_bytes = s.SW * s.SC;
+  const float inv = 1.0f / 255.0f;
+  const Div dsc(s.SC);
+  if ((row_bytes & 3) == 0) {
+    const int wpr = row_bytes >> 2;
+    const int wpi = s.SH * wpr;
+    const int total = nimg * wpi;
+    const Div dwpr(wpr), dwpi(wpi);
+    for (int e0 = threadIdx.x; e0 < total; e0 += U * blockDim.x) {
+      uint32_t w[U];
+      int img[U], sy[U], wi[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int e = e0 + u * blockDim.x;
+        img[u] = -1;
+        if (e < total) {
+          const int im = dwpi.div(e), rem = e - im * wpi;
+          const int y = dwpr.div(rem), ww = rem - y * wpr;
+          const int n = img0 + im;
+          const int gim = s.idx ? s.idx[n] : n;
+          w[u] = *reinterpret_cast<const uint32_t*>(src + ((size_t)gim * s.SH + y) * row_bytes + 4 * ww);
+          img[u] = im;
+          sy[u] = y;
+          wi[u] = ww;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (img[u] < 0) continue;
+        const int ly = tile_coord(sy[u], s, LH);
+        if (ly < 0) continue;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int flat = 4 * wi[u] + j;
+          const int sx = dsc.div(flat), c = flat - sx * s.SC;
+          const int lx = tile_coord(sx, s, LW);
+          if (lx < 0) continue;
+          lds[((img[u] * LH + ly) * LW + lx) * CL + c] = from_f<T>((float)((w[u] >> (8 * j)) & 0xffu) * inv);
+        }
+      }
+    }
+  } else {
+    const int total = nimg * s.SH * row_bytes;
+    const Div drb(row_bytes), dsh(s.SH);
+    for (int e = threadIdx.x; e < total; e += blockDim.x) {
+      const int r = drb.div(e), b = e - r * row_bytes;
+      const int im = dsh.div(r), y = r - im * s.SH;
+      const int n = img0 + im;
+      const int gim = s.idx ? s.idx[n] : n;
+      const uint8_t v = src[((size_t)gim * s.SH + y) * row_bytes + b];
+      const int sx = dsc.div(b), c = b - sx * s.SC;
+      const int ly = tile_coord(y, s, LH), lx = tile_coord(sx, s, LW);
+      if (ly >= 0 && lx >= 0) lds[((im * LH + ly) * LW + lx) * CL + c] = from_f<T>((float)v * inv);
+    }
+  }
+}
+
+// Scatter pass (after the zero fill + barrier) for an NHWC tile (DY=false) or
+// the transposed conv-output gradient (DY=true).
+template <typename T, bool DY>
+__device__ void stage_scatter(const StageSrc& s, T* lds, int img0, int nimg, int LH, int LW, int CL) {
+  const int vw = chan_vw(s.SC);
+  switch (s.mode) {
+    case IN_U8:
+      if (!DY) scatter_u8<T>(s, lds, img0, nimg, LH, LW, CL);
+      break;
+    case IN_UNPOOL:
+      if (vw == 8) scatter_unpool<T, 8, DY>(s, lds, img0, nimg, LH, LW, CL);
+      else if (vw == 2) scatter_unpool<T, 2, DY>(s, lds, img0, nimg, LH, LW, CL);
+      else scatter_unpool<T, 1, DY>(s, lds, img0, nimg, LH, LW, CL);
+      break;
+    case IN_RELU:
+      if (vw == 8) scatter_dense<T, 8, true, DY>(s, lds, img0, nimg, LH, LW, CL);
+      else if (vw == 2) scatter_dense<T, 2, true, DY>(s, lds, img0, nimg, LH, LW, CL);
+      else scatter_dense<T, 1, true, DY>(s, lds, img0, nimg, LH, LW, CL);
+      break;
+    default:
+      if (vw == 8) scatter_dense<T, 8, false, DY>(s, lds, img0, nimg, LH, LW, CL);
+      else if (vw == 2) scatter_dense<T, 2, false, DY>(s, lds, img0, nimg, LH, LW, CL);
+      else scatter_dense<T, 1, false, DY>(s, lds, img0, nimg, LH, LW, CL);
+  }
+}
+
+// Per-image conv-output pixel -> LDS offset of its top-left tap.  With a fused
+// pool the pixel order is (window, position) so a 16-row MFMA tile holds four
+// whole 2x2 windows.
+__device__ __forceinline__ void pixel_table(int* tab, int rows, bool pool, int OW, int PW, int cs, int LW, int CL) {
+  const Div dow(OW), dpw(pool ? PW : 1);
+  for (int r = threadIdx.x; r < rows; r += blockDim.x) {
+    int oy, ox;
+    if (pool) {
+      const int win = r >> 2, pos = r & 3;
+      const int ph = dpw.div(win), pw = win - ph * PW;
+      oy = 2 * ph + (pos >> 1);
+      ox = 2 * pw + (pos & 1);
+    } else {
+      oy = dow.div(r);
+      ox = r - oy * OW;
+    }
+    tab[r] = (oy * cs * LW + ox * cs) * CL;
   }
 }
 
@@ -107,16 +343,23 @@ __global__ void __launch_bounds__(256) conv_fwd_kernel(ConvParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   T* xs = reinterpret_cast<T*>(smem);
   const int img_elems = p.LH * p.LW * p.CL;
-  const int zoff = p.imgs * img_elems;
-  int* ktab = reinterpret_cast<int*>(smem + align16((zoff + 16) * (int)sizeof(T)));
+  const int xs_elems = round8(p.imgs * img_elems + 16);
+  const bool pool = p.pool == 2;
+  const int PH = p.OH >> 1, PW = p.OW >> 1;
+  const int rows_per_img = pool ? PH * PW * 4 : p.OH * p.OW;
+  const int nk = CVEC ? p.nchunks * 4 : p.nchunks * 32;
+  int* ktab = reinterpret_cast<int*>(smem + align16(xs_elems * (int)sizeof(T)));
+  int* ptab = ktab + ((nk + 3) & ~3);
   const int img0 = blockIdx.x * p.imgs;
+  const int nimg = min(p.imgs, p.N - img0);
   const int tid = threadIdx.x;
 
-  // k -> LDS offset table (relative to a pixel's top-left tap); -1 = padding.
-  const int nk = CVEC ? p.nchunks * 4 : p.nchunks * 32;
+  lds_zero(xs, xs_elems);
+  // k -> LDS offset table (relative to a pixel's top-left tap).  Padding
+  // entries point at tap 0: their weights are zero, any finite value works.
   const int KK = p.KS * p.KS;
   for (int e = tid; e < nk; e += blockDim.x) {
-    int off = -1;
+    int off = 0;
     if (CVEC) {
       const int CG = p.CL >> 3;
       const int kp = e / CG, cg = e - kp * CG;
@@ -131,18 +374,16 @@ __global__ void __launch_bounds__(256) conv_fwd_kernel(ConvParams p) {
     }
     ktab[e] = off;
   }
-  stage_tile<T>(p.in, xs, img0, p.N, p.imgs, p.LH, p.LW, p.CL, CVEC);
-  if (tid < 16) xs[zoff + tid] = T(0);
+  pixel_table(ptab, rows_per_img, pool, p.OW, PW, p.cs, p.LW, p.CL);
+  __syncthreads();
+  stage_scatter<T, false>(p.in, xs, img0, nimg, p.LH, p.LW, p.CL);
   __syncthreads();
 
   const int lane = tid & 63, wave = tid >> 6, nwaves = blockDim.x >> 6;
   const int r16 = lane & 15, g = lane >> 4;
-  const int nimg = min(p.imgs, p.N - img0);
-  const bool pool = p.pool == 2;
-  const int PH = p.OH >> 1, PW = p.OW >> 1;
-  const int rows_per_img = pool ? PH * PW * 4 : p.OH * p.OW;
   const int M = nimg * rows_per_img;
   const int mtiles = cdiv(M, 16), ntiles = cdiv(p.Cout, 16), mgroups = cdiv(mtiles, MT);
+  const Div drpi(rows_per_img);
   const T* wpk = static_cast<const T*>(p.wpk);
   T* out = static_cast<T*>(p.out);
 
@@ -151,23 +392,10 @@ __global__ void __launch_bounds__(256) conv_fwd_kernel(ConvParams p) {
     int base[MT];
 #pragma unroll
     for (int t = 0; t < MT; ++t) {
+      // rows past M read image 0 (finite, discarded by the epilogue)
       const int r = (mg * MT + t) * 16 + r16;
-      base[t] = -1;
-      if (r < M) {
-        const int img = r / rows_per_img;
-        const int rem = r - img * rows_per_img;
-        int oy, ox;
-        if (pool) {
-          const int win = rem >> 2, pos = rem & 3;
-          const int ph = win / PW, pw = win - ph * PW;
-          oy = 2 * ph + (pos >> 1);
-          ox = 2 * pw + (pos & 1);
-        } else {
-          oy = rem / p.OW;
-          ox = rem - oy * p.OW;
-        }
-        base[t] = img * img_elems + (oy * p.cs * p.LW + ox * p.cs) * p.CL;
-      }
+      const int img = drpi.div(r);
+      base[t] = r < M ? img * img_elems + ptab[r - img * rows_per_img] : 0;
     }
     f32x4 acc[MT];
 #pragma unroll
@@ -178,10 +406,7 @@ __global__ void __launch_bounds__(256) conv_fwd_kernel(ConvParams p) {
       if (CVEC) {
         const int ko = ktab[q * 4 + g];
 #pragma unroll
-        for (int t = 0; t < MT; ++t) {
-          const int a_off = (base[t] >= 0 && ko >= 0) ? base[t] + ko : zoff;
-          acc[t] = mma(acc[t], load8(xs + a_off), b);
-        }
+        for (int t = 0; t < MT; ++t) acc[t] = mma(acc[t], load8(xs + base[t] + ko), b);
       } else {
         int ko[8];
 #pragma unroll
@@ -190,7 +415,7 @@ __global__ void __launch_bounds__(256) conv_fwd_kernel(ConvParams p) {
         for (int t = 0; t < MT; ++t) {
           V8 a;
 #pragma unroll
-          for (int j = 0; j < 8; ++j) a[j] = xs[(base[t] >= 0 && ko[j] >= 0) ? base[t] + ko[j] : zoff];
+          for (int j = 0; j < 8; ++j) a[j] = xs[base[t] + ko[j]];
           acc[t] = mma(acc[t], a, b);
         }
       }
@@ -230,28 +455,29 @@ __global__ void __launch_bounds__(256) conv_dw_kernel(ConvDwParams p) {
   typedef typename Vec8<T>::type V8;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int img_elems = p.LH * p.LW * p.CL;
-  const int zoff = p.imgs * img_elems;
+  const int xs_elems = round8(p.imgs * img_elems + 16);
   T* xs = reinterpret_cast<T*>(smem);
   const int drow = p.ppad + 8;
-  T* dys = reinterpret_cast<T*>(smem + align16((zoff + 16) * (int)sizeof(T)));
+  T* dys = reinterpret_cast<T*>(smem + align16(xs_elems * (int)sizeof(T)));
   int* pixbase = reinterpret_cast<int*>(reinterpret_cast<char*>(dys) + align16(p.cout_pad * drow * (int)sizeof(T)));
+  int* ptab = pixbase + p.ppad;
+  float* red = reinterpret_cast<float*>(smem);  // reused after the main loop
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6, nwaves = blockDim.x >> 6;
   const int r16 = lane & 15, g = lane >> 4;
-  const int ncol_tiles = p.ncols_pad >> 4;
   const int KK = p.KS * p.KS;
   const int CG = p.CL >> 3;
+  const int opix = p.OH * p.OW;
 
+  // im2col column of this lane per owned column tile; padding columns read
+  // tap 0 (finite; their dW entries are never used), the bias column reads 1.
   int koff[NTW];
   bool is_bias[NTW];
-  int ntile_of[NTW];
 #pragma unroll
   for (int t = 0; t < NTW; ++t) {
-    const int nti = (blockIdx.y * nwaves + wave) * NTW + t;
-    ntile_of[t] = nti;
-    const int col = nti * 16 + r16;
-    koff[t] = -1;
+    const int col = (blockIdx.y * NTW + t) * 16 + r16;
+    koff[t] = 0;
     is_bias[t] = col == p.kbias;
     if (col < p.kbias) {
       int kp, c;
@@ -269,6 +495,7 @@ __global__ void __launch_bounds__(256) conv_dw_kernel(ConvDwParams p) {
       }
     }
   }
+  pixel_table(ptab, opix, false, p.OW, 1, p.cs, p.LW, p.CL);
 
   f32x4 acc[MTW][NTW];
 #pragma unroll
@@ -276,94 +503,108 @@ __global__ void __launch_bounds__(256) conv_dw_kernel(ConvDwParams p) {
 #pragma unroll
     for (int t = 0; t < NTW; ++t) acc[m][t] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int opix = p.OH * p.OW;
+  const Div dopix(opix);
+  const T one = T(1);
   for (int img0 = blockIdx.x * p.imgs; img0 < p.N; img0 += p.nx * p.imgs) {
-    __syncthreads();
-    stage_tile<T>(p.x, xs, img0, p.N, p.imgs, p.LH, p.LW, p.CL, CVEC);
-    if (tid < 16) xs[zoff + tid] = T(0);
     const int nimg = min(p.imgs, p.N - img0);
     const int npix = nimg * opix;
-    // dY tile, transposed to [co][pixel] (pixel-contiguous A fragments).
-    for (int e = tid; e < p.ppad * p.cout_pad; e += blockDim.x) {
-      const int pix = e / p.cout_pad, co = e - pix * p.cout_pad;
-      float v = 0.f;
-      if (pix < npix && co < p.Cout) {
-        const int img = pix / opix, rem = pix - img * opix;
-        const int oy = rem / p.OW, ox = rem - oy * p.OW;
-        v = stage_value<T>(p.dy, img0 + img, oy, ox, co);
-      }
-      dys[co * drow + pix] = from_f<T>(v);
-    }
+    __syncthreads();  // previous stage fully consumed
+    lds_zero(xs, xs_elems);
+    lds_zero(dys, p.cout_pad * drow);
+    __syncthreads();
+    stage_scatter<T, false>(p.x, xs, img0, nimg, p.LH, p.LW, p.CL);
+    stage_scatter<T, true>(p.dy, dys, img0, nimg, p.OH, p.OW, drow);
     for (int pix = tid; pix < p.ppad; pix += blockDim.x) {
-      int b = -1;
-      if (pix < npix) {
-        const int img = pix / opix, rem = pix - img * opix;
-        const int oy = rem / p.OW, ox = rem - oy * p.OW;
-        b = img * img_elems + (oy * p.cs * p.LW + ox * p.cs) * p.CL;
-      }
-      pixbase[pix] = b;
+      const int img = dopix.div(pix);
+      pixbase[pix] = pix < npix ? img * img_elems + ptab[pix - img * opix] : 0;  // dY is 0 there
     }
     __syncthreads();
     const int nq = cdiv(npix, 32);
-    for (int q = 0; q < nq; ++q) {
+    for (int q = wave; q < nq; q += nwaves) {
       int pb[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) pb[j] = pixbase[q * 32 + 8 * g + j];
-      V8 b[NTW];
+      V8 a[MTW];
+#pragma unroll
+      for (int m = 0; m < MTW; ++m) a[m] = load8(dys + (m * 16 + r16) * drow + q * 32 + 8 * g);
 #pragma unroll
       for (int t = 0; t < NTW; ++t) {
+        V8 b;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float one = is_bias[t] ? 1.f : 0.f;
-          b[t][j] = (koff[t] >= 0 && pb[j] >= 0) ? xs[pb[j] + koff[t]] : from_f<T>(one);
-        }
-      }
+        for (int j = 0; j < 8; ++j) b[j] = is_bias[t] ? one : xs[pb[j] + koff[t]];
 #pragma unroll
-      for (int m = 0; m < MTW; ++m) {
-        const V8 a = load8(dys + (m * 16 + r16) * drow + q * 32 + 8 * g);
-#pragma unroll
-        for (int t = 0; t < NTW; ++t) acc[m][t] = mma(acc[m][t], a, b[t]);
+        for (int m = 0; m < MTW; ++m) acc[m][t] = mma(acc[m][t], a[m], b);
       }
     }
   }
-  // Write this workgroup's partial sums.
+  // Combine the waves' partial sums in a fixed order (deterministic), then
+  // write this workgroup's slab.  red: [MTW*16 rows][NTW*16 cols] fp32.
+  const int rcols = NTW * 16;
+  for (int w = 0; w < nwaves; ++w) {
+    __syncthreads();
+    if (wave == w) {
 #pragma unroll
-  for (int m = 0; m < MTW; ++m) {
-    if (m * 16 >= p.cout_pad) break;
+      for (int m = 0; m < MTW; ++m)
 #pragma unroll
-    for (int t = 0; t < NTW; ++t) {
-      if (ntile_of[t] >= ncol_tiles) continue;
-      const int col = ntile_of[t] * 16 + r16;
+        for (int t = 0; t < NTW; ++t)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int row = m * 16 + 4 * g + i;
-        p.slab[((size_t)blockIdx.x * p.cout_pad + row) * p.ncols_pad + col] = acc[m][t][i];
-      }
+          for (int i = 0; i < 4; ++i) {
+            float* d = red + (m * 16 + 4 * g + i) * rcols + t * 16 + r16;
+            *d = (w == 0 ? 0.f : *d) + acc[m][t][i];
+          }
     }
+  }
+  __syncthreads();
+  for (int e = tid; e < p.cout_pad * rcols; e += blockDim.x) {
+    const int row = e / rcols, c = e - row * rcols;
+    const int col = blockIdx.y * rcols + c;
+    if (col < p.ncols_pad)
+      p.slab[((size_t)blockIdx.x * p.cout_pad + row) * p.ncols_pad + col] = red[row * rcols + c];
   }
 }
 
-__global__ void conv_dw_reduce_kernel(ConvDwReduceParams p) {
+// grid.x over 32-parameter blocks, 8 partial-sum rows of x per block.
+__global__ void __launch_bounds__(256) conv_dw_reduce_kernel(ConvDwReduceParams p) {
+  __shared__ float part[8][33];
   const int KK = p.KS * p.KS;
   const int nW = p.Cout * p.Cin * KK;
-  const int j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= nW + p.Cout) return;
-  int row, col;
-  if (j < nW) {
-    row = j / (p.Cin * KK);
-    const int rem = j - row * p.Cin * KK;
-    const int i = rem / KK, kp = rem - i * KK;
-    col = p.cvec ? (kp * p.CG + (i >> 3)) * 8 + (i & 7) : kp * p.Cin + i;
-  } else {
-    row = j - nW;
-    col = p.kbias;
-  }
-  const float* s = p.slab + (size_t)row * p.ncols_pad + col;
-  const size_t stride = (size_t)p.cout_pad * p.ncols_pad;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  const int j = blockIdx.x * 32 + tx;
   float acc = 0.f;
-  for (int x = 0; x < p.nx; ++x) acc += s[x * stride];
-  float* dst = j < nW ? p.gw + j : p.gb + (j - nW);
-  *dst = p.beta != 0.f ? p.beta * *dst + acc : acc;
+  int row = 0, col = 0;
+  const bool ok = j < nW + p.Cout;
+  if (ok) {
+    if (j < nW) {
+      row = j / (p.Cin * KK);
+      const int rem = j - row * p.Cin * KK;
+      const int i = rem / KK, kp = rem - i * KK;
+      col = p.cvec ? (kp * p.CG + (i >> 3)) * 8 + (i & 7) : kp * p.Cin + i;
+    } else {
+      row = j - nW;
+      col = p.kbias;
+    }
+    const float* s = p.slab + (size_t)row * p.ncols_pad + col;
+    const size_t stride = (size_t)p.cout_pad * p.ncols_pad;
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    int x = ty;
+    for (; x + 24 < p.nx; x += 32) {
+      a0 += s[(size_t)x * stride];
+      a1 += s[(size_t)(x + 8) * stride];
+      a2 += s[(size_t)(x + 16) * stride];
+      a3 += s[(size_t)(x + 24) * stride];
+    }
+    for (; x < p.nx; x += 8) a0 += s[(size_t)x * stride];
+    acc = (a0 + a1) + (a2 + a3);
+  }
+  part[ty][tx] = acc;
+  __syncthreads();
+  if (ty == 0 && ok) {
+    float sum = 0.f;
+#pragma unroll
+    for (int r = 0; r < 8; ++r) sum += part[r][tx];
+    float* dst = j < nW ? p.gw + j : p.gb + (j - nW);
+    *dst = p.beta != 0.f ? p.beta * *dst + sum : sum;
+  }
 }
 
 inline size_t a16(size_t b) { return (b + 15) & ~size_t(15); }
@@ -378,18 +619,25 @@ void launch_conv_fwd(const ConvParams& p, hipStream_t s) {
     hipLaunchKernelGGL((conv_fwd_kernel<T, false, 4>), grid, block, lds, s, p);
 }
 
+int dw_ntw(int mtw) { return mtw <= 1 ? 16 : (mtw <= 2 ? 8 : (mtw <= 4 ? 4 : 2)); }
+
 template <typename T, bool CVEC>
 void launch_conv_dw_c(const ConvDwParams& p, hipStream_t s, size_t lds) {
   const int mtw = p.cout_pad / 16;
   const int ncol_tiles = p.ncols_pad / 16;
   auto go = [&](auto kern, int ntw) {
-    const dim3 grid((unsigned)p.nx, (unsigned)cdiv(ncol_tiles, 4 * ntw)), block(256);
+    const dim3 grid((unsigned)p.nx, (unsigned)cdiv(ncol_tiles, ntw)), block(256);
     hipLaunchKernelGGL(kern, grid, block, lds, s, p);
   };
-  if (mtw <= 1) go(conv_dw_kernel<T, CVEC, 1, 4>, 4);
-  else if (mtw <= 2) go(conv_dw_kernel<T, CVEC, 2, 4>, 4);
-  else if (mtw <= 4) go(conv_dw_kernel<T, CVEC, 4, 2>, 2);
-  else if (mtw <= 8) go(conv_dw_kernel<T, CVEC, 8, 1>, 1);
+  // Smallest NTW that covers the column tiles keeps the register footprint low.
+  if (mtw <= 1) {
+    if (ncol_tiles <= 2) go(conv_dw_kernel<T, CVEC, 1, 2>, 2);
+    else if (ncol_tiles <= 4) go(conv_dw_kernel<T, CVEC, 1, 4>, 4);
+    else if (ncol_tiles <= 8) go(conv_dw_kernel<T, CVEC, 1, 8>, 8);
+    else go(conv_dw_kernel<T, CVEC, 1, 16>, 16);
+  } else if (mtw <= 2) go(conv_dw_kernel<T, CVEC, 2, 8>, 8);
+  else if (mtw <= 4) go(conv_dw_kernel<T, CVEC, 4, 4>, 4);
+  else if (mtw <= 8) go(conv_dw_kernel<T, CVEC, 8, 2>, 2);
   else MCC_CHECK(false, "conv_dw: Cout > 128 not supported by conv_small");
 }
 
@@ -398,13 +646,17 @@ void launch_conv_dw_c(const ConvDwParams& p, hipStream_t s, size_t lds) {
 size_t conv_forward_lds_bytes(DType t, const ConvParams& p) {
   const size_t es = t == DType::BF16 ? 2 : 4;
   const size_t nk = p.cvec ? (size_t)p.nchunks * 4 : (size_t)p.nchunks * 32;
-  return a16(((size_t)p.imgs * p.LH * p.LW * p.CL + 16) * es) + nk * 4;
+  const size_t rows = p.pool == 2 ? (size_t)(p.OH / 2) * (p.OW / 2) * 4 : (size_t)p.OH * p.OW;
+  return a16((size_t)round8(p.imgs * p.LH * p.LW * p.CL + 16) * es) + ((nk + 3) & ~size_t(3)) * 4 + rows * 4;
 }
 
 size_t conv_dw_lds_bytes(DType t, const ConvDwParams& p) {
   const size_t es = t == DType::BF16 ? 2 : 4;
-  return a16(((size_t)p.imgs * p.LH * p.LW * p.CL + 16) * es) + a16((size_t)p.cout_pad * (p.ppad + 8) * es) +
-         (size_t)p.ppad * 4;
+  const size_t stage = a16((size_t)round8(p.imgs * p.LH * p.LW * p.CL + 16) * es) +
+                       a16((size_t)p.cout_pad * (p.ppad + 8) * es) + (size_t)p.ppad * 4 + (size_t)p.OH * p.OW * 4;
+  const int mtw = p.cout_pad / 16;
+  const size_t red = (size_t)p.cout_pad * dw_ntw(mtw) * 16 * 4;
+  return stage > red ? stage : red;
 }
 
 void conv_forward(DType t, const ConvParams& p, hipStream_t s) {
@@ -412,6 +664,7 @@ void conv_forward(DType t, const ConvParams& p, hipStream_t s) {
   MCC_CHECK(!p.cvec || (p.CL % 8) == 0, "conv_forward: cvec needs CL % 8 == 0");
   MCC_CHECK(p.kpad == p.nchunks * 32, "conv_forward: kpad mismatch");
   MCC_CHECK(p.pool == 1 || (p.pool == 2 && p.bias_act && p.out_arg), "conv_forward: bad pool config");
+  MCC_CHECK((int64_t)p.imgs * p.LH * p.LW * p.CL < (1 << 24), "conv_forward: tile too large for index math");
   MCC_CHECK(conv_forward_lds_bytes(t, p) <= 160 * 1024, "conv_forward: LDS tile exceeds 160 KiB");
   if (t == DType::BF16) launch_conv_fwd<bf16>(p, s);
   else launch_conv_fwd<float>(p, s);
@@ -421,6 +674,8 @@ void conv_dw(DType t, const ConvDwParams& p, hipStream_t s) {
   MCC_CHECK(p.N > 0 && p.imgs > 0 && p.nx > 0, "conv_dw: empty problem");
   MCC_CHECK(p.ppad % 32 == 0 && p.ppad >= p.imgs * p.OH * p.OW, "conv_dw: bad ppad");
   MCC_CHECK(p.cout_pad % 16 == 0 && p.ncols_pad % 16 == 0 && p.ncols_pad > p.kbias, "conv_dw: bad padding");
+  MCC_CHECK((int64_t)p.imgs * p.LH * p.LW * p.CL < (1 << 24) && (int64_t)p.cout_pad * p.ppad < (1 << 24),
+            "conv_dw: tile too large for index math");
   const size_t lds = conv_dw_lds_bytes(t, p);
   MCC_CHECK(lds <= 160 * 1024, "conv_dw: LDS tile exceeds 160 KiB");
   if (t == DType::BF16) {
@@ -434,7 +689,7 @@ void conv_dw(DType t, const ConvDwParams& p, hipStream_t s) {
 
 void conv_dw_reduce(const ConvDwReduceParams& p, hipStream_t s) {
   const int n = p.Cout * p.Cin * p.KS * p.KS + p.Cout;
-  hipLaunchKernelGGL(conv_dw_reduce_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, s, p);
+  hipLaunchKernelGGL(conv_dw_reduce_kernel, dim3((unsigned)cdiv(n, 32)), dim3(256), 0, s, p);
 }
 
 }  // namespace gpu

@@ -1,0 +1,11 @@
+#!/bin/bash
+# tests + one bench + kernel stats profile
+set -o pipefail
+cd "$(dirname "$0")/.."
+mkdir -p gpurun_out
+timeout -k 10 400 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1; rc=$?
+tail -4 gpurun_out/pytest_gpu.log; echo "pytest rc=$rc"
+[ $rc -eq 0 ] || [ $rc -eq 1 ] || exit 1
+timeout -k 10 200 python bench.py ${BENCH_ARGS:-} > gpurun_out/bench.log 2>&1 || { tail gpurun_out/bench.log; exit 1; }
+grep metric gpurun_out/bench.log
+cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/prof -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py --steps 20 --warmup 3 ${BENCH_ARGS:-} > $GRAFT_REPO_ROOT/gpurun_out/prof.log 2>&1; echo "prof rc=$?"
