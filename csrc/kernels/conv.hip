@@ -337,24 +337,43 @@ __device__ __forceinline__ void pixel_table(int* tab, int rows, bool pool, int O
   }
 }
 
-template <typename T, bool CVEC, int MT>
+enum FwdEpi : int { FE_POOL = 0, FE_ACT = 1, FE_PLAIN = 2 };
+
+// WL: packed weights staged in LDS (rows padded by 8 elements so the 16 lanes
+// of a B-fragment read hit distinct banks); else read from global (L2).
+template <typename T, bool CVEC, int MT, int EPI, int ACT, bool WL>
 __global__ void __launch_bounds__(256) conv_fwd_kernel(ConvParams p) {
   typedef typename Vec8<T>::type V8;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   T* xs = reinterpret_cast<T*>(smem);
   const int img_elems = p.LH * p.LW * p.CL;
   const int xs_elems = round8(p.imgs * img_elems + 16);
-  const bool pool = p.pool == 2;
+  constexpr bool pool = EPI == FE_POOL;
   const int PH = p.OH >> 1, PW = p.OW >> 1;
   const int rows_per_img = pool ? PH * PW * 4 : p.OH * p.OW;
   const int nk = CVEC ? p.nchunks * 4 : p.nchunks * 32;
-  int* ktab = reinterpret_cast<int*>(smem + align16(xs_elems * (int)sizeof(T)));
+  const int ntiles = cdiv(p.Cout, 16);
+  const int wrow_ld = p.kpad + 8;
+  T* ws = reinterpret_cast<T*>(smem + align16(xs_elems * (int)sizeof(T)));
+  float* bias_s = reinterpret_cast<float*>(reinterpret_cast<char*>(ws) +
+                                           (WL ? align16(ntiles * 16 * wrow_ld * (int)sizeof(T)) : 0));
+  int* ktab = reinterpret_cast<int*>(bias_s + ntiles * 16);
   int* ptab = ktab + ((nk + 3) & ~3);
   const int img0 = blockIdx.x * p.imgs;
   const int nimg = min(p.imgs, p.N - img0);
   const int tid = threadIdx.x;
+  const T* wpk = static_cast<const T*>(p.wpk);
 
   lds_zero(xs, xs_elems);
+  if (WL) {
+    const int nv = ntiles * 16 * (p.kpad >> 3);
+    const int vpr = p.kpad >> 3;
+    for (int v = tid; v < nv; v += blockDim.x) {
+      const int r = v / vpr, c = (v - r * vpr) * 8;
+      store8(ws + r * wrow_ld + c, load8(wpk + (size_t)r * p.kpad + c));
+    }
+  }
+  for (int n = tid; n < ntiles * 16; n += blockDim.x) bias_s[n] = (EPI != FE_PLAIN && n < p.Cout) ? p.bias[n] : 0.f;
   // k -> LDS offset table (relative to a pixel's top-left tap).  Padding
   // entries point at tap 0: their weights are zero, any finite value works.
   const int KK = p.KS * p.KS;
@@ -382,10 +401,10 @@ __global__ void __launch_bounds__(256) conv_fwd_kernel(ConvParams p) {
   const int lane = tid & 63, wave = tid >> 6, nwaves = blockDim.x >> 6;
   const int r16 = lane & 15, g = lane >> 4;
   const int M = nimg * rows_per_img;
-  const int mtiles = cdiv(M, 16), ntiles = cdiv(p.Cout, 16), mgroups = cdiv(mtiles, MT);
+  const int mtiles = cdiv(M, 16), mgroups = cdiv(mtiles, MT);
   const Div drpi(rows_per_img);
-  const T* wpk = static_cast<const T*>(p.wpk);
   T* out = static_cast<T*>(p.out);
+  const size_t obase = pool ? (size_t)img0 * PH * PW : (size_t)img0 * p.OH * p.OW;
 
   for (int item = wave; item < ntiles * mgroups; item += nwaves) {
     const int nt = item / mgroups, mg = item - nt * mgroups;
@@ -400,7 +419,7 @@ __global__ void __launch_bounds__(256) conv_fwd_kernel(ConvParams p) {
     f32x4 acc[MT];
 #pragma unroll
     for (int t = 0; t < MT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-    const T* wrow = wpk + (size_t)(nt * 16 + r16) * p.kpad + 8 * g;
+    const T* wrow = WL ? ws + (nt * 16 + r16) * wrow_ld + 8 * g : wpk + (size_t)(nt * 16 + r16) * p.kpad + 8 * g;
     for (int q = 0; q < p.nchunks; ++q) {
       const V8 b = load8(wrow + q * 32);
       if (CVEC) {
@@ -423,28 +442,38 @@ __global__ void __launch_bounds__(256) conv_fwd_kernel(ConvParams p) {
     // Epilogue: rows 4g..4g+3 of each tile belong to this lane, column n.
     const int n = nt * 16 + r16;
     if (n >= p.Cout) continue;
-    const float bv = p.bias_act ? p.bias[n] : 0.f;
+    const float bv = bias_s[n];
 #pragma unroll
     for (int t = 0; t < MT; ++t) {
       const int rb = (mg * MT + t) * 16 + 4 * g;
       if (rb >= M) continue;
       float v[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) v[i] = p.bias_act ? act_apply(p.act, acc[t][i] + bv) : acc[t][i];
+      for (int i = 0; i < 4; ++i) {
+        const float x = acc[t][i] + bv;
+        v[i] = ACT == ACT_RELU ? fmaxf(x, 0.f) : (ACT == ACT_TANH ? tanhf(x) : x);
+      }
       if (pool) {
         float best = v[0];
         int arg = 0;
 #pragma unroll
-        for (int i = 1; i < 4; ++i)
-          if (v[i] > best) { best = v[i]; arg = i; }
-        const size_t o = ((size_t)img0 * PH * PW + (rb >> 2)) * p.Cout + n;
+        for (int i = 1; i < 4; ++i) {
+          const bool gt = v[i] > best;
+          best = gt ? v[i] : best;
+          arg = gt ? i : arg;
+        }
+        const size_t o = (obase + (rb >> 2)) * p.Cout + n;
         out[o] = from_f<T>(best);
         p.out_arg[o] = (uint8_t)arg;
       } else {
-        const size_t obase = (size_t)img0 * p.OH * p.OW;
+        if (rb + 4 <= M) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
-          if (rb + i < M) out[(obase + rb + i) * p.Cout + n] = from_f<T>(v[i]);
+          for (int i = 0; i < 4; ++i) out[(obase + rb + i) * p.Cout + n] = from_f<T>(v[i]);
+        } else {
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            if (rb + i < M) out[(obase + rb + i) * p.Cout + n] = from_f<T>(v[i]);
+        }
       }
     }
   }
@@ -609,14 +638,35 @@ __global__ void __launch_bounds__(256) conv_dw_reduce_kernel(ConvDwReduceParams 
 
 inline size_t a16(size_t b) { return (b + 15) & ~size_t(15); }
 
+constexpr size_t kWeightLdsMax = 48 * 1024;
+
+size_t conv_fwd_weight_lds(size_t es, const ConvParams& p) {
+  return (size_t)cdiv(p.Cout, 16) * 16 * (p.kpad + 8) * es;
+}
+
+template <typename T, bool CVEC, int EPI, int ACT>
+void launch_fwd4(const ConvParams& p, hipStream_t s, size_t lds, bool wl) {
+  const dim3 grid((unsigned)cdiv(p.N, p.imgs)), block(256);
+  if (wl) hipLaunchKernelGGL((conv_fwd_kernel<T, CVEC, 4, EPI, ACT, true>), grid, block, lds, s, p);
+  else hipLaunchKernelGGL((conv_fwd_kernel<T, CVEC, 4, EPI, ACT, false>), grid, block, lds, s, p);
+}
+
+template <typename T, bool CVEC>
+void launch_fwd_c(const ConvParams& p, hipStream_t s, size_t lds, bool wl) {
+  if (!p.bias_act) launch_fwd4<T, CVEC, FE_PLAIN, ACT_NONE>(p, s, lds, wl);
+  else if (p.pool == 2) launch_fwd4<T, CVEC, FE_POOL, ACT_RELU>(p, s, lds, wl);
+  else if (p.act == ACT_RELU) launch_fwd4<T, CVEC, FE_ACT, ACT_RELU>(p, s, lds, wl);
+  else if (p.act == ACT_TANH) launch_fwd4<T, CVEC, FE_ACT, ACT_TANH>(p, s, lds, wl);
+  else launch_fwd4<T, CVEC, FE_ACT, ACT_NONE>(p, s, lds, wl);
+}
+
 template <typename T>
 void launch_conv_fwd(const ConvParams& p, hipStream_t s) {
-  const size_t lds = conv_forward_lds_bytes(sizeof(T) == 2 ? DType::BF16 : DType::F32, p);
-  const dim3 grid((unsigned)cdiv(p.N, p.imgs)), block(256);
-  if (p.cvec)
-    hipLaunchKernelGGL((conv_fwd_kernel<T, true, 4>), grid, block, lds, s, p);
-  else
-    hipLaunchKernelGGL((conv_fwd_kernel<T, false, 4>), grid, block, lds, s, p);
+  const DType dt = sizeof(T) == 2 ? DType::BF16 : DType::F32;
+  const size_t lds = conv_forward_lds_bytes(dt, p);
+  const bool wl = conv_fwd_weight_lds(sizeof(T), p) <= kWeightLdsMax;
+  if (p.cvec) launch_fwd_c<T, true>(p, s, lds, wl);
+  else launch_fwd_c<T, false>(p, s, lds, wl);
 }
 
 int dw_ntw(int mtw) { return mtw <= 1 ? 16 : (mtw <= 2 ? 8 : (mtw <= 4 ? 4 : 2)); }
@@ -647,7 +697,9 @@ size_t conv_forward_lds_bytes(DType t, const ConvParams& p) {
   const size_t es = t == DType::BF16 ? 2 : 4;
   const size_t nk = p.cvec ? (size_t)p.nchunks * 4 : (size_t)p.nchunks * 32;
   const size_t rows = p.pool == 2 ? (size_t)(p.OH / 2) * (p.OW / 2) * 4 : (size_t)p.OH * p.OW;
-  return a16((size_t)round8(p.imgs * p.LH * p.LW * p.CL + 16) * es) + ((nk + 3) & ~size_t(3)) * 4 + rows * 4;
+  const size_t wl = conv_fwd_weight_lds(es, p);
+  return a16((size_t)round8(p.imgs * p.LH * p.LW * p.CL + 16) * es) + (wl <= kWeightLdsMax ? a16(wl) : 0) +
+         (size_t)cdiv(p.Cout, 16) * 16 * 4 + ((nk + 3) & ~size_t(3)) * 4 + rows * 4;
 }
 
 size_t conv_dw_lds_bytes(DType t, const ConvDwParams& p) {

@@ -1,0 +1,97 @@
+"""Native `cnn` program: the reference CLI contract (4 positional IDX paths,
+exit 100 / 111, stderr log lines) and exact log parity with the reference
+`cnn.c` in --ref-compat mode.
+
+The parity oracle is the reference's own C source compiled here with gcc
+into a temp dir (not a prebuilt binary); the test is skipped where the
+reference checkout is absent (e.g. on the GPU box).
+"""
+
+import os
+import re
+import shutil
+import subprocess
+
+import numpy as np
+import pytest
+
+import mpi_cuda_cnn_amd as mcc
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CNN = os.path.join(ROOT, "build", "bin", "cnn")
+REF_SRC = "/root/reference/cnn.c"
+
+
+@pytest.fixture(scope="module")
+def cnn_bin():
+    if not os.path.exists(CNN):
+        subprocess.run(["make", "-C", ROOT, "-j8", "build/bin/cnn"], check=True, capture_output=True)
+    return CNN
+
+
+def _write_set(d, n, seed, prefix):
+    imgs, labels = mcc.synth_dataset(n, 1, 28, 28, 10, seed=seed)
+    pi, pl = os.path.join(d, prefix + "-images"), os.path.join(d, prefix + "-labels")
+    mcc.idx_write(pi, imgs.reshape(n, 28, 28))
+    mcc.idx_write(pl, labels)
+    return pi, pl
+
+
+@pytest.fixture(scope="module")
+def data(tmp_path_factory):
+    d = str(tmp_path_factory.mktemp("idx"))
+    tr = _write_set(d, 300, 1, "train")
+    te = _write_set(d, 100, 2, "test")
+    return tr + te
+
+
+def test_exit_codes(cnn_bin, data, tmp_path):
+    assert subprocess.run([cnn_bin], capture_output=True).returncode == 100
+    # the reference checks argc < 4 but uses argv[4] (defect D8): 3 paths -> 100 here
+    assert subprocess.run([cnn_bin] + list(data[:3]), capture_output=True).returncode == 100
+    missing = str(tmp_path / "missing")
+    assert subprocess.run([cnn_bin, missing] + list(data[1:]), capture_output=True).returncode == 111
+    bad = tmp_path / "bad"
+    bad.write_bytes(b"\x01\x02\x03\x04")
+    assert subprocess.run([cnn_bin, str(bad)] + list(data[1:]), capture_output=True).returncode == 111
+
+
+def test_serial_training_log_and_accuracy(cnn_bin, data):
+    r = subprocess.run([cnn_bin] + list(data) + ["--epochs", "3", "--json", "-"], capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stderr
+    lines = r.stderr.strip().splitlines()
+    assert lines[0] == "training..."
+    assert re.fullmatch(r"i=0, error=\d+\.\d{4}", lines[1])
+    assert "testing..." in lines
+    assert lines[-1].startswith("ntests=100, ncorrect=")
+    ncorrect = int(lines[-1].split("=")[-1])
+    assert ncorrect >= 95, r.stderr
+    assert '"program": "cnn"' in r.stdout
+
+
+def test_weight_save_load(cnn_bin, data, tmp_path):
+    w = str(tmp_path / "w.mcnnw")
+    r = subprocess.run([cnn_bin] + list(data) + ["--epochs", "1", "--save", w], capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0 and os.path.exists(w)
+    spec, p = mcc.load_weights(w)
+    assert spec.nparams == mcc.make_model("ref").nparams
+    r2 = subprocess.run([cnn_bin] + list(data) + ["--epochs", "0", "--load", w], capture_output=True, text=True,
+                        timeout=300)
+    assert r2.returncode == 0
+    assert r2.stderr.strip().splitlines()[-1] == r.stderr.strip().splitlines()[-1]
+
+
+@pytest.mark.skipif(not os.path.exists(REF_SRC) or shutil.which("gcc") is None, reason="reference source absent")
+def test_ref_compat_log_matches_reference_program(cnn_bin, data, tmp_path):
+    """Byte-identical stderr vs the reference program built from its source:
+    same glibc init order, same rand() % N sampling, same per-sample backprop
+    with the update at i % 32 == 0, same D1 conv indexing, same log lines."""
+    ref_bin = str(tmp_path / "cnn_ref")
+    subprocess.run(["gcc", "-O2", "-o", ref_bin, REF_SRC, "-lm"], check=True, capture_output=True)
+    ref = subprocess.run([ref_bin] + list(data), capture_output=True, text=True, timeout=600)
+    assert ref.returncode == 0
+    ours = subprocess.run([cnn_bin] + list(data) + ["--ref-compat"], capture_output=True, text=True, timeout=600)
+    assert ours.returncode == 0
+    assert ours.stderr == ref.stderr

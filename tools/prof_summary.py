@@ -8,7 +8,11 @@ from collections import defaultdict
 
 
 def short(name):
-    name = re.sub(r"\(.*", "", name)
+    name = name.replace("(anonymous namespace)::", "").replace("mcc::gpu::", "")
+    name = re.sub(r"^void ", "", name)
+    i = name.rfind("(")
+    if i > 0 and name.endswith(")"):
+        name = name[:i]
     return name[:110]
 
 
