@@ -32,9 +32,9 @@ ENG_OBJ   := $(patsubst csrc/engine/%.cpp,$(OBJ)/engine/%.o,$(ENG_SRC))
 HDRS      := $(wildcard csrc/include/mcc/*.h csrc/kernels/*.h)
 
 MODULE    := mpi_cuda_cnn_amd/_C$(EXT)
-BINS      := build/bin/cnn
+BINS      := build/bin/cnn build/bin/cnn_hip build/bin/cnn_dist
 ifneq ($(MPICXX),)
-BINS      += 
+BINS      += build/bin/cnnmpi
 endif
 
 .PHONY: all module bins clean
@@ -65,9 +65,13 @@ build/bin/cnn: csrc/apps/cnn.cpp $(CORE_OBJ) $(HDRS)
 	@mkdir -p $(dir $@)
 	$(CXX) $(CXXFLAGS) -o $@ csrc/apps/cnn.cpp $(CORE_OBJ) -lm
 
+# MPICH's wrapper would put its own (older) libstdc++ first; link with the
+# system compiler against the MPI library instead, libstdc++ static.
+MPI_PREFIX := $(patsubst %/bin/mpicxx,%,$(MPICXX))
 build/bin/cnnmpi: csrc/apps/cnnmpi.cpp $(CORE_OBJ) $(HDRS)
 	@mkdir -p $(dir $@)
-	MPICH_CXX=$(CXX) $(MPICXX) $(CXXFLAGS) -o $@ csrc/apps/cnnmpi.cpp $(CORE_OBJ) -lm
+	$(CXX) $(CXXFLAGS) -I$(MPI_PREFIX)/include -o $@ csrc/apps/cnnmpi.cpp $(CORE_OBJ) \
+	  $(MPI_PREFIX)/lib/libmpi.so -Wl,-rpath,$(MPI_PREFIX)/lib -static-libstdc++ -static-libgcc -lm
 
 $(OBJ)/apps/%.o: csrc/apps/%.cpp $(HDRS)
 	@mkdir -p $(dir $@)

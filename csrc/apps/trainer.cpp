@@ -1,0 +1,304 @@
+// Native GPU training driver (see trainer.h).
+//
+// One step = device-side sampling from the rank's shard -> fused forward ->
+// softmax-CE -> backward bucket by bucket, each bucket's RCCL all-reduce
+// issued on a comm stream as soon as its gradients are final (event
+// fork/join, overlapped with the remaining backward) -> SGD + repack.  The
+// whole step is captured once into a hipGraph and replayed (the sampler reads
+// its step counter from device memory, so replays draw fresh indices).
+#include "trainer.h"
+
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <memory>
+#include <vector>
+
+#include "kernels.h"
+#include "mcc/cpu_net.h"
+#include "mcc/engine.h"
+#include "mcc/io.h"
+
+namespace mcc {
+
+#define HIPCHK(expr)                                                                        \
+  do {                                                                                      \
+    hipError_t _e = (expr);                                                                 \
+    if (_e != hipSuccess) throw Error(std::string("HIP: ") + hipGetErrorString(_e) + " @ " + #expr); \
+  } while (0)
+
+namespace {
+
+struct DevBuf {
+  void* p = nullptr;
+  explicit DevBuf(size_t bytes) { HIPCHK(hipMalloc(&p, bytes ? bytes : 1)); }
+  ~DevBuf() { if (p) (void)hipFree(p); }
+  template <typename T> T* as() const { return static_cast<T*>(p); }
+};
+
+struct PhaseTimer {
+  bool on;
+  hipEvent_t ev[5];
+  double ms[4] = {0, 0, 0, 0};
+  int n = 0;
+  explicit PhaseTimer(bool enabled) : on(enabled) {
+    if (on) for (auto& e : ev) HIPCHK(hipEventCreate(&e));
+  }
+  ~PhaseTimer() {
+    if (on) for (auto& e : ev) (void)hipEventDestroy(e);
+  }
+  void mark(int i, hipStream_t s) { if (on) HIPCHK(hipEventRecord(ev[i], s)); }
+  void collect() {
+    if (!on) return;
+    HIPCHK(hipEventSynchronize(ev[4]));
+    for (int i = 0; i < 4; ++i) {
+      float t = 0;
+      HIPCHK(hipEventElapsedTime(&t, ev[i], ev[i + 1]));
+      ms[i] += t;
+    }
+    ++n;
+  }
+};
+
+}  // namespace
+
+int run_gpu_training(const CliArgs& a, Comm& comm, const char* program) {
+  const int rank = comm.rank(), world = comm.size();
+  int ndev = 0;
+  HIPCHK(hipGetDeviceCount(&ndev));
+  if (ndev < 1) { std::fprintf(stderr, "%s: no GPU\n", program); return 111; }
+  HIPCHK(hipSetDevice(comm.local_rank() % ndev));
+  const DType dt = a.dtype == "fp32" ? DType::F32 : DType::BF16;
+
+  // ---- model + initial weights (identical on every rank, then broadcast) ----
+  ModelSpec spec;
+  std::vector<double> p64;
+  try {
+    if (!a.load.empty()) spec = load_weights(a.load, p64);
+    else {
+      spec = make_model(a.model);
+      p64.resize(spec.nparams);
+      init_params(spec, p64.data(), a.seed, InitMode::GlibcRef);
+    }
+  } catch (const Error& e) {
+    std::fprintf(stderr, "%s\n", e.what());
+    return 111;
+  }
+
+  // ---- data (IDX, device resident) ----
+  IdxFile tr_img, tr_lab, te_img, te_lab;
+  try {
+    tr_img = idx_read(a.train_images);
+    tr_lab = idx_read(a.train_labels);
+  } catch (const Error& e) {
+    std::fprintf(stderr, "%s\n", e.what());
+    return 111;
+  }
+  const int64_t in_nodes = spec.input_nodes();
+  if (tr_img.item_size() != in_nodes || tr_lab.count() < tr_img.count()) {
+    std::fprintf(stderr, "train set shape does not match the model input\n");
+    return 111;
+  }
+  int64_t N = tr_img.count();
+  if (a.max_train > 0 && a.max_train < N) N = a.max_train;
+  // contiguous per-rank shard (cnnmpi.c:457-458)
+  const int64_t shard_lo = N / world * rank, shard_hi = N / world * (rank + 1);
+  if (world > 1) std::fprintf(stderr, "%d %lld %lld\n", rank, (long long)shard_lo, (long long)shard_hi);
+
+  const int B_global = a.batch;
+  const int b = std::max(1, B_global / world);
+  const int eval_b = std::max(b, 1024);
+  GpuNet net(spec, dt, eval_b);
+  {
+    std::vector<float> p32(p64.begin(), p64.end());
+    net.set_params(p32.data());
+  }
+  DevBuf d_img((size_t)N * in_nodes), d_lab((size_t)N);
+  HIPCHK(hipMemcpy(d_img.p, tr_img.data.data(), (size_t)N * in_nodes, hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(d_lab.p, tr_lab.data.data(), (size_t)N, hipMemcpyHostToDevice));
+  DevBuf d_idx(4 * (size_t)eval_b), d_step(8);
+  HIPCHK(hipMemset(d_step.p, 0, 8));
+
+  hipStream_t S, C;
+  HIPCHK(hipStreamCreateWithFlags(&S, hipStreamNonBlocking));
+  HIPCHK(hipStreamCreateWithFlags(&C, hipStreamNonBlocking));
+  // identical weights on every rank (fixes D6: srand(rank), no broadcast)
+  comm.broadcast_f32(net.params(), net.nparams(), 0, S);
+  net.pack(S);
+  HIPCHK(hipStreamSynchronize(S));
+
+  const auto buckets = net.buckets(a.bucket_mb << 20);
+  std::vector<hipEvent_t> ev_b(buckets.size());
+  hipEvent_t ev_join;
+  for (auto& e : ev_b) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  HIPCHK(hipEventCreateWithFlags(&ev_join, hipEventDisableTiming));
+  const float grad_scale = 1.0f / (float)(b * world);
+  PhaseTimer timer(a.profile);
+
+  auto step = [&](bool timed) {
+    gpu::sample_indices(d_idx.as<int32_t>(), b, shard_lo, shard_hi, a.seed * 7919ull + rank, d_step.as<uint64_t>(), S);
+    if (timed) timer.mark(0, S);
+    net.forward(d_img.as<uint8_t>(), d_idx.as<int32_t>(), b, S);
+    net.loss(d_lab.as<uint8_t>(), d_idx.as<int32_t>(), grad_scale, true, S);
+    if (timed) timer.mark(1, S);
+    for (size_t k = 0; k < buckets.size(); ++k) {
+      net.backward(buckets[k].stage_hi, buckets[k].stage_lo, S);
+      if (world > 1) {
+        HIPCHK(hipEventRecord(ev_b[k], S));
+        HIPCHK(hipStreamWaitEvent(C, ev_b[k], 0));
+        comm.allreduce_sum_f32(net.grads() + buckets[k].off, buckets[k].count, C);
+      }
+    }
+    if (timed) timer.mark(2, S);
+    if (world > 1) {
+      HIPCHK(hipEventRecord(ev_join, C));
+      HIPCHK(hipStreamWaitEvent(S, ev_join, 0));
+    }
+    if (timed) timer.mark(3, S);
+    net.sgd((float)a.lr, (float)a.momentum, (float)a.weight_decay, S);
+    gpu::advance_counter(d_step.as<uint64_t>(), S);
+    if (timed) timer.mark(4, S);
+  };
+
+  const int64_t total = (int64_t)a.epochs * N;
+  const int64_t steps = (total + B_global - 1) / B_global;
+  if (rank == 0) std::fprintf(stderr, "training...\n");
+  net.zero_stats(S);
+
+  // Capture one step into a hipGraph (skipped with --profile: timers need
+  // host-visible event records between phases).
+  hipGraphExec_t gexec = nullptr;
+  hipGraph_t graph = nullptr;
+  bool use_graph = !a.profile && steps > 2;
+  if (use_graph) {
+    HIPCHK(hipStreamSynchronize(S));
+    if (hipStreamBeginCapture(S, hipStreamCaptureModeRelaxed) == hipSuccess) {
+      bool ok = true;
+      try { step(false); } catch (const Error&) { ok = false; }
+      hipError_t e = hipStreamEndCapture(S, &graph);
+      if (!ok || e != hipSuccess || hipGraphInstantiate(&gexec, graph, nullptr, nullptr, 0) != hipSuccess) {
+        use_graph = false;
+        (void)hipGetLastError();
+        if (rank == 0) std::fprintf(stderr, "note: hipGraph capture unavailable, running eagerly\n");
+      }
+    } else {
+      use_graph = false;
+      (void)hipGetLastError();
+    }
+  }
+
+  HIPCHK(hipDeviceSynchronize());
+  const auto t0 = std::chrono::steady_clock::now();
+  int64_t seen = 0, last_log = 0;
+  for (int64_t it = 0; it < steps; ++it) {
+    if (use_graph) HIPCHK(hipGraphLaunch(gexec, S));
+    else step(a.profile);
+    if (a.profile) timer.collect();
+    const int64_t prev = seen;
+    seen += B_global;
+    // log at i = 0 and every log_every samples (cnn.c:470-473)
+    const int64_t mark = (prev + a.log_every - 1) / a.log_every * a.log_every;
+    if (!a.quiet && (mark < seen || it == steps - 1)) {
+      float st[4];
+      HIPCHK(hipMemcpyAsync(st, net.stats(), 16, hipMemcpyDeviceToHost, S));
+      HIPCHK(hipStreamSynchronize(S));
+      double loc[2] = {st[1], (double)(seen - last_log) / world};
+      if (world > 1) {
+        DevBuf tmp(16);
+        float v[2] = {st[1], (float)loc[1]};
+        HIPCHK(hipMemcpy(tmp.p, v, 8, hipMemcpyHostToDevice));
+        comm.allreduce_sum_f32(tmp.as<float>(), 2, S);
+        HIPCHK(hipMemcpy(v, tmp.p, 8, hipMemcpyDeviceToHost));
+        loc[0] = v[0]; loc[1] = v[1];
+      }
+      if (rank == 0 && mark < seen)
+        std::fprintf(stderr, "i=%lld, error=%.4f\n", (long long)mark, loc[0] / std::max(1.0, loc[1]));
+      net.zero_stats(S);
+      last_log = seen;
+    }
+  }
+  HIPCHK(hipDeviceSynchronize());
+  double train_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  if (world > 1) {
+    DevBuf tmp(8);
+    HIPCHK(hipMemcpy(tmp.p, &train_s, 8, hipMemcpyHostToDevice));
+    comm.allreduce_max_f64(tmp.as<double>(), 1, S);
+    HIPCHK(hipStreamSynchronize(S));
+    HIPCHK(hipMemcpy(&train_s, tmp.p, 8, hipMemcpyDeviceToHost));
+  }
+  if (gexec) (void)hipGraphExecDestroy(gexec);
+  if (graph) (void)hipGraphDestroy(graph);
+
+  // ---- test (rank 0; every rank holds identical weights) ----
+  int rc = 0;
+  int64_t ntests = 0, ncorrect = 0;
+  double test_s = 0;
+  if (rank == 0) {
+    try {
+      te_img = idx_read(a.test_images);
+      te_lab = idx_read(a.test_labels);
+    } catch (const Error& e) {
+      std::fprintf(stderr, "%s\n", e.what());
+      rc = 111;
+    }
+    if (rc == 0 && (te_img.item_size() != in_nodes || te_lab.count() < te_img.count())) rc = 111;
+    if (rc == 0) {
+      std::fprintf(stderr, "testing...\n");
+      ntests = te_img.count();
+      DevBuf t_img((size_t)ntests * in_nodes), t_lab((size_t)ntests);
+      HIPCHK(hipMemcpy(t_img.p, te_img.data.data(), (size_t)ntests * in_nodes, hipMemcpyHostToDevice));
+      HIPCHK(hipMemcpy(t_lab.p, te_lab.data.data(), (size_t)ntests, hipMemcpyHostToDevice));
+      net.zero_stats(S);
+      const auto t1 = std::chrono::steady_clock::now();
+      for (int64_t i = 0; i < ntests; i += eval_b) {
+        const int nb = (int)std::min<int64_t>(eval_b, ntests - i);
+        gpu::iota_i32(d_idx.as<int32_t>(), nb, i, S);
+        net.forward(t_img.as<uint8_t>(), d_idx.as<int32_t>(), nb, S);
+        net.loss(t_lab.as<uint8_t>(), d_idx.as<int32_t>(), 1.f, false, S);
+        for (int64_t j = i; j < i + nb; ++j)
+          if (j % 1000 == 0) std::fprintf(stderr, "i=%lld\n", (long long)j);
+      }
+      float st[4];
+      HIPCHK(hipMemcpyAsync(st, net.stats(), 16, hipMemcpyDeviceToHost, S));
+      HIPCHK(hipStreamSynchronize(S));
+      test_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t1).count();
+      ncorrect = (int64_t)std::llround(st[2]);
+      std::fprintf(stderr, "ntests=%lld, ncorrect=%lld\n", (long long)ntests, (long long)ncorrect);
+      if (!a.save.empty()) {
+        std::vector<float> p32(net.nparams());
+        net.get_params(p32.data());
+        std::vector<double> pd(p32.begin(), p32.end());
+        try { save_weights(a.save, spec, pd.data()); } catch (const Error& e) { std::fprintf(stderr, "%s\n", e.what()); rc = 111; }
+      }
+    }
+  }
+  if (rank == 0 && !a.log_json.empty()) {
+    FILE* f = a.log_json == "-" ? stdout : std::fopen(a.log_json.c_str(), "w");
+    if (f) {
+      const double img_s = (double)steps * B_global / std::max(train_s, 1e-9);
+      std::fprintf(f,
+                   "{\"program\": \"%s\", \"model\": \"%s\", \"dtype\": \"%s\", \"world\": %d, \"global_batch\": %d, "
+                   "\"steps\": %lld, \"train_s\": %.6f, \"train_img_per_s\": %.1f, \"hipgraph\": %s, "
+                   "\"test_img_per_s\": %.1f, \"ntests\": %lld, \"ncorrect\": %lld",
+                   program, spec.name.c_str(), dtype_name(dt), world, B_global, (long long)steps, train_s, img_s,
+                   use_graph ? "true" : "false", ntests / std::max(test_s, 1e-9), (long long)ntests,
+                   (long long)ncorrect);
+      if (timer.on && timer.n > 0)
+        std::fprintf(f, ", \"phase_ms\": {\"forward_loss\": %.4f, \"backward_allreduce_issue\": %.4f, "
+                        "\"allreduce_wait\": %.4f, \"sgd\": %.4f}",
+                     timer.ms[0] / timer.n, timer.ms[1] / timer.n, timer.ms[2] / timer.n, timer.ms[3] / timer.n);
+      std::fprintf(f, "}\n");
+      if (f != stdout) std::fclose(f);
+    }
+  }
+  comm.barrier();
+  for (auto& e : ev_b) (void)hipEventDestroy(e);
+  (void)hipEventDestroy(ev_join);
+  (void)hipStreamDestroy(S);
+  (void)hipStreamDestroy(C);
+  return rc;
+}
+
+}  // namespace mcc

@@ -160,6 +160,15 @@ void sgd_update(float* params, const float* grads, float* mom, int64_t n, float 
 // dst[i] = idx[i] >= 0 ? T(src[idx[i]]) : 0
 void pack_gather(DType t, void* dst, const float* src, const int32_t* idx, int64_t n, hipStream_t s);
 void fill_f32(float* dst, float v, int64_t n, hipStream_t s);
+// Sampling with replacement (the reference draws rand() % N per sample,
+// cnn.c:455): idx[b] = lo + hash(seed, *step, b) % (hi - lo).  `step` lives in
+// device memory so a captured hipGraph replays with fresh indices; call
+// advance_counter once per step (after the last consumer of idx).
+void sample_indices(int32_t* idx, int B, int64_t lo, int64_t hi, uint64_t seed, const uint64_t* step,
+                    hipStream_t s);
+void advance_counter(uint64_t* step, hipStream_t s);
+// idx[b] = start + b (sequential evaluation windows)
+void iota_i32(int32_t* idx, int B, int64_t start, hipStream_t s);
 void cast_f32(DType t, void* dst, const float* src, int64_t n, hipStream_t s);
 void to_f32(DType t, float* dst, const void* src, int64_t n, hipStream_t s);
 

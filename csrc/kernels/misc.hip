@@ -108,6 +108,27 @@ __global__ void to_f32_kernel(float* dst, const T* src, int64_t n) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) dst[i] = to_f(src[i]);
 }
 
+__device__ __forceinline__ uint64_t mix64(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+
+__global__ void sample_kernel(int32_t* idx, int B, int64_t lo, int64_t span, uint64_t seed, const uint64_t* step) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  const uint64_t h = mix64(mix64(seed ^ (*step * 0xD1B54A32D192ED03ull)) + (uint64_t)b);
+  idx[b] = (int32_t)(lo + (int64_t)(h % (uint64_t)span));
+}
+
+__global__ void advance_kernel(uint64_t* step) { *step += 1; }
+
+__global__ void iota_kernel(int32_t* idx, int B, int64_t start) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b < B) idx[b] = (int32_t)(start + b);
+}
+
 inline unsigned grid_for(int64_t n, int per_thread = 1) {
   int64_t b = (n / per_thread + 255) / 256;
   if (b < 1) b = 1;
@@ -138,6 +159,20 @@ void pack_gather(DType t, void* dst, const float* src, const int32_t* idx, int64
   else
     hipLaunchKernelGGL(pack_kernel<float>, dim3(grid_for(n)), dim3(256), 0, s, static_cast<float*>(dst), src, idx,
                        n);
+}
+
+void sample_indices(int32_t* idx, int B, int64_t lo, int64_t hi, uint64_t seed, const uint64_t* step,
+                    hipStream_t s) {
+  MCC_CHECK(B > 0 && hi > lo, "sample_indices: empty range");
+  hipLaunchKernelGGL(sample_kernel, dim3((unsigned)cdiv(B, 256)), dim3(256), 0, s, idx, B, lo, hi - lo, seed, step);
+}
+
+void advance_counter(uint64_t* step, hipStream_t s) {
+  hipLaunchKernelGGL(advance_kernel, dim3(1), dim3(1), 0, s, step);
+}
+
+void iota_i32(int32_t* idx, int B, int64_t start, hipStream_t s) {
+  hipLaunchKernelGGL(iota_kernel, dim3((unsigned)cdiv(B, 256)), dim3(256), 0, s, idx, B, start);
 }
 
 void fill_f32(float* dst, float v, int64_t n, hipStream_t s) {

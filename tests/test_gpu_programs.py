@@ -1,0 +1,80 @@
+"""End-to-end GPU programs on the MI355X: the native `cnn_hip` / `cnn_dist`
+drivers (hipGraph-captured step) and the Python trainer, on synthetic
+MNIST-shaped IDX data with the reference CLI."""
+
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+import mpi_cuda_cnn_amd as mcc
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def idx_files(tmp_path_factory):
+    d = str(tmp_path_factory.mktemp("gpuidx"))
+    for n, s, p in ((4000, 1, "train"), (1000, 2, "test")):
+        i, l = mcc.synth_dataset(n, 1, 28, 28, 10, seed=s)
+        mcc.idx_write(os.path.join(d, p + "-images"), i.reshape(n, 28, 28))
+        mcc.idx_write(os.path.join(d, p + "-labels"), l)
+    return [os.path.join(d, x) for x in ("train-images", "train-labels", "test-images", "test-labels")]
+
+
+def _run(cmd, **kw):
+    return subprocess.run(cmd, capture_output=True, text=True, timeout=300, **kw)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("model,dtype,batch", [("lenet5", "bf16", 256), ("ref", "fp32", 32)])
+def test_cnn_hip_trains(idx_files, model, dtype, batch, tmp_path):
+    w = str(tmp_path / "w.mcnnw")
+    r = _run([os.path.join(ROOT, "build/bin/cnn_hip")] + idx_files +
+             ["--model", model, "--dtype", dtype, "--batch", str(batch), "--epochs", "2", "--lr", "0.05",
+              "--momentum", "0.5", "--json", "-", "--save", w])
+    assert r.returncode == 0, r.stderr
+    lines = r.stderr.strip().splitlines()
+    assert lines[0] == "training..." and lines[1].startswith("i=0, error=")
+    assert lines[-1].startswith("ntests=1000, ncorrect=")
+    assert int(lines[-1].split("=")[-1]) >= 950, r.stderr
+    js = json.loads(r.stdout.strip().splitlines()[-1])
+    assert js["hipgraph"] is True and js["train_img_per_s"] > 0
+    spec, p = mcc.load_weights(w)
+    assert spec.nparams == mcc.make_model(model).nparams
+
+
+@pytest.mark.gpu
+def test_cnn_hip_profile_phases(idx_files):
+    r = _run([os.path.join(ROOT, "build/bin/cnn_hip")] + idx_files +
+             ["--model", "lenet5", "--batch", "512", "--epochs", "1", "--profile", "--json", "-"])
+    assert r.returncode == 0, r.stderr
+    js = json.loads(r.stdout.strip().splitlines()[-1])
+    assert set(js["phase_ms"]) == {"forward_loss", "backward_allreduce_issue", "allreduce_wait", "sgd"}
+
+
+@pytest.mark.gpu
+def test_cnn_dist_single_rank(idx_files):
+    env = dict(os.environ, RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
+    r = _run([os.path.join(ROOT, "build/bin/cnn_dist")] + idx_files +
+             ["--model", "lenet5", "--batch", "256", "--epochs", "1", "--lr", "0.05"], env=env)
+    assert r.returncode == 0, r.stderr
+    assert int(r.stderr.strip().splitlines()[-1].split("=")[-1]) >= 900
+
+
+@pytest.mark.gpu
+def test_python_train_gpu(idx_files):
+    r = _run([sys.executable, "-m", "mpi_cuda_cnn_amd.train"] + idx_files +
+             ["--model", "lenet5", "--batch", "256", "--epochs", "2", "--lr", "0.05", "--momentum", "0.5",
+              "--device", "gpu"], cwd=ROOT)
+    assert r.returncode == 0, r.stderr
+    assert int(r.stderr.strip().splitlines()[-1].split("=")[-1]) >= 950, r.stderr
+
+
+@pytest.mark.gpu
+def test_exit_codes_gpu_programs(idx_files):
+    for prog in ("cnn_hip", "cnn_dist"):
+        assert _run([os.path.join(ROOT, "build/bin", prog)]).returncode == 100
+        assert _run([os.path.join(ROOT, "build/bin", prog), "/nonexistent"] + idx_files[1:]).returncode == 111
