@@ -172,6 +172,7 @@ int run_gpu_training(const CliArgs& a, Comm& comm, const char* program) {
   hipGraphExec_t gexec = nullptr;
   hipGraph_t graph = nullptr;
   bool use_graph = !a.profile && steps > 2;
+  if (a.momentum != 0.0) net.ensure_momentum();  // no allocation inside capture
   if (use_graph) {
     HIPCHK(hipStreamSynchronize(S));
     if (hipStreamBeginCapture(S, hipStreamCaptureModeRelaxed) == hipSuccess) {
@@ -181,6 +182,11 @@ int run_gpu_training(const CliArgs& a, Comm& comm, const char* program) {
       if (!ok || e != hipSuccess || hipGraphInstantiate(&gexec, graph, nullptr, nullptr, 0) != hipSuccess) {
         use_graph = false;
         (void)hipGetLastError();
+        // a failed capture can leave the stream unusable: start from fresh streams
+        (void)hipStreamDestroy(S);
+        (void)hipStreamDestroy(C);
+        HIPCHK(hipStreamCreateWithFlags(&S, hipStreamNonBlocking));
+        HIPCHK(hipStreamCreateWithFlags(&C, hipStreamNonBlocking));
         if (rank == 0) std::fprintf(stderr, "note: hipGraph capture unavailable, running eagerly\n");
       }
     } else {

@@ -435,11 +435,14 @@ void GpuNet::backward(int hi, int lo, hipStream_t s) {
   }
 }
 
+void GpuNet::ensure_momentum() {
+  if (mom_) return;
+  HIP_OK(hipMalloc(reinterpret_cast<void**>(&mom_), 4 * (size_t)spec_.nparams));
+  HIP_OK(hipMemset(mom_, 0, 4 * (size_t)spec_.nparams));
+}
+
 void GpuNet::sgd(float lr, float momentum, float weight_decay, hipStream_t s) {
-  if (momentum != 0.f && !mom_) {
-    HIP_OK(hipMalloc(reinterpret_cast<void**>(&mom_), 4 * (size_t)spec_.nparams));
-    HIP_OK(hipMemset(mom_, 0, 4 * (size_t)spec_.nparams));
-  }
+  if (momentum != 0.f) ensure_momentum();
   gpu::sgd_update(params_, grads_, momentum != 0.f ? mom_ : nullptr, spec_.nparams, lr, momentum, weight_decay, s);
   pack(s);
 }
