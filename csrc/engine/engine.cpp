@@ -46,11 +46,25 @@ struct GpuNet::Stage {
   int imgs_fwd = 1, imgs_dx = 1, imgs_dw = 1, ppad = 32, kbias = 0, ncols_pad = 16, cout_pad = 16;
   // fc geometry
   int Kin = 0, Nout = 0, permC = 0, permHW = 0, ldp = 0;
+  // large-image conv (explicit im2col + MFMA GEMM) when the image tile does
+  // not fit the whole-image LDS kernels
+  bool big = false;
+  int kgem = 0, kgem_d = 0;      // im2col row strides (fwd/dW, data grad)
+  void* conv_buf = nullptr;      // pre-pool conv output (big + pooled)
+  void* dz_buf = nullptr;        // pre-activation gradient at conv-output size (big)
 };
 
 static inline int r8(int x) { return (x + 7) & ~7; }
 static inline int r16(int x) { return (x + 15) & ~15; }
 static inline int r32(int x) { return (x + 31) & ~31; }
+// Split-K factor for a weight-gradient GEMM [M x N] reduced over K rows:
+// aim for ~512 workgroups of 64x64 tiles, each slice >= 128 rows.
+static inline int dw_splitk(int M, int N, int64_t K) {
+  const int64_t tiles = ceil_div(M, 64) * ceil_div(N, 64);
+  int64_t sk = std::max<int64_t>(1, std::min<int64_t>(512 / std::max<int64_t>(1, tiles), K / 128));
+  return (int)std::min<int64_t>(sk, 64);
+}
+
 static inline int act_kind(Act a) {
   switch (a) {
     case Act::ReLU: return gpu::ACT_RELU;
@@ -105,7 +119,6 @@ void GpuNet::build() {
         st->outH = pl.H; st->outW = pl.W;
         ++i;
       }
-      MCC_CHECK(st->OH * st->OW <= 4096, "conv_small path: conv output larger than 64x64 per image");
     } else if (l.kind == LayerKind::FC) {
       st->kind = Stage::FC;
       st->C = l.C;
@@ -148,7 +161,13 @@ void GpuNet::build() {
       const int dw_img_b = img_b + st.cout_pad * st.OH * st.OW * (int)es;
       st.imgs_dw = std::max(1, std::min(16, 65536 / dw_img_b));
       st.ppad = r32(st.imgs_dw * st.OH * st.OW);
-      MCC_CHECK(st.cout_pad <= 128, "conv_small path: Cout > 128");
+      // whole-image LDS kernels if one image fits comfortably; else im2col + GEMM
+      const int64_t lds_cap = 120 * 1024;
+      st.big = st.OH * st.OW > 4096 || st.cout_pad > 128 || (int64_t)img_b > lds_cap ||
+               (int64_t)LHd * LWd * st.CLd * (int64_t)es > lds_cap || (int64_t)dw_img_b > lds_cap;
+      st.kgem = r8(KK * st.inC);
+      st.kgem_d = r8(KK * st.C);
+      if (st.big) MCC_CHECK(st.C % 8 == 0, "im2col conv path needs Cout % 8 == 0");
     } else {
       st.out_elems = st.Nout;
       st.out_ld = r8(st.Nout);
@@ -171,7 +190,25 @@ void GpuNet::build() {
   };
   for (Stage* sp : stages_) {
     Stage& st = *sp;
-    if (st.kind == Stage::CONV) {
+    if (st.kind == Stage::CONV && st.big) {
+      const int KK = st.KS * st.KS;
+      // im2col GEMM operands: forward [C][kgem], k = kp*inC + ci; data
+      // gradient [inC][kgem_d], k = kp*C + co with flipped taps
+      st.pk_fwd = reserve((int64_t)st.C * st.kgem);
+      for (int n = 0; n < st.C; ++n)
+        for (int kp = 0; kp < KK; ++kp)
+          for (int c = 0; c < st.inC; ++c)
+            idx[st.pk_fwd + (int64_t)n * st.kgem + kp * st.inC + c] =
+                (int32_t)(st.w_off + ((int64_t)n * st.inC + c) * KK + kp);
+      if (&st != stages_[0]) {
+        st.pk_dx = reserve((int64_t)st.inC * st.kgem_d);
+        for (int ci = 0; ci < st.inC; ++ci)
+          for (int kp = 0; kp < KK; ++kp)
+            for (int co = 0; co < st.C; ++co)
+              idx[st.pk_dx + (int64_t)ci * st.kgem_d + kp * st.C + co] =
+                  (int32_t)(st.w_off + ((int64_t)co * st.inC + ci) * KK + (KK - 1 - kp));
+      }
+    } else if (st.kind == Stage::CONV) {
       const int KK = st.KS * st.KS;
       // forward: [r16(C)][kpad], k = (kp, cgroup, c8) or (kp, c)
       st.pk_fwd = reserve((int64_t)r16(st.C) * st.kpad);
@@ -222,14 +259,21 @@ void GpuNet::build() {
   // ---- arena: sizing pass then real pass ----
   const int Bm = max_batch_;
   size_t scratch = 0;
+  col_bytes_ = 0;
   for (Stage* sp : stages_) {
     const Stage& st = *sp;
-    if (st.kind == Stage::CONV) {
+    if (st.kind == Stage::CONV && st.big) {
+      const int KK = st.KS * st.KS;
+      col_bytes_ = std::max(col_bytes_, es * (size_t)Bm * st.OH * st.OW * st.kgem);
+      col_bytes_ = std::max(col_bytes_, es * (size_t)Bm * st.inH * st.inW * st.kgem_d);
+      const int sk = dw_splitk(st.C, KK * st.inC + 1, (int64_t)Bm * st.OH * st.OW);
+      scratch = std::max(scratch, (size_t)sk * st.C * r8(KK * st.inC + 1) * 4);
+    } else if (st.kind == Stage::CONV) {
       const int64_t groups = ceil_div(Bm, st.imgs_dw);
       const int64_t nx = std::min<int64_t>(groups, 512);
       scratch = std::max(scratch, (size_t)nx * st.cout_pad * st.ncols_pad * 4);
     } else {
-      scratch = std::max(scratch, (size_t)64 * st.Nout * st.ldp * 4);  // up to 64 split-K partials
+      scratch = std::max(scratch, (size_t)dw_splitk(st.Nout, st.Kin + 1, Bm) * st.Nout * st.ldp * 4);
     }
   }
   scratch_bytes_ = scratch;
@@ -243,12 +287,18 @@ void GpuNet::build() {
     packed_ = arena_alloc(es * (size_t)packed_count_);
     pack_idx_ = static_cast<int32_t*>(arena_alloc(4 * (size_t)packed_count_));
     scratch_ = static_cast<float*>(arena_alloc(scratch_bytes_));
+    col_ = col_bytes_ ? arena_alloc(col_bytes_) : nullptr;
     for (Stage* sp : stages_) {
       Stage& st = *sp;
       const int64_t per = st.kind == Stage::FC ? st.out_ld : st.out_elems;
       st.act_buf = arena_alloc(es * (size_t)Bm * per);
       st.grad_buf = arena_alloc(es * (size_t)Bm * per);
       st.arg_buf = st.pooled ? static_cast<uint8_t*>(arena_alloc((size_t)Bm * per)) : nullptr;
+      if (st.kind == Stage::CONV && st.big) {
+        const size_t conv_elems = (size_t)Bm * st.OH * st.OW * st.C;
+        st.conv_buf = st.pooled ? arena_alloc(es * conv_elems) : nullptr;
+        st.dz_buf = arena_alloc(es * conv_elems);
+      }
     }
     if (pass == 0) {
       arena_bytes_ = arena_used_ + 256;
@@ -268,7 +318,8 @@ std::string GpuNet::plan() const {
     if (st.kind == Stage::CONV) {
       os << "  [" << s << "] conv " << st.inC << "x" << st.inH << "x" << st.inW << " -> " << st.C << "x" << st.OH << "x"
          << st.OW << (st.pooled ? " +maxpool" : "") << " k" << st.KS << "s" << st.stride << "p" << st.pad
-         << (st.cvec ? " cvec" : " scalar") << " chunks=" << st.nchunks << " imgs=" << st.imgs_fwd << "/"
+         << (st.big ? " im2col+gemm" : (st.cvec ? " lds-cvec" : " lds-scalar")) << " chunks=" << st.nchunks
+         << " imgs=" << st.imgs_fwd << "/"
          << st.imgs_dx << "/" << st.imgs_dw << "\n";
     } else {
       os << "  [" << s << "] fc " << st.Kin << " -> " << st.Nout << (st.last ? " (logits)" : "")
@@ -308,7 +359,24 @@ void GpuNet::forward(const uint8_t* images, const int32_t* idx, int B, hipStream
   const size_t es = dtype_size(dtype_);
   for (size_t si = 0; si < stages_.size(); ++si) {
     Stage& st = *stages_[si];
-    if (st.kind == Stage::CONV) {
+    if (st.kind == Stage::CONV && st.big) {
+      // im2col (input transform fused) -> GEMM with bias+ReLU epilogue -> 2x2 max-pool
+      gpu::Im2colParams ic;
+      ic.N = B; ic.OH = st.OH; ic.OW = st.OW; ic.KS = st.KS; ic.cs = st.stride; ic.ldk = st.kgem;
+      ic.s.SH = st.inH; ic.s.SW = st.inW; ic.s.SC = st.inC; ic.s.off = st.pad; ic.s.up = 1;
+      if (si == 0) { ic.s.mode = gpu::IN_U8; ic.s.src = images; ic.s.idx = idx; }
+      else { ic.s.mode = gpu::IN_PLAIN; ic.s.src = stages_[si - 1]->act_buf; }
+      ic.out = col_;
+      gpu::im2col(dtype_, ic, s);
+      gpu::GemmParams g;
+      g.M = B * st.OH * st.OW; g.N = st.C; g.K = st.KS * st.KS * st.inC;
+      g.A = col_; g.lda = st.kgem;
+      g.B = static_cast<const char*>(packed_) + es * st.pk_fwd; g.ldb = st.kgem;
+      g.epi = gpu::EPI_BIAS_ACT; g.act = st.act; g.bias = params_ + st.b_off;
+      g.C = st.pooled ? st.conv_buf : st.act_buf; g.ldc = st.C;
+      gpu::gemm(dtype_, g, s);
+      if (st.pooled) gpu::maxpool2(dtype_, st.conv_buf, st.act_buf, st.arg_buf, B, st.OH, st.OW, st.C, s);
+    } else if (st.kind == Stage::CONV) {
       gpu::ConvParams p;
       p.N = B; p.imgs = st.imgs_fwd;
       p.Cin = st.inC; p.CL = st.CL; p.cvec = st.cvec;
@@ -364,6 +432,53 @@ void GpuNet::backward(int hi, int lo, hipStream_t s) {
       dy.mode = st.pooled ? gpu::IN_UNPOOL : (st.act == gpu::ACT_RELU ? gpu::IN_RELU : gpu::IN_PLAIN);
       dy.src = st.grad_buf; dy.aux_y = st.act_buf; dy.aux_arg = st.arg_buf;
       dy.SH = st.OH; dy.SW = st.OW; dy.SC = st.C; dy.PH = st.outH; dy.PW = st.outW;
+      if (st.big) {
+        const int KK = st.KS * st.KS;
+        const int kf = KK * st.inC;
+        // dZ = relu'/unpool(dY) at conv-output size
+        gpu::grad_xform(dtype_, dy, st.dz_buf, B, s);
+        // dW, db = dZ^T [im2col(X) | 1]  (split-K over B*OH*OW)
+        gpu::Im2colParams ic;
+        ic.N = B; ic.OH = st.OH; ic.OW = st.OW; ic.KS = st.KS; ic.cs = st.stride; ic.ldk = st.kgem;
+        ic.s.SH = st.inH; ic.s.SW = st.inW; ic.s.SC = st.inC; ic.s.off = st.pad; ic.s.up = 1;
+        if (si == 0) { ic.s.mode = gpu::IN_U8; ic.s.src = images_; ic.s.idx = idx_; }
+        else { ic.s.mode = gpu::IN_PLAIN; ic.s.src = stages_[si - 1]->act_buf; }
+        ic.out = col_;
+        gpu::im2col(dtype_, ic, s);
+        gpu::GemmParams w;
+        const int64_t rows = (int64_t)B * st.OH * st.OW;
+        w.M = st.C; w.N = kf + 1; w.K = (int)rows;
+        w.A = st.dz_buf; w.lda = st.C; w.ta = true;
+        w.B = col_; w.ldb = st.kgem; w.tb = true; w.ones_col = kf;
+        w.epi = gpu::EPI_PARTIAL; w.Cf = scratch_; w.ldc = r8(kf + 1);
+        w.splitk = dw_splitk(st.C, kf + 1, rows);
+        w.partial_stride = (int64_t)st.C * w.ldc;
+        MCC_CHECK((size_t)w.splitk * w.partial_stride * 4 <= scratch_bytes_, "big conv dW scratch too small");
+        gpu::gemm(dtype_, w, s);
+        gpu::DwReduceParams r;
+        r.S = w.splitk; r.Nout = st.C; r.kfeat = kf; r.ldp = w.ldc; r.part = scratch_;
+        r.partial_stride = w.partial_stride;
+        r.gw = grads_ + st.w_off; r.gb = grads_ + st.b_off;
+        r.permC = st.inC; r.permHW = KK;  // k = kp*inC + ci  ->  ci*KK + kp
+        gpu::dw_reduce(r, s);
+        if (si > 0) {
+          // dX = im2col(zero-inserted dZ) x flipped W^T
+          gpu::Im2colParams id;
+          id.N = B; id.OH = st.inH; id.OW = st.inW; id.KS = st.KS; id.cs = 1; id.ldk = st.kgem_d;
+          id.s.mode = gpu::IN_PLAIN; id.s.src = st.dz_buf;
+          id.s.SH = st.OH; id.s.SW = st.OW; id.s.SC = st.C; id.s.off = st.KS - 1 - st.pad; id.s.up = st.stride;
+          id.out = col_;
+          gpu::im2col(dtype_, id, s);
+          gpu::GemmParams d;
+          d.M = B * st.inH * st.inW; d.N = st.inC; d.K = KK * st.C;
+          d.A = col_; d.lda = st.kgem_d;
+          d.B = static_cast<const char*>(packed_) + es * st.pk_dx; d.ldb = st.kgem_d;
+          d.epi = gpu::EPI_DACT; d.act = gpu::ACT_NONE;
+          d.C = stages_[si - 1]->grad_buf; d.ldc = st.inC;
+          gpu::gemm(dtype_, d, s);
+        }
+        continue;
+      }
       // weight gradient
       gpu::ConvDwParams w;
       w.N = B; w.imgs = st.imgs_dw;
@@ -407,9 +522,7 @@ void GpuNet::backward(int hi, int lo, hipStream_t s) {
       w.A = st.grad_buf; w.lda = st.out_ld; w.ta = true;
       w.B = pv.act_buf; w.ldb = st.in_ld; w.tb = true; w.ones_col = st.Kin;
       w.epi = gpu::EPI_PARTIAL; w.Cf = scratch_; w.ldc = st.ldp;
-      const int tiles = (int)(ceil_div(st.Nout, 64) * ceil_div(st.Kin + 1, 64));
-      int sk = std::max(1, std::min(512 / std::max(1, tiles), B / 128));
-      sk = std::min(sk, 64);
+      const int sk = dw_splitk(st.Nout, st.Kin + 1, B);
       w.splitk = sk;
       w.partial_stride = (int64_t)st.Nout * st.ldp;
       gpu::gemm(dtype_, w, s);

@@ -1,0 +1,173 @@
+// Large-image convolution support (explicit im2col + MFMA GEMM path, used for
+// layers whose image does not fit the whole-image LDS kernels, e.g. VGG-11
+// at 224x224), plus the standalone 2x2 max-pool and the ReLU / max-pool
+// gradient transform for that path.
+//
+//  im2col        rows = output pixels (n, oy, ox) NHWC order, cols = (kernel
+//                position, input channel) — the packed weight K order — with
+//                the same source transforms as LDS staging (u8 /255 + index
+//                gather, ReLU mask, max-pool routing, zero insertion for the
+//                data gradient of strided convs), 16-byte vector moves when
+//                the channel count allows.
+//  maxpool2      2x2/2 max with argmax byte (first max wins, PyTorch order)
+//  grad_xform    dZ = relu' / unpool(dY) materialised at conv-output size for
+//                the weight-gradient GEMM.
+#include "kernels.h"
+#include "mfma.h"
+
+namespace mcc {
+namespace gpu {
+
+namespace {
+
+template <typename T>
+__device__ __forceinline__ float src_value(const StageSrc& s, int n, int sy, int sx, int c) {
+  switch (s.mode) {
+    case IN_U8: {
+      const int img = s.idx ? s.idx[n] : n;
+      return (float)static_cast<const uint8_t*>(s.src)[(((size_t)img * s.SH + sy) * s.SW + sx) * s.SC + c] *
+             (1.0f / 255.0f);
+    }
+    case IN_RELU: {
+      const size_t i = (((size_t)n * s.SH + sy) * s.SW + sx) * s.SC + c;
+      return to_f(static_cast<const T*>(s.aux_y)[i]) > 0.f ? to_f(static_cast<const T*>(s.src)[i]) : 0.f;
+    }
+    case IN_UNPOOL: {
+      const int py = sy >> 1, px = sx >> 1;
+      if (py >= s.PH || px >= s.PW) return 0.f;
+      const size_t i = (((size_t)n * s.PH + py) * s.PW + px) * s.SC + c;
+      if (s.aux_arg[i] != (((sy & 1) << 1) | (sx & 1))) return 0.f;
+      return to_f(static_cast<const T*>(s.aux_y)[i]) > 0.f ? to_f(static_cast<const T*>(s.src)[i]) : 0.f;
+    }
+    default:
+      return to_f(static_cast<const T*>(s.src)[(((size_t)n * s.SH + sy) * s.SW + sx) * s.SC + c]);
+  }
+}
+
+// One thread per (output pixel, 8-column group).
+template <typename T>
+__global__ void __launch_bounds__(256) im2col_kernel(Im2colParams p) {
+  typedef typename Vec8<T>::type V8;
+  const int64_t groups = p.ldk >> 3;
+  const int64_t total = (int64_t)p.N * p.OH * p.OW * groups;
+  const int K = p.KS * p.KS * p.s.SC;
+  T* out = static_cast<T*>(p.out);
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t row = e / groups;
+    const int k0 = (int)(e - row * groups) * 8;
+    const int64_t pix = row % ((int64_t)p.OH * p.OW);
+    const int n = (int)(row / ((int64_t)p.OH * p.OW));
+    const int oy = (int)(pix / p.OW), ox = (int)(pix % p.OW);
+    V8 v;
+    const bool vec = (p.s.SC & 7) == 0 && p.s.mode == IN_PLAIN;
+    if (vec && k0 + 8 <= K) {
+      const int kp = k0 / p.s.SC, c0 = k0 - kp * p.s.SC;
+      const int kh = kp / p.KS, kw = kp - kh * p.KS;
+      int ty = oy * p.cs + kh - p.s.off, tx = ox * p.cs + kw - p.s.off;
+      bool ok = ty >= 0 && tx >= 0;
+      if (p.s.up != 1) {
+        ok = ok && ty % p.s.up == 0 && tx % p.s.up == 0;
+        ty /= p.s.up;
+        tx /= p.s.up;
+      }
+      ok = ok && ty < p.s.SH && tx < p.s.SW;
+      if (ok) {
+        v = load8(static_cast<const T*>(p.s.src) + (((size_t)n * p.s.SH + ty) * p.s.SW + tx) * p.s.SC + c0);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j] = T(0);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int k = k0 + j;
+        float f = 0.f;
+        if (k < K) {
+          const int kp = k / p.s.SC, c = k - kp * p.s.SC;
+          const int kh = kp / p.KS, kw = kp - kh * p.KS;
+          int ty = oy * p.cs + kh - p.s.off, tx = ox * p.cs + kw - p.s.off;
+          bool ok = ty >= 0 && tx >= 0;
+          if (p.s.up != 1) {
+            ok = ok && ty % p.s.up == 0 && tx % p.s.up == 0;
+            ty /= p.s.up;
+            tx /= p.s.up;
+          }
+          ok = ok && ty < p.s.SH && tx < p.s.SW;
+          if (ok) f = src_value<T>(p.s, n, ty, tx, c);
+        }
+        v[j] = from_f<T>(f);
+      }
+    }
+    store8(out + (size_t)row * p.ldk + k0, v);
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) maxpool2_kernel(const T* __restrict__ in, T* __restrict__ out,
+                                                       uint8_t* __restrict__ arg, int N, int H, int W, int C) {
+  const int PH = H >> 1, PW = W >> 1;
+  const int64_t total = (int64_t)N * PH * PW * C;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    const int c = (int)(e % C);
+    const int64_t r = e / C;
+    const int px = (int)(r % PW), py = (int)((r / PW) % PH), n = (int)(r / ((int64_t)PW * PH));
+    const size_t b = (((size_t)n * H + 2 * py) * W + 2 * px) * C + c;
+    float v[4] = {to_f(in[b]), to_f(in[b + C]), to_f(in[b + (size_t)W * C]), to_f(in[b + (size_t)W * C + C])};
+    float best = v[0];
+    int a = 0;
+#pragma unroll
+    for (int i = 1; i < 4; ++i)
+      if (v[i] > best) { best = v[i]; a = i; }
+    out[e] = from_f<T>(best);
+    arg[e] = (uint8_t)a;
+  }
+}
+
+// dZ at conv-output resolution from the stage-output gradient.
+template <typename T>
+__global__ void __launch_bounds__(256) grad_xform_kernel(StageSrc s, T* __restrict__ dz, int N) {
+  const int64_t total = (int64_t)N * s.SH * s.SW * s.SC;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    const int c = (int)(e % s.SC);
+    const int64_t r = e / s.SC;
+    const int x = (int)(r % s.SW), y = (int)((r / s.SW) % s.SH), n = (int)(r / ((int64_t)s.SW * s.SH));
+    dz[e] = from_f<T>(src_value<T>(s, n, y, x, c));
+  }
+}
+
+inline unsigned grid_cap(int64_t n) {
+  int64_t b = (n + 255) / 256;
+  if (b < 1) b = 1;
+  if (b > 65536) b = 65536;
+  return (unsigned)b;
+}
+
+}  // namespace
+
+void im2col(DType t, const Im2colParams& p, hipStream_t s) {
+  MCC_CHECK(p.ldk % 8 == 0 && p.ldk >= p.KS * p.KS * p.s.SC, "im2col: bad ldk");
+  const int64_t n = (int64_t)p.N * p.OH * p.OW * (p.ldk / 8);
+  if (t == DType::BF16) hipLaunchKernelGGL(im2col_kernel<bf16>, dim3(grid_cap(n)), dim3(256), 0, s, p);
+  else hipLaunchKernelGGL(im2col_kernel<float>, dim3(grid_cap(n)), dim3(256), 0, s, p);
+}
+
+void maxpool2(DType t, const void* in, void* out, uint8_t* arg, int N, int H, int W, int C, hipStream_t s) {
+  const int64_t n = (int64_t)N * (H / 2) * (W / 2) * C;
+  if (t == DType::BF16)
+    hipLaunchKernelGGL(maxpool2_kernel<bf16>, dim3(grid_cap(n)), dim3(256), 0, s, static_cast<const bf16*>(in),
+                       static_cast<bf16*>(out), arg, N, H, W, C);
+  else
+    hipLaunchKernelGGL(maxpool2_kernel<float>, dim3(grid_cap(n)), dim3(256), 0, s, static_cast<const float*>(in),
+                       static_cast<float*>(out), arg, N, H, W, C);
+}
+
+void grad_xform(DType t, const StageSrc& src, void* dz, int N, hipStream_t s) {
+  const int64_t n = (int64_t)N * src.SH * src.SW * src.SC;
+  if (t == DType::BF16)
+    hipLaunchKernelGGL(grad_xform_kernel<bf16>, dim3(grid_cap(n)), dim3(256), 0, s, src, static_cast<bf16*>(dz), N);
+  else
+    hipLaunchKernelGGL(grad_xform_kernel<float>, dim3(grid_cap(n)), dim3(256), 0, s, src, static_cast<float*>(dz), N);
+}
+
+}  // namespace gpu
+}  // namespace mcc

@@ -143,6 +143,20 @@ struct XentParams {
   int32_t* pred = nullptr;              // optional argmax per sample
 };
 
+// Explicit im2col for the large-image path: out[(n*OH+oy)*OW+ox][k], k =
+// (kh*KS+kw)*SC + c (zero for k >= KS*KS*SC), source through `s` (tile
+// coordinate oy*cs+kh maps to source (.. - off)/up).
+struct Im2colParams {
+  int N = 0, OH = 0, OW = 0, KS = 1, cs = 1;
+  int ldk = 0;  // row stride of out (multiple of 8)
+  StageSrc s;
+  void* out = nullptr;
+};
+void im2col(DType t, const Im2colParams& p, hipStream_t s);
+void maxpool2(DType t, const void* in, void* out, uint8_t* arg, int N, int H, int W, int C, hipStream_t s);
+// dz[n][y][x][c] = transform(src) at the conv-output grid (SH x SW x SC)
+void grad_xform(DType t, const StageSrc& src, void* dz, int N, hipStream_t s);
+
 void conv_forward(DType t, const ConvParams& p, hipStream_t s);
 size_t conv_forward_lds_bytes(DType t, const ConvParams& p);
 void conv_dw(DType t, const ConvDwParams& p, hipStream_t s);
