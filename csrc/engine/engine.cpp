@@ -9,6 +9,8 @@
 
 #include "kernels.h"
 
+#include <cstdlib>
+
 namespace mcc {
 
 #define HIP_OK(expr)                                                                                    \
@@ -77,6 +79,7 @@ GpuNet::GpuNet(const ModelSpec& spec, DType dtype, int max_batch, int device)
     : spec_(spec), dtype_(dtype), max_batch_(max_batch), device_(device) {
   MCC_CHECK(dtype == DType::BF16 || dtype == DType::F32, "GpuNet: dtype must be bf16 or fp32");
   MCC_CHECK(max_batch > 0, "GpuNet: max_batch > 0");
+  if (const char* a = std::getenv("MCC_ABLATE")) ablate_ = std::atoi(a);  // kernel diagnostics only
   if (device_ >= 0) HIP_OK(hipSetDevice(device_));
   else HIP_OK(hipGetDevice(&device_));
   build();
@@ -390,6 +393,7 @@ void GpuNet::forward(const uint8_t* images, const int32_t* idx, int B, hipStream
       p.wpk = static_cast<const char*>(packed_) + es * st.pk_fwd;
       p.bias = params_ + st.b_off;
       p.out = st.act_buf; p.out_arg = st.arg_buf;
+      p.ablate = ablate_;
       gpu::conv_forward(dtype_, p, s);
     } else {
       const Stage& pv = *stages_[si - 1];
@@ -493,6 +497,7 @@ void GpuNet::backward(int hi, int lo, hipStream_t s) {
       w.dy = dy;
       w.slab = scratch_;
       MCC_CHECK((size_t)w.nx * w.cout_pad * w.ncols_pad * 4 <= scratch_bytes_, "conv dW scratch too small");
+      w.ablate = ablate_;
       gpu::conv_dw(dtype_, w, s);
       gpu::ConvDwReduceParams r;
       r.nx = w.nx; r.Cout = st.C; r.Cin = st.inC; r.KS = st.KS; r.CG = st.CL / 8; r.cvec = st.cvec;
@@ -512,6 +517,7 @@ void GpuNet::backward(int hi, int lo, hipStream_t s) {
         p.in.off = st.KS - 1 - st.pad; p.in.up = st.stride;
         p.wpk = static_cast<const char*>(packed_) + es * st.pk_dx;
         p.out = stages_[si - 1]->grad_buf;
+        p.ablate = ablate_;
         gpu::conv_forward(dtype_, p, s);
       }
     } else {

@@ -395,7 +395,7 @@ __global__ void __launch_bounds__(256) conv_fwd_kernel(ConvParams p) {
   }
   pixel_table(ptab, rows_per_img, pool, p.OW, PW, p.cs, p.LW, p.CL);
   __syncthreads();
-  stage_scatter<T, false>(p.in, xs, img0, nimg, p.LH, p.LW, p.CL);
+  if (p.ablate != 1) stage_scatter<T, false>(p.in, xs, img0, nimg, p.LH, p.LW, p.CL);
   __syncthreads();
 
   const int lane = tid & 63, wave = tid >> 6, nwaves = blockDim.x >> 6;
@@ -406,7 +406,7 @@ __global__ void __launch_bounds__(256) conv_fwd_kernel(ConvParams p) {
   T* out = static_cast<T*>(p.out);
   const size_t obase = pool ? (size_t)img0 * PH * PW : (size_t)img0 * p.OH * p.OW;
 
-  for (int item = wave; item < ntiles * mgroups; item += nwaves) {
+  for (int item = wave; item < (p.ablate == 2 ? 0 : ntiles * mgroups); item += nwaves) {
     const int nt = item / mgroups, mg = item - nt * mgroups;
     int base[MT];
 #pragma unroll
@@ -541,15 +541,17 @@ __global__ void __launch_bounds__(256) conv_dw_kernel(ConvDwParams p) {
     lds_zero(xs, xs_elems);
     lds_zero(dys, p.cout_pad * drow);
     __syncthreads();
-    stage_scatter<T, false>(p.x, xs, img0, nimg, p.LH, p.LW, p.CL);
-    stage_scatter<T, true>(p.dy, dys, img0, nimg, p.OH, p.OW, drow);
+    if (p.ablate != 1) {
+      stage_scatter<T, false>(p.x, xs, img0, nimg, p.LH, p.LW, p.CL);
+      stage_scatter<T, true>(p.dy, dys, img0, nimg, p.OH, p.OW, drow);
+    }
     for (int pix = tid; pix < p.ppad; pix += blockDim.x) {
       const int img = dopix.div(pix);
       pixbase[pix] = pix < npix ? img * img_elems + ptab[pix - img * opix] : 0;  // dY is 0 there
     }
     __syncthreads();
     const int nq = cdiv(npix, 32);
-    for (int q = wave; q < nq; q += nwaves) {
+    for (int q = wave; q < (p.ablate == 2 ? 0 : nq); q += nwaves) {
       int pb[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) pb[j] = pixbase[q * 32 + 8 * g + j];

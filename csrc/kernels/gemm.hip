@@ -1,4 +1,5 @@
-// LDS-tiled MFMA GEMM for the fully-connected layers, with fused epilogues.
+// LDS-tiled MFMA GEMM for the fully-connected layers and the im2col conv
+// path, with fused epilogues.
 //
 // Replaces the reference's scalar FC loops: forward W*x + b then tanh/softmax
 // (Layer_feedForw_full, cnn.c:113-152) and the fused dX/dW/db backward loop
@@ -7,8 +8,14 @@
 //   data grad dX = (dY W) * act'(Xprev)  EPI_DACT      (W^T shadow keeps B K-contiguous)
 //   weight    dW = dY^T X, db = dY^T 1   EPI_PARTIAL   (split-K over the batch; the
 //             bias gradient is a ones-column appended to X — no separate reduce)
-// C[M][N] = A[M][K] * B[N][K]^T; `ta`/`tb` say an operand is stored K-major, in
-// which case the staging pass transposes it into the [row][k] LDS image.
+// C[M][N] = A[M][K] * B[N][K]^T; `ta`/`tb`: the operand is stored K-major.
+//
+// gfx950 structure: 256 threads = 4 waves, BK = 32 (one 16x16x32 bf16 MFMA
+// K-step), LDS double buffer + register prefetch (the global loads of tile
+// k+1 are in flight while tile k is multiplied; one barrier per K-step).
+// K-major (transposed) bf16 operands are staged exactly as they sit in memory
+// (16-byte row copies) and read with ds_read_b64_tr_b16, the CDNA4 hardware
+// transpose read, instead of being transposed element by element.
 #include "kernels.h"
 #include "mfma.h"
 
@@ -17,66 +24,117 @@ namespace gpu {
 
 namespace {
 
+typedef short v4s __attribute__((ext_vector_type(4)));
+
+typedef __attribute__((address_space(3))) v4s lds_v4s;
+
+// ds_read_b64_tr_b16 (cdna_hip_programming.md §5.5 T10); `p` points into LDS.
+__device__ __forceinline__ v4s ds_tr16(const bf16* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(const_cast<bf16*>(p)));
+}
+
 template <typename T>
 __device__ __forceinline__ float ld_elem(const T* base, int ld, bool trans, int r, int k, int R, int K) {
   if (r >= R || k >= K) return 0.f;
   return to_f(trans ? base[(size_t)k * ld + r] : base[(size_t)r * ld + k]);
 }
 
-// Stage a ROWS x 32 tile (rows r0.., k k0..) of op(X) into lds[row][LDK].
-template <typename T, int ROWS, int LDK>
-__device__ __forceinline__ void stage_operand(T* lds, const T* X, int ld, bool trans, int r0, int k0, int R,
-                                              int K, int ones_row) {
+// One operand tile (ROWS x 32) moving global -> registers -> LDS.
+// Layout in LDS: !TRANS or !TR: [ROWS][LDK] (k contiguous);
+//                TRANS && TR:   [32][ROWS + 8] (rows of k, read by ds_read_b64_tr_b16).
+template <typename T, int ROWS, bool TRANS, bool TR>
+struct Operand {
   typedef typename Vec8<T>::type V8;
-  constexpr int NV = ROWS * 4;  // 8-element vectors in the tile
-  for (int v = threadIdx.x; v < NV; v += blockDim.x) {
-    if (!trans) {
-      const int row = v >> 2, kv = (v & 3) * 8;
-      const int gr = r0 + row, gk = k0 + kv;
-      V8 x;
-      if (gr < R && gr != ones_row && gk + 8 <= K) {
-        x = load8(X + (size_t)gr * ld + gk);
-      } else {
+  static constexpr int LDK = 32 + (sizeof(T) == 2 ? 8 : 4);
+  static constexpr int LDM = ROWS + 8;
+  static constexpr int ELEMS = (TRANS && TR) ? 32 * LDM : ROWS * LDK;
+  static constexpr int NVEC = ROWS * 4;  // 8-element vectors per tile
+  static constexpr int PER = (NVEC + 255) / 256;
+  V8 r[PER];
+
+  __device__ __forceinline__ void load(const T* X, int ld, int r0, int k0, int R, int K, int ones_row) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float f = gr == ones_row ? (gk + j < K ? 1.f : 0.f) : ld_elem(X, ld, false, gr, gk + j, R, K);
-          x[j] = from_f<T>(f);
+    for (int j = 0; j < PER; ++j) {
+      const int v = threadIdx.x + j * 256;
+      if (v >= NVEC) break;
+      if (!TRANS) {
+        const int row = v >> 2, kv = (v & 3) * 8;
+        const int gr = r0 + row, gk = k0 + kv;
+        if (gr < R && gr != ones_row && gk + 8 <= K) {
+          r[j] = load8(X + (size_t)gr * ld + gk);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+            r[j][e] = from_f<T>(gr == ones_row ? (gk + e < K ? 1.f : 0.f) : ld_elem(X, ld, false, gr, gk + e, R, K));
+        }
+      } else {
+        constexpr int RV = ROWS / 8;
+        const int kr = v / RV, rv = (v - kr * RV) * 8;
+        const int gk = k0 + kr, gr = r0 + rv;
+        if (gk < K && gr + 8 <= R && (ones_row < gr || ones_row >= gr + 8)) {
+          r[j] = load8(X + (size_t)gk * ld + gr);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+            r[j][e] = from_f<T>((gr + e) == ones_row ? (gk < K ? 1.f : 0.f) : ld_elem(X, ld, true, gr + e, gk, R, K));
         }
       }
-      store8(lds + row * LDK + kv, x);
-    } else {
-      constexpr int RV = ROWS / 8;
-      const int kr = v / RV, rv = (v - kr * RV) * 8;
-      const int gk = k0 + kr, gr = r0 + rv;
-      V8 x;
-      if (gk < K && gr + 8 <= R && (ones_row < gr || ones_row >= gr + 8)) {
-        x = load8(X + (size_t)gk * ld + gr);
-      } else {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float f = (gr + j) == ones_row ? (gk < K ? 1.f : 0.f) : ld_elem(X, ld, true, gr + j, gk, R, K);
-          x[j] = from_f<T>(f);
-        }
-      }
-#pragma unroll
-      for (int j = 0; j < 8; ++j) lds[(rv + j) * LDK + kr] = x[j];
     }
   }
-}
 
-template <typename T, int BM, int BN>
+  __device__ __forceinline__ void store(T* lds) const {
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int v = threadIdx.x + j * 256;
+      if (v >= NVEC) break;
+      if (!TRANS) {
+        store8(lds + (v >> 2) * LDK + (v & 3) * 8, r[j]);
+      } else {
+        constexpr int RV = ROWS / 8;
+        const int kr = v / RV, rv = (v - kr * RV) * 8;
+        if (TR) {
+          store8(lds + kr * LDM + rv, r[j]);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) lds[(rv + e) * LDK + kr] = r[j][e];
+        }
+      }
+    }
+  }
+
+  // MFMA fragment of the 16-row block starting at `row0`: lane (r16, g) gets
+  // rows row0 + r16, k = 8g .. 8g+7.
+  __device__ __forceinline__ static V8 frag(const T* lds, int row0, int r16, int g) {
+    if constexpr (TRANS && TR) {
+      // lane 4q+p of each 16-lane group addresses row (k) q, columns 4p..4p+3
+      const int q = r16 >> 2, pp = r16 & 3;
+      const bf16* b = reinterpret_cast<const bf16*>(lds);
+      const bf16x4 lo = __builtin_bit_cast(bf16x4, ds_tr16(b + (8 * g + q) * LDM + row0 + 4 * pp));
+      const bf16x4 hi = __builtin_bit_cast(bf16x4, ds_tr16(b + (8 * g + 4 + q) * LDM + row0 + 4 * pp));
+      return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    } else {
+      return load8(lds + (row0 + r16) * LDK + 8 * g);
+    }
+  }
+};
+
+template <typename T, int BM, int BN, int WAVES_M, bool TA, bool TB>
 __global__ void __launch_bounds__(256) gemm_kernel(GemmParams p) {
   typedef typename Vec8<T>::type V8;
-  constexpr int BK = 32;
-  constexpr int LDK = BK + (sizeof(T) == 2 ? 8 : 4);
-  __shared__ __attribute__((aligned(16))) T As[BM * LDK];
-  __shared__ __attribute__((aligned(16))) T Bs[BN * LDK];
+  constexpr bool TR = sizeof(T) == 2;
+  typedef Operand<T, BM, TA, TR> OpA;
+  typedef Operand<T, BN, TB, TR> OpB;
+  constexpr int WAVES_N = 4 / WAVES_M;
+  constexpr int WTM = BM / WAVES_M, WTN = BN / WAVES_N;
+  constexpr int FM = WTM / 16, FN = WTN / 16;
+  __shared__ __attribute__((aligned(16))) T As[2][OpA::ELEMS];
+  __shared__ __attribute__((aligned(16))) T Bs[2][OpB::ELEMS];
+
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r16 = lane & 15, g = lane >> 4;
-  const int wm = wave >> 1, wn = wave & 1;
-  constexpr int WM = BM / 2, WN = BN / 2, FM = WM / 16, FN = WN / 16;
+  const int wm = wave / WAVES_N, wn = wave % WAVES_N;
   const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
-  const int kchunks = cdiv(p.K, BK);
+  const int kchunks = cdiv(p.K, 32);
   const int per = cdiv(kchunks, (int)gridDim.z);
   const int kc0 = blockIdx.z * per, kc1 = min(kchunks, kc0 + per);
   const T* A = static_cast<const T*>(p.A);
@@ -88,21 +146,37 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmParams p) {
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  OpA la;
+  OpB lb;
+  if (kc0 < kc1) {
+    la.load(A, p.lda, m0, kc0 * 32, p.M, p.K, -1);
+    lb.load(B, p.ldb, n0, kc0 * 32, p.N, p.K, p.ones_col);
+    la.store(As[0]);
+    lb.store(Bs[0]);
+  }
+  __syncthreads();
+  int buf = 0;
   for (int kc = kc0; kc < kc1; ++kc) {
-    const int k0 = kc * BK;
-    __syncthreads();
-    stage_operand<T, BM, LDK>(As, A, p.lda, p.ta, m0, k0, p.M, p.K, -1);
-    stage_operand<T, BN, LDK>(Bs, B, p.ldb, p.tb, n0, k0, p.N, p.K, p.ones_col);
-    __syncthreads();
+    const bool more = kc + 1 < kc1;
+    if (more) {  // prefetch tile k+1 (in flight during the MFMAs below)
+      la.load(A, p.lda, m0, (kc + 1) * 32, p.M, p.K, -1);
+      lb.load(B, p.ldb, n0, (kc + 1) * 32, p.N, p.K, p.ones_col);
+    }
     V8 a[FM], b[FN];
 #pragma unroll
-    for (int i = 0; i < FM; ++i) a[i] = load8(As + (wm * WM + i * 16 + r16) * LDK + 8 * g);
+    for (int i = 0; i < FM; ++i) a[i] = OpA::frag(As[buf], wm * WTM + i * 16, r16, g);
 #pragma unroll
-    for (int j = 0; j < FN; ++j) b[j] = load8(Bs + (wn * WN + j * 16 + r16) * LDK + 8 * g);
+    for (int j = 0; j < FN; ++j) b[j] = OpB::frag(Bs[buf], wn * WTN + j * 16, r16, g);
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
       for (int j = 0; j < FN; ++j) acc[i][j] = mma(acc[i][j], a[i], b[j]);
+    if (more) {
+      la.store(As[buf ^ 1]);
+      lb.store(Bs[buf ^ 1]);
+    }
+    __syncthreads();
+    buf ^= 1;
   }
 
   T* C = static_cast<T*>(p.C);
@@ -111,12 +185,12 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmParams p) {
   for (int i = 0; i < FM; ++i) {
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
-      const int col = n0 + wn * WN + j * 16 + r16;
+      const int col = n0 + wn * WTN + j * 16 + r16;
       if (col >= p.N) continue;
       const float bv = (p.epi == EPI_BIAS_ACT || p.epi == EPI_LOGITS) && p.bias ? p.bias[col] : 0.f;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const int row = m0 + wm * WM + i * 16 + 4 * g + e;
+        const int row = m0 + wm * WTM + i * 16 + 4 * g + e;
         if (row >= p.M) continue;
         const float v = acc[i][j][e];
         switch (p.epi) {
@@ -140,14 +214,25 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmParams p) {
   }
 }
 
-__global__ void dw_reduce_kernel(DwReduceParams p) {
+// Sum split-K partials: 4 independent accumulators per thread so the S loads
+// are in flight together.
+__global__ void __launch_bounds__(256) dw_reduce_kernel(DwReduceParams p) {
   const int kc = p.kfeat + 1;
   const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= (int64_t)p.Nout * kc) return;
   const int n = (int)(j / kc), k = (int)(j - (int64_t)n * kc);
   const float* src = p.part + (size_t)n * p.ldp + k;
-  float acc = 0.f;
-  for (int s = 0; s < p.S; ++s) acc += src[(size_t)s * p.partial_stride];
+  const size_t st = (size_t)p.partial_stride;
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  int s = 0;
+  for (; s + 3 < p.S; s += 4) {
+    a0 += src[(size_t)s * st];
+    a1 += src[(size_t)(s + 1) * st];
+    a2 += src[(size_t)(s + 2) * st];
+    a3 += src[(size_t)(s + 3) * st];
+  }
+  for (; s < p.S; ++s) a0 += src[(size_t)s * st];
+  const float acc = (a0 + a1) + (a2 + a3);
   float* dst;
   if (k < p.kfeat) {
     int kk = k;
@@ -162,20 +247,34 @@ __global__ void dw_reduce_kernel(DwReduceParams p) {
   *dst = p.beta != 0.f ? p.beta * *dst + acc : acc;
 }
 
+template <typename T, int BM, int BN, int WAVES_M>
+void launch_cfg(const GemmParams& p, hipStream_t s) {
+  const dim3 grid((unsigned)cdiv(p.N, BN), (unsigned)cdiv(p.M, BM), (unsigned)p.splitk), block(256);
+  if (!p.ta && !p.tb) hipLaunchKernelGGL((gemm_kernel<T, BM, BN, WAVES_M, false, false>), grid, block, 0, s, p);
+  else if (!p.ta && p.tb) hipLaunchKernelGGL((gemm_kernel<T, BM, BN, WAVES_M, false, true>), grid, block, 0, s, p);
+  else if (p.ta && !p.tb) hipLaunchKernelGGL((gemm_kernel<T, BM, BN, WAVES_M, true, false>), grid, block, 0, s, p);
+  else hipLaunchKernelGGL((gemm_kernel<T, BM, BN, WAVES_M, true, true>), grid, block, 0, s, p);
+}
+
 template <typename T>
 void launch_gemm(const GemmParams& p, hipStream_t s) {
-  const dim3 block(256);
-  // Tile choice: wide-N tiles for the skinny forward/backward-data GEMMs
-  // (N <= 128 is one tile, A is streamed once), 64x64 otherwise.
-  if (p.N > 64 && p.N <= 128 && p.M >= 1024) {
-    const dim3 grid((unsigned)cdiv(p.N, 128), (unsigned)cdiv(p.M, 64), (unsigned)p.splitk);
-    hipLaunchKernelGGL((gemm_kernel<T, 64, 128>), grid, block, 0, s, p);
-  } else if (p.M >= 4096 && p.N >= 128) {
-    const dim3 grid((unsigned)cdiv(p.N, 128), (unsigned)cdiv(p.M, 128), (unsigned)p.splitk);
-    hipLaunchKernelGGL((gemm_kernel<T, 128, 128>), grid, block, 0, s, p);
+  // Tile choice: the largest tile that still gives >= 2 workgroups per CU
+  // (latency of the staging pipeline is hidden across co-resident groups);
+  // skinny-N problems (FC layers, N <= 128) use a full-width N tile so A is
+  // streamed once.
+  auto wgs = [&](int bm, int bn) { return (int64_t)cdiv(p.M, bm) * cdiv(p.N, bn) * p.splitk; };
+  const int64_t want = 512;
+  if (p.N > 64 && p.N <= 128) {
+    if (wgs(64, 128) >= want) launch_cfg<T, 64, 128, 2>(p, s);
+    else launch_cfg<T, 32, 128, 1>(p, s);
+  } else if (p.N <= 64) {
+    if (wgs(64, 64) >= want) launch_cfg<T, 64, 64, 2>(p, s);
+    else launch_cfg<T, 32, 64, 2>(p, s);
   } else {
-    const dim3 grid((unsigned)cdiv(p.N, 64), (unsigned)cdiv(p.M, 64), (unsigned)p.splitk);
-    hipLaunchKernelGGL((gemm_kernel<T, 64, 64>), grid, block, 0, s, p);
+    if (wgs(128, 128) >= want) launch_cfg<T, 128, 128, 2>(p, s);
+    else if (wgs(64, 128) >= want) launch_cfg<T, 64, 128, 2>(p, s);
+    else if (wgs(64, 64) >= want || p.M > 32) launch_cfg<T, 64, 64, 2>(p, s);
+    else launch_cfg<T, 32, 64, 2>(p, s);
   }
 }
 

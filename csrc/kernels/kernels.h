@@ -62,6 +62,7 @@ struct ConvParams {
   int act = ACT_RELU;
   bool bias_act = true;  // false: plain store (data-gradient form)
   StageSrc in;
+  int ablate = 0;               // diagnostics: 1 = skip staging scatter, 2 = skip MFMA loop
   const void* wpk = nullptr;    // packed weights [round_up(Cout,16)][kpad], T
   const float* bias = nullptr;  // fp32 canonical bias [Cout]
   void* out = nullptr;          // T NHWC [N][OH'][OW'][Cout]
@@ -83,6 +84,7 @@ struct ConvDwParams {
   StageSrc x;          // forward input of the layer
   StageSrc dy;         // gradient w.r.t. the conv output (via RELU/UNPOOL)
   float* slab = nullptr;  // [nx][cout_pad][ncols_pad]
+  int ablate = 0;         // diagnostics: 1 = skip staging scatter, 2 = skip MFMA loop
 };
 
 // Sum the dW slabs over x and scatter into the canonical fp32 gradient.

@@ -1,0 +1,130 @@
+"""Per-kernel numerics on the MI355X vs plain PyTorch fp32 references.
+
+GEMM: every operand orientation (A/B row- or K-major — the K-major bf16 path
+uses the ds_read_b64_tr_b16 hardware transpose), every tile configuration the
+dispatcher can pick, every epilogue, split-K partials, the ones-column bias
+trick, and an asymmetric B (a symmetric one hides a transposed C write).
+"""
+
+import numpy as np
+import pytest
+import torch
+
+import mpi_cuda_cnn_amd as mcc
+
+K_ = mcc._C.kernels
+TDT = {"bf16": torch.bfloat16, "fp32": torch.float32}
+
+
+def _s():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _stored(x, trans, ld):
+    """x: logical [R][K]; returns storage tensor and pointer with leading dim ld."""
+    R, K = x.shape
+    if not trans:
+        buf = torch.zeros(R, ld, dtype=x.dtype, device=x.device)
+        buf[:, :K] = x
+    else:
+        buf = torch.zeros(K, ld, dtype=x.dtype, device=x.device)
+        buf[:, :R] = x.t()
+    return buf
+
+
+SHAPES = [(96, 120, 400), (16384, 120, 400), (1000, 84, 120), (257, 10, 84), (120, 401, 2048), (64, 200, 1568),
+          (4096, 256, 2048), (48, 1000, 4096), (2048, 64, 27)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", ["bf16", "fp32"])
+@pytest.mark.parametrize("ta,tb", [(False, False), (False, True), (True, False), (True, True)])
+def test_gemm_orientations_and_tiles(cuda, dtype, ta, tb):
+    g = torch.Generator(device=cuda).manual_seed(0)
+    for M, N, K in SHAPES:
+        A = torch.randn(M, K, device=cuda, generator=g).to(TDT[dtype])
+        Bm = (torch.randn(N, K, device=cuda, generator=g) + torch.arange(N, device=cuda)[:, None] * 0.01).to(TDT[dtype])
+        lda = ((M if ta else K) + 7) // 8 * 8
+        ldb = ((N if tb else K) + 7) // 8 * 8
+        As, Bs = _stored(A, ta, lda), _stored(Bm, tb, ldb)
+        ldc = (N + 7) // 8 * 8
+        Cf = torch.zeros(M, ldc, device=cuda)
+        bias = torch.randn(N, device=cuda, generator=g)
+        K_.gemm(dtype, M, N, K, As.data_ptr(), lda, ta, Bs.data_ptr(), ldb, tb, epi=K_.EPI_LOGITS,
+                bias=bias.data_ptr(), ldc=ldc, Cf=Cf.data_ptr(), stream=_s())
+        torch.cuda.synchronize()
+        ref = A.float() @ Bm.float().t() + bias
+        err = (Cf[:, :N] - ref).abs().max().item() / max(1e-6, ref.abs().max().item())
+        tol = 2e-5 if dtype == "fp32" else 2e-2
+        assert err < tol, (M, N, K, ta, tb, err)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", ["bf16", "fp32"])
+def test_gemm_epilogues(cuda, dtype):
+    g = torch.Generator(device=cuda).manual_seed(1)
+    M, N, K = 300, 120, 256
+    A = torch.randn(M, K, device=cuda, generator=g).to(TDT[dtype])
+    Bm = torch.randn(N, K, device=cuda, generator=g).to(TDT[dtype])
+    bias = torch.randn(N, device=cuda, generator=g)
+    ref = A.float() @ Bm.float().t()
+    tol = 2e-5 if dtype == "fp32" else 3e-2
+    for act, fn in ((K_.ACT_RELU, torch.relu), (K_.ACT_TANH, torch.tanh), (K_.ACT_NONE, lambda x: x)):
+        C = torch.zeros(M, 120, device=cuda, dtype=TDT[dtype])
+        K_.gemm(dtype, M, N, K, A.data_ptr(), K, False, Bm.data_ptr(), K, False, epi=K_.EPI_BIAS_ACT, act=act,
+                bias=bias.data_ptr(), C=C.data_ptr(), ldc=120, stream=_s())
+        torch.cuda.synchronize()
+        torch.testing.assert_close(C.float(), fn(ref + bias), atol=tol * 10, rtol=tol)
+    # EPI_DACT: acc * act'(aux) with aux = activation output
+    aux = torch.tanh(torch.randn(M, N, device=cuda, generator=g)).to(TDT[dtype])
+    for act, d in ((K_.ACT_TANH, 1 - aux.float() ** 2), (K_.ACT_RELU, (aux.float() > 0).float())):
+        C = torch.zeros(M, 120, device=cuda, dtype=TDT[dtype])
+        K_.gemm(dtype, M, N, K, A.data_ptr(), K, False, Bm.data_ptr(), K, False, epi=K_.EPI_DACT, act=act,
+                aux=aux.data_ptr(), ldaux=120, C=C.data_ptr(), ldc=120, stream=_s())
+        torch.cuda.synchronize()
+        torch.testing.assert_close(C.float(), ref * d, atol=tol * 10, rtol=tol)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", ["bf16", "fp32"])
+def test_gemm_splitk_partials_with_ones_column(cuda, dtype):
+    """dW = dY^T [X | 1]: both operands K-major (batch-major storage)."""
+    g = torch.Generator(device=cuda).manual_seed(2)
+    Bt, Nout, Kin = 4096, 120, 400
+    dY = torch.randn(Bt, Nout, device=cuda, generator=g).to(TDT[dtype])
+    X = torch.randn(Bt, Kin, device=cuda, generator=g).to(TDT[dtype])
+    S = 8
+    ldp = (Kin + 1 + 7) // 8 * 8
+    part = torch.zeros(S, Nout, ldp, device=cuda)
+    K_.gemm(dtype, Nout, Kin + 1, Bt, dY.data_ptr(), Nout, True, X.data_ptr(), Kin, True, ones_col=Kin,
+            epi=K_.EPI_PARTIAL, Cf=part.data_ptr(), ldc=ldp, splitk=S, pstride=Nout * ldp, stream=_s())
+    torch.cuda.synchronize()
+    tot = part.sum(0)
+    refW = dY.float().t() @ X.float()
+    refb = dY.float().sum(0)
+    tol = 1e-4 if dtype == "fp32" else 2e-2
+    assert ((tot[:, :Kin] - refW).abs().max() / refW.abs().max()).item() < tol
+    assert ((tot[:, Kin] - refb).abs().max() / refb.abs().max()).item() < tol
+
+
+@pytest.mark.gpu
+def test_softmax_xent_kernel(cuda):
+    g = torch.Generator(device=cuda).manual_seed(3)
+    M, N = 1000, 10
+    logits = torch.randn(M, 16, device=cuda, generator=g) * 3
+    labels = torch.randint(0, N, (M,), device=cuda, generator=g).to(torch.uint8)
+    dl = torch.zeros(M, 16, device=cuda)
+    stats = torch.zeros(4, device=cuda)
+    pred = torch.zeros(M, dtype=torch.int32, device=cuda)
+    K_.softmax_xent("fp32", M, N, logits.data_ptr(), 16, labels.data_ptr(), dlogits=dl.data_ptr(), ldd=16,
+                    scale=0.5, stats=stats.data_ptr(), pred=pred.data_ptr(), stream=_s())
+    torch.cuda.synchronize()
+    lg = logits[:, :N]
+    p = torch.softmax(lg, 1)
+    y = torch.nn.functional.one_hot(labels.long(), N).float()
+    torch.testing.assert_close(dl[:, :N], (p - y) * 0.5, atol=1e-5, rtol=1e-4)
+    ce = torch.nn.functional.cross_entropy(lg, labels.long(), reduction="sum")
+    assert abs(stats[0].item() - ce.item()) < 1e-3 * ce.item()
+    assert abs(stats[1].item() - ((p - y) ** 2).mean(1).sum().item()) < 1e-3
+    assert int(stats[2].item()) == int((lg.argmax(1) == labels.long()).sum().item())
+    assert torch.equal(pred.long(), lg.argmax(1))
