@@ -46,6 +46,8 @@ struct GpuNet::Stage {
   int CLd = 0, nchunks_d = 0, kpad_d = 0;   // data-gradient (transposed) form
   bool cvec_d = true;
   int imgs_fwd = 1, imgs_dx = 1, imgs_dw = 1, ppad = 32, kbias = 0, ncols_pad = 16, cout_pad = 16;
+  int CLdw = 0;  // channel stride of the weight-gradient column layout
+  int nx_dw = 1;  // dW workgroup columns (each reduces a strided subset of image groups)
   // fc geometry
   int Kin = 0, Nout = 0, permC = 0, permHW = 0, ldp = 0;
   // large-image conv (explicit im2col + MFMA GEMM) when the image tile does
@@ -159,11 +161,25 @@ void GpuNet::build() {
       const int LHd = st.inH + st.KS - 1, LWd = st.inW + st.KS - 1;
       st.imgs_dx = std::max(1, std::min(16, 40960 / (LHd * LWd * st.CLd * (int)es)));
       st.cout_pad = r16(st.C);
-      st.kbias = st.cvec ? KK * st.CL : KK * st.inC;
-      st.ncols_pad = r16(st.kbias + 1);
-      const int dw_img_b = img_b + st.cout_pad * st.OH * st.OW * (int)es;
+      int dw_img_b;
+      if (dtype_ == DType::BF16) {
+        // transpose-read dW kernel: channels padded to 4, columns (tap, c4),
+        // bias gradient in its own column after the 16-aligned K columns
+        st.CLdw = (st.inC + 3) & ~3;
+        st.kbias = r16(KK * st.CLdw);
+        st.ncols_pad = st.kbias + 16;
+        dw_img_b = LH * LW * st.CLdw * (int)es + gpu::conv_dw_tr_drow(st.cout_pad) * st.OH * st.OW * (int)es;
+      } else {
+        st.CLdw = st.CL;
+        st.kbias = KK * st.CL;
+        st.ncols_pad = r16(st.kbias + 1);
+        dw_img_b = img_b + st.cout_pad * st.OH * st.OW * (int)es;
+      }
       st.imgs_dw = std::max(1, std::min(16, 65536 / dw_img_b));
       st.ppad = r32(st.imgs_dw * st.OH * st.OW);
+      // enough workgroups for ~4 per CU on 256 CUs (the dW kernel is latency
+      // bound on its staging loads); fewer when a batch has fewer groups
+      st.nx_dw = (int)std::min<int64_t>(ceil_div(max_batch_, st.imgs_dw), dtype_ == DType::BF16 ? 1024 : 512);
       // whole-image LDS kernels if one image fits comfortably; else im2col + GEMM
       const int64_t lds_cap = 120 * 1024;
       st.big = st.OH * st.OW > 4096 || st.cout_pad > 128 || (int64_t)img_b > lds_cap ||
@@ -272,9 +288,7 @@ void GpuNet::build() {
       const int sk = dw_splitk(st.C, KK * st.inC + 1, (int64_t)Bm * st.OH * st.OW);
       scratch = std::max(scratch, (size_t)sk * st.C * r8(KK * st.inC + 1) * 4);
     } else if (st.kind == Stage::CONV) {
-      const int64_t groups = ceil_div(Bm, st.imgs_dw);
-      const int64_t nx = std::min<int64_t>(groups, 512);
-      scratch = std::max(scratch, (size_t)nx * st.cout_pad * st.ncols_pad * 4);
+      scratch = std::max(scratch, (size_t)st.nx_dw * st.cout_pad * st.ncols_pad * 4);
     } else {
       scratch = std::max(scratch, (size_t)dw_splitk(st.Nout, st.Kin + 1, Bm) * st.Nout * st.ldp * 4);
     }
@@ -486,8 +500,8 @@ void GpuNet::backward(int hi, int lo, hipStream_t s) {
       // weight gradient
       gpu::ConvDwParams w;
       w.N = B; w.imgs = st.imgs_dw;
-      w.nx = (int)std::min<int64_t>(ceil_div(B, st.imgs_dw), 512);
-      w.Cin = st.inC; w.CL = st.CL; w.cvec = st.cvec;
+      w.nx = (int)std::min<int64_t>(ceil_div(B, st.imgs_dw), st.nx_dw);
+      w.Cin = st.inC; w.CL = st.CLdw; w.cvec = st.cvec;
       w.LH = (st.OH - 1) * st.stride + st.KS; w.LW = (st.OW - 1) * st.stride + st.KS;
       w.OH = st.OH; w.OW = st.OW; w.cs = st.stride; w.KS = st.KS; w.Cout = st.C;
       w.kbias = st.kbias; w.ncols_pad = st.ncols_pad; w.cout_pad = st.cout_pad; w.ppad = st.ppad;
@@ -500,7 +514,7 @@ void GpuNet::backward(int hi, int lo, hipStream_t s) {
       w.ablate = ablate_;
       gpu::conv_dw(dtype_, w, s);
       gpu::ConvDwReduceParams r;
-      r.nx = w.nx; r.Cout = st.C; r.Cin = st.inC; r.KS = st.KS; r.CG = st.CL / 8; r.cvec = st.cvec;
+      r.nx = w.nx; r.Cout = st.C; r.Cin = st.inC; r.KS = st.KS; r.CG = st.CLdw; r.cvec = st.cvec;
       r.cout_pad = st.cout_pad; r.ncols_pad = st.ncols_pad; r.kbias = st.kbias;
       r.slab = scratch_; r.gw = grads_ + st.w_off; r.gb = grads_ + st.b_off;
       gpu::conv_dw_reduce(r, s);

@@ -35,12 +35,28 @@ namespace {
 
 __device__ __forceinline__ int align16(int bytes) { return (bytes + 15) & ~15; }
 
-// Exact n / d for n < 2^24, d <= 2^16 via one 64-bit multiply-high:
+// Exact n / d for n < 2^24, d <= 2^16 via a multiply-high:
 // m = ceil(2^40 / d); the error term n*(m - 2^40/d)/2^40 < 2^-16 <= 1/d.
+// m = mh*2^32 + ml (mh <= 256), so n*m >> 40 = (n*mh + umulhi(n, ml)) >> 8
+// with every partial in 32 bits (3 VALU).  The constructor avoids a 64-bit
+// integer division (a ~100-instruction software routine): a double
+// reciprocal estimate, then an exact integer fix-up.  Construct divisors
+// once per kernel, outside stage loops.
 struct Div {
-  uint64_t m;
-  __device__ __forceinline__ explicit Div(int d) : m(((1ull << 40) + (uint64_t)d - 1) / (uint64_t)d) {}
-  __device__ __forceinline__ int div(int n) const { return (int)(((uint64_t)(uint32_t)n * m) >> 40); }
+  uint32_t mh, ml;
+  __device__ __forceinline__ explicit Div(int d) {
+    constexpr uint64_t P = 1ull << 40;
+    const uint64_t dd = (uint64_t)(d > 0 ? d : 1);
+    uint64_t q = (uint64_t)(1099511627776.0 / (double)dd);
+    while (q * dd < P) ++q;
+    while ((q - 1) * dd >= P) --q;
+    mh = (uint32_t)(q >> 32);
+    ml = (uint32_t)q;
+  }
+  __device__ __forceinline__ int div(int n) const {
+    const uint32_t u = (uint32_t)n;
+    return (int)((u * mh + __umulhi(u, ml)) >> 8);
+  }
 };
 
 // ---------------------------------------------------------------------------
@@ -53,6 +69,32 @@ struct Div {
 
 constexpr int U = 4;  // loads in flight per thread in the scatter passes
 
+__device__ __forceinline__ int chan_vw(int SC) { return (SC & 7) == 0 ? 8 : ((SC & 1) == 0 ? 2 : 1); }
+
+// The three divisors a scatter pass needs, built once per kernel (they depend
+// only on the source geometry, not on the stage's image range):
+//   dense / relu: (channel runs CV, SW, SH*SW)
+//   unpool:       (channel runs CV, PW, PH*PW)
+//   u8:           (SC, words per row, words per image) or, for rows that are
+//                 not whole words, (SC, row bytes, SH)
+__device__ __forceinline__ int plan_divisor(const StageSrc& s, int which) {
+  if (s.mode == IN_U8) {
+    const int rb = s.SW * s.SC;
+    if (which == 0) return s.SC;
+    if ((rb & 3) == 0) return which == 1 ? rb >> 2 : s.SH * (rb >> 2);
+    return which == 1 ? rb : s.SH;
+  }
+  if (which == 0) return s.SC / chan_vw(s.SC);
+  if (s.mode == IN_UNPOOL) return which == 1 ? s.PW : s.PH * s.PW;
+  return which == 1 ? s.SW : s.SH * s.SW;
+}
+
+struct ScatterPlan {
+  Div d0, d1, d2;
+  __device__ __forceinline__ explicit ScatterPlan(const StageSrc& s)
+      : d0(plan_divisor(s, 0)), d1(plan_divisor(s, 1)), d2(plan_divisor(s, 2)) {}
+};
+
 template <typename T>
 __device__ __forceinline__ void lds_zero(T* p, int n) {
   typedef typename Vec8<T>::type V8;
@@ -63,8 +105,6 @@ __device__ __forceinline__ void lds_zero(T* p, int n) {
 }
 
 __host__ __device__ __forceinline__ int round8(int n) { return (n + 7) & ~7; }
-
-__device__ __forceinline__ int chan_vw(int SC) { return (SC & 7) == 0 ? 8 : ((SC & 1) == 0 ? 2 : 1); }
 
 template <typename T, int VW>
 __device__ __forceinline__ void ld_run(const T* p, T (&v)[VW]) {
@@ -138,13 +178,13 @@ __device__ __forceinline__ int dst_index(int img, int ly, int lx, int c, int LH,
 }
 
 template <typename T, int VW, bool RELU, bool DY>
-__device__ void scatter_dense(const StageSrc& s, T* lds, int img0, int nimg, int LH, int LW, int CL) {
+__device__ void scatter_dense(const StageSrc& s, const ScatterPlan& pl, T* lds, int img0, int nimg, int LH, int LW, int CL) {
   const T* src = static_cast<const T*>(s.src);
   const T* ay = static_cast<const T*>(s.aux_y);
   const int CV = s.SC / VW;
   const int spix = s.SH * s.SW;
   const int total = nimg * spix * CV;
-  const Div dcv(CV), dsw(s.SW), dsp(spix);
+  const Div &dcv = pl.d0, &dsw = pl.d1, &dsp = pl.d2;
   for (int e0 = threadIdx.x; e0 < total; e0 += U * blockDim.x) {
     T v[U][VW], y[U][VW];
     int img[U], ly[U], lx[U], c0[U];
@@ -184,15 +224,18 @@ __device__ void scatter_dense(const StageSrc& s, T* lds, int img0, int nimg, int
 
 // Max-pool + ReLU backward folded into staging: one item per POOLED element
 // run; the gradient goes to the argmax position of its 2x2 window when the
-// pooled (= post-ReLU) output is positive.  Everything else stays zero.
-template <typename T, int VW, bool DY>
-__device__ void scatter_unpool(const StageSrc& s, T* lds, int img0, int nimg, int LH, int LW, int CL) {
+// pooled (= post-ReLU) output is positive.  Sparse form: only that position
+// is written (the tile was zero-filled).  DENSE form (channel-contiguous
+// tiles only): all four window positions are written as vector runs, so a
+// tile reused across stages needs no zero fill.
+template <typename T, int VW, bool DY, bool DENSE = false>
+__device__ void scatter_unpool(const StageSrc& s, const ScatterPlan& pl, T* lds, int img0, int nimg, int LH, int LW, int CL) {
   const T* src = static_cast<const T*>(s.src);
   const T* ay = static_cast<const T*>(s.aux_y);
   const int CV = s.SC / VW;
   const int ppix = s.PH * s.PW;
   const int total = nimg * ppix * CV;
-  const Div dcv(CV), dpw(s.PW), dpp(ppix);
+  const Div &dcv = pl.d0, &dpw = pl.d1, &dpp = pl.d2;
   for (int e0 = threadIdx.x; e0 < total; e0 += U * blockDim.x) {
     T d[U][VW], y[U][VW];
     uint32_t a[U][VW];
@@ -214,6 +257,22 @@ __device__ void scatter_unpool(const StageSrc& s, T* lds, int img0, int nimg, in
         px[u] = rem - py[u] * s.PW;
       }
     }
+    if constexpr (DENSE && !DY) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (py[u] < 0) continue;
+#pragma unroll
+        for (int pos = 0; pos < 4; ++pos) {
+          const int lx = tile_coord(2 * px[u] + (pos & 1), s, LW), ly = tile_coord(2 * py[u] + (pos >> 1), s, LH);
+          if (lx < 0 || ly < 0) continue;
+          T v[VW];
+#pragma unroll
+          for (int j = 0; j < VW; ++j) v[j] = (a[u][j] == (uint32_t)pos && to_f(y[u][j]) > 0.f) ? d[u][j] : T(0);
+          st_run<T, VW>(lds + dst_index<false>(img[u], ly, lx, c0[u], LH, LW, CL), v);
+        }
+      }
+      continue;
+    }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       if (py[u] < 0) continue;
@@ -232,16 +291,16 @@ __device__ void scatter_unpool(const StageSrc& s, T* lds, int img0, int nimg, in
 // u8 images (optionally gathered through idx), scaled by 1/255 (cnn.c:457).
 // Rows are moved as 32-bit words when a row is a whole number of words.
 template <typename T>
-__device__ void scatter_u8(const StageSrc& s, T* lds, int img0, int nimg, int LH, int LW, int CL) {
+__device__ void scatter_u8(const StageSrc& s, const ScatterPlan& pl, T* lds, int img0, int nimg, int LH, int LW, int CL) {
   const uint8_t* src = static_cast<const uint8_t*>(s.src);
   const int row_bytes = s.SW * s.SC;
   const float inv = 1.0f / 255.0f;
-  const Div dsc(s.SC);
+  const Div& dsc = pl.d0;
   if ((row_bytes & 3) == 0) {
     const int wpr = row_bytes >> 2;
     const int wpi = s.SH * wpr;
     const int total = nimg * wpi;
-    const Div dwpr(wpr), dwpi(wpi);
+    const Div &dwpr = pl.d1, &dwpi = pl.d2;
     for (int e0 = threadIdx.x; e0 < total; e0 += U * blockDim.x) {
       uint32_t w[U];
       int img[U], sy[U], wi[U];
@@ -277,7 +336,7 @@ __device__ void scatter_u8(const StageSrc& s, T* lds, int img0, int nimg, int LH
     }
   } else {
     const int total = nimg * s.SH * row_bytes;
-    const Div drb(row_bytes), dsh(s.SH);
+    const Div &drb = pl.d1, &dsh = pl.d2;
     for (int e = threadIdx.x; e < total; e += blockDim.x) {
       const int r = drb.div(e), b = e - r * row_bytes;
       const int im = dsh.div(r), y = r - im * s.SH;
@@ -293,27 +352,27 @@ __device__ void scatter_u8(const StageSrc& s, T* lds, int img0, int nimg, int LH
 
 // Scatter pass (after the zero fill + barrier) for an NHWC tile (DY=false) or
 // the transposed conv-output gradient (DY=true).
-template <typename T, bool DY>
-__device__ void stage_scatter(const StageSrc& s, T* lds, int img0, int nimg, int LH, int LW, int CL) {
+template <typename T, bool DY, bool DENSE = false>
+__device__ void stage_scatter(const StageSrc& s, const ScatterPlan& pl, T* lds, int img0, int nimg, int LH, int LW, int CL) {
   const int vw = chan_vw(s.SC);
   switch (s.mode) {
     case IN_U8:
-      if (!DY) scatter_u8<T>(s, lds, img0, nimg, LH, LW, CL);
+      if (!DY) scatter_u8<T>(s, pl, lds, img0, nimg, LH, LW, CL);
       break;
     case IN_UNPOOL:
-      if (vw == 8) scatter_unpool<T, 8, DY>(s, lds, img0, nimg, LH, LW, CL);
-      else if (vw == 2) scatter_unpool<T, 2, DY>(s, lds, img0, nimg, LH, LW, CL);
-      else scatter_unpool<T, 1, DY>(s, lds, img0, nimg, LH, LW, CL);
+      if (vw == 8) scatter_unpool<T, 8, DY, DENSE>(s, pl, lds, img0, nimg, LH, LW, CL);
+      else if (vw == 2) scatter_unpool<T, 2, DY, DENSE>(s, pl, lds, img0, nimg, LH, LW, CL);
+      else scatter_unpool<T, 1, DY, DENSE>(s, pl, lds, img0, nimg, LH, LW, CL);
       break;
     case IN_RELU:
-      if (vw == 8) scatter_dense<T, 8, true, DY>(s, lds, img0, nimg, LH, LW, CL);
-      else if (vw == 2) scatter_dense<T, 2, true, DY>(s, lds, img0, nimg, LH, LW, CL);
-      else scatter_dense<T, 1, true, DY>(s, lds, img0, nimg, LH, LW, CL);
+      if (vw == 8) scatter_dense<T, 8, true, DY>(s, pl, lds, img0, nimg, LH, LW, CL);
+      else if (vw == 2) scatter_dense<T, 2, true, DY>(s, pl, lds, img0, nimg, LH, LW, CL);
+      else scatter_dense<T, 1, true, DY>(s, pl, lds, img0, nimg, LH, LW, CL);
       break;
     default:
-      if (vw == 8) scatter_dense<T, 8, false, DY>(s, lds, img0, nimg, LH, LW, CL);
-      else if (vw == 2) scatter_dense<T, 2, false, DY>(s, lds, img0, nimg, LH, LW, CL);
-      else scatter_dense<T, 1, false, DY>(s, lds, img0, nimg, LH, LW, CL);
+      if (vw == 8) scatter_dense<T, 8, false, DY>(s, pl, lds, img0, nimg, LH, LW, CL);
+      else if (vw == 2) scatter_dense<T, 2, false, DY>(s, pl, lds, img0, nimg, LH, LW, CL);
+      else scatter_dense<T, 1, false, DY>(s, pl, lds, img0, nimg, LH, LW, CL);
   }
 }
 
@@ -395,7 +454,7 @@ __global__ void __launch_bounds__(256) conv_fwd_kernel(ConvParams p) {
   }
   pixel_table(ptab, rows_per_img, pool, p.OW, PW, p.cs, p.LW, p.CL);
   __syncthreads();
-  if (p.ablate != 1) stage_scatter<T, false>(p.in, xs, img0, nimg, p.LH, p.LW, p.CL);
+  if (p.ablate != 1) stage_scatter<T, false>(p.in, ScatterPlan(p.in), xs, img0, nimg, p.LH, p.LW, p.CL);
   __syncthreads();
 
   const int lane = tid & 63, wave = tid >> 6, nwaves = blockDim.x >> 6;
@@ -479,6 +538,161 @@ __global__ void __launch_bounds__(256) conv_fwd_kernel(ConvParams p) {
   }
 }
 
+typedef short v4s __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) v4s lds_v4s;
+
+// ds_read_b64_tr_b16 (cdna_hip_programming.md §5.5 T10): each 16-lane group
+// reads a 4-row x 16-column block of 16-bit elements; lane 4q+p supplies the
+// address of row q, columns 4p..4p+3 (rows may be anywhere in LDS), lane i
+// receives column i of the 4 rows.  One call = half an MFMA K-fragment.
+__device__ __forceinline__ bf16x4 tr4(const bf16* p) {
+  return __builtin_bit_cast(bf16x4, __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(const_cast<bf16*>(p))));
+}
+
+// Weight gradient of a conv_small layer, bf16.  Both MFMA operands are
+// pixel-major in LDS exactly as staged (no transposes):
+//   A = dY^T  from dys[pixel][co]              (row = co,      k = pixel)
+//   B = im2col from xs[img][y][x][c4]          (col = (tap,c), k = pixel)
+// and each K-fragment (8 pixels) is two transpose reads whose four "rows" are
+// four arbitrary pixels (their LDS bases come from a per-pixel table), so the
+// im2col gather costs 2 LDS instructions per 16x32 fragment.  The bias
+// gradient is the row sum of the A fragments.  Waves split the pixel chunks;
+// partial sums are combined in LDS in a fixed order (deterministic).
+template <int MTW, int NTW>
+__global__ void __launch_bounds__(256) conv_dw_tr_kernel(ConvDwParams p) {
+  typedef bf16 T;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int CL = p.CL;  // channel stride of xs (multiple of 4)
+  const int img_elems = p.LH * p.LW * CL;
+  const int xs_elems = round8(p.imgs * img_elems + 16);
+  const int drow = conv_dw_tr_drow(p.cout_pad);
+  T* xs = reinterpret_cast<T*>(smem);
+  T* dys = reinterpret_cast<T*>(smem + align16(xs_elems * 2));
+  int* pixbase = reinterpret_cast<int*>(reinterpret_cast<char*>(dys) + align16(p.ppad * drow * 2));
+  int* ptab = pixbase + p.ppad;
+  float* red = reinterpret_cast<float*>(smem);  // reused after the main loop
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6, nwaves = blockDim.x >> 6;
+  const int r16 = lane & 15, g = lane >> 4;
+  const int q = r16 >> 2, pp = r16 & 3;  // transpose-read address role
+  const int KK = p.KS * p.KS;
+  const int opix = p.OH * p.OW;
+
+  int koff[NTW];
+#pragma unroll
+  for (int t = 0; t < NTW; ++t) {
+    const int c4 = (blockIdx.y * NTW + t) * 16 + 4 * pp;  // first of this lane's 4 columns
+    const int kp = c4 / CL, c0 = c4 - kp * CL;
+    koff[t] = 0;
+    if (kp < KK) {
+      const int kh = kp / p.KS, kw = kp - kh * p.KS;
+      koff[t] = (kh * p.LW + kw) * CL + c0;
+    }
+  }
+  pixel_table(ptab, opix, false, p.OW, 1, p.cs, p.LW, CL);
+
+  f32x4 acc[MTW][NTW];
+  float bsum[MTW];
+#pragma unroll
+  for (int m = 0; m < MTW; ++m) {
+    bsum[m] = 0.f;
+#pragma unroll
+    for (int t = 0; t < NTW; ++t) acc[m][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+
+  const ScatterPlan plx(p.x), pldy(p.dy);
+  // Zero once: every stage rewrites the same interior positions (padding
+  // borders, pad channels and pad rows stay zero; UNPOOL staging is dense).
+  lds_zero(xs, xs_elems);
+  lds_zero(dys, p.ppad * drow);
+  __syncthreads();  // ptab
+  {
+    // stage-invariant pixel -> LDS base table; on a tail stage the rows past
+    // its last image read stale (finite) pixels against zeroed dY rows
+    const Div dopix(opix);
+    const int full = p.imgs * opix;
+    for (int pix = tid; pix < p.ppad; pix += blockDim.x) {
+      const int img = dopix.div(pix);
+      pixbase[pix] = pix < full ? img * img_elems + ptab[pix - img * opix] : 0;
+    }
+  }
+  for (int img0 = blockIdx.x * p.imgs; img0 < p.N; img0 += p.nx * p.imgs) {
+    const int nimg = min(p.imgs, p.N - img0);
+    const int npix = nimg * opix;
+    __syncthreads();  // previous stage fully consumed (and the zero fill done)
+    if (nimg < p.imgs) lds_zero(dys + npix * drow, (p.ppad - npix) * drow);  // stale rows of a tail stage
+    if (p.ablate != 1) {
+      stage_scatter<T, false>(p.x, plx, xs, img0, nimg, p.LH, p.LW, CL);
+      stage_scatter<T, false, true>(p.dy, pldy, dys, img0, nimg, p.OH, p.OW, drow);
+    }
+    __syncthreads();
+    const int nq = cdiv(npix, 32);
+    for (int qc = wave; qc < (p.ablate == 2 ? 0 : nq); qc += nwaves) {
+      // fragment k -> pixel: lane group g reads rows 4g..4g+3 (and +16), so
+      // the four groups of a read cover 16 consecutive 32-byte rows
+      const int pix1 = qc * 32 + 4 * g + q, pix2 = pix1 + 16;
+      const int pb1 = pixbase[pix1], pb2 = pixbase[pix2];
+      bf16x8 a[MTW];
+#pragma unroll
+      for (int m = 0; m < MTW; ++m) {
+        const bf16x4 lo = tr4(dys + pix1 * drow + m * 16 + 4 * pp);
+        const bf16x4 hi = tr4(dys + pix2 * drow + m * 16 + 4 * pp);
+        a[m] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) bsum[m] += (float)a[m][j];
+      }
+#pragma unroll
+      for (int t = 0; t < NTW; ++t) {
+        const bf16x4 lo = tr4(xs + pb1 + koff[t]);
+        const bf16x4 hi = tr4(xs + pb2 + koff[t]);
+        const bf16x8 b = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+#pragma unroll
+        for (int m = 0; m < MTW; ++m) acc[m][t] = mma(acc[m][t], a[m], b);
+      }
+    }
+  }
+  // bias: lanes r16 hold channel m*16+r16; sum the 4 lane groups
+#pragma unroll
+  for (int m = 0; m < MTW; ++m) {
+    bsum[m] += __shfl_xor(bsum[m], 16);
+    bsum[m] += __shfl_xor(bsum[m], 32);
+  }
+  // Combine the waves in a fixed order: red[MTW*16 rows][NTW*16 + 1 cols].
+  const int rcols = NTW * 16 + 1;
+  for (int w = 0; w < nwaves; ++w) {
+    __syncthreads();
+    if (wave == w) {
+#pragma unroll
+      for (int m = 0; m < MTW; ++m) {
+#pragma unroll
+        for (int t = 0; t < NTW; ++t)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            float* d = red + (m * 16 + 4 * g + i) * rcols + t * 16 + r16;
+            *d = (w == 0 ? 0.f : *d) + acc[m][t][i];
+          }
+        if (g == 0) {
+          float* d = red + (m * 16 + r16) * rcols + NTW * 16;
+          *d = (w == 0 ? 0.f : *d) + bsum[m];
+        }
+      }
+    }
+  }
+  __syncthreads();
+  for (int e = tid; e < p.cout_pad * rcols; e += blockDim.x) {
+    const int row = e / rcols, c = e - row * rcols;
+    float* srow = p.slab + ((size_t)blockIdx.x * p.cout_pad + row) * p.ncols_pad;
+    if (c < NTW * 16) {
+      const int col = blockIdx.y * NTW * 16 + c;
+      if (col < p.kbias) srow[col] = red[row * rcols + c];
+    } else if (blockIdx.y == 0) {
+      srow[p.kbias] = red[row * rcols + c];
+    }
+  }
+}
+
+// fp32 / fallback weight gradient (scalar im2col gathers, transposed dY).
 template <typename T, bool CVEC, int MTW, int NTW>
 __global__ void __launch_bounds__(256) conv_dw_kernel(ConvDwParams p) {
   typedef typename Vec8<T>::type V8;
@@ -533,6 +747,7 @@ __global__ void __launch_bounds__(256) conv_dw_kernel(ConvDwParams p) {
     for (int t = 0; t < NTW; ++t) acc[m][t] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const Div dopix(opix);
+  const ScatterPlan plx(p.x), pldy(p.dy);
   const T one = T(1);
   for (int img0 = blockIdx.x * p.imgs; img0 < p.N; img0 += p.nx * p.imgs) {
     const int nimg = min(p.imgs, p.N - img0);
@@ -542,8 +757,8 @@ __global__ void __launch_bounds__(256) conv_dw_kernel(ConvDwParams p) {
     lds_zero(dys, p.cout_pad * drow);
     __syncthreads();
     if (p.ablate != 1) {
-      stage_scatter<T, false>(p.x, xs, img0, nimg, p.LH, p.LW, p.CL);
-      stage_scatter<T, true>(p.dy, dys, img0, nimg, p.OH, p.OW, drow);
+      stage_scatter<T, false>(p.x, plx, xs, img0, nimg, p.LH, p.LW, p.CL);
+      stage_scatter<T, true>(p.dy, pldy, dys, img0, nimg, p.OH, p.OW, drow);
     }
     for (int pix = tid; pix < p.ppad; pix += blockDim.x) {
       const int img = dopix.div(pix);
@@ -609,7 +824,7 @@ __global__ void __launch_bounds__(256) conv_dw_reduce_kernel(ConvDwReduceParams 
       row = j / (p.Cin * KK);
       const int rem = j - row * p.Cin * KK;
       const int i = rem / KK, kp = rem - i * KK;
-      col = p.cvec ? (kp * p.CG + (i >> 3)) * 8 + (i & 7) : kp * p.Cin + i;
+      col = kp * p.CG + i;  // CG = channel stride of the dW column layout
     } else {
       row = j - nW;
       col = p.kbias;
@@ -693,6 +908,36 @@ void launch_conv_dw_c(const ConvDwParams& p, hipStream_t s, size_t lds) {
   else MCC_CHECK(false, "conv_dw: Cout > 128 not supported by conv_small");
 }
 
+int dw_tr_ntw(int mtw, int ncol_tiles) {
+  if (mtw <= 1) return ncol_tiles <= 2 ? 2 : (ncol_tiles <= 4 ? 4 : (ncol_tiles <= 8 ? 8 : 16));
+  return mtw <= 2 ? 8 : (mtw <= 4 ? 4 : 2);
+}
+
+size_t conv_dw_tr_lds(const ConvDwParams& p) {
+  const size_t stage = a16((size_t)round8(p.imgs * p.LH * p.LW * p.CL + 16) * 2) +
+                       a16((size_t)p.ppad * conv_dw_tr_drow(p.cout_pad) * 2) + (size_t)p.ppad * 4 +
+                       (size_t)p.OH * p.OW * 4;
+  const size_t red = (size_t)p.cout_pad * (dw_tr_ntw(p.cout_pad / 16, p.kbias / 16) * 16 + 1) * 4;
+  return stage > red ? stage : red;
+}
+
+void launch_conv_dw_tr(const ConvDwParams& p, hipStream_t s, size_t lds) {
+  const int mtw = p.cout_pad / 16;
+  const int ncol_tiles = p.kbias / 16;
+  const int ntw = dw_tr_ntw(mtw, ncol_tiles);
+  const dim3 grid((unsigned)p.nx, (unsigned)cdiv(ncol_tiles, ntw)), block(256);
+  auto go = [&](auto kern) { hipLaunchKernelGGL(kern, grid, block, lds, s, p); };
+  if (mtw <= 1) {
+    if (ntw == 2) go(conv_dw_tr_kernel<1, 2>);
+    else if (ntw == 4) go(conv_dw_tr_kernel<1, 4>);
+    else if (ntw == 8) go(conv_dw_tr_kernel<1, 8>);
+    else go(conv_dw_tr_kernel<1, 16>);
+  } else if (mtw <= 2) go(conv_dw_tr_kernel<2, 8>);
+  else if (mtw <= 4) go(conv_dw_tr_kernel<4, 4>);
+  else if (mtw <= 8) go(conv_dw_tr_kernel<8, 2>);
+  else MCC_CHECK(false, "conv_dw: Cout > 128 not supported by conv_small");
+}
+
 }  // namespace
 
 size_t conv_forward_lds_bytes(DType t, const ConvParams& p) {
@@ -705,7 +950,8 @@ size_t conv_forward_lds_bytes(DType t, const ConvParams& p) {
 }
 
 size_t conv_dw_lds_bytes(DType t, const ConvDwParams& p) {
-  const size_t es = t == DType::BF16 ? 2 : 4;
+  if (t == DType::BF16) return conv_dw_tr_lds(p);
+  const size_t es = 4;
   const size_t stage = a16((size_t)round8(p.imgs * p.LH * p.LW * p.CL + 16) * es) +
                        a16((size_t)p.cout_pad * (p.ppad + 8) * es) + (size_t)p.ppad * 4 + (size_t)p.OH * p.OW * 4;
   const int mtw = p.cout_pad / 16;
@@ -733,8 +979,8 @@ void conv_dw(DType t, const ConvDwParams& p, hipStream_t s) {
   const size_t lds = conv_dw_lds_bytes(t, p);
   MCC_CHECK(lds <= 160 * 1024, "conv_dw: LDS tile exceeds 160 KiB");
   if (t == DType::BF16) {
-    if (p.cvec) launch_conv_dw_c<bf16, true>(p, s, lds);
-    else launch_conv_dw_c<bf16, false>(p, s, lds);
+    MCC_CHECK(p.CL % 4 == 0 && p.kbias % 16 == 0, "conv_dw(bf16): needs the c4 column layout");
+    launch_conv_dw_tr(p, s, lds);
   } else {
     if (p.cvec) launch_conv_dw_c<float, true>(p, s, lds);
     else launch_conv_dw_c<float, false>(p, s, lds);

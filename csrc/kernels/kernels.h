@@ -87,6 +87,11 @@ struct ConvDwParams {
   int ablate = 0;         // diagnostics: 1 = skip staging scatter, 2 = skip MFMA loop
 };
 
+// Row stride (elements) of the pixel-major dY tile of the bf16 transpose-read
+// dW kernel.  32-byte rows are conflict-free for its 4-rows-per-lane-group
+// reads; wider rows get 16 B of skew.
+constexpr int conv_dw_tr_drow(int cout_pad) { return cout_pad == 16 ? 16 : cout_pad + 8; }
+
 // Sum the dW slabs over x and scatter into the canonical fp32 gradient.
 struct ConvDwReduceParams {
   int nx = 0, Cout = 0, Cin = 0, KS = 1, CG = 1;
