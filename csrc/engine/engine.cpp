@@ -56,6 +56,11 @@ struct GpuNet::Stage {
   int kgem = 0, kgem_d = 0;      // im2col row strides (fwd/dW, data grad)
   void* conv_buf = nullptr;      // pre-pool conv output (big + pooled)
   void* dz_buf = nullptr;        // pre-activation gradient at conv-output size (big)
+  // persistent pipelined kernels (bf16 small-image layers; geometry planned
+  // for max_batch, pointers and batch filled per call)
+  bool pipe_fwd = false, pipe_dx = false, pipe_dw = false;
+  gpu::ConvPipeParams pf, pdx;
+  gpu::ConvDwPipeParams pdw;
 };
 
 static inline int r8(int x) { return (x + 7) & ~7; }
@@ -82,6 +87,7 @@ GpuNet::GpuNet(const ModelSpec& spec, DType dtype, int max_batch, int device)
   MCC_CHECK(dtype == DType::BF16 || dtype == DType::F32, "GpuNet: dtype must be bf16 or fp32");
   MCC_CHECK(max_batch > 0, "GpuNet: max_batch > 0");
   if (const char* a = std::getenv("MCC_ABLATE")) ablate_ = std::atoi(a);  // kernel diagnostics only
+  if (const char* a = std::getenv("MCC_NO_PIPE")) no_pipe_ = std::atoi(a) != 0;  // A/B against conv_small
   if (device_ >= 0) HIP_OK(hipSetDevice(device_));
   else HIP_OK(hipGetDevice(&device_));
   build();
@@ -97,6 +103,43 @@ void* GpuNet::arena_alloc(size_t bytes) {
   const size_t a = (arena_used_ + 255) & ~size_t(255);
   arena_used_ = a + bytes;
   return arena_ ? arena_ + a : reinterpret_cast<void*>(a + 1);  // sizing pass returns dummies
+}
+
+// Plan the persistent pipelined kernels for a small-image bf16 conv stage.
+// Each direction falls back to conv_small when the planner declines it.
+void GpuNet::plan_pipe(Stage& st, bool first) {
+  const int dy_mode = st.pooled ? gpu::PM_UNPOOL : (st.act == gpu::ACT_RELU ? gpu::PM_RELU : gpu::PM_PLAIN);
+  const int dyH = st.pooled ? st.outH : st.OH, dyW = st.pooled ? st.outW : st.OW;
+  const bool x_ok = first ? st.inC == 1 : true;
+  const int x_mode = first ? gpu::PM_U8S1 : gpu::PM_PLAIN;
+  if (x_ok && (st.inC == 1 || st.cvec)) {
+    gpu::ConvPipeParams& p = st.pf;
+    p.N = max_batch_; p.Cin = st.inC; p.OH = st.OH; p.OW = st.OW; p.cs = st.stride; p.KS = st.KS; p.Cout = st.C;
+    p.epi = st.pooled ? 0 : 1; p.act = st.act;
+    p.in.mode = x_mode; p.in.SH = st.inH; p.in.SW = st.inW; p.in.SC = st.inC;
+    p.in.up = 1; p.in.offy = st.pad; p.in.offx = st.pad;
+    st.pipe_fwd = gpu::conv_pipe_plan(p);
+    // the C8 layout is conv_small's cvec packing; S1 has its own (see pack table)
+    if (st.pipe_fwd && p.layout == gpu::XL_C8)
+      st.pipe_fwd = st.cvec && st.CL == ((st.inC + 7) & ~7) && st.nchunks == p.nchunks;
+  }
+  if (!first && st.cvec_d) {
+    gpu::ConvPipeParams& p = st.pdx;
+    p.N = max_batch_; p.Cin = st.C; p.OH = st.inH; p.OW = st.inW; p.cs = 1; p.KS = st.KS; p.Cout = st.inC;
+    p.epi = 2; p.act = gpu::ACT_NONE;
+    p.in.mode = dy_mode; p.in.SH = dyH; p.in.SW = dyW; p.in.SC = st.C;
+    p.in.up = st.stride; p.in.offy = st.KS - 1 - st.pad; p.in.offx = st.KS - 1 - st.pad;
+    st.pipe_dx = gpu::conv_pipe_plan(p) && p.layout == gpu::XL_C8 && st.CLd == ((st.C + 7) & ~7) &&
+                 st.nchunks_d == p.nchunks;
+  }
+  if (x_ok) {
+    gpu::ConvDwPipeParams& p = st.pdw;
+    p.N = max_batch_; p.Cin = st.inC; p.OH = st.OH; p.OW = st.OW; p.cs = st.stride; p.KS = st.KS; p.Cout = st.C;
+    p.x.mode = x_mode; p.x.SH = st.inH; p.x.SW = st.inW; p.x.SC = st.inC;
+    p.x.up = 1; p.x.offy = st.pad; p.x.offx = st.pad;
+    p.dy.mode = dy_mode; p.dy.SH = dyH; p.dy.SW = dyW; p.dy.SC = st.C;
+    st.pipe_dw = gpu::conv_dw_pipe_plan(p);
+  }
 }
 
 void GpuNet::build() {
@@ -187,6 +230,7 @@ void GpuNet::build() {
       st.kgem = r8(KK * st.inC);
       st.kgem_d = r8(KK * st.C);
       if (st.big) MCC_CHECK(st.C % 8 == 0, "im2col conv path needs Cout % 8 == 0");
+      if (!st.big && dtype_ == DType::BF16 && !no_pipe_) plan_pipe(st, s == 0);
     } else {
       st.out_elems = st.Nout;
       st.out_ld = r8(st.Nout);
@@ -227,6 +271,17 @@ void GpuNet::build() {
               idx[st.pk_dx + (int64_t)ci * st.kgem_d + kp * st.C + co] =
                   (int32_t)(st.w_off + ((int64_t)co * st.inC + ci) * KK + (KK - 1 - kp));
       }
+    } else if (st.kind == Stage::CONV && st.pipe_fwd && st.pf.layout == gpu::XL_S1) {
+      // single-channel pipelined forward: [r16(C)][kpad], k = kh*8 + kw (kw < KS)
+      // (pair: columns 8 + n hold the right pixel of a pair, taps shifted by one)
+      st.pk_fwd = reserve((int64_t)r16(st.C) * st.pf.kpad);
+      for (int n = 0; n < st.C; ++n)
+        for (int kh = 0; kh < st.KS; ++kh)
+          for (int kw = 0; kw < st.KS; ++kw) {
+            const int32_t src = (int32_t)(st.w_off + ((int64_t)n * st.KS + kh) * st.KS + kw);
+            idx[st.pk_fwd + (int64_t)n * st.pf.kpad + kh * 8 + kw] = src;
+            if (st.pf.pair) idx[st.pk_fwd + (int64_t)(8 + n) * st.pf.kpad + kh * 8 + kw + 1] = src;
+          }
     } else if (st.kind == Stage::CONV) {
       const int KK = st.KS * st.KS;
       // forward: [r16(C)][kpad], k = (kp, cgroup, c8) or (kp, c)
@@ -289,6 +344,10 @@ void GpuNet::build() {
       scratch = std::max(scratch, (size_t)sk * st.C * r8(KK * st.inC + 1) * 4);
     } else if (st.kind == Stage::CONV) {
       scratch = std::max(scratch, (size_t)st.nx_dw * st.cout_pad * st.ncols_pad * 4);
+      if (st.pipe_dw) {
+        const size_t nv = (size_t)st.pdw.cout_pad * st.pdw.ncols_pad;
+        scratch = std::max(scratch, (st.pdw.grid + ceil_div(st.pdw.grid, 16)) * nv * 4);
+      }
     } else {
       scratch = std::max(scratch, (size_t)dw_splitk(st.Nout, st.Kin + 1, Bm) * st.Nout * st.ldp * 4);
     }
@@ -337,7 +396,15 @@ std::string GpuNet::plan() const {
          << st.OW << (st.pooled ? " +maxpool" : "") << " k" << st.KS << "s" << st.stride << "p" << st.pad
          << (st.big ? " im2col+gemm" : (st.cvec ? " lds-cvec" : " lds-scalar")) << " chunks=" << st.nchunks
          << " imgs=" << st.imgs_fwd << "/"
-         << st.imgs_dx << "/" << st.imgs_dw << "\n";
+         << st.imgs_dx << "/" << st.imgs_dw;
+      if (st.pipe_fwd || st.pipe_dx || st.pipe_dw) {
+        os << " pipe[";
+        if (st.pipe_fwd) os << "fwd:" << (st.pf.layout == gpu::XL_S1 ? (st.pf.pair ? "s1p" : "s1") : "c8") << "x" << st.pf.imgs << "/g" << st.pf.grid << " ";
+        if (st.pipe_dx) os << "dx:x" << st.pdx.imgs << "/g" << st.pdx.grid << " ";
+        if (st.pipe_dw) os << "dw:x" << st.pdw.imgs << "/g" << st.pdw.grid;
+        os << "]";
+      }
+      os << "\n";
     } else {
       os << "  [" << s << "] fc " << st.Kin << " -> " << st.Nout << (st.last ? " (logits)" : "")
          << (st.permC ? " nhwc-flatten" : "") << "\n";
@@ -393,6 +460,15 @@ void GpuNet::forward(const uint8_t* images, const int32_t* idx, int B, hipStream
       g.C = st.pooled ? st.conv_buf : st.act_buf; g.ldc = st.C;
       gpu::gemm(dtype_, g, s);
       if (st.pooled) gpu::maxpool2(dtype_, st.conv_buf, st.act_buf, st.arg_buf, B, st.OH, st.OW, st.C, s);
+    } else if (st.kind == Stage::CONV && st.pipe_fwd) {
+      gpu::ConvPipeParams p = st.pf;
+      p.N = B;
+      if (si == 0) { p.in.src = images; p.in.idx = idx; }
+      else p.in.src = stages_[si - 1]->act_buf;
+      p.wpk = static_cast<const char*>(packed_) + es * st.pk_fwd;
+      p.bias = params_ + st.b_off;
+      p.out = st.act_buf; p.out_arg = st.arg_buf;
+      gpu::conv_pipe_forward(p, s);
     } else if (st.kind == Stage::CONV) {
       gpu::ConvParams p;
       p.N = B; p.imgs = st.imgs_fwd;
@@ -497,7 +573,27 @@ void GpuNet::backward(int hi, int lo, hipStream_t s) {
         }
         continue;
       }
+      if (st.pipe_dw) {
+        gpu::ConvDwPipeParams w = st.pdw;
+        w.N = B;
+        if (si == 0) { w.x.src = images_; w.x.idx = idx_; }
+        else w.x.src = stages_[si - 1]->act_buf;
+        w.dy.src = st.grad_buf; w.dy.aux_y = st.act_buf; w.dy.aux_arg = st.arg_buf;
+        w.slab = scratch_;
+        gpu::conv_dw_pipe(w, s);
+        gpu::conv_dw_pipe_reduce(w, grads_ + st.w_off, grads_ + st.b_off, s);
+      }
+      if (st.pipe_dx && si > 0) {
+        gpu::ConvPipeParams p = st.pdx;
+        p.N = B;
+        p.in.src = st.grad_buf; p.in.aux_y = st.act_buf; p.in.aux_arg = st.arg_buf;
+        p.wpk = static_cast<const char*>(packed_) + es * st.pk_dx;
+        p.out = stages_[si - 1]->grad_buf;
+        gpu::conv_pipe_forward(p, s);
+      }
+      if (st.pipe_dw && (st.pipe_dx || si == 0)) continue;
       // weight gradient
+      if (!st.pipe_dw) {
       gpu::ConvDwParams w;
       w.N = B; w.imgs = st.imgs_dw;
       w.nx = (int)std::min<int64_t>(ceil_div(B, st.imgs_dw), st.nx_dw);
@@ -518,8 +614,9 @@ void GpuNet::backward(int hi, int lo, hipStream_t s) {
       r.cout_pad = st.cout_pad; r.ncols_pad = st.ncols_pad; r.kbias = st.kbias;
       r.slab = scratch_; r.gw = grads_ + st.w_off; r.gb = grads_ + st.b_off;
       gpu::conv_dw_reduce(r, s);
+      }
       // data gradient into the previous stage's output gradient
-      if (si > 0) {
+      if (si > 0 && !st.pipe_dx) {
         gpu::ConvParams p;
         p.N = B; p.imgs = st.imgs_dx;
         p.Cin = st.C; p.CL = st.CLd; p.cvec = st.cvec_d;

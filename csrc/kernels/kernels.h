@@ -103,6 +103,94 @@ struct ConvDwReduceParams {
   float beta = 0.f;     // grad = beta*grad + sum (0 overwrites)
 };
 
+// ---------------------------------------------------------------------------
+// Persistent, pipelined small-image convolution ("conv_pipe", bf16).
+//
+// A workgroup keeps its weights, index tables and zeroed LDS tiles for the
+// whole launch and walks image groups blockIdx.x, +gridDim.x, ...; while it
+// computes group g the global loads of group g+1 are already in flight
+// (register prefetch, written to LDS after the next barrier).  Per-thread
+// staging geometry is computed once, so the per-group staging is a few loads
+// and 16-byte LDS writes per item.  Outputs go through an LDS tile and leave
+// as coalesced 16-byte stores.
+enum PipeMode : int {
+  PM_U8S1 = 0,    // u8 single-channel images -> four shifted bf16 copies (see below)
+  PM_PLAIN = 1,   // bf16 NHWC
+  PM_RELU = 2,    // bf16 NHWC masked by (aux_y > 0)
+  PM_UNPOOL = 3,  // pooled bf16 NHWC routed to the argmax of its 2x2 window, masked by (aux_y > 0)
+};
+enum PipeLayout : int {
+  // Cin == 1: copy c (c = 0..3) holds tile[j + c] at j, so any 4 consecutive
+  // tile elements are one aligned 8-byte read from copy (e & 3).  K runs over
+  // (kernel row, 8 taps), two 8-byte reads per 8-wide K fragment.
+  XL_S1 = 0,
+  XL_C8 = 1,  // NHWC, channels padded to a multiple of 8: one 16-byte read per fragment
+};
+
+struct PipeSrc {
+  int mode = PM_PLAIN;
+  const void* src = nullptr;
+  const int32_t* idx = nullptr;      // PM_U8S1: optional per-image dataset index
+  const void* aux_y = nullptr;       // PM_RELU / PM_UNPOOL
+  const uint8_t* aux_arg = nullptr;  // PM_UNPOOL
+  int SH = 0, SW = 0, SC = 0;        // source grid (PM_UNPOOL: the pooled grid)
+  int up = 1, offy = 0, offx = 0;    // tile coordinate = (conv-grid coordinate) * up + off
+  // filled by the planners
+  int RW = 0;       // channels per staged item (PM_U8S1: 4 pixels)
+  int per_img = 0;  // items per image
+  int LWp = 0;      // destination tile row stride (pixels)
+  int CL = 0;       // destination channel stride (elements)
+  int IMG = 0;      // destination elements per image
+  int CS = 0;       // XL_S1: elements between the shifted copies
+};
+
+// Forward conv (bias + act [+ 2x2 max-pool]) or data gradient (plain).
+struct ConvPipeParams {
+  int N = 0;
+  int Cin = 0, OH = 0, OW = 0, cs = 1, KS = 1, Cout = 0;
+  int ty0 = 0, tx0 = 0;  // tile coordinate of output pixel (0,0)'s first tap
+  int epi = 0;           // 0 = pool, 1 = bias+act, 2 = plain (see FwdEpi)
+  int act = ACT_RELU;
+  PipeSrc in;
+  const void* wpk = nullptr;  // packed bf16 weights [round_up(Cout,16)][kpad]
+  const float* bias = nullptr;
+  void* out = nullptr;
+  uint8_t* out_arg = nullptr;
+  // planner outputs
+  int layout = XL_C8, imgs = 1, ngroups = 0, grid = 0, LH = 0;
+  int nchunks = 0, kpad = 0;
+  // XL_S1 with Cout <= 8: an MFMA row is a horizontal PAIR of output pixels;
+  // columns 0..7 are the left pixel's channels, 8..15 the right one's (its
+  // taps shifted by one inside the 8-wide K window).  Packed weights:
+  // [16][kpad], col n < 8: k = kh*8 + kw; col 8 + n: k = kh*8 + kw + 1.
+  int pair = 0;
+  size_t lds = 0;
+};
+// Geometry for a layer (N may be the maximum batch); false when the layer is
+// outside what the pipelined kernels cover (the caller keeps conv_small).
+bool conv_pipe_plan(ConvPipeParams& p);
+void conv_pipe_forward(const ConvPipeParams& p, hipStream_t s);
+
+// Weight gradient: slab[x][co][col], x = workgroup (grid), col < kbias the
+// packed columns (XL_S1: kh*8 + kw; XL_C8: (kh*KS + kw)*CL + c), col ==
+// kbias the bias gradient.
+struct ConvDwPipeParams {
+  int N = 0;
+  int Cin = 0, OH = 0, OW = 0, cs = 1, KS = 1, Cout = 0;
+  int ty0 = 0, tx0 = 0;
+  PipeSrc x;   // layer input (tile with halo)
+  PipeSrc dy;  // output gradient at the conv grid, pixel-major [pix][drow]
+  float* slab = nullptr;
+  // planner outputs
+  int layout = XL_C8, imgs = 1, ngroups = 0, grid = 0, LH = 0;
+  int cout_pad = 0, drow = 0, kbias = 0, ncols_pad = 0, ppad = 0;
+  size_t lds = 0;
+};
+bool conv_dw_pipe_plan(ConvDwPipeParams& p);
+void conv_dw_pipe(const ConvDwPipeParams& p, hipStream_t s);
+// Reduce the slabs of conv_dw_pipe into the canonical fp32 gradient.
+void conv_dw_pipe_reduce(const ConvDwPipeParams& p, float* gw, float* gb, hipStream_t s);
+
 enum GemmEpi : int {
   EPI_BIAS_ACT = 0,  // C = act(acc + bias[n])  (T)
   EPI_LOGITS = 1,    // Cf = acc + bias[n]      (fp32)

@@ -68,5 +68,43 @@ __device__ __forceinline__ float act_grad_y(int act, float y) {
 
 __host__ __device__ __forceinline__ int cdiv(int a, int b) { return (a + b - 1) / b; }
 
+__host__ __device__ __forceinline__ int align16(int bytes) { return (bytes + 15) & ~15; }
+
+// Exact n / d for n < 2^24, d <= 2^16 via a multiply-high:
+// m = ceil(2^40 / d); the error term n*(m - 2^40/d)/2^40 < 2^-16 <= 1/d.
+// m = mh*2^32 + ml (mh <= 256), so n*m >> 40 = (n*mh + umulhi(n, ml)) >> 8
+// with every partial in 32 bits (3 VALU).  The constructor avoids a 64-bit
+// integer division (a ~100-instruction software routine): a double
+// reciprocal estimate, then an exact integer fix-up.  Construct divisors
+// once per kernel, outside stage loops.
+struct Div {
+  uint32_t mh, ml;
+  __device__ __forceinline__ explicit Div(int d) {
+    constexpr uint64_t P = 1ull << 40;
+    const uint64_t dd = (uint64_t)(d > 0 ? d : 1);
+    uint64_t q = (uint64_t)(1099511627776.0 / (double)dd);
+    while (q * dd < P) ++q;
+    while ((q - 1) * dd >= P) --q;
+    mh = (uint32_t)(q >> 32);
+    ml = (uint32_t)q;
+  }
+  __device__ __forceinline__ int div(int n) const {
+    const uint32_t u = (uint32_t)n;
+    return (int)((u * mh + __umulhi(u, ml)) >> 8);
+  }
+};
+
+typedef short v4s __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) v4s lds_v4s;
+
+// ds_read_b64_tr_b16 (cdna_hip_programming.md §5.5 T10): each 16-lane group
+// reads a 4-row x 16-column block of 16-bit elements; lane 4q+p supplies the
+// address of row q, columns 4p..4p+3 (rows may be anywhere in LDS), lane i
+// receives column i of the 4 rows.  One call = half an MFMA K-fragment.
+__device__ __forceinline__ bf16x4 tr4(const bf16* p) {
+  return __builtin_bit_cast(bf16x4, __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(const_cast<bf16*>(p))));
+}
+
+
 }  // namespace gpu
 }  // namespace mcc
