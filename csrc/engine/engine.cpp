@@ -462,7 +462,7 @@ void GpuNet::forward(const uint8_t* images, const int32_t* idx, int B, hipStream
       if (st.pooled) gpu::maxpool2(dtype_, st.conv_buf, st.act_buf, st.arg_buf, B, st.OH, st.OW, st.C, s);
     } else if (st.kind == Stage::CONV && st.pipe_fwd) {
       gpu::ConvPipeParams p = st.pf;
-      p.N = B;
+      p.N = B; p.ablate = ablate_;
       if (si == 0) { p.in.src = images; p.in.idx = idx; }
       else p.in.src = stages_[si - 1]->act_buf;
       p.wpk = static_cast<const char*>(packed_) + es * st.pk_fwd;
@@ -575,7 +575,7 @@ void GpuNet::backward(int hi, int lo, hipStream_t s) {
       }
       if (st.pipe_dw) {
         gpu::ConvDwPipeParams w = st.pdw;
-        w.N = B;
+        w.N = B; w.ablate = ablate_;
         if (si == 0) { w.x.src = images_; w.x.idx = idx_; }
         else w.x.src = stages_[si - 1]->act_buf;
         w.dy.src = st.grad_buf; w.dy.aux_y = st.act_buf; w.dy.aux_arg = st.arg_buf;
@@ -585,7 +585,7 @@ void GpuNet::backward(int hi, int lo, hipStream_t s) {
       }
       if (st.pipe_dx && si > 0) {
         gpu::ConvPipeParams p = st.pdx;
-        p.N = B;
+        p.N = B; p.ablate = ablate_;
         p.in.src = st.grad_buf; p.in.aux_y = st.act_buf; p.in.aux_arg = st.arg_buf;
         p.wpk = static_cast<const char*>(packed_) + es * st.pk_dx;
         p.out = stages_[si - 1]->grad_buf;

@@ -165,6 +165,8 @@ struct ConvPipeParams {
   // [16][kpad], col n < 8: k = kh*8 + kw; col 8 + n: k = kh*8 + kw + 1.
   int pair = 0;
   size_t lds = 0;
+  uint32_t rows_mh = 0, rows_ml = 0;  // division magic for the GEMM rows per image (set at launch)
+  int ablate = 0;  // diagnostics (MCC_ABLATE bits): 1 no staging, 2 no MFMA loop, 4 no epilogue/copy-out
 };
 // Geometry for a layer (N may be the maximum batch); false when the layer is
 // outside what the pipelined kernels cover (the caller keeps conv_small).
@@ -185,6 +187,7 @@ struct ConvDwPipeParams {
   int layout = XL_C8, imgs = 1, ngroups = 0, grid = 0, LH = 0;
   int cout_pad = 0, drow = 0, kbias = 0, ncols_pad = 0, ppad = 0;
   size_t lds = 0;
+  int ablate = 0;  // diagnostics: 1 no staging, 2 no MFMA loop
 };
 bool conv_dw_pipe_plan(ConvDwPipeParams& p);
 void conv_dw_pipe(const ConvDwPipeParams& p, hipStream_t s);

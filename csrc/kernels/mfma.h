@@ -79,6 +79,16 @@ __host__ __device__ __forceinline__ int align16(int bytes) { return (bytes + 15)
 // once per kernel, outside stage loops.
 struct Div {
   uint32_t mh, ml;
+  Div() = default;
+  // host-side magic (exact 64-bit arithmetic); pass through kernel params
+  static __host__ Div host(int d) {
+    Div r;
+    const uint64_t dd = (uint64_t)(d > 0 ? d : 1);
+    const uint64_t q = ((1ull << 40) + dd - 1) / dd;
+    r.mh = (uint32_t)(q >> 32);
+    r.ml = (uint32_t)q;
+    return r;
+  }
   __device__ __forceinline__ explicit Div(int d) {
     constexpr uint64_t P = 1ull << 40;
     const uint64_t dd = (uint64_t)(d > 0 ? d : 1);
