@@ -29,7 +29,7 @@ KERN_SRC  := $(wildcard csrc/kernels/*.hip)
 KERN_OBJ  := $(patsubst csrc/kernels/%.hip,$(OBJ)/kernels/%.o,$(KERN_SRC))
 ENG_SRC   := $(wildcard csrc/engine/*.cpp)
 ENG_OBJ   := $(patsubst csrc/engine/%.cpp,$(OBJ)/engine/%.o,$(ENG_SRC))
-HDRS      := $(wildcard csrc/include/mcc/*.h csrc/kernels/*.h)
+HDRS      := $(wildcard csrc/include/mcc/*.h csrc/kernels/*.h csrc/apps/*.h)
 
 MODULE    := mpi_cuda_cnn_amd/_C$(EXT)
 BINS      := build/bin/cnn build/bin/cnn_hip build/bin/cnn_dist
@@ -37,7 +37,7 @@ ifneq ($(MPICXX),)
 BINS      += build/bin/cnnmpi
 endif
 
-.PHONY: all module bins clean
+.PHONY: all module bins clean asan
 all: module bins
 module: $(MODULE)
 bins: $(BINS)
@@ -84,6 +84,15 @@ build/bin/cnn_hip: $(OBJ)/apps/cnn_hip.o $(OBJ)/apps/trainer.o $(CORE_OBJ) $(KER
 build/bin/cnn_dist: $(OBJ)/apps/cnn_dist.o $(OBJ)/apps/trainer.o $(CORE_OBJ) $(KERN_OBJ) $(ENG_OBJ)
 	@mkdir -p $(dir $@)
 	$(HIPCC) --offload-arch=$(ARCH) -o $@ $^ $(LDHIP) -lrccl
+
+# Host sanitizers: the CPU trainer and the core library
+# under AddressSanitizer + UBSan.  GPU-side sanitizers are not available on
+# the MI355X pool; device code is covered by bounds reasoning + tests.
+asan: build/bin/cnn_asan
+build/bin/cnn_asan: csrc/apps/cnn.cpp $(CORE_SRC) $(HDRS)
+	@mkdir -p $(dir $@)
+	$(CXX) -O1 -g -std=c++17 $(INC) -fsanitize=address,undefined -fno-omit-frame-pointer \
+	  -fno-sanitize-recover=undefined -o $@ csrc/apps/cnn.cpp $(CORE_SRC) -lm
 
 clean:
 	rm -rf build $(MODULE)

@@ -14,6 +14,10 @@
 #include <string>
 #include <vector>
 
+#include "mcc/common.h"
+#include "mcc/io.h"
+#include "mcc/model.h"
+
 namespace mcc {
 
 struct CliArgs {
@@ -35,6 +39,7 @@ struct CliArgs {
   int64_t bucket_mb = 4;    // DP gradient bucket size
   bool profile = false;     // per-phase timers
   bool quiet = false;
+  int64_t synthetic = 0;    // --synthetic N: generated data instead of IDX files
 };
 
 inline void usage(const char* prog) {
@@ -43,7 +48,9 @@ inline void usage(const char* prog) {
                "  [--model ref|lenet5|cifar3|vgg11] [--epochs N] [--batch B] [--lr X]\n"
                "  [--momentum X] [--weight-decay X] [--seed S] [--dtype bf16|fp32]\n"
                "  [--ref-compat] [--fp32] [--save W] [--load W] [--max-train N]\n"
-               "  [--bucket-mb MB] [--log-every N] [--profile] [--json PATH|-]\n",
+               "  [--bucket-mb MB] [--log-every N] [--profile] [--json PATH|-]\n"
+               "  [--synthetic N]   (no IDX files: N generated training images, N/5 test images\n"
+               "                     of the model's input shape; positional paths optional)\n",
                prog);
 }
 
@@ -71,6 +78,7 @@ inline int parse_cli(int argc, char** argv, CliArgs& a) {
     else if (s == "--log-every") a.log_every = std::atoi(next().c_str());
     else if (s == "--json") a.log_json = next();
     else if (s == "--ref-compat") a.ref_compat = true;
+    else if (s == "--synthetic") a.synthetic = std::atoll(next().c_str());
     else if (s == "--fp32") a.fp32 = true;
     else if (s == "--profile") a.profile = true;
     else if (s == "--quiet") a.quiet = true;
@@ -78,11 +86,43 @@ inline int parse_cli(int argc, char** argv, CliArgs& a) {
     else if (s.size() > 2 && s[0] == '-' && s[1] == '-') { usage(argv[0]); std::exit(100); }
     else pos.push_back(s);
   }
+  if (a.synthetic > 0 && pos.empty()) {
+    // generated splits; the pair of a split shares its seed so labels match images
+    const std::string n = std::to_string(a.synthetic), m = std::to_string(std::max<int64_t>(1, a.synthetic / 5));
+    pos = {"synthetic:" + n + ":1:images", "synthetic:" + n + ":1:labels", "synthetic:" + m + ":2:images",
+           "synthetic:" + m + ":2:labels"};
+  }
   if (pos.size() < 4) return 100;
   a.train_images = pos[0]; a.train_labels = pos[1]; a.test_images = pos[2]; a.test_labels = pos[3];
   if (a.batch < 1) a.batch = 1;
   if (a.log_every < 1) a.log_every = 1000;
   return 0;
+}
+
+// An IDX file, or "synthetic:<N>:<seed>:images|labels": the stripe dataset
+// of io.h in the model's input shape (so the binaries run on boxes without
+// MNIST).  Throws mcc::Error like idx_read.
+inline IdxFile load_idx(const std::string& path, const ModelSpec& spec) {
+  if (path.rfind("synthetic:", 0) != 0) return idx_read(path);
+  const size_t a1 = path.find(':', 10), a2 = path.find(':', a1 + 1);
+  if (a1 == std::string::npos || a2 == std::string::npos) throw Error("bad synthetic spec: " + path);
+  const int64_t n = std::atoll(path.substr(10, a1 - 10).c_str());
+  const uint64_t seed = std::strtoull(path.substr(a1 + 1, a2 - a1 - 1).c_str(), nullptr, 10);
+  const bool labels = path.substr(a2 + 1) == "labels";
+  if (n <= 0) throw Error("bad synthetic count: " + path);
+  const auto& in = spec.input();
+  std::vector<uint8_t> img, lab;
+  synth_dataset(n, in.C, in.H, in.W, spec.num_classes(), seed, img, lab);
+  IdxFile f;
+  if (labels) {
+    f.dims = {(uint32_t)n};
+    f.data = std::move(lab);
+  } else {
+    f.dims = in.C == 1 ? std::vector<uint32_t>{(uint32_t)n, (uint32_t)in.H, (uint32_t)in.W}
+                       : std::vector<uint32_t>{(uint32_t)n, (uint32_t)in.H, (uint32_t)in.W, (uint32_t)in.C};
+    f.data = std::move(img);
+  }
+  return f;
 }
 
 }  // namespace mcc

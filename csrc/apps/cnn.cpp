@@ -41,8 +41,8 @@ static int run(const CliArgs& a) {
   const int C = spec.input().C, H = spec.input().H, W = spec.input().W;
   const int64_t in_nodes = spec.input_nodes();
   try {
-    tr_img = idx_read(a.train_images);
-    tr_lab = idx_read(a.train_labels);
+    tr_img = load_idx(a.train_images, spec);
+    tr_lab = load_idx(a.train_labels, spec);
   } catch (const Error& e) {
     std::fprintf(stderr, "%s\n", e.what());
     return 111;
@@ -107,8 +107,8 @@ static int run(const CliArgs& a) {
 
   IdxFile te_img, te_lab;
   try {
-    te_img = idx_read(a.test_images);
-    te_lab = idx_read(a.test_labels);
+    te_img = load_idx(a.test_images, spec);
+    te_lab = load_idx(a.test_labels, spec);
   } catch (const Error& e) {
     std::fprintf(stderr, "%s\n", e.what());
     return 111;

@@ -55,8 +55,8 @@ int main(int argc, char** argv) {
 
   IdxFile tr_img, tr_lab;
   try {
-    tr_img = idx_read(a.train_images);
-    tr_lab = idx_read(a.train_labels);
+    tr_img = load_idx(a.train_images, spec);
+    tr_lab = load_idx(a.train_labels, spec);
   } catch (const Error& e) {
     return fail(111, e.what());
   }
@@ -114,8 +114,8 @@ int main(int argc, char** argv) {
   if (rank == 0) {
     IdxFile te_img, te_lab;
     try {
-      te_img = idx_read(a.test_images);
-      te_lab = idx_read(a.test_labels);
+      te_img = load_idx(a.test_images, spec);
+      te_lab = load_idx(a.test_labels, spec);
     } catch (const Error& e) {
       return fail(111, e.what());
     }

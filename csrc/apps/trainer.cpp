@@ -90,8 +90,8 @@ int run_gpu_training(const CliArgs& a, Comm& comm, const char* program) {
   // ---- data (IDX, device resident) ----
   IdxFile tr_img, tr_lab, te_img, te_lab;
   try {
-    tr_img = idx_read(a.train_images);
-    tr_lab = idx_read(a.train_labels);
+    tr_img = load_idx(a.train_images, spec);
+    tr_lab = load_idx(a.train_labels, spec);
   } catch (const Error& e) {
     std::fprintf(stderr, "%s\n", e.what());
     return 111;
@@ -243,8 +243,8 @@ int run_gpu_training(const CliArgs& a, Comm& comm, const char* program) {
   double test_s = 0;
   if (rank == 0) {
     try {
-      te_img = idx_read(a.test_images);
-      te_lab = idx_read(a.test_labels);
+      te_img = load_idx(a.test_images, spec);
+      te_lab = load_idx(a.test_labels, spec);
     } catch (const Error& e) {
       std::fprintf(stderr, "%s\n", e.what());
       rc = 111;

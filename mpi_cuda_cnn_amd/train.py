@@ -40,7 +40,22 @@ def _parse(argv):
     ap.add_argument("--save", default="")
     ap.add_argument("--load", default="")
     ap.add_argument("--json", default="")
+    ap.add_argument("--synthetic", type=int, default=0,
+                    help="generated stripe data (N train / N/5 test images) instead of IDX files")
     return ap.parse_args(argv)
+
+
+def _load_idx(path, spec):
+    """An IDX file or 'synthetic:<N>:<seed>:images|labels' (same syntax as the
+    native binaries, csrc/apps/cli.h load_idx)."""
+    from . import _C
+
+    if not path.startswith("synthetic:"):
+        return _C.idx_read(path)
+    _, n, seed, kind = path.split(":")
+    C, H, W = spec.input_shape()
+    imgs, labels = _C.synth_dataset(int(n), C, H, W, spec.num_classes(), seed=int(seed))
+    return labels if kind == "labels" else imgs.reshape(int(n), H, W, C)
 
 
 def _log(rank, msg):
@@ -50,6 +65,10 @@ def _log(rank, msg):
 
 def main(argv=None) -> int:
     a = _parse(sys.argv[1:] if argv is None else argv)
+    if a.synthetic > 0 and not a.paths:
+        n, m = a.synthetic, max(1, a.synthetic // 5)
+        a.paths = [f"synthetic:{n}:1:images", f"synthetic:{n}:1:labels", f"synthetic:{m}:2:images",
+                   f"synthetic:{m}:2:labels"]
     if len(a.paths) < 4:
         return 100
     import torch
@@ -73,8 +92,8 @@ def main(argv=None) -> int:
         else:
             spec = _C.make_model(a.model)
             params = _C.init_params(spec, a.seed)
-        tr_img = _C.idx_read(a.paths[0])
-        tr_lab = _C.idx_read(a.paths[1])
+        tr_img = _load_idx(a.paths[0], spec)
+        tr_lab = _load_idx(a.paths[1], spec)
     except RuntimeError as e:
         print(e, file=sys.stderr)
         return 111
@@ -158,8 +177,8 @@ def main(argv=None) -> int:
     rc = 0
     if rank == 0:
         try:
-            te_img = _C.idx_read(a.paths[2])
-            te_lab = _C.idx_read(a.paths[3])
+            te_img = _load_idx(a.paths[2], spec)
+            te_lab = _load_idx(a.paths[3], spec)
         except RuntimeError as e:
             print(e, file=sys.stderr)
             rc = 111

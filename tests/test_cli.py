@@ -95,3 +95,27 @@ def test_ref_compat_log_matches_reference_program(cnn_bin, data, tmp_path):
     ours = subprocess.run([cnn_bin] + list(data) + ["--ref-compat"], capture_output=True, text=True, timeout=600)
     assert ours.returncode == 0
     assert ours.stderr == ref.stderr
+
+
+def test_synthetic_data_source(cnn_bin):
+    """--synthetic N: no IDX files needed (the GPU box has no MNIST); the
+    generated pair of a split shares its seed, so the task stays learnable."""
+    r = subprocess.run([cnn_bin, "--synthetic", "400", "--epochs", "2", "--model", "lenet5", "--json", "-"],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    m = re.search(r"ntests=(\d+), ncorrect=(\d+)", r.stderr)
+    assert m and int(m.group(1)) == 80 and int(m.group(2)) >= 70
+
+
+def test_host_sanitizers_clean(tmp_path):
+    """the CPU trainer + core library under ASan/UBSan."""
+    exe = os.path.join(ROOT, "build", "bin", "cnn_asan")
+    b = subprocess.run(["make", "-C", ROOT, "-j8", "asan"], capture_output=True, text=True)
+    if b.returncode != 0:
+        pytest.skip("sanitizer runtime unavailable: " + b.stderr[-300:])
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=1", UBSAN_OPTIONS="halt_on_error=1")
+    for args in (["--model", "lenet5"], ["--model", "ref", "--ref-compat"]):
+        r = subprocess.run([exe, "--synthetic", "200", "--epochs", "1"] + args, capture_output=True, text=True,
+                           env=env, timeout=600)
+        assert r.returncode == 0, r.stderr[-3000:]
+        assert "ERROR: AddressSanitizer" not in r.stderr and "runtime error" not in r.stderr
