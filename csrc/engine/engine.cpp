@@ -88,6 +88,7 @@ GpuNet::GpuNet(const ModelSpec& spec, DType dtype, int max_batch, int device)
   MCC_CHECK(max_batch > 0, "GpuNet: max_batch > 0");
   if (const char* a = std::getenv("MCC_ABLATE")) ablate_ = std::atoi(a);  // kernel diagnostics only
   if (const char* a = std::getenv("MCC_NO_PIPE")) no_pipe_ = std::atoi(a) != 0;  // A/B against conv_small
+  if (const char* a = std::getenv("MCC_NO_FC")) no_fc_ = std::atoi(a) != 0;      // A/B against the tiled GEMM
   if (device_ >= 0) HIP_OK(hipSetDevice(device_));
   else HIP_OK(hipGetDevice(&device_));
   build();
@@ -485,6 +486,16 @@ void GpuNet::forward(const uint8_t* images, const int32_t* idx, int B, hipStream
       p.out = st.act_buf; p.out_arg = st.arg_buf;
       p.ablate = ablate_;
       gpu::conv_forward(dtype_, p, s);
+    } else if (dtype_ == DType::BF16 && !no_fc_ && gpu::fc_supported(st.Nout, st.Kin)) {
+      const Stage& pv = *stages_[si - 1];
+      gpu::FcParams p;
+      p.M = B; p.N = st.Nout; p.K = st.Kin;
+      p.A = pv.act_buf; p.lda = st.in_ld;
+      p.W = static_cast<const char*>(packed_) + es * st.pk_fwd; p.ldw = r8(st.Kin);
+      p.bias = params_ + st.b_off;
+      if (st.last) { p.epi = gpu::EPI_LOGITS; p.Cf = logits_; p.ldc = logits_ld_; }
+      else { p.epi = gpu::EPI_BIAS_ACT; p.act = st.act; p.C = st.act_buf; p.ldc = st.out_ld; }
+      gpu::fc_forward(p, s);
     } else {
       const Stage& pv = *stages_[si - 1];
       gpu::GemmParams p;
@@ -650,7 +661,17 @@ void GpuNet::backward(int hi, int lo, hipStream_t s) {
       r.permC = st.permC; r.permHW = st.permHW;
       gpu::dw_reduce(r, s);
       // data gradient
-      if (si > 0) {
+      if (si > 0 && dtype_ == DType::BF16 && !no_fc_ && gpu::fc_supported(st.Kin, st.Nout)) {
+        gpu::FcParams d;
+        d.M = B; d.N = st.Kin; d.K = st.Nout;
+        d.A = st.grad_buf; d.lda = st.out_ld;
+        d.W = static_cast<const char*>(packed_) + es * st.pk_dx; d.ldw = st.out_ld;
+        d.epi = gpu::EPI_DACT;
+        d.act = pv.kind == Stage::FC ? pv.act : gpu::ACT_NONE;  // conv masks are applied by its staging
+        d.aux = pv.act_buf; d.ldaux = st.in_ld;
+        d.C = pv.grad_buf; d.ldc = st.in_ld;
+        gpu::fc_forward(d, s);
+      } else if (si > 0) {
         gpu::GemmParams d;
         d.M = B; d.N = st.Kin; d.K = st.Nout;
         d.A = st.grad_buf; d.lda = st.out_ld;

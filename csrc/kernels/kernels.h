@@ -217,6 +217,25 @@ struct GemmParams {
   int64_t partial_stride = 0;       // elements between split-K partials
 };
 
+// Weights-resident FC GEMM (bf16, fc.hip): C[M][N] = epi(A[M][K] W[N][K]^T)
+// for N*K small enough that W lives in one CU's LDS (fc_supported).
+// Epilogues: EPI_BIAS_ACT (C bf16), EPI_LOGITS (Cf fp32, ldc), EPI_DACT
+// (C = acc * act'(aux), aux = the activation OUTPUT of the producing layer).
+struct FcParams {
+  int M = 0, N = 0, K = 0;
+  const void* A = nullptr; int lda = 0;
+  const void* W = nullptr; int ldw = 0;
+  int epi = EPI_BIAS_ACT;
+  int act = ACT_NONE;
+  const float* bias = nullptr;
+  const void* aux = nullptr; int ldaux = 0;
+  void* C = nullptr; int ldc = 0;
+  float* Cf = nullptr;
+  long long* dbg = nullptr;  // diagnostics: per-wave phase timestamps [grid][4 waves][4]
+};
+bool fc_supported(int N, int K);
+void fc_forward(const FcParams& p, hipStream_t s);
+
 // Reduce split-K partials of a weight gradient into the canonical grad:
 // gw[n*Kc + perm(k)] (k < kfeat), gb[n] (k == kfeat).
 struct DwReduceParams {

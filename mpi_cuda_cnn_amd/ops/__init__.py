@@ -1,0 +1,149 @@
+"""Torch-tensor entry points for the gfx950 kernels.
+
+The training engine (``GpuNet``) calls the kernels on its own arena; these
+wrappers make the same kernels usable on ordinary torch tensors (CUDA/HIP
+device tensors, contiguous, bf16 or fp32), e.g. to build other models or to
+test a kernel in isolation.  They launch on the current torch stream and
+fail loudly on CPU tensors: there is no eager fallback.
+
+    linear(x, w, b, act)            y = act(x @ w.T + b)            (MFMA GEMM, fused epilogue)
+    linear_dgrad(dy, w, y_prev, act) dx = (dy @ w) * act'(y_prev)
+    linear_wgrad(dy, x)             (dW, db) = (dy.T @ x, dy.sum(0)) (split-K, ones-column bias)
+    softmax_xent(logits, labels)    dlogits, loss_sum, mse_sum, correct
+    sgd_(p, g, mom, lr, mu, wd)     in-place SGD / momentum / weight decay
+
+Reference counterparts: Layer_feedForw_full / Layer_feedBack_full
+(cnn.c:113-173), the softmax + error of cnn.c:125-143,275-287 and
+Layer_update (cnn.c:303-314).
+"""
+
+from __future__ import annotations
+
+import torch
+
+from .. import _C
+
+_K = _C.kernels
+_ACT = {"none": _K.ACT_NONE, "relu": _K.ACT_RELU, "tanh": _K.ACT_TANH}
+_DT = {torch.bfloat16: "bf16", torch.float32: "fp32"}
+
+
+def _check(*ts):
+    for t in ts:
+        if t is None:
+            continue
+        if not t.is_cuda:
+            raise RuntimeError("mpi_cuda_cnn_amd.ops: tensors must be on the GPU (no CPU fallback)")
+        if not t.is_contiguous():
+            raise RuntimeError("mpi_cuda_cnn_amd.ops: tensors must be contiguous")
+
+
+def _dtype(t):
+    if t.dtype not in _DT:
+        raise RuntimeError(f"mpi_cuda_cnn_amd.ops: unsupported dtype {t.dtype} (bf16 / fp32)")
+    return _DT[t.dtype]
+
+
+def _stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _ld8(n):
+    return (n + 7) // 8 * 8
+
+
+def _pad_cols(t, ld):
+    if t.shape[1] == ld:
+        return t
+    out = torch.zeros(t.shape[0], ld, dtype=t.dtype, device=t.device)
+    out[:, : t.shape[1]] = t
+    return out
+
+
+def linear(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None = None, act: str = "none") -> torch.Tensor:
+    """y = act(x @ w.T + b); x [M, K], w [N, K] (same dtype), b fp32 [N]."""
+    _check(x, w, b)
+    dt = _dtype(x)
+    M, K = x.shape
+    N = w.shape[0]
+    ldk = _ld8(K)
+    xa, wa = _pad_cols(x, ldk), _pad_cols(w, ldk)
+    ldc = _ld8(N)
+    y = torch.empty(M, ldc, dtype=x.dtype, device=x.device)
+    bias = b.float().contiguous() if b is not None else None
+    _K.gemm(dt, M, N, K, xa.data_ptr(), ldk, False, wa.data_ptr(), ldk, False, epi=_K.EPI_BIAS_ACT,
+            act=_ACT[act], bias=bias.data_ptr() if bias is not None else 0, C=y.data_ptr(), ldc=ldc,
+            stream=_stream())
+    return y[:, :N] if ldc != N else y
+
+
+def linear_dgrad(dy: torch.Tensor, w: torch.Tensor, y_prev: torch.Tensor | None = None,
+                 act: str = "none") -> torch.Tensor:
+    """dx = (dy @ w) * act'(y_prev); dy [M, N], w [N, K]; act' from the activation OUTPUT y_prev [M, K]."""
+    _check(dy, w, y_prev)
+    dt = _dtype(dy)
+    M, N = dy.shape
+    K = w.shape[1]
+    wt = _pad_cols(w.t().contiguous(), _ld8(N))  # [K, N]: the B operand stays K(=N)-contiguous
+    ldn = _ld8(N)
+    dya = _pad_cols(dy, ldn)
+    ldc = _ld8(K)
+    dx = torch.empty(M, ldc, dtype=dy.dtype, device=dy.device)
+    aux = _pad_cols(y_prev.contiguous(), ldc) if (y_prev is not None and act != "none") else None
+    _K.gemm(dt, M, K, N, dya.data_ptr(), ldn, False, wt.data_ptr(), ldn, False, epi=_K.EPI_DACT,
+            act=_ACT[act] if aux is not None else _K.ACT_NONE, aux=aux.data_ptr() if aux is not None else 0,
+            ldaux=ldc, C=dx.data_ptr(), ldc=ldc, stream=_stream())
+    return dx[:, :K] if ldc != K else dx
+
+
+def linear_wgrad(dy: torch.Tensor, x: torch.Tensor, splitk: int = 0):
+    """(dW [N, K] fp32, db [N] fp32) = (dy.T @ x, dy.sum(0)): split-K over the batch, the
+    bias gradient as a ones-column appended to x (one GEMM, no separate reduction pass)."""
+    _check(dy, x)
+    dt = _dtype(dy)
+    M, N = dy.shape
+    K = x.shape[1]
+    ldn, ldk = _ld8(N), _ld8(K)
+    dya, xa = _pad_cols(dy, ldn), _pad_cols(x, ldk)
+    ldp = _ld8(K + 1)
+    if splitk <= 0:
+        tiles = ((N + 63) // 64) * ((K + 64) // 64)
+        splitk = max(1, min(64, 512 // max(1, tiles), M // 128))
+    part = torch.empty(splitk, N, ldp, dtype=torch.float32, device=dy.device)
+    _K.gemm(dt, N, K + 1, M, dya.data_ptr(), ldn, True, xa.data_ptr(), ldk, True, ones_col=K,
+            epi=_K.EPI_PARTIAL, Cf=part.data_ptr(), ldc=ldp, splitk=splitk, pstride=N * ldp, stream=_stream())
+    tot = part.sum(0)
+    return tot[:, :K].contiguous(), tot[:, K].contiguous()
+
+
+def softmax_xent(logits: torch.Tensor, labels: torch.Tensor, scale: float = 1.0, grad_dtype=torch.float32):
+    """Fused softmax-cross-entropy forward + backward on fp32 logits [M, N] and u8 labels [M].
+
+    Returns (dlogits = (softmax - onehot) * scale [M, N], loss_sum, mse_sum, correct) where mse is
+    the reference's logged error, mean((p - y)^2) per sample (cnn.c:275-282), and correct counts
+    argmax == label with the first maximum winning (cnn.c:508-513)."""
+    _check(logits, labels)
+    if logits.dtype != torch.float32:
+        raise RuntimeError("softmax_xent: logits must be fp32")
+    M, N = logits.shape
+    lab = labels.to(torch.uint8).contiguous()
+    ldd = _ld8(N)
+    d = torch.empty(M, ldd, dtype=grad_dtype, device=logits.device)
+    stats = torch.zeros(4, dtype=torch.float32, device=logits.device)
+    _K.softmax_xent(_DT[grad_dtype], M, N, logits.data_ptr(), N, lab.data_ptr(), dlogits=d.data_ptr(), ldd=ldd,
+                    scale=scale, stats=stats.data_ptr(), stream=_stream())
+    return d[:, :N], stats[0], stats[1], stats[2]
+
+
+def sgd_(param: torch.Tensor, grad: torch.Tensor, mom: torch.Tensor | None = None, lr: float = 0.1,
+         momentum: float = 0.0, weight_decay: float = 0.0) -> torch.Tensor:
+    """In place on fp32 tensors: v = mu*v + (g + wd*p); p -= lr*v (plain SGD when mom is None)."""
+    _check(param, grad, mom)
+    if param.dtype != torch.float32 or grad.dtype != torch.float32:
+        raise RuntimeError("sgd_: fp32 master parameters and gradients")
+    _K.sgd_update(param.data_ptr(), grad.data_ptr(), mom.data_ptr() if mom is not None else 0, param.numel(), lr,
+                  momentum=momentum if mom is not None else 0.0, weight_decay=weight_decay, stream=_stream())
+    return param
+
+
+__all__ = ["linear", "linear_dgrad", "linear_wgrad", "softmax_xent", "sgd_"]

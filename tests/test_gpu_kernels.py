@@ -128,3 +128,53 @@ def test_softmax_xent_kernel(cuda):
     assert abs(stats[1].item() - ((p - y) ** 2).mean(1).sum().item()) < 1e-3
     assert int(stats[2].item()) == int((lg.argmax(1) == labels.long()).sum().item())
     assert torch.equal(pred.long(), lg.argmax(1))
+
+
+# ---- mpi_cuda_cnn_amd.ops: the kernels on ordinary torch tensors ----
+
+import mpi_cuda_cnn_amd.ops as ops  # noqa: E402
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", ["bf16", "fp32"])
+@pytest.mark.parametrize("act", ["none", "relu", "tanh"])
+def test_ops_linear_family(cuda, dtype, act):
+    g = torch.Generator(device=cuda).manual_seed(7)
+    M, N, K = 777, 84, 120  # odd shapes: ld padding paths
+    x = torch.randn(M, K, device=cuda, generator=g).to(TDT[dtype])
+    w = (torch.randn(N, K, device=cuda, generator=g) * 0.1).to(TDT[dtype])
+    b = torch.randn(N, device=cuda, generator=g)
+    fn = {"none": lambda t: t, "relu": torch.relu, "tanh": torch.tanh}[act]
+    y = ops.linear(x, w, b, act)
+    ref = fn(x.float() @ w.float().t() + b)
+    tol = 1e-4 if dtype == "fp32" else 3e-2
+    torch.testing.assert_close(y.float(), ref, atol=tol * 4, rtol=tol)
+    dy = torch.randn(M, N, device=cuda, generator=g).to(TDT[dtype])
+    dx = ops.linear_dgrad(dy, w, x if act != "none" else None, act)
+    d = {"none": torch.ones_like, "relu": lambda t: (t > 0).float(), "tanh": lambda t: 1 - t * t}[act](x.float())
+    torch.testing.assert_close(dx.float(), (dy.float() @ w.float()) * d, atol=tol * 10, rtol=tol * 2)
+    dw, db = ops.linear_wgrad(dy, x)
+    rw = dy.float().t() @ x.float()
+    assert ((dw - rw).abs().max() / rw.abs().max()).item() < (1e-4 if dtype == "fp32" else 2e-2)
+    torch.testing.assert_close(db, dy.float().sum(0), atol=1e-2, rtol=1e-2)
+
+
+@pytest.mark.gpu
+def test_ops_softmax_xent_and_sgd(cuda):
+    g = torch.Generator(device=cuda).manual_seed(8)
+    logits = torch.randn(513, 10, device=cuda, generator=g) * 2
+    labels = torch.randint(0, 10, (513,), device=cuda, generator=g)
+    d, loss, mse, correct = ops.softmax_xent(logits, labels, scale=1.0 / 513)
+    p = torch.softmax(logits, 1)
+    y = torch.nn.functional.one_hot(labels, 10).float()
+    torch.testing.assert_close(d, (p - y) / 513, atol=1e-6, rtol=1e-4)
+    assert abs(loss.item() - torch.nn.functional.cross_entropy(logits, labels, reduction="sum").item()) < 1e-2
+    assert int(correct.item()) == int((logits.argmax(1) == labels).sum().item())
+    w = torch.randn(1001, device=cuda, generator=g)
+    gr = torch.randn(1001, device=cuda, generator=g)
+    v = torch.zeros_like(w)
+    w0 = w.clone()
+    ops.sgd_(w, gr, v, lr=0.1, momentum=0.9, weight_decay=0.01)
+    torch.testing.assert_close(w, w0 - 0.1 * (gr + 0.01 * w0), atol=1e-6, rtol=1e-6)
+    with pytest.raises(RuntimeError):
+        ops.linear(torch.zeros(4, 8), torch.zeros(4, 8))
