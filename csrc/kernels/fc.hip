@@ -30,126 +30,154 @@ constexpr int kFcMaxChunks = 16;  // K <= 512
 constexpr int kFcGroupTiles = 8;  // column tiles per staged output group (128 columns)
 constexpr int kFcStageLd = kFcGroupTiles * 16 + 8;
 
-__host__ __device__ inline int fc_ldk(int K) { return ((K + 31) & ~31) + 8; }
+typedef __attribute__((address_space(1))) void gvoid;
+typedef __attribute__((address_space(3))) void lvoid;
+
+// K chunks (of 32) the kernel is unrolled for: a power of two >= the real count
+__host__ __device__ inline int fc_nchb(int K) {
+  const int n = (K + 31) >> 5;
+  return n <= 1 ? 1 : n <= 2 ? 2 : n <= 4 ? 4 : n <= 8 ? 8 : 16;
+}
 __host__ __device__ inline int fc_npad(int N) { return (N + 15) & ~15; }
-__host__ __device__ inline size_t fc_lds(int N, int K) {
-  return (size_t)fc_npad(N) * fc_ldk(K) * 2 + (size_t)4 * 16 * kFcStageLd * 2;
+// W is staged densely, exactly as packed in memory ([N][ldw]); reads run up
+// to NCH*32 columns past a row start, so the region is padded with zeros
+__host__ __device__ inline int fc_welems(int N, int ldw, int K) {
+  return ((fc_npad(N) * ldw + fc_nchb(K) * 32 + 7) & ~7);
+}
+__host__ __device__ inline size_t fc_lds(int N, int ldw, int K) {
+  return (size_t)fc_welems(N, ldw, K) * 2 + (size_t)fc_npad(N) * 4 + (size_t)4 * 16 * kFcStageLd * 2;
 }
 
-template <int EPI, int ACT>
+template <int EPI, int ACT, int NCH>
 __global__ void __launch_bounds__(kFcThreads) fc_kernel(FcParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int ldk = fc_ldk(p.K);
+  const int ldk = p.ldw;
   const int npad = fc_npad(p.N);
-  const int nch = (p.K + 31) >> 5;
+  const int wel = fc_welems(p.N, p.ldw, p.K);
   bf16* ws = reinterpret_cast<bf16*>(smem);
+  float* bias_s = reinterpret_cast<float*>(smem + (size_t)wel * 2);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r16 = lane & 15, g = lane >> 4;
-  bf16* stg = reinterpret_cast<bf16*>(smem + (size_t)npad * ldk * 2) + wave * 16 * kFcStageLd;
+  bf16* stg = reinterpret_cast<bf16*>(smem + (size_t)wel * 2 + (size_t)npad * 4) + wave * 16 * kFcStageLd;
   long long* dbg = p.dbg ? p.dbg + ((size_t)blockIdx.x * 4 + wave) * 4 : nullptr;
   if (dbg && lane == 0) dbg[0] = (long long)__builtin_amdgcn_s_memrealtime();
 
-  // ---- W -> LDS (zero padding rows/columns: they meet the K / N tails) ----
+  // ---- W -> LDS: the packed [N][ldw] block is contiguous, so it moves as
+  // 1 KB async global->LDS DMA pieces (64 lanes x 16 B, no registers, no
+  // index math), piece i by wave i % 4; the tail is zeroed by plain stores ----
   {
-    // U independent 16-byte loads in flight per thread before their LDS
-    // stores (a load->store loop would pay the L2 latency per vector)
-    constexpr int U = 16;
     const bf16* W = static_cast<const bf16*>(p.W);
-    const int vpr = ldk >> 3;  // 16-byte vectors per LDS row
-    const int nv = npad * vpr;
-    for (int v0 = tid; v0 < nv; v0 += U * kFcThreads) {
-      bf16x8 x[U];
-      int off[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int v = v0 + u * kFcThreads;
-        const int r = v / vpr, c = (v - r * vpr) * 8;
-        off[u] = v < nv ? r * ldk + c : -1;
-        if (v < nv && r < p.N && c < p.K) {  // packed weights: zero columns up to ldw
-          x[u] = load8(W + (size_t)r * p.ldw + c);
-        } else {
-#pragma unroll
-          for (int j = 0; j < 8; ++j) x[u][j] = (bf16)0.f;
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u)
-        if (off[u] >= 0) store8(ws + off[u], x[u]);
+    const int wv = p.N * p.ldw;  // elements of real weights (multiple of 8)
+    const int npieces = (wv + 511) >> 9;
+    for (int i = wave; i < npieces; i += kFcThreads / 64) {
+      const int e = i * 512 + lane * 8;
+      if (e < wv) __builtin_amdgcn_global_load_lds((gvoid*)(W + e), (lvoid*)(ws + i * 512), 16, 0, 0);
     }
+    const bf16x8 z = {};
+    for (int e = wv + tid * 8; e < wel; e += kFcThreads * 8) store8(ws + e, z);
+    for (int n = tid; n < npad; n += kFcThreads) bias_s[n] = (EPI != EPI_DACT && n < p.N && p.bias) ? p.bias[n] : 0.f;
   }
 
-  // ---- this wave's A fragments, straight from global.  K need not be a
-  // multiple of 8: the producers leave the leading-dim padding columns 0 ----
+  // ---- this wave's A fragments, straight from HBM into registers.  K need
+  // not be a multiple of 8: producers leave the leading-dim padding at 0 ----
   const int row0 = blockIdx.x * kFcRows + wave * 16;
   const int arow = row0 + r16;
   const bf16* A = static_cast<const bf16*>(p.A);
-  bf16x8 a[kFcMaxChunks];
+  bf16x8 a[NCH];
 #pragma unroll
-  for (int q = 0; q < kFcMaxChunks; ++q) {
+  for (int q = 0; q < NCH; ++q) {
     const int k = q * 32 + 8 * g;
-    if (q < nch && arow < p.M && k < p.K) {
-      a[q] = load8(A + (size_t)arow * p.lda + k);
-    } else {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) a[q][j] = (bf16)0.f;
-    }
+    if (arow < p.M && k < p.K) a[q] = load8(A + (size_t)arow * p.lda + k);
+    else a[q] = bf16x8{};
   }
   if (dbg && lane == 0) dbg[1] = (long long)__builtin_amdgcn_s_memrealtime();
-  __syncthreads();
+  __syncthreads();  // also drains the DMA (vmcnt)
   if (dbg && lane == 0) dbg[2] = (long long)__builtin_amdgcn_s_memrealtime();
+
+  auto epilogue = [&](const f32x4& acc, int tile, int slot) {
+    const int col = tile * 16 + r16;
+    const bool cv = col < p.N;
+    const float bv = bias_s[col];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = row0 + 4 * g + i;
+      float v = acc[i] + bv;
+      if (EPI == EPI_BIAS_ACT) {
+        v = ACT == ACT_RELU ? fmaxf(v, 0.f) : (ACT == ACT_TANH ? tanhf(v) : v);
+      } else if (EPI == EPI_DACT) {
+        if (ACT != ACT_NONE && cv && row < p.M) {
+          const float y = (float)static_cast<const bf16*>(p.aux)[(size_t)row * p.ldaux + col];
+          v *= ACT == ACT_RELU ? (y > 0.f ? 1.f : 0.f) : (1.f - y * y);
+        }
+      }
+      if (EPI == EPI_LOGITS) {
+        if (cv && row < p.M) p.Cf[(size_t)row * p.ldc + col] = v;
+      } else {
+        stg[(4 * g + i) * kFcStageLd + slot * 16 + r16] = (bf16)v;
+      }
+    }
+  };
 
   const int ntiles = npad >> 4;
   for (int t0 = 0; t0 < ntiles; t0 += kFcGroupTiles) {
     const int tn = min(kFcGroupTiles, ntiles - t0);
-    for (int tt = 0; tt < tn; ++tt) {
-      const int col = (t0 + tt) * 16 + r16;
-      const bf16* wrow = ws + col * ldk + 8 * g;
-      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int tt = 0; tt < tn; tt += 2) {
+      // two column tiles per pass: independent accumulator chains, all B
+      // fragment reads unconditional (rows zero-padded to NCH*32) so they
+      // can be issued ahead of the MFMAs; the odd tile may be a dummy
+      const bool two = tt + 1 < tn;
+      const bf16* wa = ws + ((t0 + tt) * 16 + r16) * ldk + 8 * g;
+      const bf16* wb = two ? wa + 16 * ldk : wa;
+      f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = {0.f, 0.f, 0.f, 0.f};
+      // all of the pair's B fragments in flight before the first MFMA
+      // (left to itself the compiler keeps only ~2 reads ahead, exposing the
+      // LDS latency on every MFMA)
+      bf16x8 ba[NCH], bb[NCH];
 #pragma unroll
-      for (int q = 0; q < kFcMaxChunks; ++q)
-        if (q < nch) acc = mma(acc, a[q], load8(wrow + q * 32));
-      const bool cv = col < p.N;
-      float bv = 0.f;
-      if (EPI != EPI_DACT && cv && p.bias) bv = p.bias[col];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int row = row0 + 4 * g + i;
-        float v = acc[i] + bv;
-        if (EPI == EPI_BIAS_ACT) {
-          v = ACT == ACT_RELU ? fmaxf(v, 0.f) : (ACT == ACT_TANH ? tanhf(v) : v);
-        } else if (EPI == EPI_DACT) {
-          if (ACT != ACT_NONE && cv && row < p.M) {
-            const float y = (float)static_cast<const bf16*>(p.aux)[(size_t)row * p.ldaux + col];
-            v *= ACT == ACT_RELU ? (y > 0.f ? 1.f : 0.f) : (1.f - y * y);
-          }
-        } else if (EPI == EPI_LOGITS) {
-          if (cv && row < p.M) p.Cf[(size_t)row * p.ldc + col] = v;
-          continue;
-        }
-        stg[(4 * g + i) * kFcStageLd + tt * 16 + r16] = (bf16)v;
+      for (int q = 0; q < NCH; ++q) {
+        ba[q] = load8(wa + q * 32);
+        bb[q] = load8(wb + q * 32);
       }
+      __builtin_amdgcn_sched_barrier(0);
+      if (!(p.ablate & 2)) {
+#pragma unroll
+        for (int q = 0; q < NCH; ++q) {
+          c0 = mma(c0, a[q], ba[q]);
+          c1 = mma(c1, a[q], bb[q]);
+        }
+      } else {
+        c0[0] = (float)ba[0][0] + (float)bb[NCH - 1][7];
+      }
+      epilogue(c0, t0 + tt, tt);
+      if (two) epilogue(c1, t0 + tt + 1, tt + 1);
     }
-    if (EPI == EPI_LOGITS) continue;
+    if (EPI == EPI_LOGITS || (p.ablate & 1)) continue;
     // wave-private tile -> 16 rows x (tn*16) columns, 16-byte stores (ldc % 8 == 0)
     __builtin_amdgcn_wave_barrier();
     const int c0 = t0 * 16;
-    const int ncols = min(tn * 16, p.ldc - c0);  // write up to the leading dim (pad columns too)
-    const int vpr = ncols >> 3;
+    const int ncols = min(tn * 16, p.ldc - c0);  // up to the leading dim (padding columns written as 0)
     bf16* C = static_cast<bf16*>(p.C);
-    for (int v = lane; v < 16 * vpr; v += 64) {
-      const int r = v / vpr, c = (v - r * vpr) * 8;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {  // 16 rows x 16 vectors of 8 columns, 4 per lane
+      const int v = lane + 64 * j;
+      const int r = v >> 4, c = (v & 15) * 8;
       const int row = row0 + r;
-      if (row < p.M) store8(C + (size_t)row * p.ldc + c0 + c, load8(stg + r * kFcStageLd + c));
+      if (c < ncols && row < p.M) store8(C + (size_t)row * p.ldc + c0 + c, load8(stg + r * kFcStageLd + c));
     }
     __builtin_amdgcn_wave_barrier();
   }
   if (dbg && lane == 0) dbg[3] = (long long)__builtin_amdgcn_s_memrealtime();
 }
 
+template <int E, int A>
+struct EpiTag {
+  static constexpr int epi = E, act = A;
+};
+
 }  // namespace
 
 bool fc_supported(int N, int K) {
-  return N > 0 && K > 0 && K <= kFcMaxChunks * 32 && fc_lds(N, K) <= 160 * 1024;
+  return N > 0 && K > 0 && K <= kFcMaxChunks * 32 && fc_lds(N, (K + 7) & ~7, K) <= 160 * 1024;
 }
 
 void fc_forward(const FcParams& p, hipStream_t s) {
@@ -159,21 +187,33 @@ void fc_forward(const FcParams& p, hipStream_t s) {
             "fc_forward: leading dims must be multiples of 8 covering K");
   if (p.M <= 0) return;
   const dim3 grid((unsigned)cdiv(p.M, kFcRows)), block(kFcThreads);
-  const size_t lds = fc_lds(p.N, p.K);
+  const size_t lds = fc_lds(p.N, p.ldw, p.K);
+  MCC_CHECK(lds <= 160 * 1024, "fc_forward: weights do not fit in LDS");
+  const int nchb = fc_nchb(p.K);
   auto go = [&](auto kern) { hipLaunchKernelGGL(kern, grid, block, lds, s, p); };
+  auto by_nch = [&](auto tag) {
+    constexpr int EPI = decltype(tag)::epi, ACT = decltype(tag)::act;
+    switch (nchb) {
+      case 1: go(fc_kernel<EPI, ACT, 1>); break;
+      case 2: go(fc_kernel<EPI, ACT, 2>); break;
+      case 4: go(fc_kernel<EPI, ACT, 4>); break;
+      case 8: go(fc_kernel<EPI, ACT, 8>); break;
+      default: go(fc_kernel<EPI, ACT, 16>); break;
+    }
+  };
   switch (p.epi) {
     case EPI_BIAS_ACT:
-      if (p.act == ACT_RELU) go(fc_kernel<EPI_BIAS_ACT, ACT_RELU>);
-      else if (p.act == ACT_TANH) go(fc_kernel<EPI_BIAS_ACT, ACT_TANH>);
-      else go(fc_kernel<EPI_BIAS_ACT, ACT_NONE>);
+      if (p.act == ACT_RELU) by_nch(EpiTag<EPI_BIAS_ACT, ACT_RELU>{});
+      else if (p.act == ACT_TANH) by_nch(EpiTag<EPI_BIAS_ACT, ACT_TANH>{});
+      else by_nch(EpiTag<EPI_BIAS_ACT, ACT_NONE>{});
       break;
     case EPI_LOGITS:
-      go(fc_kernel<EPI_LOGITS, ACT_NONE>);
+      by_nch(EpiTag<EPI_LOGITS, ACT_NONE>{});
       break;
     case EPI_DACT:
-      if (p.act == ACT_RELU) go(fc_kernel<EPI_DACT, ACT_RELU>);
-      else if (p.act == ACT_TANH) go(fc_kernel<EPI_DACT, ACT_TANH>);
-      else go(fc_kernel<EPI_DACT, ACT_NONE>);
+      if (p.act == ACT_RELU) by_nch(EpiTag<EPI_DACT, ACT_RELU>{});
+      else if (p.act == ACT_TANH) by_nch(EpiTag<EPI_DACT, ACT_TANH>{});
+      else by_nch(EpiTag<EPI_DACT, ACT_NONE>{});
       break;
     default:
       MCC_CHECK(false, "fc_forward: unsupported epilogue");

@@ -232,6 +232,7 @@ struct FcParams {
   void* C = nullptr; int ldc = 0;
   float* Cf = nullptr;
   long long* dbg = nullptr;  // diagnostics: per-wave phase timestamps [grid][4 waves][4]
+  int ablate = 0;            // diagnostics: 1 skip the output copy, 2 skip the MFMAs
 };
 bool fc_supported(int N, int K);
 void fc_forward(const FcParams& p, hipStream_t s);
