@@ -200,10 +200,18 @@ __global__ void __launch_bounds__(256) dw_slab_sum_kernel(const float* slab, int
   const int tv = threadIdx.x & 63, tx = threadIdx.x >> 6;
   const int v = blockIdx.x * 64 + tv;
   const int x0 = blockIdx.y * xs_per, x1 = min(nx, x0 + xs_per);
-  float acc = 0.f;
-  if (v < nv)
-    for (int x = x0 + tx; x < x1; x += 4) acc += slab[(size_t)x * nv + v];
-  red[tx][tv] = acc;
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;  // four loads in flight per thread
+  if (v < nv) {
+    int x = x0 + tx;
+    for (; x + 12 < x1; x += 16) {
+      a0 += slab[(size_t)x * nv + v];
+      a1 += slab[(size_t)(x + 4) * nv + v];
+      a2 += slab[(size_t)(x + 8) * nv + v];
+      a3 += slab[(size_t)(x + 12) * nv + v];
+    }
+    for (; x < x1; x += 4) a0 += slab[(size_t)x * nv + v];
+  }
+  red[tx][tv] = (a0 + a1) + (a2 + a3);
   __syncthreads();
   if (tx == 0 && v < nv) part[(size_t)blockIdx.y * nv + v] = (red[0][tv] + red[1][tv]) + (red[2][tv] + red[3][tv]);
 }
@@ -228,8 +236,16 @@ __global__ void __launch_bounds__(256) dw_slab_final_kernel(const float* part, i
     col = kbias;
   }
   const int v = row * ncols_pad + col;
-  float s = 0.f;
-  for (int xc = 0; xc < nxc; ++xc) s += part[(size_t)xc * nv + v];
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;  // fixed order, loads in flight
+  int xc = 0;
+  for (; xc + 3 < nxc; xc += 4) {
+    s0 += part[(size_t)xc * nv + v];
+    s1 += part[(size_t)(xc + 1) * nv + v];
+    s2 += part[(size_t)(xc + 2) * nv + v];
+    s3 += part[(size_t)(xc + 3) * nv + v];
+  }
+  for (; xc < nxc; ++xc) s0 += part[(size_t)xc * nv + v];
+  const float s = (s0 + s1) + (s2 + s3);
   if (j < nW) gw[j] = s;
   else gb[row] = s;
 }
@@ -326,7 +342,7 @@ void conv_dw_pipe_reduce(const ConvDwPipeParams& pin, float* gw, float* gb, hipS
   const int nx = std::min(ngroups, std::min(pin.grid, kCUs * wgs_per_cu(p.lds, 2)));
   if (nx <= 0) return;
   const int nv = p.cout_pad * p.ncols_pad;
-  const int xs_per = 16;
+  const int xs_per = 64;
   const int nxc = cdiv(nx, xs_per);
   float* part = p.slab + (size_t)pin.grid * nv;  // after the slabs (scratch sized by the planner's grid)
   hipLaunchKernelGGL(dw_slab_sum_kernel, dim3((unsigned)cdiv(nv, 64), (unsigned)nxc), dim3(256), 0, st, p.slab, nx,

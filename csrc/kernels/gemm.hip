@@ -216,23 +216,32 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmParams p) {
 
 // Sum split-K partials: 4 independent accumulators per thread so the S loads
 // are in flight together.
+// Four lanes per output, each summing every 4th split-K partial with two
+// accumulators (the loads of ~S/4 partials are in flight together), then a
+// fixed-order shuffle reduction: deterministic, ~4x shorter dependency chain
+// than one lane per output.
 __global__ void __launch_bounds__(256) dw_reduce_kernel(DwReduceParams p) {
   const int kc = p.kfeat + 1;
-  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= (int64_t)p.Nout * kc) return;
-  const int n = (int)(j / kc), k = (int)(j - (int64_t)n * kc);
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t j = t >> 2;
+  const int s4 = (int)(t & 3);
+  const bool ok = j < (int64_t)p.Nout * kc;
+  const int n = ok ? (int)(j / kc) : 0, k = ok ? (int)(j - (int64_t)n * kc) : 0;
   const float* src = p.part + (size_t)n * p.ldp + k;
   const size_t st = (size_t)p.partial_stride;
-  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
-  int s = 0;
-  for (; s + 3 < p.S; s += 4) {
-    a0 += src[(size_t)s * st];
-    a1 += src[(size_t)(s + 1) * st];
-    a2 += src[(size_t)(s + 2) * st];
-    a3 += src[(size_t)(s + 3) * st];
+  float a0 = 0.f, a1 = 0.f;
+  if (ok) {
+    int s = s4;
+    for (; s + 4 < p.S; s += 8) {
+      a0 += src[(size_t)s * st];
+      a1 += src[(size_t)(s + 4) * st];
+    }
+    for (; s < p.S; s += 4) a0 += src[(size_t)s * st];
   }
-  for (; s < p.S; ++s) a0 += src[(size_t)s * st];
-  const float acc = (a0 + a1) + (a2 + a3);
+  float acc = a0 + a1;
+  acc += __shfl_xor(acc, 1);
+  acc += __shfl_xor(acc, 2);
+  if (!ok || s4 != 0) return;
   float* dst;
   if (k < p.kfeat) {
     int kk = k;
@@ -291,7 +300,7 @@ void gemm(DType t, const GemmParams& p, hipStream_t s) {
 
 void dw_reduce(const DwReduceParams& p, hipStream_t s) {
   const int64_t n = (int64_t)p.Nout * (p.kfeat + 1);
-  hipLaunchKernelGGL(dw_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, p);
+  hipLaunchKernelGGL(dw_reduce_kernel, dim3((unsigned)((4 * n + 255) / 256)), dim3(256), 0, s, p);
 }
 
 }  // namespace gpu

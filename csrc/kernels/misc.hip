@@ -17,44 +17,75 @@ namespace gpu {
 
 namespace {
 
-template <typename T>
+// Softmax-cross-entropy forward + backward, one thread per sample.  For
+// N <= 16 classes (ldl % 4 == 0) the row is held in registers after 16-byte
+// loads; the three statistics are reduced per workgroup in LDS and leave as
+// one atomic each per workgroup.
+template <typename T, int NMAX>
 __global__ void __launch_bounds__(256) softmax_xent_kernel(XentParams p) {
+  __shared__ float red[3][4];
   const int row = blockIdx.x * blockDim.x + threadIdx.x;
   float loss = 0.f, mse = 0.f, correct = 0.f;
   if (row < p.M) {
     const float* l = p.logits + (size_t)row * p.ldl;
     const int sample = p.labels_idx ? p.labels_idx[row] : row;
     const int label = p.labels[sample];
-    float m = l[0];
+    float v[NMAX > 0 ? NMAX : 1];
+    if constexpr (NMAX > 0) {
+#pragma unroll
+      for (int j = 0; j < NMAX; j += 4) {
+        if (j < p.N) {
+          const float4 q = *reinterpret_cast<const float4*>(l + j);
+          v[j] = q.x; v[j + 1] = q.y; v[j + 2] = q.z; v[j + 3] = q.w;
+        }
+      }
+    }
+    auto at = [&](int j) { return NMAX > 0 ? v[j] : l[j]; };
+    float m = at(0);
     int am = 0;
-    for (int j = 1; j < p.N; ++j)
-      if (l[j] > m) { m = l[j]; am = j; }  // first max wins (cnn.c:510)
-    float s = 0.f;
-    for (int j = 0; j < p.N; ++j) s += __expf(l[j] - m);
-    const float inv = 1.f / s;
-    loss = __logf(s) - (l[label] - m);
+#pragma unroll
+    for (int j = 1; j < (NMAX > 0 ? NMAX : 1 << 30); ++j) {
+      if (j >= p.N) break;
+      if (at(j) > m) { m = at(j); am = j; }  // first max wins (cnn.c:510)
+    }
+    float sum = 0.f;
+#pragma unroll
+    for (int j = 0; j < (NMAX > 0 ? NMAX : 1 << 30); ++j) {
+      if (j >= p.N) break;
+      sum += __expf(at(j) - m);
+    }
+    const float inv = 1.f / sum;
+    loss = __logf(sum) - (at(label) - m);
     correct = (am == label) ? 1.f : 0.f;
-    T* d = static_cast<T*>(p.dlogits);
-    for (int j = 0; j < p.N; ++j) {
-      const float pj = __expf(l[j] - m) * inv;
+    T* d = p.dlogits ? static_cast<T*>(p.dlogits) + (size_t)row * p.ldd : nullptr;
+#pragma unroll
+    for (int j = 0; j < (NMAX > 0 ? NMAX : 1 << 30); ++j) {
+      if (j >= p.N) break;
+      const float pj = __expf(at(j) - m) * inv;
       const float e = pj - (j == label ? 1.f : 0.f);
       mse += e * e;
-      if (d) d[(size_t)row * p.ldd + j] = from_f<T>(e * p.scale);
+      if (d) d[j] = from_f<T>(e * p.scale);
       if (p.probs) p.probs[(size_t)row * p.N + j] = pj;
     }
     mse /= (float)p.N;
     if (p.pred) p.pred[row] = am;
   }
-  // wave reduce (64 lanes) then one atomic per wave
+  // wave reduce (64 lanes), then across the workgroup's waves in LDS
   for (int o = 32; o > 0; o >>= 1) {
     loss += __shfl_xor(loss, o);
     mse += __shfl_xor(mse, o);
     correct += __shfl_xor(correct, o);
   }
-  if ((threadIdx.x & 63) == 0 && p.stats) {
-    atomicAdd(p.stats + 0, loss);
-    atomicAdd(p.stats + 1, mse);
-    atomicAdd(p.stats + 2, correct);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    red[0][w] = loss;
+    red[1][w] = mse;
+    red[2][w] = correct;
+  }
+  __syncthreads();
+  if (threadIdx.x < 3 && p.stats) {
+    const float t = (red[threadIdx.x][0] + red[threadIdx.x][1]) + (red[threadIdx.x][2] + red[threadIdx.x][3]);
+    atomicAdd(p.stats + threadIdx.x, t);
   }
 }
 
@@ -141,8 +172,14 @@ inline unsigned grid_for(int64_t n, int per_thread = 1) {
 void softmax_xent(DType t, const XentParams& p, hipStream_t s) {
   MCC_CHECK(p.M > 0 && p.N > 0, "softmax_xent: empty");
   const dim3 grid((unsigned)cdiv(p.M, 256)), block(256);
-  if (t == DType::BF16) hipLaunchKernelGGL(softmax_xent_kernel<bf16>, grid, block, 0, s, p);
-  else hipLaunchKernelGGL(softmax_xent_kernel<float>, grid, block, 0, s, p);
+  const bool vec = p.N <= 16 && p.ldl % 4 == 0 && (reinterpret_cast<uintptr_t>(p.logits) & 15) == 0;
+  if (t == DType::BF16) {
+    if (vec) hipLaunchKernelGGL((softmax_xent_kernel<bf16, 16>), grid, block, 0, s, p);
+    else hipLaunchKernelGGL((softmax_xent_kernel<bf16, 0>), grid, block, 0, s, p);
+  } else {
+    if (vec) hipLaunchKernelGGL((softmax_xent_kernel<float, 16>), grid, block, 0, s, p);
+    else hipLaunchKernelGGL((softmax_xent_kernel<float, 0>), grid, block, 0, s, p);
+  }
 }
 
 void sgd_update(float* params, const float* grads, float* mom, int64_t n, float lr, float mu, float wd,
