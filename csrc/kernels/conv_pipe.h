@@ -12,7 +12,7 @@ namespace gpu {
 namespace {
 
 
-constexpr int kT = 256;  // threads per workgroup (4 waves)
+constexpr int kT = 256;  // default threads per workgroup (4 waves); kernels take NT
 enum { FE_POOL = 0, FE_ACT = 1, FE_PLAIN = 2 };
 
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
@@ -79,8 +79,8 @@ __device__ __forceinline__ uint32_t relu_mask(uint32_t d, uint32_t y) {
   return d & (lo | hi);
 }
 
-// Per-thread staging of one image group: items e = tid + i*kT (i < NI).
-template <int MODE>
+// Per-thread staging of one image group: items e = tid + i*NT (i < NI).
+template <int MODE, int NT = kT>
 struct Loader {
   static constexpr int W = ModeInfo<MODE>::W, NI = ModeInfo<MODE>::NI;
   int im[NI];     // image within the group, -1: no item
@@ -93,7 +93,7 @@ struct Loader {
     const int total = imgs * s.per_img;
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
-      const int e = threadIdx.x + i * kT;
+      const int e = threadIdx.x + i * NT;
       im[i] = -1; soff[i] = 0; dst[i] = 0; fl[i] = 0;
 #pragma unroll
       for (int k = 0; k < W; ++k) r[i][k] = 0;

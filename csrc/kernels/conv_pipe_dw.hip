@@ -58,8 +58,8 @@ __global__ void __launch_bounds__(kT) conv_dw_pipe_kernel(ConvDwPipeParams p) {
   zero_lds(dys, p.ppad * drow + 8);
   if (tid < 8) ones[tid] = (bf16)1.0f;
   row_table(ptab, opix, false, p.OW, p.cs, p.ty0, p.tx0, sx.LWp, S1 ? 1 : sx.CL);
-  Loader<XM> lx;
-  Loader<DM> ld;
+  Loader<XM, kT> lx;
+  Loader<DM, kT> ld;
   lx.init(sx, p.imgs);
   ld.init(sd, p.imgs);
   int grp = blockIdx.x;

@@ -38,8 +38,8 @@ __device__ __forceinline__ float swap8(float v) {
   return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x128, 0xf, 0xf, false));
 }
 
-template <int MODE, int EPI, int ACT, bool PAIR = false>
-__global__ void __launch_bounds__(kT) conv_pipe_fwd_kernel(ConvPipeParams p) {
+template <int MODE, int EPI, int ACT, bool PAIR, int NT>
+__global__ void __launch_bounds__(NT) conv_pipe_fwd_kernel(ConvPipeParams p) {
   constexpr int MT = 4;
   constexpr bool S1 = MODE == PM_U8S1;
   constexpr bool pool = EPI == FE_POOL;
@@ -67,16 +67,16 @@ __global__ void __launch_bounds__(kT) conv_pipe_fwd_kernel(ConvPipeParams p) {
   {
     const bf16* wpk = static_cast<const bf16*>(p.wpk);
     const int vpr = p.kpad >> 3, nv = ntiles * 16 * vpr;
-    for (int v = tid; v < nv; v += kT) {
+    for (int v = tid; v < nv; v += NT) {
       const int r = v / vpr, c = (v - r * vpr) * 8;
       store8(ws + r * wld + c, load8(wpk + (size_t)r * p.kpad + c));
     }
   }
-  for (int n = tid; n < ntiles * 16; n += kT) {
+  for (int n = tid; n < ntiles * 16; n += NT) {
     const int c = PAIR ? (n & 7) : n;
     bias_s[n] = (EPI != FE_PLAIN && c < p.Cout) ? p.bias[c] : 0.f;
   }
-  for (int gi = tid; gi < (p.nchunks + 2) * 4; gi += kT) {
+  for (int gi = tid; gi < (p.nchunks + 2) * 4; gi += NT) {
     int off = 0;
     if (S1) {
       if (gi < p.KS) off = gi * s.LWp;
@@ -92,13 +92,13 @@ __global__ void __launch_bounds__(kT) conv_pipe_fwd_kernel(ConvPipeParams p) {
   }
   row_table(ptab, rows_img, pool, p.OW, p.cs, p.ty0, p.tx0, s.LWp, S1 ? 1 : s.CL, PAIR);
   if (S1) {  // bake the shifted-copy choice into the table (IMG and K offsets are multiples of 4)
-    for (int r = tid; r < rows_img; r += kT) {
+    for (int r = tid; r < rows_img; r += NT) {
       const int b = ptab[r], c = b & 3;
       ptab[r] = c * s.CS + b - c;
     }
   }
 
-  Loader<MODE> ld;
+  Loader<MODE, NT> ld;
   ld.init(s, p.imgs);
   int grp = blockIdx.x;
   if (grp < p.ngroups) ld.load(s, grp * p.imgs, p.N);
@@ -120,7 +120,7 @@ __global__ void __launch_bounds__(kT) conv_pipe_fwd_kernel(ConvPipeParams p) {
     const int M = nimg * rows_img;
     const int mtiles = cdiv(M, 16), mgroups = cdiv(mtiles, MT);
     const int ko_s0 = ktab[g], ko_s1 = ktab[4 + g];  // XL_S1: at most two chunks, item-invariant
-    for (int item = wave; item < ((p.ablate & 2) ? 0 : ntiles * mgroups); item += kT / 64) {
+    for (int item = wave; item < ((p.ablate & 2) ? 0 : ntiles * mgroups); item += NT / 64) {
       const int nt = ntiles == 1 ? 0 : item / mgroups, mg = item - nt * mgroups;
       // rows past M (last tile of a partial group) re-read row M-1: finite, discarded
       int base[MT], ti[MT];
@@ -312,8 +312,9 @@ bool conv_pipe_plan(ConvPipeParams& p) {
   p.kpad = p.nchunks * 32;
   // images per group: prefetch items within the thread budget, LDS ~64 KB
   const int ni = mode_ni(s.mode);
-  if (s.per_img > ni * kT) return false;
-  int imgs = std::max(1, std::min(16, ni * kT / std::max(1, s.per_img)));
+  const int nt = p.pair ? 512 : 256;
+  if (s.per_img > ni * nt) return false;
+  int imgs = std::max(1, std::min(16, ni * nt / std::max(1, s.per_img)));
   for (; imgs >= 1; --imgs) {
     p.imgs = imgs;
     if (s1) s.CS = r8h(imgs * s.IMG + 8);
@@ -340,18 +341,21 @@ void conv_pipe_forward(const ConvPipeParams& pin, hipStream_t st) {
   p.ngroups = cdiv(p.N, p.imgs);
   p.grid = std::min(p.ngroups, kCUs * wgs_per_cu(p.lds, 4));
   if (p.grid <= 0) return;
-  const dim3 grid((unsigned)p.grid), block(kT);
+  // the single-channel pair kernel has long per-group MFMA phases: 8 waves
+  // hide more LDS latency; the others are barrier-bound at 4 waves
+  const int nt = p.pair ? 512 : 256;
+  const dim3 grid((unsigned)p.grid), block((unsigned)nt);
   auto go = [&](auto kern) { hipLaunchKernelGGL(kern, grid, block, p.lds, st, p); };
 #define MCC_PIPE_EPI(MODE)                                                                      \
-  if (p.epi == FE_POOL) go(conv_pipe_fwd_kernel<MODE, FE_POOL, ACT_RELU>);                      \
-  else if (p.epi == FE_PLAIN) go(conv_pipe_fwd_kernel<MODE, FE_PLAIN, ACT_NONE>);               \
-  else if (p.act == ACT_RELU) go(conv_pipe_fwd_kernel<MODE, FE_ACT, ACT_RELU>);                 \
-  else if (p.act == ACT_TANH) go(conv_pipe_fwd_kernel<MODE, FE_ACT, ACT_TANH>);                 \
-  else go(conv_pipe_fwd_kernel<MODE, FE_ACT, ACT_NONE>);
+  if (p.epi == FE_POOL) go(conv_pipe_fwd_kernel<MODE, FE_POOL, ACT_RELU, false, 256>);                      \
+  else if (p.epi == FE_PLAIN) go(conv_pipe_fwd_kernel<MODE, FE_PLAIN, ACT_NONE, false, 256>);               \
+  else if (p.act == ACT_RELU) go(conv_pipe_fwd_kernel<MODE, FE_ACT, ACT_RELU, false, 256>);                 \
+  else if (p.act == ACT_TANH) go(conv_pipe_fwd_kernel<MODE, FE_ACT, ACT_TANH, false, 256>);                 \
+  else go(conv_pipe_fwd_kernel<MODE, FE_ACT, ACT_NONE, false, 256>);
   if (p.pair) {
-    if (p.epi == FE_POOL) go(conv_pipe_fwd_kernel<PM_U8S1, FE_POOL, ACT_RELU, true>);
-    else if (p.act == ACT_RELU) go(conv_pipe_fwd_kernel<PM_U8S1, FE_ACT, ACT_RELU, true>);
-    else go(conv_pipe_fwd_kernel<PM_U8S1, FE_ACT, ACT_NONE, true>);
+    if (p.epi == FE_POOL) go(conv_pipe_fwd_kernel<PM_U8S1, FE_POOL, ACT_RELU, true, 512>);
+    else if (p.act == ACT_RELU) go(conv_pipe_fwd_kernel<PM_U8S1, FE_ACT, ACT_RELU, true, 512>);
+    else go(conv_pipe_fwd_kernel<PM_U8S1, FE_ACT, ACT_NONE, true, 512>);
     return;
   }
   switch (p.in.mode) {
