@@ -24,7 +24,7 @@ sys.path.insert(0, ROOT)
 
 BASELINE_IMG_S = 2510.0  # best reference number (8-rank MPI CPU)
 METRIC = "images/sec (whole node), LeNet-5 MNIST-shaped, at 1/2/4/8 MI355X"
-DEFAULT_BATCH = {"lenet5": 16384, "ref": 16384, "cifar3": 4096, "vgg11": 32}
+DEFAULT_BATCH = {"lenet5": 16384, "ref": 16384, "cifar3": 4096, "vgg11": 256}
 
 
 def metric_for(model):

@@ -341,6 +341,38 @@ PYBIND11_MODULE(_C, m) {
         py::arg("C") = 0, py::arg("ldc") = 0, py::arg("Cf") = 0, py::arg("dbg") = 0, py::arg("ablate") = 0,
         py::arg("stream") = 0);
   k.def("fc_supported", &gpu::fc_supported);
+  k.def("igemm_conv_supported", &gpu::igemm_conv_supported);
+  k.def("igemm_conv",
+        [](int B, int H, int W, int C, int N, int KS, int stride, int pad, uintptr_t in, uintptr_t w, int ldw,
+           uintptr_t bias, bool bias_act, int act, uintptr_t out, int ldo, uintptr_t s) {
+          gpu::IgemmParams p;
+          p.B = B; p.H = H; p.W = W; p.C = C; p.N = N; p.KS = KS; p.stride = stride; p.pad = pad;
+          p.OH = (H + 2 * pad - KS) / stride + 1; p.OW = (W + 2 * pad - KS) / stride + 1;
+          p.M = B * p.OH * p.OW; p.K = KS * KS * C;
+          p.in = ptr<void>(in); p.w = ptr<void>(w); p.ldw = ldw;
+          p.bias = ptr<float>(bias); p.epi_bias_act = bias_act; p.act = act;
+          p.out = ptr<void>(out); p.ldo = ldo;
+          gpu::igemm_conv(p, stream_of(s));
+        },
+        py::arg("B"), py::arg("H"), py::arg("W"), py::arg("C"), py::arg("N"), py::arg("KS"), py::arg("stride"),
+        py::arg("pad"), py::arg("input"), py::arg("w"), py::arg("ldw"), py::arg("bias") = 0,
+        py::arg("bias_act") = true, py::arg("act") = 0, py::arg("out") = 0, py::arg("ldo") = 0,
+        py::arg("stream") = 0);
+  k.def("igemm_dw_splitk", &gpu::igemm_dw_splitk);
+  k.def("igemm_dw",
+        [](int B, int H, int W, int C, int Cout, int KS, int stride, int pad, uintptr_t dz, int ldz, uintptr_t in,
+           uintptr_t slab, int64_t slab_stride, int splitk, uintptr_t gw, uintptr_t gb, float beta, uintptr_t s) {
+          gpu::IgemmDwParams p;
+          p.B = B; p.H = H; p.W = W; p.C = C; p.Cout = Cout; p.KS = KS; p.stride = stride; p.pad = pad;
+          p.OH = (H + 2 * pad - KS) / stride + 1; p.OW = (W + 2 * pad - KS) / stride + 1;
+          p.M = B * p.OH * p.OW; p.kf = KS * KS * C;
+          p.dz = ptr<void>(dz); p.ldz = ldz; p.in = ptr<void>(in);
+          p.slab = ptr<float>(slab); p.slab_stride = slab_stride; p.splitk = splitk;
+          gpu::igemm_dw(p, ptr<float>(gw), ptr<float>(gb), beta, stream_of(s));
+        },
+        py::arg("B"), py::arg("H"), py::arg("W"), py::arg("C"), py::arg("Cout"), py::arg("KS"), py::arg("stride"),
+        py::arg("pad"), py::arg("dz"), py::arg("ldz"), py::arg("input"), py::arg("slab"), py::arg("slab_stride"),
+        py::arg("splitk"), py::arg("gw"), py::arg("gb"), py::arg("beta") = 0.f, py::arg("stream") = 0);
   k.def("sgd_update",
         [](uintptr_t p, uintptr_t g, uintptr_t v, int64_t n, float lr, float mu, float wd, uintptr_t s) {
           gpu::sgd_update(ptr<float>(p), ptr<const float>(g), ptr<float>(v), n, lr, mu, wd, stream_of(s));

@@ -118,7 +118,11 @@ std::vector<Bucket> plan_buckets(const ModelSpec& spec, int64_t bucket_bytes) {
     cur.stage_lo = s;
     cur.count += L.nweights + L.nbiases;
     cur.off = L.w_off;
-    if (cur.count * 4 >= bucket_bytes || s == 0) {
+    // Stage 0 finishes LAST in backward, so whatever shares its bucket waits
+    // for it and only the final collective is exposed: cut before it so the
+    // rest of the gradient is reduced while stage 0's dW kernel runs and the
+    // exposed tail is one small (latency-bound) all-reduce.
+    if (cur.count * 4 >= bucket_bytes || s <= 1) {
       out.push_back(cur);
       open = false;
     }

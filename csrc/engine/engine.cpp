@@ -54,6 +54,15 @@ struct GpuNet::Stage {
   // not fit the whole-image LDS kernels
   bool big = false;
   int kgem = 0, kgem_d = 0;      // im2col row strides (fwd/dW, data grad)
+  // implicit-GEMM kernels (igemm.hip) per direction of a large-image conv;
+  // the explicit im2col + GEMM path remains for what they do not cover
+  // (the u8 input layer, C % 64 != 0, strided data gradients, fp32)
+  bool ig_fwd = false, ig_dw = false, ig_dx = false;
+  bool ig_dw0 = false;  // stage 0: im2col rows through the implicit-GEMM dW kernel
+  // large FC layers (VGG heads): no W^T shadow (the data gradient reads the
+  // forward copy K-major) and the weight gradient on the implicit-GEMM dW
+  // kernel as a 1x1 "conv" over the batch
+  bool fc_big = false, fc_igdw = false;
   void* conv_buf = nullptr;      // pre-pool conv output (big + pooled)
   void* dz_buf = nullptr;        // pre-activation gradient at conv-output size (big)
   // persistent pipelined kernels (bf16 small-image layers; geometry planned
@@ -89,6 +98,7 @@ GpuNet::GpuNet(const ModelSpec& spec, DType dtype, int max_batch, int device)
   if (const char* a = std::getenv("MCC_ABLATE")) ablate_ = std::atoi(a);  // kernel diagnostics only
   if (const char* a = std::getenv("MCC_NO_PIPE")) no_pipe_ = std::atoi(a) != 0;  // A/B against conv_small
   if (const char* a = std::getenv("MCC_NO_FC")) no_fc_ = std::atoi(a) != 0;      // A/B against the tiled GEMM
+  if (const char* a = std::getenv("MCC_NO_IGEMM")) no_igemm_ = std::atoi(a) != 0;  // A/B against im2col + GEMM
   if (device_ >= 0) HIP_OK(hipSetDevice(device_));
   else HIP_OK(hipGetDevice(&device_));
   build();
@@ -231,11 +241,20 @@ void GpuNet::build() {
       st.kgem = r8(KK * st.inC);
       st.kgem_d = r8(KK * st.C);
       if (st.big) MCC_CHECK(st.C % 8 == 0, "im2col conv path needs Cout % 8 == 0");
+      st.ig_dw0 = st.big && dtype_ == DType::BF16 && !no_igemm_ && s == 0 && st.C % 8 == 0 &&
+                  (int64_t)max_batch_ * st.OH * st.OW < (1ll << 31);
+      if (st.big && dtype_ == DType::BF16 && !no_igemm_ && s > 0) {
+        st.ig_fwd = gpu::igemm_conv_supported(st.inC, st.C, st.KS);
+        st.ig_dw = st.inC % 8 == 0;
+        st.ig_dx = st.stride == 1 && gpu::igemm_conv_supported(st.C, st.inC, st.KS);
+      }
       if (!st.big && dtype_ == DType::BF16 && !no_pipe_) plan_pipe(st, s == 0);
     } else {
       st.out_elems = st.Nout;
       st.out_ld = r8(st.Nout);
       st.ldp = r8(st.Kin + 1);
+      st.fc_big = (int64_t)st.Nout * st.Kin >= (1 << 20) &&
+                  !(dtype_ == DType::BF16 && !no_fc_ && gpu::fc_supported(st.Kin, st.Nout));
     }
     if (s > 0) {
       const Stage& pv = *stages_[s - 1];
@@ -243,6 +262,9 @@ void GpuNet::build() {
       if (st.kind == Stage::FC) st.in_ld = pv.kind == Stage::FC ? pv.out_ld : (int)pv.out_elems;
     }
     if (st.kind == Stage::FC) MCC_CHECK(st.in_ld % 8 == 0, "fc input leading dim must be a multiple of 8");
+    if (st.kind == Stage::FC)
+      st.fc_igdw = st.fc_big && dtype_ == DType::BF16 && !no_igemm_ && s > 0 && st.Kin % 8 == 0 &&
+                   st.Nout % 8 == 0 && st.in_ld == st.Kin;
   }
 
   // ---- packed weight table ----
@@ -311,17 +333,13 @@ void GpuNet::build() {
           }
       }
     } else {
-      auto perm = [&](int k) {
-        if (st.permC <= 0) return k;
-        const int hw = k / st.permC, c = k % st.permC;
-        return c * st.permHW + hw;
-      };
+      auto perm = [&](int k) { return k; };  // device order == activation order (see set_params)
       const int ldk = r8(st.Kin);
       st.pk_fwd = reserve((int64_t)st.Nout * ldk);
       for (int n = 0; n < st.Nout; ++n)
         for (int k = 0; k < st.Kin; ++k)
           idx[st.pk_fwd + (int64_t)n * ldk + k] = (int32_t)(st.w_off + (int64_t)n * st.Kin + perm(k));
-      if (&st != stages_[0]) {
+      if (&st != stages_[0] && !st.fc_big) {
         st.pk_dx = reserve((int64_t)st.Kin * st.out_ld);
         for (int k = 0; k < st.Kin; ++k)
           for (int n = 0; n < st.Nout; ++n)
@@ -339,16 +357,29 @@ void GpuNet::build() {
     const Stage& st = *sp;
     if (st.kind == Stage::CONV && st.big) {
       const int KK = st.KS * st.KS;
-      col_bytes_ = std::max(col_bytes_, es * (size_t)Bm * st.OH * st.OW * st.kgem);
-      col_bytes_ = std::max(col_bytes_, es * (size_t)Bm * st.inH * st.inW * st.kgem_d);
-      const int sk = dw_splitk(st.C, KK * st.inC + 1, (int64_t)Bm * st.OH * st.OW);
-      scratch = std::max(scratch, (size_t)sk * st.C * r8(KK * st.inC + 1) * 4);
+      const int64_t rows = (int64_t)Bm * st.OH * st.OW;
+      if (!st.ig_fwd || !st.ig_dw) col_bytes_ = std::max(col_bytes_, es * (size_t)rows * st.kgem);
+      if (sp != stages_[0] && !st.ig_dx)
+        col_bytes_ = std::max(col_bytes_, es * (size_t)Bm * st.inH * st.inW * st.kgem_d);
+      if (st.ig_dw0) {
+        const int sk = gpu::igemm_dw_splitk((int)rows, st.C, st.kgem);
+        scratch = std::max(scratch, gpu::igemm_dw_slab_bytes(st.C, st.kgem, sk));
+      } else if (st.ig_dw) {
+        MCC_CHECK(rows < (1ll << 31), "igemm dW: too many pixels per batch");
+        const int sk = gpu::igemm_dw_splitk((int)rows, st.C, KK * st.inC);
+        scratch = std::max(scratch, gpu::igemm_dw_slab_bytes(st.C, KK * st.inC, sk));
+      } else {
+        const int sk = dw_splitk(st.C, KK * st.inC + 1, rows);
+        scratch = std::max(scratch, (size_t)sk * st.C * r8(KK * st.inC + 1) * 4);
+      }
     } else if (st.kind == Stage::CONV) {
       scratch = std::max(scratch, (size_t)st.nx_dw * st.cout_pad * st.ncols_pad * 4);
       if (st.pipe_dw) {
         const size_t nv = (size_t)st.pdw.cout_pad * st.pdw.ncols_pad;
         scratch = std::max(scratch, (st.pdw.grid + ceil_div(st.pdw.grid, 16)) * nv * 4);
       }
+    } else if (st.fc_igdw) {
+      scratch = std::max(scratch, gpu::igemm_dw_slab_bytes(st.Nout, st.Kin, gpu::igemm_dw_splitk(Bm, st.Nout, st.Kin)));
     } else {
       scratch = std::max(scratch, (size_t)dw_splitk(st.Nout, st.Kin + 1, Bm) * st.Nout * st.ldp * 4);
     }
@@ -395,7 +426,7 @@ std::string GpuNet::plan() const {
     if (st.kind == Stage::CONV) {
       os << "  [" << s << "] conv " << st.inC << "x" << st.inH << "x" << st.inW << " -> " << st.C << "x" << st.OH << "x"
          << st.OW << (st.pooled ? " +maxpool" : "") << " k" << st.KS << "s" << st.stride << "p" << st.pad
-         << (st.big ? " im2col+gemm" : (st.cvec ? " lds-cvec" : " lds-scalar")) << " chunks=" << st.nchunks
+         << (st.big ? (st.ig_fwd ? " igemm" : " im2col+gemm") : (st.cvec ? " lds-cvec" : " lds-scalar")) << " chunks=" << st.nchunks
          << " imgs=" << st.imgs_fwd << "/"
          << st.imgs_dx << "/" << st.imgs_dw;
       if (st.pipe_fwd || st.pipe_dx || st.pipe_dw) {
@@ -414,20 +445,59 @@ std::string GpuNet::plan() const {
   return os.str();
 }
 
+// Device parameter layout: the canonical reference layouts (cnn.c:318-342)
+// except the weight of an FC layer fed by a conv, whose columns are kept in
+// the activation (NHWC-flatten) order k = hw*C + c instead of the canonical
+// CHW order c*HW + hw: its packed copy is then a straight cast and its weight
+// gradient needs no scatter.  The host API speaks canonical order only.
+void GpuNet::to_device_order(const float* canon, float* dev) const {
+  std::copy(canon, canon + spec_.nparams, dev);
+  for (const Stage* sp : stages_) {
+    const Stage& st = *sp;
+    if (st.kind != Stage::FC || st.permC <= 0) continue;
+    for (int n = 0; n < st.Nout; ++n) {
+      const float* src = canon + st.w_off + (int64_t)n * st.Kin;
+      float* dst = dev + st.w_off + (int64_t)n * st.Kin;
+      for (int hw = 0; hw < st.permHW; ++hw)
+        for (int c = 0; c < st.permC; ++c) dst[hw * st.permC + c] = src[c * st.permHW + hw];
+    }
+  }
+}
+
+void GpuNet::to_canonical_order(const float* dev, float* canon) const {
+  std::copy(dev, dev + spec_.nparams, canon);
+  for (const Stage* sp : stages_) {
+    const Stage& st = *sp;
+    if (st.kind != Stage::FC || st.permC <= 0) continue;
+    for (int n = 0; n < st.Nout; ++n) {
+      const float* src = dev + st.w_off + (int64_t)n * st.Kin;
+      float* dst = canon + st.w_off + (int64_t)n * st.Kin;
+      for (int hw = 0; hw < st.permHW; ++hw)
+        for (int c = 0; c < st.permC; ++c) dst[c * st.permHW + hw] = src[hw * st.permC + c];
+    }
+  }
+}
+
 void GpuNet::set_params(const float* host) {
-  HIP_OK(hipMemcpy(params_, host, 4 * (size_t)spec_.nparams, hipMemcpyHostToDevice));
+  std::vector<float> d((size_t)spec_.nparams);
+  to_device_order(host, d.data());
+  HIP_OK(hipMemcpy(params_, d.data(), 4 * (size_t)spec_.nparams, hipMemcpyHostToDevice));
   pack(nullptr);
   HIP_OK(hipDeviceSynchronize());
 }
 
 void GpuNet::get_params(float* host) const {
   HIP_OK(hipDeviceSynchronize());
-  HIP_OK(hipMemcpy(host, params_, 4 * (size_t)spec_.nparams, hipMemcpyDeviceToHost));
+  std::vector<float> d((size_t)spec_.nparams);
+  HIP_OK(hipMemcpy(d.data(), params_, 4 * (size_t)spec_.nparams, hipMemcpyDeviceToHost));
+  to_canonical_order(d.data(), host);
 }
 
 void GpuNet::get_grads(float* host) const {
   HIP_OK(hipDeviceSynchronize());
-  HIP_OK(hipMemcpy(host, grads_, 4 * (size_t)spec_.nparams, hipMemcpyDeviceToHost));
+  std::vector<float> d((size_t)spec_.nparams);
+  HIP_OK(hipMemcpy(d.data(), grads_, 4 * (size_t)spec_.nparams, hipMemcpyDeviceToHost));
+  to_canonical_order(d.data(), host);
 }
 
 void GpuNet::pack(hipStream_t s) {
@@ -444,7 +514,19 @@ void GpuNet::forward(const uint8_t* images, const int32_t* idx, int B, hipStream
   const size_t es = dtype_size(dtype_);
   for (size_t si = 0; si < stages_.size(); ++si) {
     Stage& st = *stages_[si];
-    if (st.kind == Stage::CONV && st.big) {
+    if (st.kind == Stage::CONV && st.big && st.ig_fwd) {
+      // implicit GEMM with bias+ReLU epilogue -> 2x2 max-pool
+      gpu::IgemmParams g;
+      g.B = B; g.H = st.inH; g.W = st.inW; g.C = st.inC;
+      g.OH = st.OH; g.OW = st.OW; g.KS = st.KS; g.stride = st.stride; g.pad = st.pad;
+      g.M = B * st.OH * st.OW; g.N = st.C; g.K = st.KS * st.KS * st.inC;
+      g.in = stages_[si - 1]->act_buf;
+      g.w = static_cast<const char*>(packed_) + es * st.pk_fwd; g.ldw = st.kgem;
+      g.bias = params_ + st.b_off; g.epi_bias_act = true; g.act = st.act;
+      g.out = st.pooled ? st.conv_buf : st.act_buf; g.ldo = st.C;
+      gpu::igemm_conv(g, s);
+      if (st.pooled) gpu::maxpool2(dtype_, st.conv_buf, st.act_buf, st.arg_buf, B, st.OH, st.OW, st.C, s);
+    } else if (st.kind == Stage::CONV && st.big) {
       // im2col (input transform fused) -> GEMM with bias+ReLU epilogue -> 2x2 max-pool
       gpu::Im2colParams ic;
       ic.N = B; ic.OH = st.OH; ic.OW = st.OW; ic.KS = st.KS; ic.cs = st.stride; ic.ldk = st.kgem;
@@ -542,7 +624,40 @@ void GpuNet::backward(int hi, int lo, hipStream_t s) {
         const int kf = KK * st.inC;
         // dZ = relu'/unpool(dY) at conv-output size
         gpu::grad_xform(dtype_, dy, st.dz_buf, B, s);
+        if (st.ig_dw0) {
+          // stage 0 (u8 input, few channels): the explicit im2col rows as a 1x1
+          // "conv" through the implicit-GEMM dW kernel (split-K over the pixels)
+          gpu::Im2colParams ic;
+          ic.N = B; ic.OH = st.OH; ic.OW = st.OW; ic.KS = st.KS; ic.cs = st.stride; ic.ldk = st.kgem;
+          ic.s.SH = st.inH; ic.s.SW = st.inW; ic.s.SC = st.inC; ic.s.off = st.pad; ic.s.up = 1;
+          ic.s.mode = gpu::IN_U8; ic.s.src = images_; ic.s.idx = idx_;
+          ic.out = col_;
+          gpu::im2col(dtype_, ic, s);
+          gpu::IgemmDwParams w;
+          w.B = B * st.OH * st.OW; w.H = 1; w.W = 1; w.C = st.kgem;
+          w.OH = 1; w.OW = 1; w.KS = 1; w.stride = 1; w.pad = 0;
+          w.M = w.B; w.Cout = st.C; w.kf = st.kgem; w.kreal = kf;
+          w.perm_c = st.inC; w.perm_hw = KK;  // k = kp*inC + ci  ->  ci*KK + kp
+          w.dz = st.dz_buf; w.ldz = st.C; w.in = col_;
+          w.splitk = gpu::igemm_dw_splitk(w.M, st.C, st.kgem);
+          w.slab = scratch_; w.slab_stride = (int64_t)(st.kgem + 1) * st.C;
+          MCC_CHECK(gpu::igemm_dw_slab_bytes(st.C, st.kgem, w.splitk) <= scratch_bytes_, "igemm dW0 scratch too small");
+          gpu::igemm_dw(w, grads_ + st.w_off, grads_ + st.b_off, 0.f, s);
+        }
+        if (st.ig_dw) {
+          // dW, db: implicit GEMM over the pixels (split-K slabs + ordered reduce)
+          gpu::IgemmDwParams w;
+          w.B = B; w.H = st.inH; w.W = st.inW; w.C = st.inC;
+          w.OH = st.OH; w.OW = st.OW; w.KS = st.KS; w.stride = st.stride; w.pad = st.pad;
+          w.M = B * st.OH * st.OW; w.Cout = st.C; w.kf = kf;
+          w.dz = st.dz_buf; w.ldz = st.C; w.in = stages_[si - 1]->act_buf;
+          w.splitk = gpu::igemm_dw_splitk(w.M, st.C, kf);
+          w.slab = scratch_; w.slab_stride = (int64_t)(kf + 1) * st.C;
+          MCC_CHECK(gpu::igemm_dw_slab_bytes(st.C, kf, w.splitk) <= scratch_bytes_, "igemm dW scratch too small");
+          gpu::igemm_dw(w, grads_ + st.w_off, grads_ + st.b_off, 0.f, s);
+        }
         // dW, db = dZ^T [im2col(X) | 1]  (split-K over B*OH*OW)
+        if (!st.ig_dw && !st.ig_dw0) {
         gpu::Im2colParams ic;
         ic.N = B; ic.OH = st.OH; ic.OW = st.OW; ic.KS = st.KS; ic.cs = st.stride; ic.ldk = st.kgem;
         ic.s.SH = st.inH; ic.s.SW = st.inW; ic.s.SC = st.inC; ic.s.off = st.pad; ic.s.up = 1;
@@ -566,7 +681,19 @@ void GpuNet::backward(int hi, int lo, hipStream_t s) {
         r.gw = grads_ + st.w_off; r.gb = grads_ + st.b_off;
         r.permC = st.inC; r.permHW = KK;  // k = kp*inC + ci  ->  ci*KK + kp
         gpu::dw_reduce(r, s);
-        if (si > 0) {
+        }
+        if (si > 0 && st.ig_dx) {
+          // dX = stride-1 conv of dZ with the flipped weights (pad KS-1-pad)
+          gpu::IgemmParams d;
+          d.B = B; d.H = st.OH; d.W = st.OW; d.C = st.C;
+          d.OH = st.inH; d.OW = st.inW; d.KS = st.KS; d.stride = 1; d.pad = st.KS - 1 - st.pad;
+          d.M = B * st.inH * st.inW; d.N = st.inC; d.K = KK * st.C;
+          d.in = st.dz_buf;
+          d.w = static_cast<const char*>(packed_) + es * st.pk_dx; d.ldw = st.kgem_d;
+          d.epi_bias_act = false;
+          d.out = stages_[si - 1]->grad_buf; d.ldo = st.inC;
+          gpu::igemm_conv(d, s);
+        } else if (si > 0) {
           // dX = im2col(zero-inserted dZ) x flipped W^T
           gpu::Im2colParams id;
           id.N = B; id.OH = st.inH; id.OW = st.inW; id.KS = st.KS; id.cs = 1; id.ldk = st.kgem_d;
@@ -644,6 +771,17 @@ void GpuNet::backward(int hi, int lo, hipStream_t s) {
       }
     } else {
       const Stage& pv = *stages_[si - 1];
+      if (st.fc_igdw) {
+        gpu::IgemmDwParams w;
+        w.B = B; w.H = 1; w.W = 1; w.C = st.Kin;
+        w.OH = 1; w.OW = 1; w.KS = 1; w.stride = 1; w.pad = 0;
+        w.M = B; w.Cout = st.Nout; w.kf = st.Kin;
+        w.dz = st.grad_buf; w.ldz = st.out_ld; w.in = pv.act_buf;
+        w.splitk = gpu::igemm_dw_splitk(B, st.Nout, st.Kin);
+        w.slab = scratch_; w.slab_stride = (int64_t)(st.Kin + 1) * st.Nout;
+        MCC_CHECK(gpu::igemm_dw_slab_bytes(st.Nout, st.Kin, w.splitk) <= scratch_bytes_, "fc dW scratch too small");
+        gpu::igemm_dw(w, grads_ + st.w_off, grads_ + st.b_off, 0.f, s);
+      } else {
       // weight + bias gradient: [Nout][Kin+1] = dZ^T [X | 1], split-K over the batch
       gpu::GemmParams w;
       w.M = st.Nout; w.N = st.Kin + 1; w.K = B;
@@ -658,8 +796,9 @@ void GpuNet::backward(int hi, int lo, hipStream_t s) {
       r.S = sk; r.Nout = st.Nout; r.kfeat = st.Kin; r.ldp = st.ldp; r.part = scratch_;
       r.partial_stride = w.partial_stride;
       r.gw = grads_ + st.w_off; r.gb = grads_ + st.b_off;
-      r.permC = st.permC; r.permHW = st.permHW;
+      r.permC = 0; r.permHW = 0;  // device order (see set_params)
       gpu::dw_reduce(r, s);
+      }
       // data gradient
       if (si > 0 && dtype_ == DType::BF16 && !no_fc_ && gpu::fc_supported(st.Kin, st.Nout)) {
         gpu::FcParams d;
@@ -675,7 +814,11 @@ void GpuNet::backward(int hi, int lo, hipStream_t s) {
         gpu::GemmParams d;
         d.M = B; d.N = st.Kin; d.K = st.Nout;
         d.A = st.grad_buf; d.lda = st.out_ld;
-        d.B = static_cast<const char*>(packed_) + es * st.pk_dx; d.ldb = st.out_ld;
+        if (st.fc_big) {  // the forward copy [Nout][r8(Kin)] read K-major
+          d.B = static_cast<const char*>(packed_) + es * st.pk_fwd; d.ldb = r8(st.Kin); d.tb = true;
+        } else {
+          d.B = static_cast<const char*>(packed_) + es * st.pk_dx; d.ldb = st.out_ld;
+        }
         d.epi = gpu::EPI_DACT;
         d.act = pv.kind == Stage::FC ? pv.act : gpu::ACT_NONE;  // conv masks are applied by its staging
         d.aux = pv.act_buf; d.ldaux = st.in_ld;

@@ -67,6 +67,8 @@ struct ModelSpec {
 // and is fused into the conv before it).  Buckets walk the stages from the
 // LAST one (first to finish in backward) and cut whenever the gradient bytes
 // reach `bucket_bytes`; each bucket is a contiguous range of the flat buffer.
+// Stage 0 (the last to finish) always gets a bucket of its own, so the big
+// collective overlaps its weight-gradient kernel.
 struct Bucket {
   int stage_hi = 0, stage_lo = 0;  // inclusive, stage_hi >= stage_lo
   int64_t off = 0, count = 0;      // elements of the flat fp32 gradient

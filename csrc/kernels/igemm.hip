@@ -1,0 +1,451 @@
+// Implicit-GEMM convolution for large images (VGG-11 @ 224^2, bf16, NHWC).
+//
+// Replaces the explicit im2col + GEMM pair of the large-image path (the im2col
+// matrix of a VGG layer is up to 1.9 GB per step and was written and re-read
+// once per direction).  Reference math: Layer_feedForw_conv / Layer_feedBack_conv
+// (cnn.c:175-247), with the correct OIHW indexing of CUDAcnn.cu:167-195.
+//
+//   forward   out[m][n]  = act(bias[n] + sum_k X(m, k) W[n][k])
+//   data grad dX[m][n]   = sum_k dZ(m, k) Wflip[n][k]   (same kernel: stride-1
+//             conv of dZ with pad KS-1-pad and the flipped/transposed weights)
+//   weights   dW[co][k]  = sum_m dZ[m][co] X(m, k),  db = dZ^T 1 (ones column)
+//
+// where m is an output pixel (b, oy, ox), k = (ky*KS + kx)*C + c, and
+// X(m, k) = in[b][oy*s - pad + ky][ox*s - pad + kx][c] (0 outside the image)
+// is never materialised: each 16-byte piece (8 channels of one tap) of an
+// operand tile is fetched straight into LDS by global_load_lds_dwordx4 with a
+// per-lane source address; padding taps and tile tails point at a zero page.
+//
+// gfx950 structure (cdna_hip_programming.md §5): 256 threads = 4 waves (2x2),
+// 128x128 output tile per workgroup, BK = 64, two LDS buffers (64 KiB, two
+// workgroups per CU), one barrier per K-step, bijective XCD-aware tile order
+// (T1).  The LDS images are lane-linear (glds) with the bank swizzle applied
+// on the SOURCE address and undone on the read (§5.4 rule 21):
+//   * [rows][64] images (128-byte rows, ds_read_b128 fragments): 16-byte slot
+//     s of row r holds logical slot s ^ ((r >> 1) & 7) -> conflict-free reads
+//     of 16 rows at one k range;
+//   * [64][128] images (256-byte rows, ds_read_b64_tr_b16 fragments of the
+//     weight gradient, K = pixel axis): slot s of row r holds s ^ f(r),
+//     f(r) = 2*(r & 3) + 8*((r >> 3) & 1) -> the 8 rows read by a 32-lane
+//     group land on 8 distinct 32-byte bank ranges.
+// The forward computes C^T (MFMA A = weights, B = pixels) so a lane's four
+// accumulators are four consecutive channels of one pixel: one 8-byte NHWC
+// store.  The weight gradient computes dW[co][k] per tile into fp32 split-K
+// slabs laid out [k][co] (16-byte stores), reduced by a deterministic pass.
+#include "kernels.h"
+#include "mfma.h"
+
+#include <algorithm>
+
+namespace mcc {
+namespace gpu {
+
+namespace {
+
+typedef __attribute__((address_space(1))) void gvoid;
+typedef __attribute__((address_space(3))) void lvoid;
+
+constexpr int kIgT = 256;  // threads per workgroup
+constexpr int kIgBM = 128;
+constexpr int kIgBK = 64;
+
+// zero page (and a bf16 "1, 0 x 7" piece for the ones column), >= 16 bytes each
+__device__ __attribute__((aligned(64))) const unsigned short kIgZero[32] = {0};
+__device__ __attribute__((aligned(64))) const unsigned short kIgOnes[32] = {0x3f80};
+
+__device__ __forceinline__ void glds16(const void* src, bf16* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((gvoid*)src, (lvoid*)lds_wave_base, 16, 0, 0);
+}
+
+// bijective XCD-aware remap (cdna_hip_programming.md §5, T1): consecutive
+// logical tiles land on the same XCD (8 XCDs, blocks dealt round-robin)
+__device__ __forceinline__ int xcd_remap(int orig, int nwg) {
+  const int q = nwg >> 3, r = nwg & 7, xcd = orig & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+}
+
+__device__ __forceinline__ int mdiv(const DivMagic& d, int n) {  // exact n / d (Div in mfma.h)
+  const uint32_t u = (uint32_t)n;
+  return (int)((u * d.mh + __umulhi(u, d.ml)) >> 8);
+}
+DivMagic magic(int d) {
+  const Div v = Div::host(d);
+  DivMagic r;
+  r.mh = v.mh; r.ml = v.ml;
+  return r;
+}
+
+__device__ __forceinline__ int swz64(int row) { return (row >> 1) & 7; }
+__device__ __forceinline__ int swz128(int row) { return 2 * (row & 3) + 8 * ((row >> 3) & 1); }
+
+// ---------------------------------------------------------------------------
+// forward / data gradient
+// ---------------------------------------------------------------------------
+template <int BN, bool BIAS_ACT>
+__global__ void __launch_bounds__(kIgT, 2) igemm_conv_kernel(IgemmParams p) {
+  constexpr int BM = kIgBM;
+  constexpr int AJ = BM * 8 / kIgT;  // glds per thread for the pixel tile (4)
+  constexpr int BJ = BN * 8 / kIgT;  // ... and for the weight tile (4 or 2)
+  constexpr int IMG = (BM + BN) * kIgBK;  // elements per buffer
+  constexpr int FM = 4;              // pixel fragments per wave (64 rows)
+  constexpr int FN = BN / 32;        // channel fragments per wave (BN/2 cols)
+  __shared__ __attribute__((aligned(16))) bf16 smem[2 * IMG];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r16 = lane & 15, g = lane >> 4;
+  const int wm = wave >> 1, wn = wave & 1;
+
+  const int ntn = cdiv(p.N, BN);
+  const int nwg = gridDim.x;
+  const int tile = xcd_remap(blockIdx.x, nwg);
+  const int tn = tile % ntn, tm = tile / ntn;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const bf16* in = static_cast<const bf16*>(p.in);
+  const bf16* w = static_cast<const bf16*>(p.w);
+  const bf16* zero = reinterpret_cast<const bf16*>(kIgZero);
+
+  // ---- per-thread staging geometry (fixed for the whole K loop) ----
+  int a_iy[AJ], a_ix[AJ], a_base[AJ], a_seg[AJ];
+#pragma unroll
+  for (int j = 0; j < AJ; ++j) {
+    const int s = j * kIgT + tid;
+    const int row = s >> 3;
+    a_seg[j] = ((s & 7) ^ swz64(row)) * 8;
+    const int m = m0 + row;
+    if (m < p.M) {
+      const int b = mdiv(p.div_ohw, m), rem = m - b * p.OH * p.OW;
+      const int oy = mdiv(p.div_ow, rem), ox = rem - oy * p.OW;
+      a_iy[j] = oy * p.stride - p.pad;
+      a_ix[j] = ox * p.stride - p.pad;
+      a_base[j] = ((b * p.H + a_iy[j]) * p.W + a_ix[j]) * p.C;
+    } else {
+      a_iy[j] = -(1 << 20);  // fails every bounds test
+      a_ix[j] = 0;
+      a_base[j] = 0;
+    }
+  }
+  const bf16* b_ptr[BJ];
+#pragma unroll
+  for (int j = 0; j < BJ; ++j) {
+    const int s = j * kIgT + tid;
+    const int row = s >> 3;
+    const int n = n0 + row;
+    b_ptr[j] = n < p.N ? w + (size_t)n * p.ldw + ((s & 7) ^ swz64(row)) * 8 : nullptr;
+  }
+
+  const int nk = p.K / kIgBK;  // host guarantees K % 64 == 0 and C % 64 == 0
+  auto stage = [&](int kt, int buf) {
+    const int k0 = kt * kIgBK;
+    const int tap = k0 / p.C;  // wave-uniform
+    const int c0 = k0 - tap * p.C;
+    const int ky = tap / p.KS, kx = tap - ky * p.KS;
+    const int toff = (ky * p.W + kx) * p.C + c0;
+    bf16* A = smem + buf * IMG;
+    bf16* Bw = A + BM * kIgBK;
+#pragma unroll
+    for (int j = 0; j < AJ; ++j) {
+      const int iy = a_iy[j] + ky, ix = a_ix[j] + kx;
+      const bool ok = (unsigned)iy < (unsigned)p.H && (unsigned)ix < (unsigned)p.W;
+      const bf16* src = ok ? in + (a_base[j] + toff + a_seg[j]) : zero;
+      glds16(src, A + (j * kIgT + wave * 64) * 8);
+    }
+#pragma unroll
+    for (int j = 0; j < BJ; ++j) {
+      const bf16* src = b_ptr[j] ? b_ptr[j] + k0 : zero;
+      glds16(src, Bw + (j * kIgT + wave * 64) * 8);
+    }
+  };
+
+  f32x4 acc[FN][FM];
+#pragma unroll
+  for (int i = 0; i < FN; ++i)
+#pragma unroll
+    for (int j = 0; j < FM; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  stage(0, 0);
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < nk) stage(kt + 1, buf ^ 1);
+    const bf16* A = smem + buf * IMG;
+    const bf16* Bw = A + BM * kIgBK;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int seg = 4 * h + g;
+      bf16x8 xa[FM], wb[FN];
+#pragma unroll
+      for (int f = 0; f < FM; ++f) {
+        const int row = wm * 64 + f * 16 + r16;
+        xa[f] = load8(A + row * kIgBK + ((seg ^ swz64(row)) << 3));
+      }
+#pragma unroll
+      for (int f = 0; f < FN; ++f) {
+        const int row = wn * (BN / 2) + f * 16 + r16;
+        wb[f] = load8(Bw + row * kIgBK + ((seg ^ swz64(row)) << 3));
+      }
+#pragma unroll
+      for (int i = 0; i < FN; ++i)
+#pragma unroll
+        for (int j = 0; j < FM; ++j) acc[i][j] = mma(acc[i][j], wb[i], xa[j]);
+    }
+    __syncthreads();
+  }
+
+  // ---- epilogue: lane holds channels 4g..4g+3 of pixel r16 per fragment ----
+  bf16* out = static_cast<bf16*>(p.out);
+#pragma unroll
+  for (int i = 0; i < FN; ++i) {
+    const int ch = n0 + wn * (BN / 2) + i * 16 + 4 * g;
+    if (ch >= p.N) continue;
+    float bv[4] = {0.f, 0.f, 0.f, 0.f};
+    if (BIAS_ACT && p.bias) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) bv[e] = p.bias[ch + e];
+    }
+#pragma unroll
+    for (int j = 0; j < FM; ++j) {
+      const int m = m0 + wm * 64 + j * 16 + r16;
+      if (m >= p.M) continue;
+      float v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v[e] = acc[i][j][e] + bv[e];
+        if (BIAS_ACT) v[e] = act_apply(p.act, v[e]);
+      }
+      const bf16x4 o = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+      *reinterpret_cast<bf16x4*>(out + (size_t)m * p.ldo + ch) = o;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// weight gradient (split-K over pixels)
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(kIgT, 2) igemm_dw_kernel(IgemmDwParams p) {
+  constexpr int BM = 128, BN = 128, BK = 64;  // co x k x pixels
+  constexpr int J = BK * 16 / kIgT;            // glds per thread per operand (4)
+  constexpr int IMG = (BM + BN) * BK;
+  __shared__ __attribute__((aligned(16))) bf16 smem[2 * IMG];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r16 = lane & 15, g = lane >> 4;
+  const int q = r16 >> 2, pp = r16 & 3;
+  const int wm = wave >> 1, wn = wave & 1;
+
+  const int ntm = cdiv(p.Cout, BM), ntn = cdiv(p.kf + 1, BN);
+  const int ntiles = ntm * ntn;
+  const int id = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = id % p.splitk, tile = id / p.splitk;
+  if (tile >= ntiles) return;
+  const int tm = tile % ntm, tn = tile / ntm;
+  const int co0 = tm * BM, k0 = tn * BN;
+  const int nks = cdiv(p.M, BK);
+  const int per = cdiv(nks, p.splitk);
+  const int ks0 = split * per, ks1 = min(nks, ks0 + per);
+
+  const bf16* dz = static_cast<const bf16*>(p.dz);
+  const bf16* in = static_cast<const bf16*>(p.in);
+  const bf16* zero = reinterpret_cast<const bf16*>(kIgZero);
+  const bf16* ones = reinterpret_cast<const bf16*>(kIgOnes);
+
+  // per-thread staging geometry: row (pixel within the K-step) and the
+  // logical 16-byte slot (8 output channels / 8 im2col columns)
+  int d_row[J], d_col[J];
+  int x_ky[J], x_kx[J], x_c[J], x_kind[J];  // kind: 0 tap, 1 ones, 2 zero
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    const int s = j * kIgT + tid;
+    const int row = s >> 4;
+    const int ls = (s & 15) ^ swz128(row);
+    d_row[j] = row;
+    d_col[j] = co0 + ls * 8;
+    const int k = k0 + ls * 8;
+    if (k < p.kf) {
+      const int tap = k / p.C;
+      x_c[j] = k - tap * p.C;
+      x_ky[j] = tap / p.KS;
+      x_kx[j] = tap - x_ky[j] * p.KS;
+      x_kind[j] = 0;
+    } else {
+      x_c[j] = 0; x_ky[j] = 0; x_kx[j] = 0;
+      x_kind[j] = k == p.kf ? 1 : 2;
+    }
+  }
+
+  auto stage = [&](int ks, int buf) {
+    bf16* D = smem + buf * IMG;
+    bf16* X = D + BK * BM;
+    const int mb = ks * BK;
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+      const int m = mb + d_row[j];
+      const bool mok = m < p.M;
+      const bf16* dsrc = (mok && d_col[j] < p.Cout) ? dz + (size_t)m * p.ldz + d_col[j] : zero;
+      glds16(dsrc, D + (j * kIgT + wave * 64) * 8);
+      const bf16* xsrc = zero;
+      if (mok) {
+        if (x_kind[j] == 0) {
+          const int b = mdiv(p.div_ohw, m), rem = m - b * p.OH * p.OW;
+          const int oy = mdiv(p.div_ow, rem), ox = rem - oy * p.OW;
+          const int iy = oy * p.stride - p.pad + x_ky[j], ix = ox * p.stride - p.pad + x_kx[j];
+          if ((unsigned)iy < (unsigned)p.H && (unsigned)ix < (unsigned)p.W)
+            xsrc = in + (((size_t)b * p.H + iy) * p.W + ix) * p.C + x_c[j];
+        } else if (x_kind[j] == 1) {
+          xsrc = ones;
+        }
+      }
+      glds16(xsrc, X + (j * kIgT + wave * 64) * 8);
+    }
+  };
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // transpose-read of a [BK][128] image: 4 consecutive K rows (pixels) of
+  // 16 columns; lane 4q+p of a 16-lane group addresses row kr+q, columns 4p..
+  auto tr = [&](const bf16* img, int kr, int col0) {
+    const int row = kr + q;
+    const int col = col0 + 4 * pp;
+    return tr4(img + row * 128 + (((col >> 3) ^ swz128(row)) << 3) + (col & 7));
+  };
+
+  if (ks0 < ks1) {
+    stage(ks0, 0);
+    __syncthreads();
+    for (int ks = ks0; ks < ks1; ++ks) {
+      const int buf = (ks - ks0) & 1;
+      if (ks + 1 < ks1) stage(ks + 1, buf ^ 1);
+      const bf16* D = smem + buf * IMG;
+      const bf16* X = D + BK * BM;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int kr = 32 * h + 8 * g;
+        bf16x8 a[4], b[4];
+#pragma unroll
+        for (int f = 0; f < 4; ++f) {
+          const bf16x4 lo = tr(D, kr, wm * 64 + f * 16), hi = tr(D, kr + 4, wm * 64 + f * 16);
+          a[f] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+        }
+#pragma unroll
+        for (int f = 0; f < 4; ++f) {
+          const bf16x4 lo = tr(X, kr, wn * 64 + f * 16), hi = tr(X, kr + 4, wn * 64 + f * 16);
+          b[f] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[i][j] = mma(acc[i][j], a[i], b[j]);
+      }
+      __syncthreads();
+    }
+  }
+
+  // slab[split][k][co]: lane holds co 4g..4g+3 of column k = r16
+  float* slab = p.slab + (size_t)split * p.slab_stride;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int co = co0 + wm * 64 + i * 16 + 4 * g;
+    if (co >= p.Cout) continue;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int k = k0 + wn * 64 + j * 16 + r16;
+      if (k > p.kf) continue;
+      *reinterpret_cast<f32x4*>(slab + (size_t)k * p.Cout + co) = acc[i][j];
+    }
+  }
+}
+
+// gw[co][c*KK + tap] (+)= sum_s slab[s][tap*C + c][co];  gb[co] from k == kf.
+// One thread per (k, co), co fastest: coalesced slab reads, fixed-order sum.
+__global__ void __launch_bounds__(256) igemm_dw_reduce_kernel(IgemmDwParams p, float* gw, float* gb, float beta) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t total = (int64_t)(p.kf + 1) * p.Cout;
+  if (t >= total) return;
+  const int k = (int)(t / p.Cout), co = (int)(t - (int64_t)k * p.Cout);
+  const float* src = p.slab + t;
+  float a0 = 0.f, a1 = 0.f;
+  int s = 0;
+  for (; s + 1 < p.splitk; s += 2) {
+    a0 += src[(size_t)s * p.slab_stride];
+    a1 += src[(size_t)(s + 1) * p.slab_stride];
+  }
+  if (s < p.splitk) a0 += src[(size_t)s * p.slab_stride];
+  const float v = a0 + a1;
+  float* dst;
+  const int kreal = p.kreal > 0 ? p.kreal : p.kf;
+  if (k < p.kf && k >= kreal) return;
+  if (k < p.kf && p.perm_c > 0) {
+    const int hw = k / p.perm_c, c = k - hw * p.perm_c;
+    dst = gw + (size_t)co * kreal + (size_t)c * p.perm_hw + hw;
+  } else if (k < p.kf) {
+    const int tap = k / p.C, c = k - tap * p.C;
+    dst = gw + ((size_t)co * p.C + c) * (p.KS * p.KS) + tap;
+  } else {
+    dst = gb + co;
+  }
+  *dst = beta != 0.f ? beta * *dst + v : v;
+}
+
+template <int BN, bool BA>
+void launch_conv(const IgemmParams& p, hipStream_t s) {
+  const int nwg = cdiv(p.M, kIgBM) * cdiv(p.N, BN);
+  hipLaunchKernelGGL((igemm_conv_kernel<BN, BA>), dim3((unsigned)nwg), dim3(kIgT), 0, s, p);
+}
+
+}  // namespace
+
+bool igemm_conv_supported(int C, int N, int KS) {
+  return C % 64 == 0 && N % 8 == 0 && (KS * KS * C) % kIgBK == 0;
+}
+
+void igemm_conv(const IgemmParams& p0, hipStream_t s) {
+  IgemmParams p = p0;
+  MCC_CHECK(igemm_conv_supported(p.C, p.N, p.KS), "igemm_conv: needs C % 64 == 0 and N % 8 == 0");
+  MCC_CHECK(p.K == p.KS * p.KS * p.C, "igemm_conv: K must be KS*KS*C");
+  MCC_CHECK(p.M == p.B * p.OH * p.OW && p.M > 0, "igemm_conv: M must be B*OH*OW");
+  MCC_CHECK(p.ldw >= p.K && p.ldw % 8 == 0 && p.ldo >= p.N && p.ldo % 4 == 0, "igemm_conv: bad leading dims");
+  MCC_CHECK((int64_t)p.B * p.H * p.W * p.C < (1ll << 31), "igemm_conv: input exceeds 2^31 elements");
+  MCC_CHECK(p.OH == (p.H + 2 * p.pad - p.KS) / p.stride + 1 && p.OW == (p.W + 2 * p.pad - p.KS) / p.stride + 1,
+            "igemm_conv: output geometry mismatch");
+  p.div_ohw = magic(p.OH * p.OW);
+  p.div_ow = magic(p.OW);
+  const bool ba = p.epi_bias_act;
+  if (p.N <= 64) {
+    if (ba) launch_conv<64, true>(p, s); else launch_conv<64, false>(p, s);
+  } else {
+    if (ba) launch_conv<128, true>(p, s); else launch_conv<128, false>(p, s);
+  }
+}
+
+int igemm_dw_splitk(int M, int Cout, int kf) {
+  const int tiles = cdiv(Cout, 128) * cdiv(kf + 1, 128);
+  const int nks = cdiv(M, kIgBK);
+  int sk = std::max(1, 1024 / tiles);         // ~4 workgroups per CU in flight
+  sk = std::min(sk, std::max(1, nks / 8));    // >= 8 K-steps per slice
+  return std::min(sk, 1024);
+}
+
+size_t igemm_dw_slab_bytes(int Cout, int kf, int splitk) { return (size_t)splitk * (kf + 1) * Cout * 4; }
+
+void igemm_dw(const IgemmDwParams& p0, float* gw, float* gb, float beta, hipStream_t s) {
+  IgemmDwParams p = p0;
+  MCC_CHECK(p.C % 8 == 0 && p.Cout % 8 == 0 && p.kf == p.KS * p.KS * p.C, "igemm_dw: needs C, Cout % 8 == 0");
+  MCC_CHECK(p.M == p.B * p.OH * p.OW && p.M > 0 && p.ldz >= p.Cout && p.ldz % 8 == 0, "igemm_dw: bad shapes");
+  MCC_CHECK((int64_t)p.B * p.H * p.W * p.C < (1ll << 31), "igemm_dw: input exceeds 2^31 elements");
+  MCC_CHECK(p.splitk >= 1 && p.slab_stride >= (int64_t)(p.kf + 1) * p.Cout, "igemm_dw: bad split/slab");
+  MCC_CHECK(p.kreal == 0 || (p.KS == 1 && p.kreal <= p.kf), "igemm_dw: kreal needs KS == 1");
+  MCC_CHECK(p.perm_c == 0 || (p.KS == 1 && (int64_t)p.perm_c * p.perm_hw == (p.kreal ? p.kreal : p.kf)),
+            "igemm_dw: bad permutation");
+  p.div_ohw = magic(p.OH * p.OW);
+  p.div_ow = magic(p.OW);
+  const int nwg = cdiv(p.Cout, 128) * cdiv(p.kf + 1, 128) * p.splitk;
+  hipLaunchKernelGGL(igemm_dw_kernel, dim3((unsigned)nwg), dim3(kIgT), 0, s, p);
+  const int64_t total = (int64_t)(p.kf + 1) * p.Cout;
+  hipLaunchKernelGGL(igemm_dw_reduce_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, p, gw, gb, beta);
+}
+
+}  // namespace gpu
+}  // namespace mcc

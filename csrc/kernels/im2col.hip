@@ -135,6 +135,89 @@ __global__ void __launch_bounds__(256) grad_xform_kernel(StageSrc s, T* __restri
   }
 }
 
+// bf16, C % 8 == 0: one thread per (pixel, 8 channels), 16-byte moves,
+// 32-bit index math (host checks the element count).
+__global__ void __launch_bounds__(256) maxpool2_vec_kernel(const bf16* __restrict__ in, bf16* __restrict__ out,
+                                                           uint8_t* __restrict__ arg, int N, int H, int W, int C) {
+  const int PH = H >> 1, PW = W >> 1, C8 = C >> 3;
+  const int total = N * PH * PW * C8;
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
+    const int c8 = e % C8, r = e / C8;
+    const int px = r % PW, r2 = r / PW, py = r2 % PH, n = r2 / PH;
+    const size_t b = (((size_t)n * H + 2 * py) * W + 2 * px) * C + c8 * 8;
+    const bf16x8 v0 = load8(in + b), v1 = load8(in + b + C), v2 = load8(in + b + (size_t)W * C),
+                 v3 = load8(in + b + (size_t)W * C + C);
+    bf16x8 o;
+    uint32_t a0 = 0, a1 = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float best = (float)v0[j];
+      uint32_t a = 0;
+      if ((float)v1[j] > best) { best = (float)v1[j]; a = 1; }
+      if ((float)v2[j] > best) { best = (float)v2[j]; a = 2; }
+      if ((float)v3[j] > best) { best = (float)v3[j]; a = 3; }
+      o[j] = (bf16)best;
+      if (j < 4) a0 |= a << (8 * j); else a1 |= a << (8 * (j - 4));
+    }
+    store8(out + (size_t)r * C + c8 * 8, o);
+    *reinterpret_cast<uint2*>(arg + (size_t)r * C + c8 * 8) = make_uint2(a0, a1);
+  }
+}
+
+// dZ = relu' (IN_RELU) or unpool + relu' (IN_UNPOOL) of dY, bf16, C % 8 == 0.
+// UNPOOL: one thread per (pooled pixel, 8 channels) writes the whole 2x2
+// window (odd-size borders beyond the last window are written as zero).
+__global__ void __launch_bounds__(256) grad_xform_vec_kernel(StageSrc s, bf16* __restrict__ dz, int N) {
+  const int C8 = s.SC >> 3;
+  const bf16* dy = static_cast<const bf16*>(s.src);
+  const bf16* y = static_cast<const bf16*>(s.aux_y);
+  if (s.mode == IN_RELU) {
+    const int total = N * s.SH * s.SW * C8;
+    for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
+      const bf16x8 d = load8(dy + (size_t)e * 8), yv = load8(y + (size_t)e * 8);
+      bf16x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = (float)yv[j] > 0.f ? d[j] : (bf16)0.f;
+      store8(dz + (size_t)e * 8, o);
+    }
+    return;
+  }
+  const int total = N * s.PH * s.PW * C8;
+  for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
+    const int c8 = e % C8, r = e / C8;
+    const int px = r % s.PW, r2 = r / s.PW, py = r2 % s.PH, n = r2 / s.PH;
+    const bf16x8 d = load8(dy + (size_t)e * 8), yv = load8(y + (size_t)e * 8);
+    const uint2 av = *reinterpret_cast<const uint2*>(s.aux_arg + (size_t)e * 8);
+    bf16x8 o[4];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const uint32_t a = ((j < 4 ? av.x : av.y) >> (8 * (j & 3))) & 0xffu;
+      const bf16 v = (float)yv[j] > 0.f ? d[j] : (bf16)0.f;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) o[q][j] = a == (uint32_t)q ? v : (bf16)0.f;
+    }
+    const size_t b = (((size_t)n * s.SH + 2 * py) * s.SW + 2 * px) * s.SC + c8 * 8;
+    store8(dz + b, o[0]);
+    store8(dz + b + s.SC, o[1]);
+    store8(dz + b + (size_t)s.SW * s.SC, o[2]);
+    store8(dz + b + (size_t)s.SW * s.SC + s.SC, o[3]);
+  }
+  // odd borders (conv output row/column past the last full window)
+  if ((s.SH & 1) || (s.SW & 1)) {
+    const int rows = s.SH & 1, cols = s.SW & 1;
+    const int per = (rows ? s.SW : 0) + (cols ? s.SH - rows : 0);
+    const int tot = N * per * C8;
+    const bf16x8 z = {};
+    for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < tot; e += gridDim.x * blockDim.x) {
+      const int c8 = e % C8, r = e / C8, n = r / per, k = r - n * per;
+      int yy, xx;
+      if (rows && k < s.SW) { yy = s.SH - 1; xx = k; }
+      else { yy = k - (rows ? s.SW : 0); xx = s.SW - 1; }
+      store8(dz + (((size_t)n * s.SH + yy) * s.SW + xx) * s.SC + c8 * 8, z);
+    }
+  }
+}
+
 inline unsigned grid_cap(int64_t n) {
   int64_t b = (n + 255) / 256;
   if (b < 1) b = 1;
@@ -153,6 +236,11 @@ void im2col(DType t, const Im2colParams& p, hipStream_t s) {
 
 void maxpool2(DType t, const void* in, void* out, uint8_t* arg, int N, int H, int W, int C, hipStream_t s) {
   const int64_t n = (int64_t)N * (H / 2) * (W / 2) * C;
+  if (t == DType::BF16 && C % 8 == 0 && (int64_t)N * H * W * C < (1ll << 31)) {
+    hipLaunchKernelGGL(maxpool2_vec_kernel, dim3(grid_cap(n / 8)), dim3(256), 0, s, static_cast<const bf16*>(in),
+                       static_cast<bf16*>(out), arg, N, H, W, C);
+    return;
+  }
   if (t == DType::BF16)
     hipLaunchKernelGGL(maxpool2_kernel<bf16>, dim3(grid_cap(n)), dim3(256), 0, s, static_cast<const bf16*>(in),
                        static_cast<bf16*>(out), arg, N, H, W, C);
@@ -163,6 +251,11 @@ void maxpool2(DType t, const void* in, void* out, uint8_t* arg, int N, int H, in
 
 void grad_xform(DType t, const StageSrc& src, void* dz, int N, hipStream_t s) {
   const int64_t n = (int64_t)N * src.SH * src.SW * src.SC;
+  if (t == DType::BF16 && src.SC % 8 == 0 && n < (1ll << 31) &&
+      (src.mode == IN_RELU || (src.mode == IN_UNPOOL && src.PH == src.SH / 2 && src.PW == src.SW / 2))) {
+    hipLaunchKernelGGL(grad_xform_vec_kernel, dim3(grid_cap(n / 8)), dim3(256), 0, s, src, static_cast<bf16*>(dz), N);
+    return;
+  }
   if (t == DType::BF16)
     hipLaunchKernelGGL(grad_xform_kernel<bf16>, dim3(grid_cap(n)), dim3(256), 0, s, src, static_cast<bf16*>(dz), N);
   else

@@ -275,6 +275,51 @@ void maxpool2(DType t, const void* in, void* out, uint8_t* arg, int N, int H, in
 // dz[n][y][x][c] = transform(src) at the conv-output grid (SH x SW x SC)
 void grad_xform(DType t, const StageSrc& src, void* dz, int N, hipStream_t s);
 
+// ---------------------------------------------------------------------------
+// Implicit-GEMM convolution for large images (igemm.hip, bf16 NHWC): no
+// im2col matrix; 16-byte pieces of the implicit operand are DMA'd straight
+// into LDS.  Forward / data gradient:
+//   out[m][n] = epi(sum_k in(m, k) w[n][k]),  m = (b, oy, ox),
+//   k = (ky*KS + kx)*C + c,  in(m, k) = in[b][oy*stride-pad+ky][ox*stride-pad+kx][c]
+struct DivMagic { uint32_t mh = 0, ml = 0; };  // exact division by a constant (set at launch)
+struct IgemmParams {
+  int B = 0, H = 0, W = 0, C = 0;    // input NHWC
+  int OH = 0, OW = 0, KS = 1, stride = 1, pad = 0;
+  int M = 0, N = 0, K = 0;           // M = B*OH*OW, N = out channels, K = KS*KS*C
+  const void* in = nullptr;          // bf16 [B][H][W][C]
+  const void* w = nullptr;           // bf16 [N][ldw], k order as above
+  int ldw = 0;
+  const float* bias = nullptr;       // [N] (epi_bias_act)
+  bool epi_bias_act = true;          // false: plain store (data gradient)
+  int act = ACT_RELU;
+  void* out = nullptr;               // bf16 [M][ldo]
+  int ldo = 0;
+  DivMagic div_ohw, div_ow;
+};
+bool igemm_conv_supported(int C, int N, int KS);
+void igemm_conv(const IgemmParams& p, hipStream_t s);
+
+// Weight gradient: dW[co][k] = sum_m dz[m][co] in(m, k), db[co] = sum_m dz[m][co],
+// split-K over m into fp32 slabs [splitk][kf+1][Cout], then reduced into the
+// canonical gw[Cout][C][KS][KS], gb[Cout] (grad = beta*grad + sum).
+struct IgemmDwParams {
+  int B = 0, H = 0, W = 0, C = 0;
+  int OH = 0, OW = 0, KS = 1, stride = 1, pad = 0;
+  int M = 0, Cout = 0, kf = 0;       // kf = KS*KS*C
+  const void* dz = nullptr;          // bf16 [M][ldz]
+  int ldz = 0;
+  const void* in = nullptr;          // bf16 [B][H][W][C]
+  float* slab = nullptr;
+  int64_t slab_stride = 0;           // >= (kf+1)*Cout
+  int splitk = 1;
+  int perm_c = 0, perm_hw = 0;       // KS == 1 only: feature k = hw*perm_c + c -> c*perm_hw + hw
+  int kreal = 0;                     // KS == 1 only: features >= kreal (< kf) are padding, dropped (0: kf)
+  DivMagic div_ohw, div_ow;
+};
+int igemm_dw_splitk(int M, int Cout, int kf);
+size_t igemm_dw_slab_bytes(int Cout, int kf, int splitk);
+void igemm_dw(const IgemmDwParams& p, float* gw, float* gb, float beta, hipStream_t s);
+
 void conv_forward(DType t, const ConvParams& p, hipStream_t s);
 size_t conv_forward_lds_bytes(DType t, const ConvParams& p);
 void conv_dw(DType t, const ConvDwParams& p, hipStream_t s);

@@ -89,6 +89,68 @@ __global__ void __launch_bounds__(256) softmax_xent_kernel(XentParams p) {
   }
 }
 
+// Wide class counts (ImageNet-style heads): one wave per row, lanes stride
+// over the classes, shuffle reductions; same outputs and tie rule as above.
+template <typename T>
+__global__ void __launch_bounds__(256) softmax_xent_wide_kernel(XentParams p) {
+  __shared__ float red[3][4];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int row = blockIdx.x * 4 + w;
+  float loss = 0.f, mse = 0.f, correct = 0.f;
+  if (row < p.M) {
+    const float* l = p.logits + (size_t)row * p.ldl;
+    const int sample = p.labels_idx ? p.labels_idx[row] : row;
+    const int label = p.labels[sample];
+    float m = -INFINITY;
+    int am = 0x7fffffff;
+    for (int j = lane; j < p.N; j += 64) {
+      const float x = l[j];
+      if (x > m) { m = x; am = j; }
+    }
+    for (int o = 32; o > 0; o >>= 1) {  // max, smallest index among equal maxima (first max wins)
+      const float om = __shfl_xor(m, o);
+      const int oa = __shfl_xor(am, o);
+      if (om > m || (om == m && oa < am)) { m = om; am = oa; }
+    }
+    float sum = 0.f;
+    for (int j = lane; j < p.N; j += 64) sum += __expf(l[j] - m);
+    for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
+    const float inv = 1.f / sum;
+    T* d = p.dlogits ? static_cast<T*>(p.dlogits) + (size_t)row * p.ldd : nullptr;
+    for (int j = lane; j < p.N; j += 64) {
+      const float pj = __expf(l[j] - m) * inv;
+      const float e = pj - (j == label ? 1.f : 0.f);
+      mse += e * e;
+      if (d) d[j] = from_f<T>(e * p.scale);
+      if (p.probs) p.probs[(size_t)row * p.N + j] = pj;
+    }
+    for (int o = 32; o > 0; o >>= 1) mse += __shfl_xor(mse, o);
+    mse /= (float)p.N;
+    if (lane == 0) {
+      loss = __logf(sum) - (l[label] - m);
+      correct = am == label ? 1.f : 0.f;
+      if (p.pred) p.pred[row] = am;
+    } else {
+      mse = 0.f;
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    loss += __shfl_xor(loss, o);
+    mse += __shfl_xor(mse, o);
+    correct += __shfl_xor(correct, o);
+  }
+  if (lane == 0) {
+    red[0][w] = loss;
+    red[1][w] = mse;
+    red[2][w] = correct;
+  }
+  __syncthreads();
+  if (threadIdx.x < 3 && p.stats) {
+    const float t = (red[threadIdx.x][0] + red[threadIdx.x][1]) + (red[threadIdx.x][2] + red[threadIdx.x][3]);
+    atomicAdd(p.stats + threadIdx.x, t);
+  }
+}
+
 __global__ void sgd_kernel(float* __restrict__ w, const float* __restrict__ g, float* __restrict__ v, int64_t n,
                            float lr, float mu, float wd) {
   const int64_t n4 = n >> 2;
@@ -173,6 +235,12 @@ void softmax_xent(DType t, const XentParams& p, hipStream_t s) {
   MCC_CHECK(p.M > 0 && p.N > 0, "softmax_xent: empty");
   const dim3 grid((unsigned)cdiv(p.M, 256)), block(256);
   const bool vec = p.N <= 16 && p.ldl % 4 == 0 && (reinterpret_cast<uintptr_t>(p.logits) & 15) == 0;
+  if (p.N > 64) {
+    const dim3 g4((unsigned)cdiv(p.M, 4));
+    if (t == DType::BF16) hipLaunchKernelGGL(softmax_xent_wide_kernel<bf16>, g4, block, 0, s, p);
+    else hipLaunchKernelGGL(softmax_xent_wide_kernel<float>, g4, block, 0, s, p);
+    return;
+  }
   if (t == DType::BF16) {
     if (vec) hipLaunchKernelGGL((softmax_xent_kernel<bf16, 16>), grid, block, 0, s, p);
     else hipLaunchKernelGGL((softmax_xent_kernel<bf16, 0>), grid, block, 0, s, p);

@@ -11,9 +11,13 @@ fail loudly on CPU tensors: there is no eager fallback.
     linear_wgrad(dy, x)             (dW, db) = (dy.T @ x, dy.sum(0)) (split-K, ones-column bias)
     softmax_xent(logits, labels)    dlogits, loss_sum, mse_sum, correct
     sgd_(p, g, mom, lr, mu, wd)     in-place SGD / momentum / weight decay
+    conv2d_nhwc(x, w, b, s, p, act) y = act(conv2d(x, w) + b), NHWC bf16 (implicit-GEMM MFMA)
+    conv2d_dgrad_nhwc(dy, w, ...)   dx of a stride-1 conv (the same kernel on flipped weights)
+    conv2d_wgrad_nhwc(dy, x, ...)   (dW OIHW fp32, db fp32) split-K implicit GEMM
 
 Reference counterparts: Layer_feedForw_full / Layer_feedBack_full
-(cnn.c:113-173), the softmax + error of cnn.c:125-143,275-287 and
+(cnn.c:113-173), Layer_feedForw_conv / Layer_feedBack_conv (cnn.c:175-247) and
+the CUDA offload forward_convolution_layer (CUDAcnn.cu:167-218), the softmax + error of cnn.c:125-143,275-287 and
 Layer_update (cnn.c:303-314).
 """
 
@@ -146,4 +150,71 @@ def sgd_(param: torch.Tensor, grad: torch.Tensor, mom: torch.Tensor | None = Non
     return param
 
 
-__all__ = ["linear", "linear_dgrad", "linear_wgrad", "softmax_xent", "sgd_"]
+def _conv_geom(H, W, KS, stride, pad):
+    return (H + 2 * pad - KS) // stride + 1, (W + 2 * pad - KS) // stride + 1
+
+
+def pack_conv_weight(w: torch.Tensor) -> torch.Tensor:
+    """OIHW -> [O][(kh*KS + kw)*I + i] bf16 (the implicit-GEMM K order)."""
+    O, I, KH, KW = w.shape
+    return w.permute(0, 2, 3, 1).reshape(O, KH * KW * I).to(torch.bfloat16).contiguous()
+
+
+def conv2d_nhwc(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None = None, stride: int = 1, pad: int = 0,
+                act: str = "none") -> torch.Tensor:
+    """y = act(conv2d(x, w, b)) on channels-last bf16: x [B, H, W, C] (C % 64 == 0), w OIHW -> y [B, OH, OW, O]."""
+    _check(x, b)
+    if x.dtype != torch.bfloat16:
+        raise RuntimeError("conv2d_nhwc: bf16 activations")
+    B, H, W, C = x.shape
+    O, I, KS, KS2 = w.shape
+    if I != C or KS != KS2 or not _K.igemm_conv_supported(C, O, KS):
+        raise RuntimeError("conv2d_nhwc: needs square kernels, C % 64 == 0 and O % 8 == 0")
+    wp = pack_conv_weight(w)
+    OH, OW = _conv_geom(H, W, KS, stride, pad)
+    y = torch.empty(B, OH, OW, O, dtype=torch.bfloat16, device=x.device)
+    bias = b.float().contiguous() if b is not None else None
+    _K.igemm_conv(B, H, W, C, O, KS, stride, pad, x.data_ptr(), wp.data_ptr(), wp.shape[1],
+                  bias=bias.data_ptr() if bias is not None else 0, bias_act=True, act=_ACT[act], out=y.data_ptr(),
+                  ldo=O, stream=_stream())
+    return y
+
+
+def conv2d_dgrad_nhwc(dy: torch.Tensor, w: torch.Tensor, pad: int = 0) -> torch.Tensor:
+    """dx of a stride-1 conv: dy [B, OH, OW, O] bf16 (O % 64 == 0), w OIHW -> dx [B, H, W, I]."""
+    _check(dy)
+    B, OH, OW, O = dy.shape
+    Oc, I, KS, _ = w.shape
+    if Oc != O or not _K.igemm_conv_supported(O, I, KS):
+        raise RuntimeError("conv2d_dgrad_nhwc: needs O % 64 == 0 and I % 8 == 0")
+    wf = w.flip(2, 3).permute(1, 2, 3, 0).reshape(I, KS * KS * O).to(torch.bfloat16).contiguous()
+    pd = KS - 1 - pad
+    H, W = _conv_geom(OH, OW, KS, 1, pd)
+    dx = torch.empty(B, H, W, I, dtype=torch.bfloat16, device=dy.device)
+    _K.igemm_conv(B, OH, OW, O, I, KS, 1, pd, dy.data_ptr(), wf.data_ptr(), wf.shape[1], bias_act=False,
+                  out=dx.data_ptr(), ldo=I, stream=_stream())
+    return dx
+
+
+def conv2d_wgrad_nhwc(dy: torch.Tensor, x: torch.Tensor, KS: int, stride: int = 1, pad: int = 0, splitk: int = 0):
+    """(dW [O, I, KS, KS] fp32, db [O] fp32) for dy [B, OH, OW, O], x [B, H, W, I] bf16 NHWC."""
+    _check(dy, x)
+    B, H, W, C = x.shape
+    O = dy.shape[3]
+    OH, OW = _conv_geom(H, W, KS, stride, pad)
+    if tuple(dy.shape) != (B, OH, OW, O) or C % 8 or O % 8:
+        raise RuntimeError("conv2d_wgrad_nhwc: shape mismatch or channels not multiples of 8")
+    kf = KS * KS * C
+    M = B * OH * OW
+    if splitk <= 0:
+        splitk = _K.igemm_dw_splitk(M, O, kf)
+    slab = torch.empty(splitk, kf + 1, O, dtype=torch.float32, device=x.device)
+    gw = torch.empty(O, C, KS, KS, dtype=torch.float32, device=x.device)
+    gb = torch.empty(O, dtype=torch.float32, device=x.device)
+    _K.igemm_dw(B, H, W, C, O, KS, stride, pad, dy.data_ptr(), O, x.data_ptr(), slab.data_ptr(), (kf + 1) * O,
+                splitk, gw.data_ptr(), gb.data_ptr(), stream=_stream())
+    return gw, gb
+
+
+__all__ = ["linear", "linear_dgrad", "linear_wgrad", "softmax_xent", "sgd_", "conv2d_nhwc", "conv2d_dgrad_nhwc",
+           "conv2d_wgrad_nhwc", "pack_conv_weight"]

@@ -64,6 +64,10 @@ def test_plan_buckets_cover_reverse_order():
                 hi_prev = lo
                 end = off
             assert end == 0
+            # the last stage to finish in backward (stage 0) is reduced alone
+            assert b[-1][0] == 0 and b[-1][1] == 0
+            if mb >= 4 and name in ("ref", "lenet5", "cifar3"):
+                assert len(b) == 2  # small models: one big collective + the stage-0 tail
 
 
 # ------------------------------------------------------------ CPU oracle

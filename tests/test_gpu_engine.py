@@ -148,6 +148,43 @@ def test_im2col_gemm_conv_path_matches_torch(cuda, dtype):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("no_igemm", [False, True])
+def test_igemm_conv_path_matches_torch(cuda, no_igemm, monkeypatch):
+    """Large-image path on implicit-GEMM kernels (bf16, C % 64 == 0 layers:
+    forward with the bias+ReLU epilogue, the flipped-weight data gradient and
+    the split-K weight gradient) vs the fp64 oracle; the same model with
+    MCC_NO_IGEMM=1 runs the explicit im2col + GEMM path."""
+    if no_igemm:
+        monkeypatch.setenv("MCC_NO_IGEMM", "1")
+    spec = mcc.parse_model_spec("input 3 80 80; conv 64 k3 s1 p1 relu; pool 2; conv 64 k3 s1 p1 relu; "
+                                "conv 128 k3 s1 p1 relu; pool 2; fc 32 relu; fc 10 softmax", "big80")
+    B = 5
+    imgs, labels = mcc.synth_dataset(B, 3, 80, 80, 10, seed=5)
+    params = mcc.init_params(spec, seed=3).astype(np.float32)
+    net = mcc.GpuNet(spec, "bf16", B)
+    plan = net.plan()
+    assert ("igemm" in plan) != no_igemm, plan
+    net.set_params(params)
+    d_img = torch.from_numpy(imgs).to(cuda)
+    d_lab = torch.from_numpy(labels).to(cuda)
+    s = torch.cuda.current_stream().cuda_stream
+    net.zero_stats(s)
+    net.forward(d_img.data_ptr(), 0, B, s)
+    net.loss(d_lab.data_ptr(), 0, 1.0 / B, True, s)
+    net.backward_all(s)
+    torch.cuda.synchronize()
+    ref_logits, ref_grads, _ = _oracle(spec, params, imgs, labels)
+    assert _relerr(net.get_logits(B), ref_logits) < TOL["bf16"]["logit"]
+    grads = net.get_grads()
+    for L in spec.layers():
+        if L["nweights"] == 0:
+            continue
+        for off, n, what in ((L["w_off"], L["nweights"], "W"), (L["b_off"], L["nbiases"], "b")):
+            err = _relerr(grads[off : off + n], ref_grads[off : off + n])
+            assert err < 0.15, f"{L['kind']} {what} rel err {err:.3e}"
+
+
+@pytest.mark.gpu
 def test_vgg11_step_runs(cuda):
     spec = mcc.make_model("vgg11")
     B = 4

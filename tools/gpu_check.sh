@@ -3,7 +3,7 @@
 set -o pipefail
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
-timeout -k 10 400 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1; echo "pytest rc=$?" >> gpurun_out/pytest_gpu.log
+timeout -k 10 400 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1; echo "pytest rc=$?" >> gpurun_out/pytest_gpu.log
 tail -5 gpurun_out/pytest_gpu.log
 for b in 4096 16384 65536; do
   timeout -k 10 200 python bench.py --steps 30 --warmup 5 --batch-per-gpu $b >> gpurun_out/bench_sweep.log 2>&1 || { echo "bench $b failed"; exit 1; }

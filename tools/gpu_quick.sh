@@ -3,7 +3,7 @@
 set -o pipefail
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
-timeout -k 10 400 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1; rc=$?
+timeout -k 10 400 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1; rc=$?
 tail -4 gpurun_out/pytest_gpu.log; echo "pytest rc=$rc"
 [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit 1
 timeout -k 10 200 python bench.py ${BENCH_ARGS:-} > gpurun_out/bench.log 2>&1 || { tail gpurun_out/bench.log; exit 1; }
