@@ -59,6 +59,7 @@ struct GpuNet::Stage {
   // (the u8 input layer, C % 64 != 0, strided data gradients, fp32)
   bool ig_fwd = false, ig_dw = false, ig_dx = false;
   bool ig_dw0 = false;  // stage 0: im2col rows through the implicit-GEMM dW kernel
+  bool ig_pool = false; // forward max-pool fused into the implicit-GEMM epilogue
   // large FC layers (VGG heads): no W^T shadow (the data gradient reads the
   // forward copy K-major) and the weight gradient on the implicit-GEMM dW
   // kernel as a 1x1 "conv" over the batch
@@ -79,8 +80,8 @@ static inline int r32(int x) { return (x + 31) & ~31; }
 // aim for ~512 workgroups of 64x64 tiles, each slice >= 128 rows.
 static inline int dw_splitk(int M, int N, int64_t K) {
   const int64_t tiles = ceil_div(M, 64) * ceil_div(N, 64);
-  int64_t sk = std::max<int64_t>(1, std::min<int64_t>(512 / std::max<int64_t>(1, tiles), K / 128));
-  return (int)std::min<int64_t>(sk, 64);
+  int64_t sk = std::max<int64_t>(1, std::min<int64_t>(512 / std::max<int64_t>(1, tiles), K / 64));
+  return (int)std::min<int64_t>(sk, 256);
 }
 
 static inline int act_kind(Act a) {
@@ -243,11 +244,14 @@ void GpuNet::build() {
       if (st.big) MCC_CHECK(st.C % 8 == 0, "im2col conv path needs Cout % 8 == 0");
       st.ig_dw0 = st.big && dtype_ == DType::BF16 && !no_igemm_ && s == 0 && st.C % 8 == 0 &&
                   (int64_t)max_batch_ * st.OH * st.OW < (1ll << 31);
+      // first layer forward: u8 gather through registers (K = KS*KS*inC small)
+      if (st.ig_dw0 && st.KS * st.KS * st.inC <= 64) st.ig_fwd = true;
       if (st.big && dtype_ == DType::BF16 && !no_igemm_ && s > 0) {
         st.ig_fwd = gpu::igemm_conv_supported(st.inC, st.C, st.KS);
         st.ig_dw = st.inC % 8 == 0;
         st.ig_dx = st.stride == 1 && gpu::igemm_conv_supported(st.C, st.inC, st.KS);
       }
+      st.ig_pool = st.ig_fwd && st.pooled && st.OH % 2 == 0 && st.OW % 2 == 0;
       if (!st.big && dtype_ == DType::BF16 && !no_pipe_) plan_pipe(st, s == 0);
     } else {
       st.out_elems = st.Nout;
@@ -262,9 +266,11 @@ void GpuNet::build() {
       if (st.kind == Stage::FC) st.in_ld = pv.kind == Stage::FC ? pv.out_ld : (int)pv.out_elems;
     }
     if (st.kind == Stage::FC) MCC_CHECK(st.in_ld % 8 == 0, "fc input leading dim must be a multiple of 8");
+    // FC weight gradient on the implicit-GEMM dW kernel (a 1x1 "conv" over the
+    // batch, C = in_ld with the pad columns dropped by the reduce)
     if (st.kind == Stage::FC)
-      st.fc_igdw = st.fc_big && dtype_ == DType::BF16 && !no_igemm_ && s > 0 && st.Kin % 8 == 0 &&
-                   st.Nout % 8 == 0 && st.in_ld == st.Kin;
+      st.fc_igdw = dtype_ == DType::BF16 && !no_igemm_ && s > 0 && st.Nout % 4 == 0 && st.out_ld % 8 == 0 &&
+                   st.in_ld % 8 == 0 && st.in_ld >= st.Kin && (int64_t)st.Nout * st.Kin >= 8192;
   }
 
   // ---- packed weight table ----
@@ -379,10 +385,16 @@ void GpuNet::build() {
         scratch = std::max(scratch, (st.pdw.grid + ceil_div(st.pdw.grid, 16)) * nv * 4);
       }
     } else if (st.fc_igdw) {
-      scratch = std::max(scratch, gpu::igemm_dw_slab_bytes(st.Nout, st.Kin, gpu::igemm_dw_splitk(Bm, st.Nout, st.Kin)));
+      scratch = std::max(scratch, gpu::igemm_dw_slab_bytes(st.Nout, st.in_ld, gpu::igemm_dw_splitk(Bm, st.Nout, st.in_ld)));
     } else {
       scratch = std::max(scratch, (size_t)dw_splitk(st.Nout, st.Kin + 1, Bm) * st.Nout * st.ldp * 4);
     }
+  }
+  for (Stage* sp : stages_) {
+    const Stage& st = *sp;
+    if (st.kind != Stage::FC) continue;
+    const int ld = st.last ? r8(spec_.num_classes()) : st.out_ld;
+    scratch = std::max(scratch, (size_t)gpu::gemm_fwd_splitk(Bm, st.Nout, st.Kin) * Bm * ld * 4);
   }
   scratch_bytes_ = scratch;
   for (int pass = 0; pass < 2; ++pass) {
@@ -404,7 +416,7 @@ void GpuNet::build() {
       st.arg_buf = st.pooled ? static_cast<uint8_t*>(arena_alloc((size_t)Bm * per)) : nullptr;
       if (st.kind == Stage::CONV && st.big) {
         const size_t conv_elems = (size_t)Bm * st.OH * st.OW * st.C;
-        st.conv_buf = st.pooled ? arena_alloc(es * conv_elems) : nullptr;
+        st.conv_buf = st.pooled && !st.ig_pool ? arena_alloc(es * conv_elems) : nullptr;
         st.dz_buf = arena_alloc(es * conv_elems);
       }
     }
@@ -520,12 +532,14 @@ void GpuNet::forward(const uint8_t* images, const int32_t* idx, int B, hipStream
       g.B = B; g.H = st.inH; g.W = st.inW; g.C = st.inC;
       g.OH = st.OH; g.OW = st.OW; g.KS = st.KS; g.stride = st.stride; g.pad = st.pad;
       g.M = B * st.OH * st.OW; g.N = st.C; g.K = st.KS * st.KS * st.inC;
-      g.in = stages_[si - 1]->act_buf;
+      g.in = si > 0 ? stages_[si - 1]->act_buf : nullptr;
       g.w = static_cast<const char*>(packed_) + es * st.pk_fwd; g.ldw = st.kgem;
       g.bias = params_ + st.b_off; g.epi_bias_act = true; g.act = st.act;
-      g.out = st.pooled ? st.conv_buf : st.act_buf; g.ldo = st.C;
+      g.out = st.pooled && !st.ig_pool ? st.conv_buf : st.act_buf; g.ldo = st.C;
+      g.pool = st.ig_pool; g.out_arg = st.arg_buf;
+      if (si == 0) { g.u8 = true; g.in = images; g.idx = idx; }
       gpu::igemm_conv(g, s);
-      if (st.pooled) gpu::maxpool2(dtype_, st.conv_buf, st.act_buf, st.arg_buf, B, st.OH, st.OW, st.C, s);
+      if (st.pooled && !st.ig_pool) gpu::maxpool2(dtype_, st.conv_buf, st.act_buf, st.arg_buf, B, st.OH, st.OW, st.C, s);
     } else if (st.kind == Stage::CONV && st.big) {
       // im2col (input transform fused) -> GEMM with bias+ReLU epilogue -> 2x2 max-pool
       gpu::Im2colParams ic;
@@ -587,7 +601,9 @@ void GpuNet::forward(const uint8_t* images, const int32_t* idx, int B, hipStream
       p.bias = params_ + st.b_off;
       if (st.last) { p.epi = gpu::EPI_LOGITS; p.Cf = logits_; p.ldc = logits_ld_; }
       else { p.epi = gpu::EPI_BIAS_ACT; p.act = st.act; p.C = st.act_buf; p.ldc = st.out_ld; }
-      gpu::gemm(dtype_, p, s);
+      const int sk = gpu::gemm_fwd_splitk(B, st.Nout, st.Kin);
+      MCC_CHECK((size_t)sk * B * p.ldc * 4 <= scratch_bytes_ || sk == 1, "fc forward split-K scratch too small");
+      gpu::gemm_splitk_fwd(dtype_, p, scratch_, sk, s);
     }
   }
 }
@@ -773,13 +789,13 @@ void GpuNet::backward(int hi, int lo, hipStream_t s) {
       const Stage& pv = *stages_[si - 1];
       if (st.fc_igdw) {
         gpu::IgemmDwParams w;
-        w.B = B; w.H = 1; w.W = 1; w.C = st.Kin;
+        w.B = B; w.H = 1; w.W = 1; w.C = st.in_ld;
         w.OH = 1; w.OW = 1; w.KS = 1; w.stride = 1; w.pad = 0;
-        w.M = B; w.Cout = st.Nout; w.kf = st.Kin;
+        w.M = B; w.Cout = st.Nout; w.kf = st.in_ld; w.kreal = st.Kin;
         w.dz = st.grad_buf; w.ldz = st.out_ld; w.in = pv.act_buf;
-        w.splitk = gpu::igemm_dw_splitk(B, st.Nout, st.Kin);
-        w.slab = scratch_; w.slab_stride = (int64_t)(st.Kin + 1) * st.Nout;
-        MCC_CHECK(gpu::igemm_dw_slab_bytes(st.Nout, st.Kin, w.splitk) <= scratch_bytes_, "fc dW scratch too small");
+        w.splitk = gpu::igemm_dw_splitk(B, st.Nout, st.in_ld);
+        w.slab = scratch_; w.slab_stride = (int64_t)(st.in_ld + 1) * st.Nout;
+        MCC_CHECK(gpu::igemm_dw_slab_bytes(st.Nout, st.in_ld, w.splitk) <= scratch_bytes_, "fc dW scratch too small");
         gpu::igemm_dw(w, grads_ + st.w_off, grads_ + st.b_off, 0.f, s);
       } else {
       // weight + bias gradient: [Nout][Kin+1] = dZ^T [X | 1], split-K over the batch

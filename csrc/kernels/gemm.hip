@@ -19,6 +19,8 @@
 #include "kernels.h"
 #include "mfma.h"
 
+#include <algorithm>
+
 namespace mcc {
 namespace gpu {
 
@@ -256,6 +258,26 @@ __global__ void __launch_bounds__(256) dw_reduce_kernel(DwReduceParams p) {
   *dst = p.beta != 0.f ? p.beta * *dst + acc : acc;
 }
 
+// Finishing pass of a split-K forward GEMM: out = epi(sum_s part[s] + bias).
+template <typename T>
+__global__ void __launch_bounds__(256) splitk_finish_kernel(GemmParams p, const float* __restrict__ part, int S) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (int64_t)p.M * p.N) return;
+  const int m = (int)(t / p.N), n = (int)(t - (int64_t)m * p.N);
+  const size_t stride = (size_t)p.M * p.ldc;
+  const float* src = part + (size_t)m * p.ldc + n;
+  float a0 = 0.f, a1 = 0.f;
+  int z = 0;
+  for (; z + 1 < S; z += 2) {
+    a0 += src[z * stride];
+    a1 += src[(z + 1) * stride];
+  }
+  if (z < S) a0 += src[z * stride];
+  float v = a0 + a1 + (p.bias ? p.bias[n] : 0.f);
+  if (p.epi == EPI_LOGITS) p.Cf[(size_t)m * p.ldc + n] = v;
+  else static_cast<T*>(p.C)[(size_t)m * p.ldc + n] = from_f<T>(act_apply(p.act, v));
+}
+
 template <typename T, int BM, int BN, int WAVES_M>
 void launch_cfg(const GemmParams& p, hipStream_t s) {
   const dim3 grid((unsigned)cdiv(p.N, BN), (unsigned)cdiv(p.M, BM), (unsigned)p.splitk), block(256);
@@ -296,6 +318,29 @@ void gemm(DType t, const GemmParams& p, hipStream_t s) {
   MCC_CHECK(p.splitk == 1 || p.epi == EPI_PARTIAL, "gemm: split-K needs the partial epilogue");
   if (t == DType::BF16) launch_gemm<bf16>(p, s);
   else launch_gemm<float>(p, s);
+}
+
+int gemm_fwd_splitk(int M, int N, int K) {
+  const int64_t tiles = (int64_t)cdiv(M, 64) * cdiv(N, 64);
+  if (tiles >= 512 || K < 1024) return 1;
+  int sk = (int)std::min<int64_t>(16, 1024 / std::max<int64_t>(1, tiles));
+  sk = std::min(sk, K / 256);
+  return std::max(1, sk);
+}
+
+void gemm_splitk_fwd(DType t, const GemmParams& p0, float* scratch, int splitk, hipStream_t s) {
+  MCC_CHECK(p0.epi == EPI_BIAS_ACT || p0.epi == EPI_LOGITS, "gemm_splitk_fwd: forward epilogues only");
+  if (splitk <= 1) { gemm(t, p0, s); return; }
+  GemmParams p = p0;
+  p.epi = EPI_PARTIAL;
+  p.Cf = scratch;
+  p.splitk = splitk;
+  p.partial_stride = (int64_t)p.M * p.ldc;
+  gemm(t, p, s);
+  const int64_t n = (int64_t)p0.M * p0.N;
+  const dim3 grid((unsigned)((n + 255) / 256));
+  if (t == DType::BF16) hipLaunchKernelGGL(splitk_finish_kernel<bf16>, grid, dim3(256), 0, s, p0, scratch, splitk);
+  else hipLaunchKernelGGL(splitk_finish_kernel<float>, grid, dim3(256), 0, s, p0, scratch, splitk);
 }
 
 void dw_reduce(const DwReduceParams& p, hipStream_t s) {

@@ -81,7 +81,25 @@ __device__ __forceinline__ int swz128(int row) { return 2 * (row & 3) + 8 * ((ro
 // ---------------------------------------------------------------------------
 // forward / data gradient
 // ---------------------------------------------------------------------------
-template <int BN, bool BIAS_ACT>
+// DPP quad permutations (lanes 4q..4q+3): xor 1, xor 2
+__device__ __forceinline__ float qswap1(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0xB1, 0xf, 0xf, false));
+}
+__device__ __forceinline__ float qswap2(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x4E, 0xf, 0xf, false));
+}
+__device__ __forceinline__ int qswap1i(int v) { return __builtin_amdgcn_mov_dpp(v, 0xB1, 0xf, 0xf, false); }
+__device__ __forceinline__ int qswap2i(int v) { return __builtin_amdgcn_mov_dpp(v, 0x4E, 0xf, 0xf, false); }
+
+// POOL: fused 2x2/2 max-pool epilogue.  The GEMM rows enumerate (b, py, px,
+// pos) so each pooling window is four consecutive rows = four lanes of one
+// DPP quad (the C^T fragment holds pixel r16 in lane r16); the max and its
+// first-max-wins argmax (PyTorch order) come out of two quad exchanges, and
+// the pre-pool conv output is never written.
+// U8: the input is the u8 image set (optional sample-index gather, /255 as
+// cnn.c:457) with few channels (the first layer): the pixel tile is gathered
+// through registers (bytes -> bf16) into the same swizzled LDS image.
+template <int BN, bool BIAS_ACT, bool POOL, bool U8>
 __global__ void __launch_bounds__(kIgT, 2) igemm_conv_kernel(IgemmParams p) {
   constexpr int BM = kIgBM;
   constexpr int AJ = BM * 8 / kIgT;  // glds per thread for the pixel tile (4)
@@ -89,11 +107,26 @@ __global__ void __launch_bounds__(kIgT, 2) igemm_conv_kernel(IgemmParams p) {
   constexpr int IMG = (BM + BN) * kIgBK;  // elements per buffer
   constexpr int FM = 4;              // pixel fragments per wave (64 rows)
   constexpr int FN = BN / 32;        // channel fragments per wave (BN/2 cols)
-  __shared__ __attribute__((aligned(16))) bf16 smem[2 * IMG];
+  constexpr int KT = U8 ? 64 : 0;   // u8: per-k tap table (offset, ky, kx); K <= 64: one K-step,
+  constexpr int NB = U8 ? 1 : 2;    // one LDS buffer (higher occupancy for this latency-bound layer)
+  __shared__ __attribute__((aligned(16))) bf16 smem[NB * IMG + 2 * KT];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r16 = lane & 15, g = lane >> 4;
   const int wm = wave >> 1, wn = wave & 1;
+  int* ktab = reinterpret_cast<int*>(smem + NB * IMG);
+  if constexpr (U8) {
+    for (int k = tid; k < KT; k += kIgT) {
+      int v = -1;  // k >= K: zero
+      if (k < p.K) {
+        const int tap = k / p.C, c = k - tap * p.C;
+        const int ky = tap / p.KS, kx = tap - ky * p.KS;
+        v = (((ky * p.W + kx) * p.C + c) << 8) | (ky << 4) | kx;  // offset < 2^22, ky, kx < 16
+      }
+      ktab[k] = v;
+    }
+    __syncthreads();
+  }
 
   const int ntn = cdiv(p.N, BN);
   const int nwg = gridDim.x;
@@ -101,23 +134,44 @@ __global__ void __launch_bounds__(kIgT, 2) igemm_conv_kernel(IgemmParams p) {
   const int tn = tile % ntn, tm = tile / ntn;
   const int m0 = tm * BM, n0 = tn * BN;
   const bf16* in = static_cast<const bf16*>(p.in);
+  const uint8_t* in8 = static_cast<const uint8_t*>(p.in);
   const bf16* w = static_cast<const bf16*>(p.w);
   const bf16* zero = reinterpret_cast<const bf16*>(kIgZero);
 
   // ---- per-thread staging geometry (fixed for the whole K loop) ----
   int a_iy[AJ], a_ix[AJ], a_base[AJ], a_seg[AJ];
+  const uint8_t* a_img[AJ];
 #pragma unroll
   for (int j = 0; j < AJ; ++j) {
     const int s = j * kIgT + tid;
     const int row = s >> 3;
     a_seg[j] = ((s & 7) ^ swz64(row)) * 8;
+    a_img[j] = in8;
     const int m = m0 + row;
     if (m < p.M) {
-      const int b = mdiv(p.div_ohw, m), rem = m - b * p.OH * p.OW;
-      const int oy = mdiv(p.div_ow, rem), ox = rem - oy * p.OW;
+      int b, oy, ox;
+      if (POOL) {  // m = ((b*PH + py)*PW + px)*4 + pos
+        const int q = m >> 2, pos = m & 3;
+        b = mdiv(p.div_ohw, q);  // div_ohw = PH*PW here
+        const int rq = q - b * (p.OH >> 1) * (p.OW >> 1);
+        const int py = mdiv(p.div_ow, rq), px = rq - py * (p.OW >> 1);  // div_ow = PW
+        oy = 2 * py + (pos >> 1);
+        ox = 2 * px + (pos & 1);
+      } else {
+        b = mdiv(p.div_ohw, m);
+        const int rem = m - b * p.OH * p.OW;
+        oy = mdiv(p.div_ow, rem);
+        ox = rem - oy * p.OW;
+      }
       a_iy[j] = oy * p.stride - p.pad;
       a_ix[j] = ox * p.stride - p.pad;
-      a_base[j] = ((b * p.H + a_iy[j]) * p.W + a_ix[j]) * p.C;
+      if (U8) {  // image base in a 64-bit pointer (large image sets), pixel offset in a_base
+        const int img = p.idx ? p.idx[b] : b;
+        a_img[j] = in8 + (size_t)img * p.H * p.W * p.C;
+        a_base[j] = (a_iy[j] * p.W + a_ix[j]) * p.C;
+      } else {
+        a_base[j] = ((b * p.H + a_iy[j]) * p.W + a_ix[j]) * p.C;
+      }
     } else {
       a_iy[j] = -(1 << 20);  // fails every bounds test
       a_ix[j] = 0;
@@ -125,33 +179,56 @@ __global__ void __launch_bounds__(kIgT, 2) igemm_conv_kernel(IgemmParams p) {
     }
   }
   const bf16* b_ptr[BJ];
+  int b_k[BJ];
 #pragma unroll
   for (int j = 0; j < BJ; ++j) {
     const int s = j * kIgT + tid;
     const int row = s >> 3;
     const int n = n0 + row;
-    b_ptr[j] = n < p.N ? w + (size_t)n * p.ldw + ((s & 7) ^ swz64(row)) * 8 : nullptr;
+    b_k[j] = ((s & 7) ^ swz64(row)) * 8;
+    b_ptr[j] = n < p.N ? w + (size_t)n * p.ldw + b_k[j] : nullptr;
   }
 
-  const int nk = p.K / kIgBK;  // host guarantees K % 64 == 0 and C % 64 == 0
+  const int nk = cdiv(p.K, kIgBK);  // !U8: host guarantees K % 64 == 0 and C % 64 == 0
   auto stage = [&](int kt, int buf) {
     const int k0 = kt * kIgBK;
-    const int tap = k0 / p.C;  // wave-uniform
-    const int c0 = k0 - tap * p.C;
-    const int ky = tap / p.KS, kx = tap - ky * p.KS;
-    const int toff = (ky * p.W + kx) * p.C + c0;
     bf16* A = smem + buf * IMG;
     bf16* Bw = A + BM * kIgBK;
+    if constexpr (U8) {
+      const float sc = 1.0f / 255.0f;
 #pragma unroll
-    for (int j = 0; j < AJ; ++j) {
-      const int iy = a_iy[j] + ky, ix = a_ix[j] + kx;
-      const bool ok = (unsigned)iy < (unsigned)p.H && (unsigned)ix < (unsigned)p.W;
-      const bf16* src = ok ? in + (a_base[j] + toff + a_seg[j]) : zero;
-      glds16(src, A + (j * kIgT + wave * 64) * 8);
+      for (int j = 0; j < AJ; ++j) {
+        bf16x8 v;
+        const int4 t0 = *reinterpret_cast<const int4*>(ktab + k0 + a_seg[j]);
+        const int4 t1 = *reinterpret_cast<const int4*>(ktab + k0 + a_seg[j] + 4);
+        const int tv[8] = {t0.x, t0.y, t0.z, t0.w, t1.x, t1.y, t1.z, t1.w};
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          float f = 0.f;
+          const int t = tv[e];
+          const int iy = a_iy[j] + ((t >> 4) & 15), ix = a_ix[j] + (t & 15);
+          if (t >= 0 && (unsigned)iy < (unsigned)p.H && (unsigned)ix < (unsigned)p.W)
+            f = (float)a_img[j][a_base[j] + (t >> 8)] * sc;
+          v[e] = (bf16)f;
+        }
+        store8(A + (j * kIgT + tid) * 8, v);
+      }
+    } else {
+      const int tap = k0 / p.C;  // wave-uniform
+      const int c0 = k0 - tap * p.C;
+      const int ky = tap / p.KS, kx = tap - ky * p.KS;
+      const int toff = (ky * p.W + kx) * p.C + c0;
+#pragma unroll
+      for (int j = 0; j < AJ; ++j) {
+        const int iy = a_iy[j] + ky, ix = a_ix[j] + kx;
+        const bool ok = (unsigned)iy < (unsigned)p.H && (unsigned)ix < (unsigned)p.W;
+        const bf16* src = ok ? in + (a_base[j] + toff + a_seg[j]) : zero;
+        glds16(src, A + (j * kIgT + wave * 64) * 8);
+      }
     }
 #pragma unroll
     for (int j = 0; j < BJ; ++j) {
-      const bf16* src = b_ptr[j] ? b_ptr[j] + k0 : zero;
+      const bf16* src = (b_ptr[j] && (!U8 || k0 + b_k[j] < p.ldw)) ? b_ptr[j] + k0 : zero;
       glds16(src, Bw + (j * kIgT + wave * 64) * 8);
     }
   };
@@ -165,8 +242,8 @@ __global__ void __launch_bounds__(kIgT, 2) igemm_conv_kernel(IgemmParams p) {
   stage(0, 0);
   __syncthreads();
   for (int kt = 0; kt < nk; ++kt) {
-    const int buf = kt & 1;
-    if (kt + 1 < nk) stage(kt + 1, buf ^ 1);
+    const int buf = NB == 1 ? 0 : (kt & 1);
+    if (NB == 2 && kt + 1 < nk) stage(kt + 1, buf ^ 1);
     const bf16* A = smem + buf * IMG;
     const bf16* Bw = A + BM * kIgBK;
 #pragma unroll
@@ -196,24 +273,44 @@ __global__ void __launch_bounds__(kIgT, 2) igemm_conv_kernel(IgemmParams p) {
 #pragma unroll
   for (int i = 0; i < FN; ++i) {
     const int ch = n0 + wn * (BN / 2) + i * 16 + 4 * g;
-    if (ch >= p.N) continue;
+    const bool chok = ch < p.N;
     float bv[4] = {0.f, 0.f, 0.f, 0.f};
-    if (BIAS_ACT && p.bias) {
+    if (BIAS_ACT && p.bias && chok) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) bv[e] = p.bias[ch + e];
     }
 #pragma unroll
     for (int j = 0; j < FM; ++j) {
       const int m = m0 + wm * 64 + j * 16 + r16;
-      if (m >= p.M) continue;
       float v[4];
 #pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = acc[i][j][e];
+      uint32_t arg = 0;
+      if constexpr (POOL) {  // every lane of the quad takes part in the exchange
+        const int pos = r16 & 3;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          int a = pos;
+          float o = qswap1(v[e]);
+          int oa = qswap1i(a);
+          if (o > v[e] || (o == v[e] && oa < a)) { v[e] = o; a = oa; }
+          o = qswap2(v[e]);
+          oa = qswap2i(a);
+          if (o > v[e] || (o == v[e] && oa < a)) { v[e] = o; a = oa; }
+          arg |= (uint32_t)a << (8 * e);
+        }
+      }
+      if (!chok || m >= p.M) continue;
+      if (POOL && (r16 & 3) != 0) continue;
+#pragma unroll
       for (int e = 0; e < 4; ++e) {
-        v[e] = acc[i][j][e] + bv[e];
+        v[e] += bv[e];
         if (BIAS_ACT) v[e] = act_apply(p.act, v[e]);
       }
       const bf16x4 o = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
-      *reinterpret_cast<bf16x4*>(out + (size_t)m * p.ldo + ch) = o;
+      const int orow = POOL ? (m >> 2) : m;
+      *reinterpret_cast<bf16x4*>(out + (size_t)orow * p.ldo + ch) = o;
+      if (POOL) *reinterpret_cast<uint32_t*>(p.out_arg + (size_t)orow * p.N + ch) = arg;
     }
   }
 }
@@ -280,7 +377,7 @@ __global__ void __launch_bounds__(kIgT, 2) igemm_dw_kernel(IgemmDwParams p) {
     for (int j = 0; j < J; ++j) {
       const int m = mb + d_row[j];
       const bool mok = m < p.M;
-      const bf16* dsrc = (mok && d_col[j] < p.Cout) ? dz + (size_t)m * p.ldz + d_col[j] : zero;
+      const bf16* dsrc = (mok && d_col[j] < p.Cout) ? dz + (size_t)m * p.ldz + d_col[j] : zero;  // piece may span the pad
       glds16(dsrc, D + (j * kIgT + wave * 64) * 8);
       const bf16* xsrc = zero;
       if (mok) {
@@ -343,6 +440,27 @@ __global__ void __launch_bounds__(kIgT, 2) igemm_dw_kernel(IgemmDwParams p) {
     }
   }
 
+  if (p.direct) {
+    // single split, canonical layout (KS == 1, no permutation): write the
+    // gradient in place; for a fixed i the 16 lanes of a group cover 16
+    // consecutive k of one row: 64-byte runs
+    const int kreal = p.kreal > 0 ? p.kreal : p.kf;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int k = k0 + wn * 64 + j * 16 + r16;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int co = co0 + wm * 64 + i * 16 + 4 * g + e;
+          if (co >= p.Cout) continue;
+          if (k < kreal) p.gw[(size_t)co * kreal + k] = acc[i][j][e];
+          else if (k == p.kf) p.gb[co] = acc[i][j][e];
+        }
+      }
+    }
+    return;
+  }
   // slab[split][k][co]: lane holds co 4g..4g+3 of column k = r16
   float* slab = p.slab + (size_t)split * p.slab_stride;
 #pragma unroll
@@ -359,21 +477,37 @@ __global__ void __launch_bounds__(kIgT, 2) igemm_dw_kernel(IgemmDwParams p) {
 }
 
 // gw[co][c*KK + tap] (+)= sum_s slab[s][tap*C + c][co];  gb[co] from k == kf.
-// One thread per (k, co), co fastest: coalesced slab reads, fixed-order sum.
+// A workgroup owns 64 consecutive slab floats (16 groups of 4 co); its 16
+// waves-lanes per group stride the splits (16 independent 16-byte load
+// chains in flight per output group), then the 16 partials are combined in
+// LDS in a fixed order: deterministic, latency-parallel over the splits.
 __global__ void __launch_bounds__(256) igemm_dw_reduce_kernel(IgemmDwParams p, float* gw, float* gb, float beta) {
-  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int64_t total = (int64_t)(p.kf + 1) * p.Cout;
-  if (t >= total) return;
-  const int k = (int)(t / p.Cout), co = (int)(t - (int64_t)k * p.Cout);
-  const float* src = p.slab + t;
-  float a0 = 0.f, a1 = 0.f;
-  int s = 0;
-  for (; s + 1 < p.splitk; s += 2) {
-    a0 += src[(size_t)s * p.slab_stride];
-    a1 += src[(size_t)(s + 1) * p.slab_stride];
+  __shared__ f32x4 part[16][17];
+  const int grp = threadIdx.x & 15, sl = threadIdx.x >> 4;
+  const int64_t total4 = (int64_t)(p.kf + 1) * p.Cout / 4;
+  const int64_t e4 = (int64_t)blockIdx.x * 16 + grp;
+  f32x4 a0 = {0.f, 0.f, 0.f, 0.f}, a1 = a0;
+  if (e4 < total4) {
+    const f32x4* src = reinterpret_cast<const f32x4*>(p.slab) + e4;
+    const int64_t st4 = p.slab_stride / 4;
+    int s = sl;
+    for (; s + 16 < p.splitk; s += 32) {
+      a0 += src[(size_t)s * st4];
+      a1 += src[(size_t)(s + 16) * st4];
+    }
+    if (s < p.splitk) a0 += src[(size_t)s * st4];
   }
-  if (s < p.splitk) a0 += src[(size_t)s * p.slab_stride];
-  const float v = a0 + a1;
+  part[sl][grp] = a0 + a1;
+  __syncthreads();
+  if (threadIdx.x >= 64) return;
+  // 64 threads: output float (grp, lane-in-4)
+  const int g4 = threadIdx.x >> 2, c4 = threadIdx.x & 3;
+  const int64_t e = ((int64_t)blockIdx.x * 16 + g4) * 4 + c4;
+  if (e >= total4 * 4) return;
+  float v = 0.f;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) v += part[q][g4][c4];
+  const int k = (int)(e / p.Cout), co = (int)(e - (int64_t)k * p.Cout);
   float* dst;
   const int kreal = p.kreal > 0 ? p.kreal : p.kf;
   if (k < p.kf && k >= kreal) return;
@@ -381,18 +515,18 @@ __global__ void __launch_bounds__(256) igemm_dw_reduce_kernel(IgemmDwParams p, f
     const int hw = k / p.perm_c, c = k - hw * p.perm_c;
     dst = gw + (size_t)co * kreal + (size_t)c * p.perm_hw + hw;
   } else if (k < p.kf) {
-    const int tap = k / p.C, c = k - tap * p.C;
-    dst = gw + ((size_t)co * p.C + c) * (p.KS * p.KS) + tap;
+    const int tap = k / p.C, c = k - tap * p.C;  // KS == 1: tap 0, c = k; row stride kreal
+    dst = gw + (size_t)co * kreal + (size_t)c * (p.KS * p.KS) + tap;
   } else {
     dst = gb + co;
   }
   *dst = beta != 0.f ? beta * *dst + v : v;
 }
 
-template <int BN, bool BA>
+template <int BN, bool BA, bool POOL, bool U8>
 void launch_conv(const IgemmParams& p, hipStream_t s) {
   const int nwg = cdiv(p.M, kIgBM) * cdiv(p.N, BN);
-  hipLaunchKernelGGL((igemm_conv_kernel<BN, BA>), dim3((unsigned)nwg), dim3(kIgT), 0, s, p);
+  hipLaunchKernelGGL((igemm_conv_kernel<BN, BA, POOL, U8>), dim3((unsigned)nwg), dim3(kIgT), 0, s, p);
 }
 
 }  // namespace
@@ -403,20 +537,44 @@ bool igemm_conv_supported(int C, int N, int KS) {
 
 void igemm_conv(const IgemmParams& p0, hipStream_t s) {
   IgemmParams p = p0;
-  MCC_CHECK(igemm_conv_supported(p.C, p.N, p.KS), "igemm_conv: needs C % 64 == 0 and N % 8 == 0");
+  if (p.u8) {
+    MCC_CHECK(p.N % 8 == 0 && p.epi_bias_act && p.ldw % 8 == 0 && p.ldw >= p.K && p.K <= 64 && p.KS <= 16 &&
+                  (int64_t)p.KS * p.W * p.C < (1 << 22),
+              "igemm_conv(u8): bad shapes");
+  } else {
+    MCC_CHECK(igemm_conv_supported(p.C, p.N, p.KS), "igemm_conv: needs C % 64 == 0 and N % 8 == 0");
+  }
   MCC_CHECK(p.K == p.KS * p.KS * p.C, "igemm_conv: K must be KS*KS*C");
   MCC_CHECK(p.M == p.B * p.OH * p.OW && p.M > 0, "igemm_conv: M must be B*OH*OW");
   MCC_CHECK(p.ldw >= p.K && p.ldw % 8 == 0 && p.ldo >= p.N && p.ldo % 4 == 0, "igemm_conv: bad leading dims");
-  MCC_CHECK((int64_t)p.B * p.H * p.W * p.C < (1ll << 31), "igemm_conv: input exceeds 2^31 elements");
+  MCC_CHECK((int64_t)(p.u8 ? 1 : p.B) * p.H * p.W * p.C < (1ll << 31), "igemm_conv: input exceeds 2^31");
   MCC_CHECK(p.OH == (p.H + 2 * p.pad - p.KS) / p.stride + 1 && p.OW == (p.W + 2 * p.pad - p.KS) / p.stride + 1,
             "igemm_conv: output geometry mismatch");
-  p.div_ohw = magic(p.OH * p.OW);
-  p.div_ow = magic(p.OW);
-  const bool ba = p.epi_bias_act;
-  if (p.N <= 64) {
-    if (ba) launch_conv<64, true>(p, s); else launch_conv<64, false>(p, s);
+  if (p.pool) {
+    MCC_CHECK(p.OH % 2 == 0 && p.OW % 2 == 0 && p.out_arg && p.epi_bias_act && p.ldo == p.N,
+              "igemm_conv: fused pool needs even output dims, argmax buffer, dense output");
+    p.div_ohw = magic((p.OH / 2) * (p.OW / 2));
+    p.div_ow = magic(p.OW / 2);
   } else {
-    if (ba) launch_conv<128, true>(p, s); else launch_conv<128, false>(p, s);
+    p.div_ohw = magic(p.OH * p.OW);
+    p.div_ow = magic(p.OW);
+  }
+  const bool ba = p.epi_bias_act;
+  if (p.u8) {
+    MCC_CHECK(p.N > 64 || p.N % 8 == 0, "igemm_conv(u8): N");
+    if (p.pool) {
+      if (p.N <= 64) launch_conv<64, true, true, true>(p, s); else launch_conv<128, true, true, true>(p, s);
+    } else {
+      if (p.N <= 64) launch_conv<64, true, false, true>(p, s); else launch_conv<128, true, false, true>(p, s);
+    }
+    return;
+  }
+  if (p.pool) {
+    if (p.N <= 64) launch_conv<64, true, true, false>(p, s); else launch_conv<128, true, true, false>(p, s);
+  } else if (p.N <= 64) {
+    if (ba) launch_conv<64, true, false, false>(p, s); else launch_conv<64, false, false, false>(p, s);
+  } else {
+    if (ba) launch_conv<128, true, false, false>(p, s); else launch_conv<128, false, false, false>(p, s);
   }
 }
 
@@ -424,7 +582,7 @@ int igemm_dw_splitk(int M, int Cout, int kf) {
   const int tiles = cdiv(Cout, 128) * cdiv(kf + 1, 128);
   const int nks = cdiv(M, kIgBK);
   int sk = std::max(1, 1024 / tiles);         // ~4 workgroups per CU in flight
-  sk = std::min(sk, std::max(1, nks / 8));    // >= 8 K-steps per slice
+  sk = std::min(sk, std::max(1, nks / 4));    // >= 4 K-steps per slice
   return std::min(sk, 1024);
 }
 
@@ -432,8 +590,11 @@ size_t igemm_dw_slab_bytes(int Cout, int kf, int splitk) { return (size_t)splitk
 
 void igemm_dw(const IgemmDwParams& p0, float* gw, float* gb, float beta, hipStream_t s) {
   IgemmDwParams p = p0;
-  MCC_CHECK(p.C % 8 == 0 && p.Cout % 8 == 0 && p.kf == p.KS * p.KS * p.C, "igemm_dw: needs C, Cout % 8 == 0");
-  MCC_CHECK(p.M == p.B * p.OH * p.OW && p.M > 0 && p.ldz >= p.Cout && p.ldz % 8 == 0, "igemm_dw: bad shapes");
+  // dz rows are read in 8-channel pieces up to round_up(Cout, 8) <= ldz (pad
+  // columns only feed output rows that are never written)
+  MCC_CHECK(p.C % 8 == 0 && p.Cout % 4 == 0 && p.kf == p.KS * p.KS * p.C, "igemm_dw: needs C % 8, Cout % 4 == 0");
+  MCC_CHECK(p.M == p.B * p.OH * p.OW && p.M > 0 && p.ldz >= ((p.Cout + 7) & ~7) && p.ldz % 8 == 0,
+            "igemm_dw: bad shapes");
   MCC_CHECK((int64_t)p.B * p.H * p.W * p.C < (1ll << 31), "igemm_dw: input exceeds 2^31 elements");
   MCC_CHECK(p.splitk >= 1 && p.slab_stride >= (int64_t)(p.kf + 1) * p.Cout, "igemm_dw: bad split/slab");
   MCC_CHECK(p.kreal == 0 || (p.KS == 1 && p.kreal <= p.kf), "igemm_dw: kreal needs KS == 1");
@@ -442,9 +603,13 @@ void igemm_dw(const IgemmDwParams& p0, float* gw, float* gb, float beta, hipStre
   p.div_ohw = magic(p.OH * p.OW);
   p.div_ow = magic(p.OW);
   const int nwg = cdiv(p.Cout, 128) * cdiv(p.kf + 1, 128) * p.splitk;
+  p.direct = p.splitk == 1 && p.KS == 1 && p.perm_c == 0 && beta == 0.f;
+  p.gw = gw;
+  p.gb = gb;
   hipLaunchKernelGGL(igemm_dw_kernel, dim3((unsigned)nwg), dim3(kIgT), 0, s, p);
-  const int64_t total = (int64_t)(p.kf + 1) * p.Cout;
-  hipLaunchKernelGGL(igemm_dw_reduce_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, p, gw, gb, beta);
+  if (p.direct) return;
+  const int64_t total4 = (int64_t)(p.kf + 1) * p.Cout / 4;  // Cout % 8 == 0
+  hipLaunchKernelGGL(igemm_dw_reduce_kernel, dim3((unsigned)((total4 + 15) / 16)), dim3(256), 0, s, p, gw, gb, beta);
 }
 
 }  // namespace gpu

@@ -292,8 +292,12 @@ struct IgemmParams {
   const float* bias = nullptr;       // [N] (epi_bias_act)
   bool epi_bias_act = true;          // false: plain store (data gradient)
   int act = ACT_RELU;
-  void* out = nullptr;               // bf16 [M][ldo]
+  void* out = nullptr;               // bf16 [M][ldo]   (pool: [M/4][N] pooled)
   int ldo = 0;
+  bool pool = false;                 // fused 2x2/2 max-pool (+ argmax bytes [M/4][N])
+  uint8_t* out_arg = nullptr;
+  bool u8 = false;                   // input = u8 image set (first layer), scaled 1/255
+  const int32_t* idx = nullptr;      // u8: optional per-sample image index
   DivMagic div_ohw, div_ow;
 };
 bool igemm_conv_supported(int C, int N, int KS);
@@ -314,6 +318,9 @@ struct IgemmDwParams {
   int splitk = 1;
   int perm_c = 0, perm_hw = 0;       // KS == 1 only: feature k = hw*perm_c + c -> c*perm_hw + hw
   int kreal = 0;                     // KS == 1 only: features >= kreal (< kf) are padding, dropped (0: kf)
+  bool direct = false;               // set at launch: one split, write gw/gb in place (no slab pass)
+  float* gw = nullptr;               // set at launch
+  float* gb = nullptr;
   DivMagic div_ohw, div_ow;
 };
 int igemm_dw_splitk(int M, int Cout, int kf);
@@ -327,6 +334,11 @@ size_t conv_dw_lds_bytes(DType t, const ConvDwParams& p);
 void conv_dw_reduce(const ConvDwReduceParams& p, hipStream_t s);
 
 void gemm(DType t, const GemmParams& p, hipStream_t s);
+// Split-K forward GEMM for skinny-M / long-K problems (large FC heads at a
+// small batch): fp32 partials in `scratch` ([splitk][M][ldc]), then a pass
+// applying the forward epilogue (bias + act -> T, or fp32 logits).
+int gemm_fwd_splitk(int M, int N, int K);
+void gemm_splitk_fwd(DType t, const GemmParams& p, float* scratch, int splitk, hipStream_t s);
 void dw_reduce(const DwReduceParams& p, hipStream_t s);
 
 void softmax_xent(DType t, const XentParams& p, hipStream_t s);

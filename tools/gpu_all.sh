@@ -13,3 +13,4 @@ for b in ${VGG_BATCHES:-128}; do
   grep metric gpurun_out/vgg_$b.log
 done
 cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_vgg -o run --output-format csv -- python3 $R/bench.py --model vgg11 --batch-per-gpu 128 --steps 5 --warmup 2 > $R/gpurun_out/prof_vgg.log 2>&1
+cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_lenet -o run --output-format csv -- python3 $R/bench.py --steps 20 --warmup 3 > $R/gpurun_out/prof_lenet.log 2>&1
