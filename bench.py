@@ -25,6 +25,8 @@ sys.path.insert(0, ROOT)
 BASELINE_IMG_S = 2510.0  # best reference number (8-rank MPI CPU)
 METRIC = "images/sec (whole node), LeNet-5 MNIST-shaped, at 1/2/4/8 MI355X"
 DEFAULT_BATCH = {"lenet5": 16384, "ref": 16384, "cifar3": 4096, "vgg11": 256}
+# models whose step is faster with the dW side stream (engine.cpp, measured A/B)
+SIDE_STREAM = {"cifar3"}
 
 
 def metric_for(model):
@@ -66,6 +68,8 @@ def main():
 
     spec = mcc.make_model(args.model)
     C, H, W = spec.input_shape()
+    if args.model in SIDE_STREAM:
+        os.environ.setdefault("MCC_SIDE_STREAM", "1")
     B = args.batch_per_gpu or DEFAULT_BATCH.get(args.model, 1024)
     if not args.dataset:
         args.dataset = 65536 if H * W <= 32 * 32 else max(256, 8 * B)

@@ -100,12 +100,27 @@ GpuNet::GpuNet(const ModelSpec& spec, DType dtype, int max_batch, int device)
   if (const char* a = std::getenv("MCC_NO_PIPE")) no_pipe_ = std::atoi(a) != 0;  // A/B against conv_small
   if (const char* a = std::getenv("MCC_NO_FC")) no_fc_ = std::atoi(a) != 0;      // A/B against the tiled GEMM
   if (const char* a = std::getenv("MCC_NO_IGEMM")) no_igemm_ = std::atoi(a) != 0;  // A/B against im2col + GEMM
+  // dW side stream: opt-in (MCC_SIDE_STREAM=1).  Measured on MI355X (one GPU,
+  // bench.py): CIFAR-3conv 2.27 -> 2.17 ms/step, but LeNet-5 0.452 -> 0.502 and
+  // VGG-11 12.14 -> 12.40: the persistent conv kernels are sized to own every
+  // CU, so a concurrent dW kernel steals their slots and stretches both.
+  no_side_ = true;
+  if (const char* a = std::getenv("MCC_SIDE_STREAM")) no_side_ = std::atoi(a) == 0;
   if (device_ >= 0) HIP_OK(hipSetDevice(device_));
   else HIP_OK(hipGetDevice(&device_));
   build();
+  if (!no_side_) {
+    HIP_OK(hipStreamCreateWithFlags(&wstream_, hipStreamNonBlocking));
+    fork_ev_.resize(stages_.size());
+    for (auto& e : fork_ev_) HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    HIP_OK(hipEventCreateWithFlags(&join_ev_, hipEventDisableTiming));
+  }
 }
 
 GpuNet::~GpuNet() {
+  for (auto e : fork_ev_) (void)hipEventDestroy(e);
+  if (join_ev_) (void)hipEventDestroy(join_ev_);
+  if (wstream_) (void)hipStreamDestroy(wstream_);
   for (Stage* st : stages_) delete st;
   if (arena_) (void)hipFree(arena_);
   if (mom_) (void)hipFree(mom_);
@@ -628,8 +643,30 @@ void GpuNet::backward(int hi, int lo, hipStream_t s) {
   MCC_CHECK(hi >= lo && lo >= 0 && hi < (int)stages_.size(), "backward: bad stage range");
   const int B = B_;
   const size_t es = dtype_size(dtype_);
+  const hipStream_t s_main = s;
+  bool forked = false;
   for (int si = hi; si >= lo; --si) {
     Stage& st = *stages_[si];
+    s = s_main;
+    // Side stream for this stage's weight gradient when the two directions
+    // share no scratch: every path except the im2col fallbacks of the
+    // large-image conv (col_ is shared by their dW and dX).  All dW work is
+    // serialised on wstream_, so scratch_ (split-K slabs) stays single-user;
+    // the dX kernels never touch scratch_.
+    const bool side = wstream_ && !(st.kind == Stage::CONV && st.big && !((st.ig_dw || st.ig_dw0) && (st.ig_dx || si == 0)));
+    hipStream_t ws = s_main;
+    if (!side && forked) {  // this stage's dW uses scratch_ on the main stream: drain the side stream first
+      HIP_OK(hipEventRecord(join_ev_, wstream_));
+      HIP_OK(hipStreamWaitEvent(s_main, join_ev_, 0));
+      forked = false;
+    }
+    auto fork = [&]() {
+      if (!side) return;
+      HIP_OK(hipEventRecord(fork_ev_[si], s_main));
+      HIP_OK(hipStreamWaitEvent(wstream_, fork_ev_[si], 0));
+      ws = wstream_;
+      forked = true;
+    };
     if (st.kind == Stage::CONV) {
       gpu::StageSrc dy;
       dy.mode = st.pooled ? gpu::IN_UNPOOL : (st.act == gpu::ACT_RELU ? gpu::IN_RELU : gpu::IN_PLAIN);
@@ -640,6 +677,7 @@ void GpuNet::backward(int hi, int lo, hipStream_t s) {
         const int kf = KK * st.inC;
         // dZ = relu'/unpool(dY) at conv-output size
         gpu::grad_xform(dtype_, dy, st.dz_buf, B, s);
+        fork();
         if (st.ig_dw0) {
           // stage 0 (u8 input, few channels): the explicit im2col rows as a 1x1
           // "conv" through the implicit-GEMM dW kernel (split-K over the pixels)
@@ -648,7 +686,7 @@ void GpuNet::backward(int hi, int lo, hipStream_t s) {
           ic.s.SH = st.inH; ic.s.SW = st.inW; ic.s.SC = st.inC; ic.s.off = st.pad; ic.s.up = 1;
           ic.s.mode = gpu::IN_U8; ic.s.src = images_; ic.s.idx = idx_;
           ic.out = col_;
-          gpu::im2col(dtype_, ic, s);
+          gpu::im2col(dtype_, ic, ws);
           gpu::IgemmDwParams w;
           w.B = B * st.OH * st.OW; w.H = 1; w.W = 1; w.C = st.kgem;
           w.OH = 1; w.OW = 1; w.KS = 1; w.stride = 1; w.pad = 0;
@@ -658,7 +696,7 @@ void GpuNet::backward(int hi, int lo, hipStream_t s) {
           w.splitk = gpu::igemm_dw_splitk(w.M, st.C, st.kgem);
           w.slab = scratch_; w.slab_stride = (int64_t)(st.kgem + 1) * st.C;
           MCC_CHECK(gpu::igemm_dw_slab_bytes(st.C, st.kgem, w.splitk) <= scratch_bytes_, "igemm dW0 scratch too small");
-          gpu::igemm_dw(w, grads_ + st.w_off, grads_ + st.b_off, 0.f, s);
+          gpu::igemm_dw(w, grads_ + st.w_off, grads_ + st.b_off, 0.f, ws);
         }
         if (st.ig_dw) {
           // dW, db: implicit GEMM over the pixels (split-K slabs + ordered reduce)
@@ -670,7 +708,7 @@ void GpuNet::backward(int hi, int lo, hipStream_t s) {
           w.splitk = gpu::igemm_dw_splitk(w.M, st.C, kf);
           w.slab = scratch_; w.slab_stride = (int64_t)(kf + 1) * st.C;
           MCC_CHECK(gpu::igemm_dw_slab_bytes(st.C, kf, w.splitk) <= scratch_bytes_, "igemm dW scratch too small");
-          gpu::igemm_dw(w, grads_ + st.w_off, grads_ + st.b_off, 0.f, s);
+          gpu::igemm_dw(w, grads_ + st.w_off, grads_ + st.b_off, 0.f, ws);
         }
         // dW, db = dZ^T [im2col(X) | 1]  (split-K over B*OH*OW)
         if (!st.ig_dw && !st.ig_dw0) {
@@ -727,6 +765,7 @@ void GpuNet::backward(int hi, int lo, hipStream_t s) {
         }
         continue;
       }
+      fork();
       if (st.pipe_dw) {
         gpu::ConvDwPipeParams w = st.pdw;
         w.N = B; w.ablate = ablate_;
@@ -734,8 +773,8 @@ void GpuNet::backward(int hi, int lo, hipStream_t s) {
         else w.x.src = stages_[si - 1]->act_buf;
         w.dy.src = st.grad_buf; w.dy.aux_y = st.act_buf; w.dy.aux_arg = st.arg_buf;
         w.slab = scratch_;
-        gpu::conv_dw_pipe(w, s);
-        gpu::conv_dw_pipe_reduce(w, grads_ + st.w_off, grads_ + st.b_off, s);
+        gpu::conv_dw_pipe(w, ws);
+        gpu::conv_dw_pipe_reduce(w, grads_ + st.w_off, grads_ + st.b_off, ws);
       }
       if (st.pipe_dx && si > 0) {
         gpu::ConvPipeParams p = st.pdx;
@@ -762,12 +801,12 @@ void GpuNet::backward(int hi, int lo, hipStream_t s) {
       w.slab = scratch_;
       MCC_CHECK((size_t)w.nx * w.cout_pad * w.ncols_pad * 4 <= scratch_bytes_, "conv dW scratch too small");
       w.ablate = ablate_;
-      gpu::conv_dw(dtype_, w, s);
+      gpu::conv_dw(dtype_, w, ws);
       gpu::ConvDwReduceParams r;
       r.nx = w.nx; r.Cout = st.C; r.Cin = st.inC; r.KS = st.KS; r.CG = st.CLdw; r.cvec = st.cvec;
       r.cout_pad = st.cout_pad; r.ncols_pad = st.ncols_pad; r.kbias = st.kbias;
       r.slab = scratch_; r.gw = grads_ + st.w_off; r.gb = grads_ + st.b_off;
-      gpu::conv_dw_reduce(r, s);
+      gpu::conv_dw_reduce(r, ws);
       }
       // data gradient into the previous stage's output gradient
       if (si > 0 && !st.pipe_dx) {
@@ -787,6 +826,7 @@ void GpuNet::backward(int hi, int lo, hipStream_t s) {
       }
     } else {
       const Stage& pv = *stages_[si - 1];
+      fork();
       if (st.fc_igdw) {
         gpu::IgemmDwParams w;
         w.B = B; w.H = 1; w.W = 1; w.C = st.in_ld;
@@ -796,7 +836,7 @@ void GpuNet::backward(int hi, int lo, hipStream_t s) {
         w.splitk = gpu::igemm_dw_splitk(B, st.Nout, st.in_ld);
         w.slab = scratch_; w.slab_stride = (int64_t)(st.in_ld + 1) * st.Nout;
         MCC_CHECK(gpu::igemm_dw_slab_bytes(st.Nout, st.in_ld, w.splitk) <= scratch_bytes_, "fc dW scratch too small");
-        gpu::igemm_dw(w, grads_ + st.w_off, grads_ + st.b_off, 0.f, s);
+        gpu::igemm_dw(w, grads_ + st.w_off, grads_ + st.b_off, 0.f, ws);
       } else {
       // weight + bias gradient: [Nout][Kin+1] = dZ^T [X | 1], split-K over the batch
       gpu::GemmParams w;
@@ -807,13 +847,13 @@ void GpuNet::backward(int hi, int lo, hipStream_t s) {
       const int sk = dw_splitk(st.Nout, st.Kin + 1, B);
       w.splitk = sk;
       w.partial_stride = (int64_t)st.Nout * st.ldp;
-      gpu::gemm(dtype_, w, s);
+      gpu::gemm(dtype_, w, ws);
       gpu::DwReduceParams r;
       r.S = sk; r.Nout = st.Nout; r.kfeat = st.Kin; r.ldp = st.ldp; r.part = scratch_;
       r.partial_stride = w.partial_stride;
       r.gw = grads_ + st.w_off; r.gb = grads_ + st.b_off;
       r.permC = 0; r.permHW = 0;  // device order (see set_params)
-      gpu::dw_reduce(r, s);
+      gpu::dw_reduce(r, ws);
       }
       // data gradient
       if (si > 0 && dtype_ == DType::BF16 && !no_fc_ && gpu::fc_supported(st.Kin, st.Nout)) {
@@ -842,6 +882,10 @@ void GpuNet::backward(int hi, int lo, hipStream_t s) {
         gpu::gemm(dtype_, d, s);
       }
     }
+  }
+  if (forked) {
+    HIP_OK(hipEventRecord(join_ev_, wstream_));
+    HIP_OK(hipStreamWaitEvent(s_main, join_ev_, 0));
   }
 }
 

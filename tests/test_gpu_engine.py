@@ -37,6 +37,20 @@ def _relerr(a, b):
 @pytest.mark.parametrize("dtype", ["fp32", "bf16"])
 @pytest.mark.parametrize("model", ["lenet5", "ref", "cifar3"])
 def test_step_matches_torch(cuda, model, dtype):
+    _check_step(cuda, model, dtype)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+@pytest.mark.parametrize("model", ["lenet5", "cifar3"])
+def test_step_matches_torch_side_stream(cuda, model, dtype, monkeypatch):
+    """Weight gradients on the engine's side stream (MCC_SIDE_STREAM=1), data
+    gradients on the caller's: same numbers as the single-stream step."""
+    monkeypatch.setenv("MCC_SIDE_STREAM", "1")
+    _check_step(cuda, model, dtype)
+
+
+def _check_step(cuda, model, dtype):
     spec = mcc.make_model(model)
     C, H, W = spec.input_shape()
     B = 96  # not a multiple of the per-workgroup image count on purpose
