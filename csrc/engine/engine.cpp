@@ -27,6 +27,7 @@ struct GpuNet::Stage {
   bool pooled = false;   // fused 2x2/2 maxpool
   int act = gpu::ACT_NONE;
   bool last = false;
+  bool head = false;  // last FC: backward fused into the loss kernel (xent_head)
   bool cvec = true;      // conv input gathered in 8-channel vectors
   int inC = 0, inH = 1, inW = 1;
   int C = 0, OH = 1, OW = 1;   // conv grid (pre-pool)
@@ -100,6 +101,7 @@ GpuNet::GpuNet(const ModelSpec& spec, DType dtype, int max_batch, int device)
   if (const char* a = std::getenv("MCC_NO_PIPE")) no_pipe_ = std::atoi(a) != 0;  // A/B against conv_small
   if (const char* a = std::getenv("MCC_NO_FC")) no_fc_ = std::atoi(a) != 0;      // A/B against the tiled GEMM
   if (const char* a = std::getenv("MCC_NO_IGEMM")) no_igemm_ = std::atoi(a) != 0;  // A/B against im2col + GEMM
+  if (const char* a = std::getenv("MCC_NO_HEAD")) no_head_ = std::atoi(a) != 0;    // A/B against softmax_xent + FC backward
   // dW side stream: opt-in (MCC_SIDE_STREAM=1).  Measured on MI355X (one GPU,
   // bench.py): CIFAR-3conv 2.27 -> 2.17 ms/step, but LeNet-5 0.452 -> 0.502 and
   // VGG-11 12.14 -> 12.40: the persistent conv kernels are sized to own every
@@ -281,6 +283,8 @@ void GpuNet::build() {
       if (st.kind == Stage::FC) st.in_ld = pv.kind == Stage::FC ? pv.out_ld : (int)pv.out_elems;
     }
     if (st.kind == Stage::FC) MCC_CHECK(st.in_ld % 8 == 0, "fc input leading dim must be a multiple of 8");
+    st.head = st.kind == Stage::FC && st.last && s > 0 && dtype_ == DType::BF16 && !no_head_ &&
+              gpu::xent_head_supported(st.Nout, st.Kin, st.in_ld);
     // FC weight gradient on the implicit-GEMM dW kernel (a 1x1 "conv" over the
     // batch, C = in_ld with the pad columns dropped by the reduce)
     if (st.kind == Stage::FC)
@@ -399,6 +403,8 @@ void GpuNet::build() {
         const size_t nv = (size_t)st.pdw.cout_pad * st.pdw.ncols_pad;
         scratch = std::max(scratch, (st.pdw.grid + ceil_div(st.pdw.grid, 16)) * nv * 4);
       }
+    } else if (st.head) {
+      scratch = std::max(scratch, (size_t)gpu::xent_head_slabs(Bm) * st.Nout * st.ldp * 4);
     } else if (st.fc_igdw) {
       scratch = std::max(scratch, gpu::igemm_dw_slab_bytes(st.Nout, st.in_ld, gpu::igemm_dw_splitk(Bm, st.Nout, st.in_ld)));
     } else {
@@ -538,6 +544,7 @@ void GpuNet::forward(const uint8_t* images, const int32_t* idx, int B, hipStream
   B_ = B;
   images_ = images;
   idx_ = idx;
+  head_done_ = false;
   const size_t es = dtype_size(dtype_);
   for (size_t si = 0; si < stages_.size(); ++si) {
     Stage& st = *stages_[si];
@@ -635,6 +642,28 @@ void GpuNet::loss(const uint8_t* labels, const int32_t* idx, float grad_scale, b
   p.scale = grad_scale;
   p.stats = stats_;
   p.pred = pred;
+  if (backward && last.head) {
+    // softmax-CE + the last FC layer's dX, dW, db in one kernel; the per-
+    // workgroup dW slabs are summed in a fixed order by dw_reduce
+    const Stage& pv = *stages_[stages_.size() - 2];
+    gpu::XentHeadParams h;
+    h.x = p;
+    h.x.dlogits = nullptr;
+    h.h = pv.act_buf; h.ldh = last.in_ld;
+    h.w = params_ + last.w_off; h.Kin = last.Kin;
+    h.act = pv.kind == Stage::FC ? pv.act : gpu::ACT_NONE;  // conv masks are applied by its staging
+    h.dh = pv.grad_buf;
+    h.slab = scratch_; h.ldp = last.ldp;
+    gpu::xent_head(h, s);
+    gpu::DwReduceParams r;
+    r.S = gpu::xent_head_slabs(B_); r.Nout = last.Nout; r.kfeat = last.Kin; r.ldp = last.ldp; r.part = scratch_;
+    r.partial_stride = (int64_t)last.Nout * last.ldp;
+    r.gw = grads_ + last.w_off; r.gb = grads_ + last.b_off;
+    r.permC = 0; r.permHW = 0;  // device order (see set_params)
+    gpu::dw_reduce(r, s);
+    head_done_ = true;
+    return;
+  }
   gpu::softmax_xent(dtype_, p, s);
 }
 
@@ -826,6 +855,7 @@ void GpuNet::backward(int hi, int lo, hipStream_t s) {
       }
     } else {
       const Stage& pv = *stages_[si - 1];
+      if (st.head && head_done_) continue;  // done by loss() (xent_head)
       fork();
       if (st.fc_igdw) {
         gpu::IgemmDwParams w;

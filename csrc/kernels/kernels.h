@@ -261,6 +261,25 @@ struct XentParams {
   int32_t* pred = nullptr;              // optional argmax per sample
 };
 
+// Fused classifier head (bf16): softmax-CE forward+backward of XentParams
+// plus the last FC layer's backward, so dlogits never leave the workgroup:
+//   e      = (softmax(logits) - onehot) * scale         (bf16-rounded)
+//   dh     = (e W) * act'(h)          -> bf16 [M][ldh], pad columns zeroed
+//   slab_b = e^T [h | 1] over the workgroup's 128 rows: slab[b][n][ldp]
+//            (n < N, k <= Kin, k == Kin the bias) for dw_reduce (S = nwg)
+// Needs N <= 16, Kin < 128, ldh % 8 == 0.
+struct XentHeadParams {
+  XentParams x;
+  const void* h = nullptr; int ldh = 0;     // last FC input activations, bf16 [M][ldh]
+  const float* w = nullptr;                // last FC weights, fp32 [N][Kin]
+  int Kin = 0, act = 0;                    // act of h's producer (ACT_*)
+  void* dh = nullptr;                      // bf16 [M][ldh]
+  float* slab = nullptr; int ldp = 0;      // [nwg][N][ldp]
+};
+bool xent_head_supported(int N, int Kin, int ldh);
+int xent_head_slabs(int M);
+void xent_head(const XentHeadParams& p, hipStream_t s);
+
 // Explicit im2col for the large-image path: out[(n*OH+oy)*OW+ox][k], k =
 // (kh*KS+kw)*SC + c (zero for k >= KS*KS*SC), source through `s` (tile
 // coordinate oy*cs+kh maps to source (.. - off)/up).

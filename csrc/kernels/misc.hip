@@ -89,6 +89,172 @@ __global__ void __launch_bounds__(256) softmax_xent_kernel(XentParams p) {
   }
 }
 
+// Fused classifier head (XentHeadParams): 128 samples per workgroup, four
+// threads per sample.  Each computes the sample's softmax-CE (as
+// softmax_xent_kernel<., 16>; statistics counted once), then, without
+// writing dlogits, a quarter of the last FC layer's data gradient on the VALU
+// (e x W from LDS, N <= 16 FMAs per input feature, fused act') and of the
+// H^T image; the weight/bias gradient over the workgroup's 128 rows is
+// [e]^T [h | 1] on MFMA (E^T and H^T staged in LDS K(=row)-contiguous, one
+// 16-column tile per wave), written as this workgroup's slab.  Replaces
+// softmax_xent + last-FC dgrad + split-K dW GEMM (3 launches and the dlogits
+// round trip) for small heads (LeNet-5: 84 -> 10).
+constexpr int kHeadRows = 128;
+constexpr int kHeadThreads = 512;
+constexpr int kHeadLd = kHeadRows + 8;  // bf16 row stride of the transposed images (16-byte aligned)
+constexpr int kHeadLds = 16 * 128 * 4 + 16 * kHeadLd * 2 + 128 * kHeadLd * 2;
+
+__global__ void __launch_bounds__(kHeadThreads) xent_head_kernel(XentHeadParams hp) {
+  __shared__ __attribute__((aligned(16))) char smem[kHeadLds];
+  __shared__ float red[3][kHeadThreads / 64];
+  const XentParams& p = hp.x;
+  float* Ws = reinterpret_cast<float*>(smem);
+  bf16* E = reinterpret_cast<bf16*>(smem + 16 * 128 * 4);
+  bf16* HT = E + 16 * kHeadLd;
+  const int tid = threadIdx.x;
+  const int r = tid >> 2, q = tid & 3;
+  const int N = p.N, Kin = hp.Kin;
+  // weights rounded through bf16, as the packed compute copy of the FC path
+  for (int i = tid; i < 16 * 128; i += kHeadThreads) {
+    const int n = i >> 7, k = i & 127;
+    Ws[i] = (n < N && k < Kin) ? (float)(bf16)hp.w[(size_t)n * Kin + k] : 0.f;
+  }
+  const int row = blockIdx.x * kHeadRows + r;
+  const bool live = row < p.M;
+  float loss = 0.f, mse = 0.f, correct = 0.f;
+  float e[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) e[j] = 0.f;
+  if (live) {
+    const float* l = p.logits + (size_t)row * p.ldl;
+    const int sample = p.labels_idx ? p.labels_idx[row] : row;
+    const int label = p.labels[sample];
+    float v[16];
+#pragma unroll
+    for (int j = 0; j < 16; j += 4) {
+      if (j < N) {
+        const float4 t4 = *reinterpret_cast<const float4*>(l + j);
+        v[j] = t4.x; v[j + 1] = t4.y; v[j + 2] = t4.z; v[j + 3] = t4.w;
+      } else {
+        v[j] = v[j + 1] = v[j + 2] = v[j + 3] = 0.f;
+      }
+    }
+    float m = v[0];
+    int am = 0;
+#pragma unroll
+    for (int j = 1; j < 16; ++j)
+      if (j < N && v[j] > m) { m = v[j]; am = j; }  // first max wins (cnn.c:510)
+    float sum = 0.f;
+#pragma unroll
+    for (int j = 0; j < 16; ++j)
+      if (j < N) sum += __expf(v[j] - m);
+    const float inv = 1.f / sum;
+    float vl = 0.f;
+#pragma unroll
+    for (int j = 0; j < 16; ++j)
+      if (j == label) vl = v[j];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      if (j < N) {
+        const float pj = __expf(v[j] - m) * inv;
+        const float d = pj - (j == label ? 1.f : 0.f);
+        mse += d * d;
+        e[j] = (float)(bf16)(d * p.scale);  // the bf16 dlogits of the unfused path
+        if (p.probs && q == 0) p.probs[(size_t)row * N + j] = pj;
+      }
+    }
+    if (q == 0) {
+      loss = __logf(sum) - (vl - m);
+      correct = (am == label) ? 1.f : 0.f;
+      mse /= (float)N;
+      if (p.pred) p.pred[row] = am;
+    } else {
+      mse = 0.f;
+    }
+  }
+  if (q == 0) {
+#pragma unroll
+    for (int j = 0; j < 16; ++j) E[j * kHeadLd + r] = (bf16)e[j];
+  }
+  __syncthreads();  // Ws
+
+  // data gradient of the head input + the H^T image (row Kin = ones: bias);
+  // thread q of a sample owns the 8-feature chunks q, q+4, ...
+  const bf16* hrow = static_cast<const bf16*>(hp.h) + (size_t)row * hp.ldh;
+  bf16* drow = static_cast<bf16*>(hp.dh) + (size_t)row * hp.ldh;
+  const int K8 = (Kin + 7) & ~7;
+  const int NT = (Kin + 1 + 15) >> 4;
+  for (int k0 = 8 * q; k0 < K8; k0 += 32) {
+    bf16x8 hv;
+    if (live) hv = load8(hrow + k0);
+    else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) hv[i] = (bf16)0.f;
+    }
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int n = 0; n < 16; ++n) {
+      if (n >= N) break;
+      const f32x4 w0 = *reinterpret_cast<const f32x4*>(Ws + n * 128 + k0);
+      const f32x4 w1 = *reinterpret_cast<const f32x4*>(Ws + n * 128 + k0 + 4);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        acc[i] += e[n] * w0[i];
+        acc[4 + i] += e[n] * w1[i];
+      }
+    }
+    bf16x8 o;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int k = k0 + i;
+      const float y = (float)hv[i];
+      o[i] = k < Kin ? (bf16)(acc[i] * act_grad_y(hp.act, y)) : (bf16)0.f;
+      HT[k * kHeadLd + r] = (k < Kin && live) ? hv[i] : (bf16)((k == Kin && live) ? 1.f : 0.f);
+    }
+    if (live) store8(drow + k0, o);
+  }
+  if (q == 0)
+    for (int k = K8; k < 16 * NT; ++k) HT[k * kHeadLd + r] = (bf16)((k == Kin && live) ? 1.f : 0.f);
+  __syncthreads();
+
+  // weight + bias gradient of the workgroup's rows: wave w computes the
+  // 16-column tile t = w of C[n][k] = sum_rows E[n][row] HT[k][row]
+  const int lane = tid & 63, wave = tid >> 6, r16 = lane & 15, g = lane >> 4;
+  if (wave < NT) {
+    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < kHeadRows / 32; ++ks) {
+      const int kb = ks * 32 + 8 * g;
+      acc = mma(acc, load8(E + r16 * kHeadLd + kb), load8(HT + (16 * wave + r16) * kHeadLd + kb));
+    }
+    float* slab = hp.slab + (size_t)blockIdx.x * N * hp.ldp;
+    const int k = 16 * wave + r16;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int n = 4 * g + i;
+      if (n < N && k <= Kin) slab[n * hp.ldp + k] = acc[i];
+    }
+  }
+  // statistics (wave reduce, then across the waves in a fixed order)
+  for (int o = 32; o > 0; o >>= 1) {
+    loss += __shfl_xor(loss, o);
+    mse += __shfl_xor(mse, o);
+    correct += __shfl_xor(correct, o);
+  }
+  if (lane == 0) {
+    red[0][wave] = loss;
+    red[1][wave] = mse;
+    red[2][wave] = correct;
+  }
+  __syncthreads();
+  if (tid < 3 && p.stats) {
+    float t = 0.f;
+#pragma unroll
+    for (int w = 0; w < kHeadThreads / 64; ++w) t += red[tid][w];
+    atomicAdd(p.stats + tid, t);
+  }
+}
+
 // Wide class counts (ImageNet-style heads): one wave per row, lanes stride
 // over the classes, shuffle reductions; same outputs and tie rule as above.
 template <typename T>
@@ -230,6 +396,22 @@ inline unsigned grid_for(int64_t n, int per_thread = 1) {
 }
 
 }  // namespace
+
+bool xent_head_supported(int N, int Kin, int ldh) {
+  return N >= 1 && N <= 16 && Kin >= 1 && Kin < 128 && ldh % 8 == 0 && ldh >= Kin;
+}
+
+int xent_head_slabs(int M) { return cdiv(M, kHeadRows); }
+
+void xent_head(const XentHeadParams& p, hipStream_t s) {
+  MCC_CHECK(p.x.M > 0 && xent_head_supported(p.x.N, p.Kin, p.ldh), "xent_head: needs N <= 16, Kin < 128, ldh % 8 == 0");
+  MCC_CHECK(p.x.ldl % 4 == 0 && (reinterpret_cast<uintptr_t>(p.x.logits) & 15) == 0 && p.x.ldl >= ((p.x.N + 3) & ~3),
+            "xent_head: logits rows must be 16-byte aligned");
+  MCC_CHECK(p.h && p.dh && p.w && p.slab && p.ldp >= p.Kin + 1 && (reinterpret_cast<uintptr_t>(p.h) & 15) == 0 &&
+                (reinterpret_cast<uintptr_t>(p.dh) & 15) == 0,
+            "xent_head: bad buffers");
+  hipLaunchKernelGGL(xent_head_kernel, dim3((unsigned)xent_head_slabs(p.x.M)), dim3(kHeadThreads), 0, s, p);
+}
 
 void softmax_xent(DType t, const XentParams& p, hipStream_t s) {
   MCC_CHECK(p.M > 0 && p.N > 0, "softmax_xent: empty");
