@@ -79,11 +79,11 @@ $(OBJ)/apps/%.o: csrc/apps/%.cpp $(HDRS)
 
 build/bin/cnn_hip: $(OBJ)/apps/cnn_hip.o $(OBJ)/apps/trainer.o $(CORE_OBJ) $(KERN_OBJ) $(ENG_OBJ)
 	@mkdir -p $(dir $@)
-	$(HIPCC) --offload-arch=$(ARCH) -o $@ $^ $(LDHIP)
+	$(HIPCC) --offload-arch=$(ARCH) -o $@ $^ $(LDHIP) -lrocprofiler-sdk-roctx
 
 build/bin/cnn_dist: $(OBJ)/apps/cnn_dist.o $(OBJ)/apps/trainer.o $(CORE_OBJ) $(KERN_OBJ) $(ENG_OBJ)
 	@mkdir -p $(dir $@)
-	$(HIPCC) --offload-arch=$(ARCH) -o $@ $^ $(LDHIP) -lrccl
+	$(HIPCC) --offload-arch=$(ARCH) -o $@ $^ $(LDHIP) -lrccl -lrocprofiler-sdk-roctx
 
 # Host sanitizers: the CPU trainer and the core library
 # under AddressSanitizer + UBSan.  GPU-side sanitizers are not available on

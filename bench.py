@@ -24,7 +24,11 @@ sys.path.insert(0, ROOT)
 
 BASELINE_IMG_S = 2510.0  # best reference number (8-rank MPI CPU)
 METRIC = "images/sec (whole node), LeNet-5 MNIST-shaped, at 1/2/4/8 MI355X"
-DEFAULT_BATCH = {"lenet5": 16384, "ref": 16384, "cifar3": 4096, "vgg11": 256}
+# Per-GPU batch sized for 288 GB HBM3E: LeNet-5 throughput keeps rising with
+# batch (profiles/lenet5_batch_sweep_r1g.txt: 36.7 M img/s at 16,384 ->
+# 45.3 M at 65,536 -> 47.3 M at 131,072) as the persistent conv kernels'
+# per-step prologue/tail and the launch chain amortise; 65,536 is the knee.
+DEFAULT_BATCH = {"lenet5": 65536, "ref": 65536, "cifar3": 4096, "vgg11": 256}
 # models whose step is faster with the dW side stream (engine.cpp, measured A/B)
 SIDE_STREAM = {"cifar3"}
 

@@ -16,6 +16,8 @@
 #include <memory>
 #include <vector>
 
+#include <rocprofiler-sdk-roctx/roctx.h>
+
 #include "kernels.h"
 #include "mcc/cpu_net.h"
 #include "mcc/engine.h"
@@ -49,7 +51,16 @@ struct PhaseTimer {
   ~PhaseTimer() {
     if (on) for (auto& e : ev) (void)hipEventDestroy(e);
   }
-  void mark(int i, hipStream_t s) { if (on) HIPCHK(hipEventRecord(ev[i], s)); }
+  // hipEvent per-phase timing plus a roctx range per phase, so a
+  // `rocprofv3 --marker-trace` run attributes kernels to fwd/bwd/sync/update
+  // (the reference has no instrumentation at all).
+  static constexpr const char* kPhase[4] = {"mcc.forward+loss", "mcc.backward+allreduce", "mcc.allreduce_join", "mcc.sgd"};
+  void mark(int i, hipStream_t s) {
+    if (!on) return;
+    HIPCHK(hipEventRecord(ev[i], s));
+    if (i > 0) roctxRangePop();
+    if (i < 4) roctxRangePush(kPhase[i]);
+  }
   void collect() {
     if (!on) return;
     HIPCHK(hipEventSynchronize(ev[4]));

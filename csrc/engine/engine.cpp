@@ -97,6 +97,11 @@ GpuNet::GpuNet(const ModelSpec& spec, DType dtype, int max_batch, int device)
     : spec_(spec), dtype_(dtype), max_batch_(max_batch), device_(device) {
   MCC_CHECK(dtype == DType::BF16 || dtype == DType::F32, "GpuNet: dtype must be bf16 or fp32");
   MCC_CHECK(max_batch > 0, "GpuNet: max_batch > 0");
+  // Kernels index activations with 32-bit element offsets; channel counts are
+  // padded up to 16 in the packed layouts, so bound the padded tensor size.
+  for (const LayerSpec& l : spec.layers)
+    MCC_CHECK((int64_t)max_batch * ((l.C + 15) / 16 * 16) * l.H * l.W < (1ll << 31),
+              "GpuNet: max_batch too large for 32-bit activation indexing");
   if (const char* a = std::getenv("MCC_ABLATE")) ablate_ = std::atoi(a);  // kernel diagnostics only
   if (const char* a = std::getenv("MCC_NO_PIPE")) no_pipe_ = std::atoi(a) != 0;  // A/B against conv_small
   if (const char* a = std::getenv("MCC_NO_FC")) no_fc_ = std::atoi(a) != 0;      // A/B against the tiled GEMM

@@ -218,3 +218,58 @@ def test_vgg11_step_runs(cuda):
     assert np.isfinite(st["loss_sum"]) and 0 < st["loss_sum"] / B < 20
     g = net.get_grads()
     assert np.isfinite(g).all() and np.abs(g).max() > 0
+
+
+@pytest.mark.gpu
+def test_bench_batch_step_matches_small_batches(cuda):
+    """bench.py's per-GPU batch (65,536, plus a ragged tail): the persistent
+    kernels' many-group loops and 32-bit activation offsets at full size must
+    give the same logits and summed gradients as 1,024-image chunks through
+    the small-batch path (which test_step_matches_torch pins to PyTorch).
+    A PyTorch reference at this size would spend minutes in MIOpen's first
+    backward-convolution search on a fresh box."""
+    spec = mcc.make_model("lenet5")
+    B, b = 65536 + 37, 1024
+    imgs, labels = mcc.synth_dataset(B, 1, 28, 28, 10, seed=21)
+    params = mcc.init_params(spec, seed=4).astype(np.float32)
+    d_img = torch.from_numpy(imgs).to(cuda)
+    d_lab = torch.from_numpy(labels).to(cuda)
+    s = torch.cuda.current_stream().cuda_stream
+
+    big = mcc.GpuNet(spec, "bf16", B)
+    big.set_params(params)
+    big.zero_stats(s)
+    big.forward(d_img.data_ptr(), 0, B, s)
+    big.loss(d_lab.data_ptr(), 0, 1.0 / B, True, s)
+    big.backward_all(s)
+    torch.cuda.synchronize()
+    logits, grads = big.get_logits(B), big.get_grads()
+    del big
+
+    small = mcc.GpuNet(spec, "bf16", b)
+    small.set_params(params)
+    ref_logits = np.empty_like(logits)
+    ref_grads = np.zeros_like(grads, dtype=np.float64)
+    for i in range(0, B, b):
+        nb = min(b, B - i)
+        idx = torch.arange(i, i + nb, device=cuda, dtype=torch.int32)
+        small.forward(d_img.data_ptr(), idx.data_ptr(), nb, s)
+        small.loss(d_lab.data_ptr(), idx.data_ptr(), 1.0 / B, True, s)
+        small.backward_all(s)
+        torch.cuda.synchronize()
+        ref_logits[i : i + nb] = small.get_logits(nb)
+        ref_grads += small.get_grads()
+    assert _relerr(logits, ref_logits) < 1e-2
+    for L in spec.layers():
+        if L["nweights"] == 0:
+            continue
+        for off, n, what in ((L["w_off"], L["nweights"], "W"), (L["b_off"], L["nbiases"], "b")):
+            err = _relerr(grads[off : off + n], ref_grads[off : off + n])
+            assert err < 2e-2, f"layer {L['kind']} {what} grad rel err {err:.3e}"
+
+
+@pytest.mark.gpu
+def test_max_batch_guard(cuda):
+    spec = mcc.make_model("lenet5")
+    with pytest.raises(Exception, match="32-bit activation indexing"):
+        mcc.GpuNet(spec, "bf16", 1 << 20)
