@@ -2,6 +2,8 @@
 // See conv_pipe_fwd.hip for the design notes.
 #pragma once
 
+#include <cstdlib>
+
 #include <algorithm>
 
 #include "kernels.h"
@@ -329,6 +331,17 @@ bool plan_src(PipeSrc& s, int layout, int CLdst, int LH, int LWp, int IMGextra) 
   s.LWp = LWp;
   return true;
 }
+
+// Occupancy / group-size knobs of the pipelined conv planners, read once
+// (A/B tuning only; defaults are the measured choices).
+inline int pipe_knob(const char* name, int def) {
+  const char* v = std::getenv(name);
+  return v && *v ? std::atoi(v) : def;
+}
+inline int dw_wgs_cap() { static const int v = pipe_knob("MCC_DW_WGS", 2); return v; }
+inline int fwd_wgs_cap() { static const int v = pipe_knob("MCC_FWD_WGS", 4); return v; }
+inline size_t dw_lds_target() { static const size_t v = (size_t)pipe_knob("MCC_DW_LDS_KB", 64) * 1024; return v; }
+inline size_t fwd_lds_target() { static const size_t v = (size_t)pipe_knob("MCC_FWD_LDS_KB", 64) * 1024; return v; }
 
 int wgs_per_cu(size_t lds, int cap) {
   int w = (int)(kLdsPerCU / (lds + 512));

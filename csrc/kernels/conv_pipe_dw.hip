@@ -294,21 +294,21 @@ bool conv_dw_pipe_plan(ConvDwPipeParams& p) {
     p.imgs = imgs;
     p.ppad = r32h(imgs * p.OH * p.OW);
     if (s1) x.CS = r8h(imgs * x.IMG + 8);
-    if ((size_t)dw_layout(p).total <= 64 * 1024 || imgs == 1) break;
+    if ((size_t)dw_layout(p).total <= dw_lds_target() || imgs == 1) break;
   }
   if (nix < 1 || nid < 1) return false;
   const DwLayout L = dw_layout(p);
   if ((size_t)L.total > kLdsPerCU) return false;
   p.lds = (size_t)L.total;
   p.ngroups = cdiv(p.N, p.imgs);
-  p.grid = std::min(p.ngroups, kCUs * wgs_per_cu(p.lds, 2));
+  p.grid = std::min(p.ngroups, kCUs * wgs_per_cu(p.lds, dw_wgs_cap()));
   return true;
 }
 
 void conv_dw_pipe(const ConvDwPipeParams& pin, hipStream_t st) {
   ConvDwPipeParams p = pin;
   p.ngroups = cdiv(p.N, p.imgs);
-  p.grid = std::min(p.ngroups, std::min(pin.grid, kCUs * wgs_per_cu(p.lds, 2)));
+  p.grid = std::min(p.ngroups, std::min(pin.grid, kCUs * wgs_per_cu(p.lds, dw_wgs_cap())));
   if (p.grid <= 0) return;
   const int mtw = p.cout_pad / 16;
   const int ncol_tiles = p.ncols_pad / 16;
@@ -339,7 +339,7 @@ void conv_dw_pipe(const ConvDwPipeParams& pin, hipStream_t st) {
 void conv_dw_pipe_reduce(const ConvDwPipeParams& pin, float* gw, float* gb, hipStream_t st) {
   ConvDwPipeParams p = pin;
   const int ngroups = cdiv(p.N, p.imgs);
-  const int nx = std::min(ngroups, std::min(pin.grid, kCUs * wgs_per_cu(p.lds, 2)));
+  const int nx = std::min(ngroups, std::min(pin.grid, kCUs * wgs_per_cu(p.lds, dw_wgs_cap())));
   if (nx <= 0) return;
   const int nv = p.cout_pad * p.ncols_pad;
   const int xs_per = 64;

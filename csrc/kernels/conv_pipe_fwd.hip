@@ -318,14 +318,14 @@ bool conv_pipe_plan(ConvPipeParams& p) {
   for (; imgs >= 1; --imgs) {
     p.imgs = imgs;
     if (s1) s.CS = r8h(imgs * s.IMG + 8);
-    if ((size_t)fwd_layout(p).total <= 64 * 1024 || imgs == 1) break;
+    if ((size_t)fwd_layout(p).total <= fwd_lds_target() || imgs == 1) break;
   }
   if (imgs < 1) return false;
   const FwdLayout L = fwd_layout(p);
   if ((size_t)L.total > kLdsPerCU) return false;
   p.lds = (size_t)L.total;
   p.ngroups = cdiv(p.N, p.imgs);
-  p.grid = std::min(p.ngroups, kCUs * wgs_per_cu(p.lds, 4));
+  p.grid = std::min(p.ngroups, kCUs * wgs_per_cu(p.lds, fwd_wgs_cap()));
   return true;
 }
 
@@ -339,7 +339,7 @@ void conv_pipe_forward(const ConvPipeParams& pin, hipStream_t st) {
     p.rows_ml = d.ml;
   }
   p.ngroups = cdiv(p.N, p.imgs);
-  p.grid = std::min(p.ngroups, kCUs * wgs_per_cu(p.lds, 4));
+  p.grid = std::min(p.ngroups, kCUs * wgs_per_cu(p.lds, fwd_wgs_cap()));
   if (p.grid <= 0) return;
   // the single-channel pair kernel has long per-group MFMA phases: 8 waves
   // hide more LDS latency; the others are barrier-bound at 4 waves
