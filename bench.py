@@ -28,7 +28,8 @@ METRIC = "images/sec (whole node), LeNet-5 MNIST-shaped, at 1/2/4/8 MI355X"
 # batch (profiles/lenet5_batch_sweep_r1g.txt: 36.7 M img/s at 16,384 ->
 # 45.3 M at 65,536 -> 47.3 M at 131,072) as the persistent conv kernels'
 # per-step prologue/tail and the launch chain amortise; 65,536 is the knee.
-DEFAULT_BATCH = {"lenet5": 65536, "ref": 65536, "cifar3": 4096, "vgg11": 256}
+# CIFAR-3conv: 1.88 M img/s at 4,096 -> 2.58 M at 16,384 (profiles/bench_models_r1g.jsonl).
+DEFAULT_BATCH = {"lenet5": 65536, "ref": 65536, "cifar3": 16384, "vgg11": 256}
 # models whose step is faster with the dW side stream (engine.cpp, measured A/B)
 SIDE_STREAM = {"cifar3"}
 
