@@ -36,6 +36,8 @@ def _parse(argv):
     ap.add_argument("--dtype", default="bf16")
     ap.add_argument("--device", default="auto", choices=["auto", "gpu", "cpu"])
     ap.add_argument("--bucket-mb", type=float, default=4.0)
+    ap.add_argument("--dist-backend", default="auto", choices=["auto", "nccl", "gloo"],
+                    help="torch.distributed backend for world > 1 (auto: nccl = RCCL on GPUs, gloo on CPU)")
     ap.add_argument("--log-every", type=int, default=1000)
     ap.add_argument("--save", default="")
     ap.add_argument("--load", default="")
@@ -80,9 +82,14 @@ def main(argv=None) -> int:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if use_gpu:
+        # more ranks than GPUs (rehearsal on a small box, gloo only): share devices
+        local_rank %= max(1, torch.cuda.device_count())
     if world > 1:
+        backend = a.dist_backend if a.dist_backend != "auto" else ("nccl" if use_gpu else "gloo")
         if use_gpu:
             torch.cuda.set_device(local_rank)
+        if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
         else:
             dist.init_process_group("gloo")

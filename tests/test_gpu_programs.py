@@ -74,6 +74,32 @@ def test_python_train_gpu(idx_files):
 
 
 @pytest.mark.gpu
+def test_python_train_gpu_two_ranks(idx_files):
+    """The train CLI under torch.distributed.run with two ranks sharing the
+    box's one GPU (gloo transport; RCCL needs a GPU per rank): per-rank shard
+    lines, rank-0 log and test accuracy, the same GpuTrainer DP path as the
+    driver's multi-GPU runs."""
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    r = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+              "--master-addr=127.0.0.1", f"--master-port={_free_port()}", "-m", "mpi_cuda_cnn_amd.train"] +
+             idx_files + ["--model", "lenet5", "--batch", "512", "--epochs", "2", "--lr", "0.05",
+                          "--momentum", "0.5", "--device", "gpu", "--dist-backend", "gloo"], cwd=ROOT, env=env)
+    assert r.returncode == 0, r.stderr
+    lines = r.stderr.strip().splitlines()
+    assert "0 0 2000" in lines and "1 2000 4000" in lines, r.stderr
+    last = [l for l in lines if l.startswith("ntests=")]
+    assert len(last) == 1 and int(last[0].split("=")[-1]) >= 950, r.stderr
+
+
+def _free_port():
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.mark.gpu
 def test_exit_codes_gpu_programs(idx_files):
     for prog in ("cnn_hip", "cnn_dist"):
         assert _run([os.path.join(ROOT, "build/bin", prog)]).returncode == 100
