@@ -37,7 +37,7 @@ ifneq ($(MPICXX),)
 BINS      += build/bin/cnnmpi
 endif
 
-.PHONY: all module bins clean asan
+.PHONY: all module bins clean asan checked
 all: module bins
 module: $(MODULE)
 bins: $(BINS)
@@ -93,6 +93,15 @@ build/bin/cnn_asan: csrc/apps/cnn.cpp $(CORE_SRC) $(HDRS)
 	@mkdir -p $(dir $@)
 	$(CXX) -O1 -g -std=c++17 $(INC) -fsanitize=address,undefined -fno-omit-frame-pointer \
 	  -fno-sanitize-recover=undefined -o $@ csrc/apps/cnn.cpp $(CORE_SRC) -lm
+
+# Device bounds checks (MCC_DCHECK in the pipelined conv kernels): a separate
+# module under build/checked/ (same Python package, checked _C); run e.g.
+#   MCC_PKG_ROOT=build/checked python -m pytest tests/test_gpu_engine.py -m gpu
+checked:
+	mkdir -p build/checked/mpi_cuda_cnn_amd
+	$(MAKE) OBJ=build/obj_checked OPT="-O3 -DMCC_DEVICE_CHECKS" MODULE=build/checked/mpi_cuda_cnn_amd/_C$(EXT) \
+	  build/checked/mpi_cuda_cnn_amd/_C$(EXT)
+	cd mpi_cuda_cnn_amd && find . -name '*.py' -exec install -D -m 644 {} ../build/checked/mpi_cuda_cnn_amd/{} \;
 
 clean:
 	rm -rf build $(MODULE)

@@ -9,6 +9,22 @@
 #include "kernels.h"
 #include "mfma.h"
 
+// Device-side bounds checks, compiled in with
+// `make checked` (-DMCC_DEVICE_CHECKS).  A failed check prints and the
+// kernel carries on: it never traps, so a bad index is reported without
+// faulting the GPU.  Compiles to nothing in the default build.
+#ifdef MCC_DEVICE_CHECKS
+#define MCC_DCHECK(cond)                                                                         \
+  do {                                                                                           \
+    if (!(cond)) printf("MCC_DCHECK failed %s:%d: %s (block %d thread %d)\n", __FILE__, __LINE__, \
+                        #cond, (int)blockIdx.x, (int)threadIdx.x);                               \
+  } while (0)
+#else
+#define MCC_DCHECK(cond) \
+  do {                   \
+  } while (0)
+#endif
+
 namespace mcc {
 namespace gpu {
 namespace {
@@ -116,6 +132,7 @@ struct Loader {
         const int ty = (MODE == PM_UNPOOL ? 2 * sy : sy) * s.up + s.offy;
         const int tx = (MODE == PM_UNPOOL ? 2 * sx : sx) * s.up + s.offx;
         dst[i] = m * s.IMG + (ty * s.LWp + tx) * s.CL + run * s.RW;
+        MCC_DCHECK(dst[i] >= 0 && dst[i] + s.RW <= imgs * s.IMG);
       }
     }
   }

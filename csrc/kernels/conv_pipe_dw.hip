@@ -189,6 +189,7 @@ __global__ void __launch_bounds__(kT) conv_dw_pipe_kernel(ConvDwPipeParams p) {
   for (int e = tid; e < p.cout_pad * rcols; e += kT) {
     const int row = e / rcols, c = e - row * rcols;
     const int col = blockIdx.y * rcols + c;
+    MCC_DCHECK(row < p.cout_pad && (int)blockIdx.x < p.grid);
     if (col < p.ncols_pad) p.slab[((size_t)blockIdx.x * p.cout_pad + row) * p.ncols_pad + col] = red[e];
   }
 }

@@ -132,7 +132,10 @@ __global__ void __launch_bounds__(NT) conv_pipe_fwd_kernel(ConvPipeParams p) {
         base[t] = img * s.IMG;
       }
 #pragma unroll
-      for (int t = 0; t < MT; ++t) base[t] += ptab[ti[t]];
+      for (int t = 0; t < MT; ++t) {
+        base[t] += ptab[ti[t]];
+        MCC_DCHECK(base[t] >= 0 && base[t] < L.xs_elems);
+      }
       f32x4 acc[MT];
 #pragma unroll
       for (int t = 0; t < MT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -225,6 +228,7 @@ __global__ void __launch_bounds__(NT) conv_pipe_fwd_kernel(ConvPipeParams p) {
             const int win = (rb >> 1) + (right ? 1 : 0);
             if (c < p.Cout && 2 * win < M) {
               const int o = win * p.Cout + c;
+              MCC_DCHECK(o < p.imgs * out_img);
               outs[o] = (bf16)y;
               args[o] = (uint8_t)arg;
             }
@@ -257,6 +261,7 @@ __global__ void __launch_bounds__(NT) conv_pipe_fwd_kernel(ConvPipeParams p) {
             arg = gt ? i : arg;
           }
           const int o = (rb >> 2) * p.Cout + n;
+          MCC_DCHECK(o < p.imgs * out_img);
           outs[o] = (bf16)fmaxf(best + bv, 0.f);
           args[o] = (uint8_t)arg;
         } else {

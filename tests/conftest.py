@@ -6,6 +6,10 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
+# MCC_PKG_ROOT=build/checked: import the package built by `make checked`
+# (device bounds checks compiled in) instead of the in-tree one
+if os.environ.get("MCC_PKG_ROOT"):
+    sys.path.insert(0, os.path.join(ROOT, os.environ["MCC_PKG_ROOT"]))
 
 
 def pytest_configure(config):
