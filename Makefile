@@ -32,7 +32,7 @@ ENG_OBJ   := $(patsubst csrc/engine/%.cpp,$(OBJ)/engine/%.o,$(ENG_SRC))
 HDRS      := $(wildcard csrc/include/mcc/*.h csrc/kernels/*.h csrc/apps/*.h)
 
 MODULE    := mpi_cuda_cnn_amd/_C$(EXT)
-BINS      := build/bin/cnn build/bin/cnn_hip build/bin/cnn_dist
+BINS      := build/bin/cnn build/bin/cnn_hip build/bin/cnn_dist build/bin/test_watchdog
 ifneq ($(MPICXX),)
 BINS      += build/bin/cnnmpi
 endif
@@ -64,6 +64,10 @@ $(MODULE): $(OBJ)/bindings/module.o $(CORE_OBJ) $(KERN_OBJ) $(ENG_OBJ)
 build/bin/cnn: csrc/apps/cnn.cpp $(CORE_OBJ) $(HDRS)
 	@mkdir -p $(dir $@)
 	$(CXX) $(CXXFLAGS) -o $@ csrc/apps/cnn.cpp $(CORE_OBJ) -lm
+
+build/bin/test_watchdog: csrc/tests/test_watchdog.cpp csrc/apps/watchdog.h
+	@mkdir -p $(dir $@)
+	$(CXX) $(CXXFLAGS) -Icsrc/apps -o $@ csrc/tests/test_watchdog.cpp
 
 # MPICH's wrapper would put its own (older) libstdc++ first; link with the
 # system compiler against the MPI library instead, libstdc++ static.

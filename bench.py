@@ -53,6 +53,8 @@ def main():
     ap.add_argument("--bucket-mb", type=float, default=4.0)
     ap.add_argument("--lr", type=float, default=0.05)
     ap.add_argument("--momentum", type=float, default=0.9)
+    ap.add_argument("--no-dist", action="store_true",
+                    help="N=1 only: no process group, no collectives (A/B against the RCCL path)")
     args = ap.parse_args()
 
     import torch
@@ -65,8 +67,12 @@ def main():
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+    if world > 1 or not args.no_dist:
+        # RCCL process group at every N, 1 included: the N=1 step runs the
+        # same broadcast + bucketed all-reduce on RCCL's stream as N=8
+        from mpi_cuda_cnn_amd.parallel.ddp import init_process_group
+
+        init_process_group("nccl", dev)
 
     import mpi_cuda_cnn_amd as mcc
     from mpi_cuda_cnn_amd.trainer import GpuTrainer
@@ -103,19 +109,21 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
     torch.cuda.synchronize()
     tr.zero_stats()
+    issued0 = tr.sync.issued
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
     torch.cuda.synchronize()
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    if world > 1:
+    coll_per_step = (tr.sync.issued - issued0) / max(1, args.steps)
+    if dist.is_initialized():
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
@@ -144,12 +152,14 @@ def main():
                 "batch_per_gpu": B,
                 "input_shape": f"{C}x{H}x{W}",
                 "optimizer": f"sgd lr={args.lr} momentum={args.momentum}",
-                "allreduce": f"rccl bucketed {args.bucket_mb} MiB, overlapped",
+                "allreduce": (f"rccl: {coll_per_step:g} all-reduce(s)/step over {len(tr.sync.buckets)} "
+                              f"bucket(s) <= {args.bucket_mb} MiB, async on RCCL's stream, joined before SGD"
+                              if coll_per_step else "none (--no-dist)"),
                 "train_loss_last": round(st["loss_sum"] / (B * args.steps), 4),
             },
         }
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 

@@ -36,8 +36,9 @@ struct CliArgs {
   bool ref_compat = false;  // CPU: reference D1 indexing + per-sample loop
   bool fp32 = false;        // CPU: fp32 instead of fp64
   int64_t max_train = -1;   // limit training samples
-  int64_t bucket_mb = 4;    // DP gradient bucket size
+  double bucket_mb = 4.0;   // DP gradient bucket size (MiB)
   bool profile = false;     // per-phase timers
+  bool no_graph = false;    // run the step eagerly instead of replaying a hipGraph
   bool quiet = false;
   int64_t synthetic = 0;    // --synthetic N: generated data instead of IDX files
 };
@@ -48,7 +49,7 @@ inline void usage(const char* prog) {
                "  [--model ref|lenet5|cifar3|vgg11] [--epochs N] [--batch B] [--lr X]\n"
                "  [--momentum X] [--weight-decay X] [--seed S] [--dtype bf16|fp32]\n"
                "  [--ref-compat] [--fp32] [--save W] [--load W] [--max-train N]\n"
-               "  [--bucket-mb MB] [--log-every N] [--profile] [--json PATH|-]\n"
+               "  [--bucket-mb MB] [--log-every N] [--profile] [--no-graph] [--json PATH|-]\n"
                "  [--synthetic N]   (no IDX files: N generated training images, N/5 test images\n"
                "                     of the model's input shape; positional paths optional)\n",
                prog);
@@ -74,13 +75,14 @@ inline int parse_cli(int argc, char** argv, CliArgs& a) {
     else if (s == "--save") a.save = next();
     else if (s == "--load") a.load = next();
     else if (s == "--max-train") a.max_train = std::atoll(next().c_str());
-    else if (s == "--bucket-mb") a.bucket_mb = std::atoll(next().c_str());
+    else if (s == "--bucket-mb") a.bucket_mb = std::atof(next().c_str());
     else if (s == "--log-every") a.log_every = std::atoi(next().c_str());
     else if (s == "--json") a.log_json = next();
     else if (s == "--ref-compat") a.ref_compat = true;
     else if (s == "--synthetic") a.synthetic = std::atoll(next().c_str());
     else if (s == "--fp32") a.fp32 = true;
     else if (s == "--profile") a.profile = true;
+    else if (s == "--no-graph") a.no_graph = true;
     else if (s == "--quiet") a.quiet = true;
     else if (s == "-h" || s == "--help") { usage(argv[0]); std::exit(0); }
     else if (s.size() > 2 && s[0] == '-' && s[1] == '-') { usage(argv[0]); std::exit(100); }
@@ -101,9 +103,14 @@ inline int parse_cli(int argc, char** argv, CliArgs& a) {
 
 // An IDX file, or "synthetic:<N>:<seed>:images|labels": the stripe dataset
 // of io.h in the model's input shape (so the binaries run on boxes without
-// MNIST).  Throws mcc::Error like idx_read.
+// MNIST).  Throws mcc::Error like idx_read; a 1-D (label) file with a label
+// outside the model's classes is rejected here (labels index the loss).
 inline IdxFile load_idx(const std::string& path, const ModelSpec& spec) {
-  if (path.rfind("synthetic:", 0) != 0) return idx_read(path);
+  if (path.rfind("synthetic:", 0) != 0) {
+    IdxFile f = idx_read(path);
+    if (f.dims.size() == 1) check_labels(f, f.count(), spec.num_classes(), path);
+    return f;
+  }
   const size_t a1 = path.find(':', 10), a2 = path.find(':', a1 + 1);
   if (a1 == std::string::npos || a2 == std::string::npos) throw Error("bad synthetic spec: " + path);
   const int64_t n = std::atoll(path.substr(10, a1 - 10).c_str());

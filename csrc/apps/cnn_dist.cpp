@@ -11,7 +11,15 @@
 // Rendezvous: rank 0 creates the RCCL unique id and serves it over TCP on
 // MASTER_ADDR:(MCC_BOOTSTRAP_PORT or MASTER_PORT+1); every wait is bounded
 // (MCC_BOOTSTRAP_TIMEOUT seconds, default 300) so a dead rank cannot hang
-// the others forever (defect D9).
+// the others forever (defect D9).  After the rendezvous every host-side wait
+// goes through the collective watchdog (watchdog.h: ncclCommGetAsyncError +
+// deadline MCC_COMM_TIMEOUT); on expiry the rank aborts its communicator and
+// exits 111.
+//
+// The RCCL communicator is created at every world size, 1 included, so a
+// single-GPU run executes the same broadcast, bucketed all-reduce on the comm
+// stream and graph-captured collectives as an 8-GPU one.  MCC_LOCAL_COMM=1
+// (world 1 only) swaps in the collective-free LocalComm for A/B runs.
 #include <arpa/inet.h>
 #include <netdb.h>
 #include <netinet/in.h>
@@ -31,6 +39,7 @@
 
 #include "cli.h"
 #include "trainer.h"
+#include "watchdog.h"
 
 namespace mcc {
 namespace {
@@ -80,6 +89,7 @@ void bootstrap_id(ncclUniqueId& id, int rank, int world) {
   const auto deadline = std::chrono::steady_clock::now() + std::chrono::seconds(timeout_s);
   if (rank == 0) {
     NCCLCHK(ncclGetUniqueId(&id));
+    if (world == 1) return;  // nobody to serve
     int srv = ::socket(AF_INET, SOCK_STREAM, 0);
     int one = 1;
     ::setsockopt(srv, SOL_SOCKET, SO_REUSEADDR, &one, sizeof(one));
@@ -131,6 +141,9 @@ struct RcclComm : Comm {
   int rank_ = 0, world_ = 1, local_ = 0;
   ncclComm_t comm_ = nullptr;
   float* dummy_ = nullptr;
+  hipStream_t bs_ = nullptr;  // barrier stream
+  hipEvent_t bev_ = nullptr;
+  double timeout_s_ = comm_timeout_s();
 
   RcclComm(int rank, int world, int local) : rank_(rank), world_(world), local_(local) {
     int ndev = 0;
@@ -140,16 +153,25 @@ struct RcclComm : Comm {
     bootstrap_id(id, rank_, world_);
     NCCLCHK(ncclCommInitRank(&comm_, world_, id, rank_));
     if (hipMalloc(&dummy_, 64) != hipSuccess) throw Error("hipMalloc failed");
+    if (hipStreamCreateWithFlags(&bs_, hipStreamNonBlocking) != hipSuccess) throw Error("hipStreamCreate failed");
+    if (hipEventCreateWithFlags(&bev_, hipEventDisableTiming) != hipSuccess) throw Error("hipEventCreate failed");
   }
   ~RcclComm() override {
+    if (bev_) (void)hipEventDestroy(bev_);
+    if (bs_) (void)hipStreamDestroy(bs_);
     if (dummy_) (void)hipFree(dummy_);
     if (comm_) ncclCommDestroy(comm_);
   }
   int rank() const override { return rank_; }
   int size() const override { return world_; }
   int local_rank() const override { return local_; }
+  const char* name() const override { return "rccl"; }
+  bool collective() const override { return true; }
   void allreduce_sum_f32(float* buf, int64_t n, hipStream_t s) override {
     NCCLCHK(ncclAllReduce(buf, buf, (size_t)n, ncclFloat32, ncclSum, comm_, s));
+  }
+  void allreduce_avg_f32(float* buf, int64_t n, hipStream_t s) override {
+    NCCLCHK(ncclAllReduce(buf, buf, (size_t)n, ncclFloat32, ncclAvg, comm_, s));
   }
   void allreduce_max_f64(double* buf, int64_t n, hipStream_t s) override {
     NCCLCHK(ncclAllReduce(buf, buf, (size_t)n, ncclFloat64, ncclMax, comm_, s));
@@ -157,9 +179,35 @@ struct RcclComm : Comm {
   void broadcast_f32(float* buf, int64_t n, int root, hipStream_t s) override {
     NCCLCHK(ncclBroadcast(buf, buf, (size_t)n, ncclFloat32, root, comm_, s));
   }
+  // Collective watchdog: poll the event and the communicator's async error
+  // state until the deadline (watchdog.h).
+  void wait(hipEvent_t ev) override {
+    ncclResult_t async = ncclSuccess;
+    hipError_t herr = hipSuccess;
+    const WaitStatus st = bounded_wait(
+        [&] {
+          herr = hipEventQuery(ev);
+          return herr != hipErrorNotReady;
+        },
+        [&] {
+          if (herr != hipSuccess && herr != hipErrorNotReady) return 1;
+          if (comm_ && ncclCommGetAsyncError(comm_, &async) == ncclSuccess && async != ncclSuccess &&
+              async != ncclInProgress)
+            return 2;
+          return 0;
+        },
+        timeout_s_);
+    if (st == WaitStatus::Done && herr == hipSuccess) return;
+    if (st == WaitStatus::Timeout)
+      throw Error("collective watchdog: no progress within " + std::to_string(timeout_s_) +
+                  " s (MCC_COMM_TIMEOUT); a peer rank is gone or hung");
+    if (herr != hipSuccess && herr != hipErrorNotReady) throw Error(std::string("HIP: ") + hipGetErrorString(herr));
+    throw Error(std::string("RCCL async error: ") + ncclGetErrorString(async));
+  }
   void barrier() override {
-    NCCLCHK(ncclAllReduce(dummy_, dummy_, 1, ncclFloat32, ncclSum, comm_, nullptr));
-    (void)hipStreamSynchronize(nullptr);
+    NCCLCHK(ncclAllReduce(dummy_, dummy_, 1, ncclFloat32, ncclSum, comm_, bs_));
+    if (hipEventRecord(bev_, bs_) != hipSuccess) throw Error("hipEventRecord failed");
+    wait(bev_);
   }
   void abort(const char* why) override {
     std::fprintf(stderr, "rank %d aborting: %s\n", rank_, why);
@@ -182,8 +230,9 @@ int main(int argc, char** argv) {
       mcc::env_int((const char*[]){"LOCAL_RANK", "OMPI_COMM_WORLD_LOCAL_RANK", "MPI_LOCALRANKID", nullptr}, rank);
   std::unique_ptr<mcc::Comm> comm;
   try {
-    if (world > 1) comm.reset(new mcc::RcclComm(rank, world, local));
-    else comm.reset(new mcc::LocalComm());
+    const char* lc = std::getenv("MCC_LOCAL_COMM");
+    if (world == 1 && lc && std::atoi(lc) != 0) comm.reset(new mcc::LocalComm());
+    else comm.reset(new mcc::RcclComm(rank, world, local));
   } catch (const mcc::Error& e) {
     std::fprintf(stderr, "rank %d: %s\n", rank, e.what());
     return 111;

@@ -118,8 +118,12 @@ int run_gpu_training(const CliArgs& a, Comm& comm, const char* program) {
   const int64_t shard_lo = N / world * rank, shard_hi = N / world * (rank + 1);
   if (world > 1) std::fprintf(stderr, "%d %lld %lld\n", rank, (long long)shard_lo, (long long)shard_hi);
 
-  const int B_global = a.batch;
-  const int b = std::max(1, B_global / world);
+  // Each rank trains b = floor(B / world) samples per step: the effective
+  // global batch (the SGD mean, the sample count and img/s) is b * world.
+  const int b = std::max(1, a.batch / world);
+  const int B_eff = b * world;
+  if (rank == 0 && B_eff != a.batch)
+    std::fprintf(stderr, "note: --batch %d is not a multiple of %d ranks; global batch %d\n", a.batch, world, B_eff);
   const int eval_b = std::max(b, 1024);
   GpuNet net(spec, dt, eval_b);
   {
@@ -130,22 +134,33 @@ int run_gpu_training(const CliArgs& a, Comm& comm, const char* program) {
   HIPCHK(hipMemcpy(d_img.p, tr_img.data.data(), (size_t)N * in_nodes, hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(d_lab.p, tr_lab.data.data(), (size_t)N, hipMemcpyHostToDevice));
   DevBuf d_idx(4 * (size_t)eval_b), d_step(8);
+  DevBuf d_red(64);  // log / timing / exit-code reductions (no allocation in the loop)
+  float* h_red = nullptr;
+  HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&h_red), 64, hipHostMallocDefault));
+  std::unique_ptr<float, hipError_t (*)(void*)> h_red_guard(h_red, hipHostFree);
   HIPCHK(hipMemset(d_step.p, 0, 8));
 
   hipStream_t S, C;
   HIPCHK(hipStreamCreateWithFlags(&S, hipStreamNonBlocking));
   HIPCHK(hipStreamCreateWithFlags(&C, hipStreamNonBlocking));
+  const bool coll = comm.collective();
   // identical weights on every rank (fixes D6: srand(rank), no broadcast)
   comm.broadcast_f32(net.params(), net.nparams(), 0, S);
   net.pack(S);
-  HIPCHK(hipStreamSynchronize(S));
+  hipEvent_t ev_sync;
+  HIPCHK(hipEventCreateWithFlags(&ev_sync, hipEventDisableTiming));
+  HIPCHK(hipEventRecord(ev_sync, S));
+  comm.wait(ev_sync);
 
-  const auto buckets = net.buckets(a.bucket_mb << 20);
+  const auto buckets = net.buckets((int64_t)(a.bucket_mb * (1 << 20)));
   std::vector<hipEvent_t> ev_b(buckets.size());
   hipEvent_t ev_join;
   for (auto& e : ev_b) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   HIPCHK(hipEventCreateWithFlags(&ev_join, hipEventDisableTiming));
-  const float grad_scale = 1.0f / (float)(b * world);
+  // The loss is scaled by 1/b (this rank's batch) and the bucket all-reduce
+  // averages over ranks (ncclAvg), so the update uses the global-batch mean.
+  // (At one rank RCCL still runs its one-rank reduce kernel on stream C.)
+  const float grad_scale = 1.0f / (float)b;
   PhaseTimer timer(a.profile);
 
   auto step = [&](bool timed) {
@@ -156,14 +171,16 @@ int run_gpu_training(const CliArgs& a, Comm& comm, const char* program) {
     if (timed) timer.mark(1, S);
     for (size_t k = 0; k < buckets.size(); ++k) {
       net.backward(buckets[k].stage_hi, buckets[k].stage_lo, S);
-      if (world > 1) {
+      if (coll) {
+        // fork: the bucket's all-reduce runs on the comm stream C while S
+        // continues with the earlier stages' backward
         HIPCHK(hipEventRecord(ev_b[k], S));
         HIPCHK(hipStreamWaitEvent(C, ev_b[k], 0));
-        comm.allreduce_sum_f32(net.grads() + buckets[k].off, buckets[k].count, C);
+        comm.allreduce_avg_f32(net.grads() + buckets[k].off, buckets[k].count, C);
       }
     }
     if (timed) timer.mark(2, S);
-    if (world > 1) {
+    if (coll) {  // join before the update
       HIPCHK(hipEventRecord(ev_join, C));
       HIPCHK(hipStreamWaitEvent(S, ev_join, 0));
     }
@@ -174,15 +191,16 @@ int run_gpu_training(const CliArgs& a, Comm& comm, const char* program) {
   };
 
   const int64_t total = (int64_t)a.epochs * N;
-  const int64_t steps = (total + B_global - 1) / B_global;
+  const int64_t steps = (total + B_eff - 1) / B_eff;
   if (rank == 0) std::fprintf(stderr, "training...\n");
   net.zero_stats(S);
 
   // Capture one step into a hipGraph (skipped with --profile: timers need
-  // host-visible event records between phases).
+  // host-visible event records between phases).  With RCCL the captured
+  // graph holds the bucket fork/join and the ncclAllReduce nodes.
   hipGraphExec_t gexec = nullptr;
   hipGraph_t graph = nullptr;
-  bool use_graph = !a.profile && steps > 2;
+  bool use_graph = !a.profile && steps > 2 && !a.no_graph;
   if (a.momentum != 0.0) net.ensure_momentum();  // no allocation inside capture
   if (use_graph) {
     HIPCHK(hipStreamSynchronize(S));
@@ -206,45 +224,54 @@ int run_gpu_training(const CliArgs& a, Comm& comm, const char* program) {
     }
   }
 
+  // At most kInFlight steps are queued ahead of the host: before enqueueing
+  // step it, the host waits (bounded, watchdog) for step it - kInFlight.  A
+  // hung collective is then detected within the deadline instead of the
+  // host blocking forever inside a full launch queue.
+  constexpr int kInFlight = 4;
+  hipEvent_t ev_step[kInFlight];
+  for (auto& e : ev_step) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   HIPCHK(hipDeviceSynchronize());
   const auto t0 = std::chrono::steady_clock::now();
   int64_t seen = 0, last_log = 0;
   for (int64_t it = 0; it < steps; ++it) {
+    if (it >= kInFlight) comm.wait(ev_step[it % kInFlight]);
     if (use_graph) HIPCHK(hipGraphLaunch(gexec, S));
     else step(a.profile);
+    HIPCHK(hipEventRecord(ev_step[it % kInFlight], S));
     if (a.profile) timer.collect();
     const int64_t prev = seen;
-    seen += B_global;
+    seen += B_eff;
     // log at i = 0 and every log_every samples (cnn.c:470-473)
     const int64_t mark = (prev + a.log_every - 1) / a.log_every * a.log_every;
     if (!a.quiet && (mark < seen || it == steps - 1)) {
-      float st[4];
-      HIPCHK(hipMemcpyAsync(st, net.stats(), 16, hipMemcpyDeviceToHost, S));
-      HIPCHK(hipStreamSynchronize(S));
-      double loc[2] = {st[1], (double)(seen - last_log) / world};
-      if (world > 1) {
-        DevBuf tmp(16);
-        float v[2] = {st[1], (float)loc[1]};
-        HIPCHK(hipMemcpy(tmp.p, v, 8, hipMemcpyHostToDevice));
-        comm.allreduce_sum_f32(tmp.as<float>(), 2, S);
-        HIPCHK(hipMemcpy(v, tmp.p, 8, hipMemcpyDeviceToHost));
-        loc[0] = v[0]; loc[1] = v[1];
-      }
+      // [mse sum of this rank, samples of this rank]; summed over ranks
+      float* d = d_red.as<float>();
+      HIPCHK(hipMemcpyAsync(d, net.stats() + 1, 4, hipMemcpyDeviceToDevice, S));
+      h_red[1] = (float)((seen - last_log) / world);
+      HIPCHK(hipMemcpyAsync(d + 1, h_red + 1, 4, hipMemcpyHostToDevice, S));
+      comm.allreduce_sum_f32(d, 2, S);
+      HIPCHK(hipMemcpyAsync(h_red, d, 8, hipMemcpyDeviceToHost, S));
+      HIPCHK(hipEventRecord(ev_sync, S));
+      comm.wait(ev_sync);
       if (rank == 0 && mark < seen)
-        std::fprintf(stderr, "i=%lld, error=%.4f\n", (long long)mark, loc[0] / std::max(1.0, loc[1]));
+        std::fprintf(stderr, "i=%lld, error=%.4f\n", (long long)mark, h_red[0] / std::max(1.0f, h_red[1]));
       net.zero_stats(S);
       last_log = seen;
     }
   }
-  HIPCHK(hipDeviceSynchronize());
+  HIPCHK(hipEventRecord(ev_sync, S));
+  comm.wait(ev_sync);
   double train_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-  if (world > 1) {
-    DevBuf tmp(8);
-    HIPCHK(hipMemcpy(tmp.p, &train_s, 8, hipMemcpyHostToDevice));
-    comm.allreduce_max_f64(tmp.as<double>(), 1, S);
-    HIPCHK(hipStreamSynchronize(S));
-    HIPCHK(hipMemcpy(&train_s, tmp.p, 8, hipMemcpyDeviceToHost));
+  if (coll) {  // the slowest rank's time
+    double* d = d_red.as<double>();
+    HIPCHK(hipMemcpyAsync(d, &train_s, 8, hipMemcpyHostToDevice, S));
+    comm.allreduce_max_f64(d, 1, S);
+    HIPCHK(hipMemcpyAsync(&train_s, d, 8, hipMemcpyDeviceToHost, S));
+    HIPCHK(hipEventRecord(ev_sync, S));
+    comm.wait(ev_sync);
   }
+  for (auto& e : ev_step) (void)hipEventDestroy(e);
   if (gexec) (void)hipGraphExecDestroy(gexec);
   if (graph) (void)hipGraphDestroy(graph);
 
@@ -256,12 +283,8 @@ int run_gpu_training(const CliArgs& a, Comm& comm, const char* program) {
     try {
       te_img = load_idx(a.test_images, spec);
       te_lab = load_idx(a.test_labels, spec);
-    } catch (const Error& e) {
-      std::fprintf(stderr, "%s\n", e.what());
-      rc = 111;
-    }
-    if (rc == 0 && (te_img.item_size() != in_nodes || te_lab.count() < te_img.count())) rc = 111;
-    if (rc == 0) {
+      if (te_img.item_size() != in_nodes || te_lab.count() < te_img.count())
+        throw Error("test set shape does not match the model input");
       std::fprintf(stderr, "testing...\n");
       ntests = te_img.count();
       DevBuf t_img((size_t)ntests * in_nodes), t_lab((size_t)ntests);
@@ -277,31 +300,46 @@ int run_gpu_training(const CliArgs& a, Comm& comm, const char* program) {
         for (int64_t j = i; j < i + nb; ++j)
           if (j % 1000 == 0) std::fprintf(stderr, "i=%lld\n", (long long)j);
       }
-      float st[4];
-      HIPCHK(hipMemcpyAsync(st, net.stats(), 16, hipMemcpyDeviceToHost, S));
+      HIPCHK(hipMemcpyAsync(h_red, net.stats(), 16, hipMemcpyDeviceToHost, S));
       HIPCHK(hipStreamSynchronize(S));
       test_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t1).count();
-      ncorrect = (int64_t)std::llround(st[2]);
+      ncorrect = (int64_t)std::llround(h_red[2]);
       std::fprintf(stderr, "ntests=%lld, ncorrect=%lld\n", (long long)ntests, (long long)ncorrect);
       if (!a.save.empty()) {
         std::vector<float> p32(net.nparams());
         net.get_params(p32.data());
         std::vector<double> pd(p32.begin(), p32.end());
-        try { save_weights(a.save, spec, pd.data()); } catch (const Error& e) { std::fprintf(stderr, "%s\n", e.what()); rc = 111; }
+        save_weights(a.save, spec, pd.data());
       }
+    } catch (const Error& e) {
+      std::fprintf(stderr, "%s\n", e.what());
+      rc = 111;
     }
+  }
+  // every rank leaves with rank 0's verdict (a failed test phase must not
+  // leave the others in the final barrier; advisor finding, D9)
+  if (coll) {
+    double* d = d_red.as<double>();
+    double v = rc;
+    HIPCHK(hipMemcpyAsync(d, &v, 8, hipMemcpyHostToDevice, S));
+    comm.allreduce_max_f64(d, 1, S);
+    HIPCHK(hipMemcpyAsync(&v, d, 8, hipMemcpyDeviceToHost, S));
+    HIPCHK(hipEventRecord(ev_sync, S));
+    comm.wait(ev_sync);
+    rc = (int)v;
   }
   if (rank == 0 && !a.log_json.empty()) {
     FILE* f = a.log_json == "-" ? stdout : std::fopen(a.log_json.c_str(), "w");
     if (f) {
-      const double img_s = (double)steps * B_global / std::max(train_s, 1e-9);
+      const double img_s = (double)steps * B_eff / std::max(train_s, 1e-9);
       std::fprintf(f,
                    "{\"program\": \"%s\", \"model\": \"%s\", \"dtype\": \"%s\", \"world\": %d, \"global_batch\": %d, "
                    "\"steps\": %lld, \"train_s\": %.6f, \"train_img_per_s\": %.1f, \"hipgraph\": %s, "
+                   "\"comm\": \"%s\", \"buckets\": %d, "
                    "\"test_img_per_s\": %.1f, \"ntests\": %lld, \"ncorrect\": %lld",
-                   program, spec.name.c_str(), dtype_name(dt), world, B_global, (long long)steps, train_s, img_s,
-                   use_graph ? "true" : "false", ntests / std::max(test_s, 1e-9), (long long)ntests,
-                   (long long)ncorrect);
+                   program, spec.name.c_str(), dtype_name(dt), world, B_eff, (long long)steps, train_s, img_s,
+                   use_graph ? "true" : "false", comm.name(), (int)buckets.size(), ntests / std::max(test_s, 1e-9),
+                   (long long)ntests, (long long)ncorrect);
       if (timer.on && timer.n > 0)
         std::fprintf(f, ", \"phase_ms\": {\"forward_loss\": %.4f, \"backward_allreduce_issue\": %.4f, "
                         "\"allreduce_wait\": %.4f, \"sgd\": %.4f}",
@@ -313,6 +351,7 @@ int run_gpu_training(const CliArgs& a, Comm& comm, const char* program) {
   comm.barrier();
   for (auto& e : ev_b) (void)hipEventDestroy(e);
   (void)hipEventDestroy(ev_join);
+  (void)hipEventDestroy(ev_sync);
   (void)hipStreamDestroy(S);
   (void)hipStreamDestroy(C);
   return rc;

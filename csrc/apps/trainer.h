@@ -4,7 +4,7 @@
 // hybrid CUDAMPI.c + CUDAMPI.cu program (which never compiled).
 #pragma once
 
-#include <hip/hip_runtime_api.h>
+#include <hip/hip_runtime.h>
 
 #include <cstdint>
 
@@ -14,14 +14,26 @@
 namespace mcc {
 
 // Collective interface of the data-parallel driver.  Implementations:
-// LocalComm (world 1) and RcclComm (cnn_dist.cpp).  Every call is enqueued on
-// the given stream; nothing blocks the host except barrier().
+// LocalComm (no collectives: cnn_hip, or cnn_dist with MCC_LOCAL_COMM=1) and
+// RcclComm (cnn_dist.cpp, any world size including 1).  Every collective is
+// enqueued on the given stream; the host blocks only in wait() and barrier(),
+// which RcclComm bounds with the collective watchdog (watchdog.h).
 struct Comm {
   virtual ~Comm() = default;
   virtual int rank() const = 0;
   virtual int size() const = 0;
   virtual int local_rank() const { return rank(); }
+  virtual const char* name() const = 0;
+  // true when the collectives really execute (RCCL, even at world 1)
+  virtual bool collective() const = 0;
+  // Block until `ev` has completed (throws mcc::Error on a communicator
+  // error or when the watchdog deadline passes).
+  virtual void wait(hipEvent_t ev) {
+    if (hipEventSynchronize(ev) != hipSuccess) throw Error("hipEventSynchronize failed");
+  }
   virtual void allreduce_sum_f32(float* buf, int64_t n, hipStream_t s) = 0;
+  // mean over ranks (the gradient buckets: RCCL scales inside the collective)
+  virtual void allreduce_avg_f32(float* buf, int64_t n, hipStream_t s) = 0;
   virtual void allreduce_max_f64(double* buf, int64_t n, hipStream_t s) = 0;
   virtual void broadcast_f32(float* buf, int64_t n, int root, hipStream_t s) = 0;
   virtual void barrier() = 0;
@@ -31,7 +43,10 @@ struct Comm {
 struct LocalComm : Comm {
   int rank() const override { return 0; }
   int size() const override { return 1; }
+  const char* name() const override { return "local"; }
+  bool collective() const override { return false; }
   void allreduce_sum_f32(float*, int64_t, hipStream_t) override {}
+  void allreduce_avg_f32(float*, int64_t, hipStream_t) override {}
   void allreduce_max_f64(double*, int64_t, hipStream_t) override {}
   void broadcast_f32(float*, int64_t, int, hipStream_t) override {}
   void barrier() override {}

@@ -36,6 +36,14 @@ IdxFile idx_read(const std::string& path) {
   return f;
 }
 
+void check_labels(const IdxFile& labels, int64_t n, int num_classes, const std::string& what) {
+  n = std::min<int64_t>(n, (int64_t)labels.data.size());
+  for (int64_t i = 0; i < n; ++i)
+    if (labels.data[i] >= num_classes)
+      throw Error(what + ": label " + std::to_string((int)labels.data[i]) + " at index " + std::to_string(i) +
+                  " is not a class of the model (" + std::to_string(num_classes) + " classes)");
+}
+
 void idx_write(const std::string& path, const std::vector<uint32_t>& dims, const uint8_t* data) {
   std::unique_ptr<FILE, int (*)(FILE*)> fp(fopen(path.c_str(), "wb"), fclose);
   if (!fp) throw Error("cannot create IDX file '" + path + "'");
@@ -93,6 +101,7 @@ void synth_dataset(int64_t N, int C, int H, int W, int num_classes, uint64_t see
 // ------------------------------------------------------------ weights ----
 
 static const char kMagic[8] = {'M', 'C', 'N', 'N', 'W', 0, 0, 0};
+static const uint32_t kByteOrder = 0x01020304u;
 
 static int32_t ref_ltype(LayerKind k) {
   switch (k) {
@@ -110,7 +119,8 @@ void save_weights(const std::string& path, const ModelSpec& spec, const double* 
   auto w32 = [&](int32_t v) { os.write(reinterpret_cast<const char*>(&v), 4); };
   auto w64 = [&](int64_t v) { os.write(reinterpret_cast<const char*>(&v), 8); };
   os.write(kMagic, 8);
-  w32(1);
+  w32(2);
+  w32((int32_t)kByteOrder);
   w32((int32_t)spec.layers.size());
   w64(spec.nparams);
   for (const auto& L : spec.layers) {
@@ -135,20 +145,29 @@ ModelSpec load_weights(const std::string& path, std::vector<double>& params) {
   auto r32 = [&]() { int32_t v; is.read(reinterpret_cast<char*>(&v), 4); return v; };
   auto r64 = [&]() { int64_t v; is.read(reinterpret_cast<char*>(&v), 8); return v; };
   const int32_t version = r32();
-  if (version != 1) throw Error("unsupported MCNNW version");
+  if (version == 0x02000000 || version == 0x01000000) throw Error("big-endian MCNNW file: '" + path + "'");
+  if (version != 1 && version != 2) throw Error("unsupported MCNNW version");
+  if (version >= 2 && (uint32_t)r32() != kByteOrder) throw Error("bad MCNNW byte-order mark in '" + path + "'");
   const int32_t nl = r32();
   const int64_t np = r64();
   if (!is || nl < 2 || nl > 4096) throw Error("corrupt MCNNW header");
   ModelSpec spec;
   spec.name = "loaded";
+  std::vector<int64_t> stored_nb, stored_nw;
+  std::vector<int32_t> stored_shape;
   for (int i = 0; i < nl; ++i) {
     LayerSpec L;
     const int32_t t = r32();
     L.C = r32(); L.W = r32(); L.H = r32();
     L.ks = r32(); L.pad = r32(); L.stride = r32();
-    L.act = (Act)r32();
-    const int64_t nb = r64(), nw = r64();
-    (void)nb; (void)nw;
+    const int32_t act = r32();
+    if (act < (int32_t)Act::None || act > (int32_t)Act::Softmax) throw Error("corrupt MCNNW activation");
+    L.act = (Act)act;
+    stored_shape.insert(stored_shape.end(), {L.C, L.W, L.H});
+    stored_nb.push_back(r64());
+    stored_nw.push_back(r64());
+    if (L.C < 1 || L.W < 1 || L.H < 1 || L.C > (1 << 20) || L.W > (1 << 16) || L.H > (1 << 16))
+      throw Error("corrupt MCNNW layer shape");
     switch (t) {
       case 0: L.kind = LayerKind::Input; break;
       case 1: L.kind = LayerKind::FC; break;
@@ -161,12 +180,18 @@ ModelSpec load_weights(const std::string& path, std::vector<double>& params) {
   if (!is) throw Error("truncated MCNNW layer table");
   spec.finalize();
   if (spec.nparams != np) throw Error("MCNNW parameter count mismatch");
+  for (int i = 0; i < nl; ++i)
+    if (spec.layers[i].nbiases != stored_nb[i] || spec.layers[i].nweights != stored_nw[i] ||
+        spec.layers[i].C != stored_shape[3 * i] || spec.layers[i].W != stored_shape[3 * i + 1] ||
+        spec.layers[i].H != stored_shape[3 * i + 2])
+      throw Error("MCNNW layer " + std::to_string(i) + ": stored shape / parameter counts do not match its geometry");
   params.assign(np, 0.0);
   for (const auto& L : spec.layers) {
     if (L.nbiases) is.read(reinterpret_cast<char*>(params.data() + L.b_off), 8 * L.nbiases);
     if (L.nweights) is.read(reinterpret_cast<char*>(params.data() + L.w_off), 8 * L.nweights);
   }
   if (!is) throw Error("truncated MCNNW payload");
+  if (is.peek() != std::char_traits<char>::eof()) throw Error("trailing bytes after the MCNNW payload");
   return spec;
 }
 

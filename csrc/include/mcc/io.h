@@ -9,11 +9,15 @@
 // (Layer.weights/biases, cnn.c:26-30) and has no file format; this is the
 // framework's serialisation of exactly those arrays, in the reference's
 // layouts and precision (fp64), in layer order.  Little-endian:
-//   char[8] magic "MCNNW\0\0\0"; u32 version(=1); u32 nlayers; u64 nparams
+//   char[8] magic "MCNNW\0\0\0"; u32 version(=2); u32 byte-order mark
+//   0x01020304 (version 2; absent in version 1); u32 nlayers; u64 nparams
 //   per layer: i32 ltype (0 input, 1 full, 2 conv — cnn.c:8-12 — 3 maxpool),
 //              i32 depth, width, height, kernsize, padding, stride, act;
 //              i64 nbiases, nweights
 //   per layer: f64 biases[nbiases], f64 weights[nweights]
+// The loader re-derives every layer's shapes and parameter counts from the
+// stored geometry and rejects a file whose stored nbiases / nweights / act
+// disagree, a big-endian file, or a truncated / oversized payload.
 #pragma once
 
 #include <string>
@@ -35,6 +39,10 @@ struct IdxFile {
 };
 
 IdxFile idx_read(const std::string& path);  // throws mcc::Error
+// Labels are used as indices by the loss kernels (the reference only ever
+// compared j == label, cnn.c:462): reject any of the first n labels that is
+// not a valid class.  Throws mcc::Error naming the file and the offender.
+void check_labels(const IdxFile& labels, int64_t n, int num_classes, const std::string& what);
 void idx_write(const std::string& path, const std::vector<uint32_t>& dims, const uint8_t* data);
 
 // Synthetic, learnable, MNIST/CIFAR/ImageNet-shaped data: a noisy background

@@ -11,7 +11,10 @@ the wrong buffer (cnnmpi.c:487-498, defects D4/D5) with:
   stages' backward kernels are enqueued: RCCL runs it on its own HIP stream
   (ordered after the producing kernels by an event) while the compute stream
   continues with the earlier stages' backward — comm/compute overlap on xGMI;
-* the loss gradient is pre-scaled by 1/(global batch), so SUM == mean;
+* with RCCL ("nccl") the collective is AVG (ncclAvg: RCCL scales inside the
+  reduction) and the loss gradient is scaled by 1/(local batch); with gloo
+  (no AVG) the loss is pre-scaled by 1/(global batch) and the op is SUM —
+  either way the update uses the global-batch mean gradient;
 * initial weights are broadcast from rank 0 (fixes D6: ``srand(rank)``).
 
 Bucket size: xGMI is point-to-point (7 links x ~153 GB/s per MI355X); a ring
@@ -22,19 +25,66 @@ VGG-11's 532 MB splits into ~25 MB buckets that overlap with backward.
 
 from __future__ import annotations
 
+import datetime
+import os
+import socket
+
 import torch
 import torch.distributed as dist
 
 
+def comm_timeout() -> datetime.timedelta:
+    """Deadline of every collective (MCC_COMM_TIMEOUT seconds, default 300):
+    a rank that dies mid-step makes its peers' collectives fail after this
+    long instead of hanging forever (reference defect D9, cnnmpi.c:443-453)."""
+    try:
+        t = float(os.environ.get("MCC_COMM_TIMEOUT", "300"))
+    except ValueError:
+        t = 300.0
+    return datetime.timedelta(seconds=t if t > 0 else 300.0)
+
+
+def init_process_group(backend: str, device: torch.device | None = None):
+    """torch.distributed init with the framework's defaults: env:// rendezvous
+    on 127.0.0.1 (a free port when launched without a launcher, world 1), the
+    collective deadline of comm_timeout(), and for "nccl" (= RCCL) the device
+    bound eagerly so the communicator is created now, not at the first
+    collective.  World 1 is a real process group too: the single-GPU run
+    executes the same RCCL broadcast and bucketed all-reduce as an 8-GPU one."""
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("RANK", "0")
+    os.environ.setdefault("WORLD_SIZE", "1")
+    if "MASTER_PORT" not in os.environ:
+        with socket.socket() as s:
+            s.bind(("127.0.0.1", 0))
+            os.environ["MASTER_PORT"] = str(s.getsockname()[1])
+    kw = {"timeout": comm_timeout()}
+    if backend == "nccl" and device is not None:
+        kw["device_id"] = device
+    dist.init_process_group(backend, **kw)
+
+
 class BucketedAllReduce:
+    """Issues one SUM all-reduce per bucket whenever a process group exists
+    (any world size, 1 included: with the "nccl" backend that is a real RCCL
+    collective on RCCL's stream)."""
+
     def __init__(self, net, grads: torch.Tensor, group=None, bucket_bytes: int = 4 << 20):
         self.net = net
         self.grads = grads
         self.group = group
-        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.active = dist.is_initialized()
+        self.world = dist.get_world_size(group) if self.active else 1
+        self.avg = self.active and dist.get_backend(group) == "nccl"
+        self.op = dist.ReduceOp.AVG if self.avg else dist.ReduceOp.SUM
         self.buckets = [tuple(b) for b in net.buckets(int(bucket_bytes))]
+        self.issued = 0  # collectives issued so far (introspection / tests)
         covered = sum(b[3] for b in self.buckets)
         assert covered == grads.numel(), "buckets must cover the whole gradient buffer"
+
+    def loss_scale(self, local_batch: int) -> float:
+        """Gradient scale for the loss of `local_batch` samples on this rank."""
+        return 1.0 / (local_batch if self.avg else local_batch * self.world)
 
     def backward(self, stream_handle: int):
         """Run the engine backward bucket by bucket, launching each bucket's
@@ -44,14 +94,15 @@ class BucketedAllReduce:
         works = []
         for hi, lo, off, cnt in self.buckets:
             self.net.backward(hi, lo, stream_handle)
-            if self.world > 1:
+            if self.active:
                 works.append(
-                    dist.all_reduce(self.grads[off : off + cnt], op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+                    dist.all_reduce(self.grads[off : off + cnt], op=self.op, group=self.group, async_op=True)
                 )
+        self.issued += len(works)
         for w in works:
             w.wait()
 
 
 def broadcast_params(params: torch.Tensor, src: int = 0, group=None):
-    if dist.is_initialized() and dist.get_world_size(group) > 1:
+    if dist.is_initialized():
         dist.broadcast(params, src=src, group=group)

@@ -36,8 +36,9 @@ def _parse(argv):
     ap.add_argument("--dtype", default="bf16")
     ap.add_argument("--device", default="auto", choices=["auto", "gpu", "cpu"])
     ap.add_argument("--bucket-mb", type=float, default=4.0)
-    ap.add_argument("--dist-backend", default="auto", choices=["auto", "nccl", "gloo"],
-                    help="torch.distributed backend for world > 1 (auto: nccl = RCCL on GPUs, gloo on CPU)")
+    ap.add_argument("--dist-backend", default="auto", choices=["auto", "nccl", "gloo", "none"],
+                    help="torch.distributed backend (auto: nccl = RCCL on GPUs at any world size, "
+                         "gloo on CPU when world > 1; none: no process group, world 1 only)")
     ap.add_argument("--log-every", type=int, default=1000)
     ap.add_argument("--save", default="")
     ap.add_argument("--load", default="")
@@ -53,7 +54,12 @@ def _load_idx(path, spec):
     from . import _C
 
     if not path.startswith("synthetic:"):
-        return _C.idx_read(path)
+        arr = _C.idx_read(path)
+        if arr.ndim == 1 and arr.size and int(arr.max()) >= spec.num_classes():
+            # labels index the loss kernels (the reference only compared j == label, cnn.c:462)
+            raise RuntimeError(f"{path}: label {int(arr.max())} is not a class of the model "
+                               f"({spec.num_classes()} classes)")
+        return arr
     _, n, seed, kind = path.split(":")
     C, H, W = spec.input_shape()
     imgs, labels = _C.synth_dataset(int(n), C, H, W, spec.num_classes(), seed=int(seed))
@@ -85,14 +91,38 @@ def main(argv=None) -> int:
     if use_gpu:
         # more ranks than GPUs (rehearsal on a small box, gloo only): share devices
         local_rank %= max(1, torch.cuda.device_count())
-    if world > 1:
-        backend = a.dist_backend if a.dist_backend != "auto" else ("nccl" if use_gpu else "gloo")
-        if use_gpu:
-            torch.cuda.set_device(local_rank)
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-        else:
-            dist.init_process_group("gloo")
+    backend = a.dist_backend
+    if backend == "auto":
+        backend = "nccl" if use_gpu else ("gloo" if world > 1 else "none")
+    if backend == "none" and world > 1:
+        backend = "nccl" if use_gpu else "gloo"
+    if use_gpu:
+        torch.cuda.set_device(local_rank)
+    if backend != "none":
+        from .parallel.ddp import init_process_group
+
+        init_process_group(backend, torch.device("cuda", local_rank) if use_gpu else None)
+    try:
+        return _train(a, world, rank, local_rank, use_gpu)
+    except (RuntimeError, dist.DistBackendError) as e:  # a failed collective (peer gone, deadline passed)
+        print(f"rank {rank}: {e}", file=sys.stderr, flush=True)
+        return 111
+
+
+def _fault(rank, it):
+    """Fault injection for the failure-detection tests: MCC_FAULT_RANK=r
+    MCC_FAULT_STEP=k makes rank r die abruptly before step k."""
+    if os.environ.get("MCC_FAULT_RANK") == str(rank) and os.environ.get("MCC_FAULT_STEP") == str(it):
+        print(f"rank {rank}: injected fault at step {it}", file=sys.stderr, flush=True)
+        os._exit(17)
+
+
+def _train(a, world, rank, local_rank, use_gpu) -> int:
+    import torch
+    import torch.distributed as dist
+
+    from . import _C
+
     try:
         if a.load:
             spec, params = _C.load_weights(a.load)
@@ -112,8 +142,8 @@ def main(argv=None) -> int:
     lo, hi = N // world * rank, N // world * (rank + 1)
     if world > 1:
         print(f"{rank} {lo} {hi}", file=sys.stderr, flush=True)
-    B = a.batch
-    b = max(1, B // world)
+    b = max(1, a.batch // world)
+    B = b * world  # effective global batch (SGD mean, sample count, img/s)
     total = a.epochs * N
     steps = (total + B - 1) // B
     rng = np.random.default_rng(a.seed * 7919 + rank)
@@ -133,16 +163,18 @@ def main(argv=None) -> int:
         gen.manual_seed(a.seed * 7919 + rank)
         tr.zero_stats()
         for it in range(steps):
+            _fault(rank, it)
             idx = torch.randint(lo, hi, (b,), device=dev, dtype=torch.int32, generator=gen)
             tr.step(d_img, d_lab, idx, b)
             prev, seen = seen, seen + B
             mark = (prev + a.log_every - 1) // a.log_every * a.log_every
             if mark < seen:
                 st = tr.net.get_stats()
-                mse = torch.tensor([st["mse_sum"], float(seen - ecount)], dtype=torch.float64, device=dev)
-                if world > 1:
+                # [this rank's MSE sum, this rank's samples], summed over ranks
+                mse = torch.tensor([st["mse_sum"], float((seen - ecount) // world)], dtype=torch.float64, device=dev)
+                if dist.is_initialized():
                     dist.all_reduce(mse)
-                _log(rank, f"i={mark}, error={mse[0].item() / max(1.0, mse[1].item() / world * world):.4f}")
+                _log(rank, f"i={mark}, error={mse[0].item() / max(1.0, mse[1].item()):.4f}")
                 ecount = seen
                 tr.zero_stats()
         torch.cuda.synchronize()
@@ -158,6 +190,7 @@ def main(argv=None) -> int:
 
         dp = CpuDataParallel(spec, params, dtype="fp64", bucket_bytes=int(a.bucket_mb * (1 << 20)), lr=a.lr)
         for it in range(steps):
+            _fault(rank, it)
             sel = rng.integers(lo, hi, size=b)
             x = tr_img[sel].transpose(0, 3, 1, 2).reshape(b, -1) / 255.0
             st = dp.step(x, tr_lab[sel].astype(np.int32), b * world)
@@ -210,8 +243,11 @@ def main(argv=None) -> int:
                     else:
                         with open(a.json, "w") as f:
                             json.dump(out, f)
-    if world > 1:
-        dist.barrier()
+    if dist.is_initialized():
+        # every rank leaves with rank 0's verdict (no rank waits on a failed peer)
+        v = torch.tensor([rc], dtype=torch.int64, device=torch.device("cuda", local_rank) if use_gpu else None)
+        dist.all_reduce(v, op=dist.ReduceOp.MAX)
+        rc = int(v.item())
         dist.destroy_process_group()
     return rc
 

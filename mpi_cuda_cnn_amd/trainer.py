@@ -52,7 +52,7 @@ class GpuTrainer:
         self.stats = _alias(self.net.stats_ptr, 4, "float32", self.device)
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
-        if self.world > 1:
+        if dist.is_initialized():  # identical replicas (fixes D6: srand(rank), no broadcast)
             broadcast_params(self.params, 0, group)
             self.net.pack(self.stream)
         self.sync = BucketedAllReduce(self.net, self.grads, group, bucket_bytes)
@@ -67,7 +67,7 @@ class GpuTrainer:
         s = self.stream
         idx_ptr = 0 if idx is None else idx.data_ptr()
         self.net.forward(images.data_ptr(), idx_ptr, B, s)
-        self.net.loss(labels.data_ptr(), idx_ptr, 1.0 / (B * self.world), True, s)
+        self.net.loss(labels.data_ptr(), idx_ptr, self.sync.loss_scale(B), True, s)
         self.sync.backward(s)
         self.net.sgd(self.lr, self.momentum, self.weight_decay, s)
 

@@ -119,3 +119,22 @@ def test_host_sanitizers_clean(tmp_path):
                            env=env, timeout=600)
         assert r.returncode == 0, r.stderr[-3000:]
         assert "ERROR: AddressSanitizer" not in r.stderr and "runtime error" not in r.stderr
+
+
+def test_out_of_range_label_rejected(cnn_bin, data, tmp_path):
+    """Labels index the loss (the reference only compared j == label,
+    cnn.c:462): a label outside the model's classes is a load error (111)
+    in the native CLI and in the Python trainer, not an out-of-bounds read."""
+    import sys
+
+    lab = mcc.idx_read(data[1]).copy()
+    lab[7] = 10
+    badl = str(tmp_path / "bad-labels")
+    mcc.idx_write(badl, lab)
+    r = subprocess.run([cnn_bin, data[0], badl, data[2], data[3], "--epochs", "1"], capture_output=True, text=True)
+    assert r.returncode == 111 and "label 10" in r.stderr, r.stderr
+    r = subprocess.run([cnn_bin, data[0], data[1], data[2], badl, "--epochs", "1"], capture_output=True, text=True)
+    assert r.returncode == 111
+    r = subprocess.run([sys.executable, "-m", "mpi_cuda_cnn_amd.train", data[0], badl, data[2], data[3],
+                        "--epochs", "1", "--device", "cpu"], capture_output=True, text=True, cwd=ROOT)
+    assert r.returncode == 111 and "label 10" in r.stderr, r.stderr

@@ -198,3 +198,56 @@ def test_weight_file_roundtrip(tmp_path):
         assert raw[:5] == b"MCNNW"
     with pytest.raises(RuntimeError):
         mcc.load_weights(str(tmp_path / "nope"))
+
+
+def test_weight_file_validation(tmp_path):
+    """The loader re-derives every layer's shape and parameter counts and
+    rejects disagreeing stored counts, a bad activation, a big-endian file
+    and trailing bytes; version-1 files (no byte-order mark) still load."""
+    import struct
+
+    spec = mcc.make_model("lenet5")
+    p = mcc.init_params(spec, seed=2)
+    path = tmp_path / "w.mcnnw"
+    mcc.save_weights(str(path), spec, p)
+    raw = bytearray(path.read_bytes())
+    assert struct.unpack_from("<II", raw, 8) == (2, 0x01020304)
+    nl = struct.unpack_from("<I", raw, 16)[0]
+    hdr, rec = 28, 48  # magic+version+bom+nlayers+nparams; per layer 8 x i32 + 2 x i64
+
+    def bad(mut):
+        b = bytearray(raw)
+        mut(b)
+        q = tmp_path / "bad.mcnnw"
+        q.write_bytes(bytes(b))
+        with pytest.raises(RuntimeError):
+            mcc.load_weights(str(q))
+
+    bad(lambda b: struct.pack_into("<q", b, hdr + rec * 1 + 40, 7))      # conv1 stored nweights
+    bad(lambda b: struct.pack_into("<q", b, hdr + rec * 1 + 32, 5))      # conv1 stored nbiases
+    bad(lambda b: struct.pack_into("<i", b, hdr + rec * 1 + 28, 9))      # activation out of range
+    bad(lambda b: struct.pack_into("<i", b, hdr + rec * 2 + 8, 13))      # pool stored width
+    bad(lambda b: struct.pack_into(">II", b, 8, 2, 0x01020304))          # big-endian header
+    bad(lambda b: struct.pack_into("<I", b, 12, 0x04030201))             # byte-order mark
+    bad(lambda b: b.extend(b"\0" * 8))                                    # trailing bytes
+    bad(lambda b: b.__delitem__(slice(len(b) - 8, len(b))))               # truncated payload
+    # version 1 (round-1 files): no byte-order mark
+    v1 = bytearray(raw[:8]) + struct.pack("<I", 1) + raw[16:]
+    q = tmp_path / "v1.mcnnw"
+    q.write_bytes(bytes(v1))
+    spec1, p1 = mcc.load_weights(str(q))
+    assert nl == len(spec.layers()) and spec1.nparams == spec.nparams
+    np.testing.assert_array_equal(p1, p)
+
+
+def test_watchdog_policy():
+    """Collective watchdog of cnn_dist (csrc/apps/watchdog.h): completion,
+    async-error and deadline branches, as a native CPU test binary."""
+    import subprocess
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    binp = os.path.join(root, "build", "bin", "test_watchdog")
+    if not os.path.exists(binp):
+        subprocess.run(["make", "-C", root, "build/bin/test_watchdog"], check=True, capture_output=True)
+    r = subprocess.run([binp], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0 and "watchdog ok" in r.stdout, r.stderr

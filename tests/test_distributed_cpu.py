@@ -126,3 +126,36 @@ def test_cnnmpi_trains_and_replicas_agree(tmp_path):
     assert int(last.split("=")[-1]) >= 95
     spec, p = mcc.load_weights(w)
     assert np.isfinite(p).all()
+
+
+def test_rank_death_mid_training_fails_every_rank(tmp_path):
+    """Failure detection (reference defect D9, cnnmpi.c:443-453): rank 1 dies
+    abruptly mid-training; with NO launcher to kill the survivor, rank 0 must
+    leave its collective and exit non-zero (111) within the deadline."""
+    import time
+
+    d = str(tmp_path)
+    for n, s, p in ((512, 1, "train"), (64, 2, "test")):
+        i, l = mcc.synth_dataset(n, 1, 28, 28, 10, seed=s)
+        mcc.idx_write(os.path.join(d, p + "-images"), i.reshape(n, 28, 28))
+        mcc.idx_write(os.path.join(d, p + "-labels"), l)
+    args = [os.path.join(d, x) for x in ("train-images", "train-labels", "test-images", "test-labels")]
+    port = str(_free_port())
+    procs = []
+    t0 = time.time()
+    for r in range(2):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE="2", LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=port, MCC_COMM_TIMEOUT="30", MCC_FAULT_RANK="1", MCC_FAULT_STEP="3")
+        procs.append(subprocess.Popen([sys.executable, "-m", "mpi_cuda_cnn_amd.train"] + args +
+                                      ["--model", "lenet5", "--epochs", "4", "--batch", "16", "--device", "cpu"],
+                                      cwd=ROOT, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
+    try:
+        outs = [p.communicate(timeout=120) for p in procs]
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    elapsed = time.time() - t0
+    assert procs[1].returncode == 17, outs[1][1]
+    assert procs[0].returncode == 111, outs[0][1]
+    assert elapsed < 100

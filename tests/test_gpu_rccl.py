@@ -1,0 +1,112 @@
+"""RCCL on the hardware path at one rank (the box has one MI355X; RCCL refuses
+two ranks on one device).  A world-1 RCCL communicator executes the same
+broadcast, bucketed all-reduce on a separate stream and (native) graph-captured
+collectives as the 8-GPU runs; at one rank the sum is the identity, so the
+trained weights must be BIT-equal to the collective-free path.
+
+  * Python: GpuTrainer under a world-1 "nccl" process group (bench.py's N=1
+    path) vs no process group.
+  * Native: cnn_dist with its RcclComm (hipGraph replay, eager, --profile)
+    vs MCC_LOCAL_COMM=1.
+"""
+
+import json
+import os
+import subprocess
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+import mpi_cuda_cnn_amd as mcc
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+STEPS, B, LR, MOM, BUCKET = 4, 256, 0.05, 0.9, 16 << 10
+
+
+def _train(model, dtype):
+    from mpi_cuda_cnn_amd.trainer import GpuTrainer
+
+    dev = torch.device("cuda", 0)
+    spec = mcc.make_model(model)
+    C, H, W = spec.input_shape()
+    imgs, labels = mcc.synth_dataset(STEPS * B, C, H, W, spec.num_classes(), seed=9)
+    d_img, d_lab = torch.from_numpy(imgs).to(dev), torch.from_numpy(labels).to(dev)
+    tr = GpuTrainer(spec, dtype=dtype, batch=B, device=0, lr=LR, momentum=MOM,
+                    params=mcc.init_params(spec, seed=3, mode="fast"), bucket_bytes=BUCKET)
+    for s in range(STEPS):
+        idx = torch.arange(s * B, (s + 1) * B, device=dev, dtype=torch.int32)
+        tr.step(d_img, d_lab, idx)
+    torch.cuda.synchronize()
+    return tr.state_dict(), len(tr.sync.buckets), tr.sync.issued
+
+
+def _rccl_worker(rank, model, dtype, out):
+    import torch.distributed as dist
+
+    from mpi_cuda_cnn_amd.parallel.ddp import init_process_group
+
+    os.environ.pop("MASTER_PORT", None)
+    os.environ.update(RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
+    torch.cuda.set_device(0)
+    init_process_group("nccl", torch.device("cuda", 0))
+    assert dist.get_backend() == "nccl" and dist.get_world_size() == 1
+    p, nb, issued = _train(model, dtype)
+    np.save(os.path.join(out, "p.npy"), p)
+    np.save(os.path.join(out, "n.npy"), np.array([nb, issued]))
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("model,dtype", [("lenet5", "bf16"), ("cifar3", "bf16"), ("ref", "fp32")])
+def test_python_rccl_world1_bit_equal(cuda, model, dtype, tmp_path):
+    mp.spawn(_rccl_worker, args=(model, dtype, str(tmp_path)), nprocs=1, join=True)
+    p_rccl = np.load(tmp_path / "p.npy")
+    nb, issued = np.load(tmp_path / "n.npy")
+    assert nb > 1, "expected several buckets"
+    assert issued == STEPS * nb, "one RCCL all-reduce per bucket per step"
+    import torch.distributed as dist
+
+    assert not dist.is_initialized()
+    p_local, nb2, issued2 = _train(model, dtype)
+    assert issued2 == 0 and nb2 == nb
+    np.testing.assert_array_equal(p_rccl, p_local)
+
+
+@pytest.fixture(scope="module")
+def idx_files(tmp_path_factory):
+    d = str(tmp_path_factory.mktemp("rcclidx"))
+    for n, s, p in ((4096, 1, "train"), (512, 2, "test")):
+        i, l = mcc.synth_dataset(n, 1, 28, 28, 10, seed=s)
+        mcc.idx_write(os.path.join(d, p + "-images"), i.reshape(n, 28, 28))
+        mcc.idx_write(os.path.join(d, p + "-labels"), l)
+    return [os.path.join(d, x) for x in ("train-images", "train-labels", "test-images", "test-labels")]
+
+
+def _cnn_dist(idx_files, w, extra, env_extra=None):
+    env = dict(os.environ, RANK="0", WORLD_SIZE="1", LOCAL_RANK="0", MCC_COMM_TIMEOUT="120")
+    env.pop("MCC_LOCAL_COMM", None)
+    env.update(env_extra or {})
+    r = subprocess.run([os.path.join(ROOT, "build/bin/cnn_dist")] + idx_files +
+                       ["--model", "lenet5", "--batch", "512", "--epochs", "1", "--lr", "0.05", "--momentum", "0.9",
+                        "--bucket-mb", "0.01", "--json", "-", "--save", w] + extra,
+                       capture_output=True, text=True, timeout=240, env=env)
+    assert r.returncode == 0, r.stderr
+    return json.loads(r.stdout.strip().splitlines()[-1]), mcc.load_weights(w)[1]
+
+
+@pytest.mark.gpu
+def test_cnn_dist_rccl_world1_bit_equal(idx_files, tmp_path):
+    js_g, p_g = _cnn_dist(idx_files, str(tmp_path / "g.w"), [])
+    assert js_g["comm"] == "rccl" and js_g["hipgraph"] is True and js_g["buckets"] > 1
+    js_e, p_e = _cnn_dist(idx_files, str(tmp_path / "e.w"), ["--no-graph"])
+    assert js_e["comm"] == "rccl" and js_e["hipgraph"] is False
+    js_p, p_p = _cnn_dist(idx_files, str(tmp_path / "p.w"), ["--profile"])
+    assert js_p["comm"] == "rccl" and "phase_ms" in js_p
+    js_l, p_l = _cnn_dist(idx_files, str(tmp_path / "l.w"), [], {"MCC_LOCAL_COMM": "1"})
+    assert js_l["comm"] == "local" and js_l["hipgraph"] is True
+    np.testing.assert_array_equal(p_g, p_l)  # RCCL world-1 == no collectives
+    np.testing.assert_array_equal(p_g, p_e)  # graph replay == eager
+    np.testing.assert_array_equal(p_g, p_p)  # --profile (event-timed phases) == graph
+    assert js_g["ncorrect"] >= 0.9 * js_g["ntests"]
