@@ -124,7 +124,9 @@ int run_gpu_training(const CliArgs& a, Comm& comm, const char* program) {
   const int B_eff = b * world;
   if (rank == 0 && B_eff != a.batch)
     std::fprintf(stderr, "note: --batch %d is not a multiple of %d ranks; global batch %d\n", a.batch, world, B_eff);
-  const int eval_b = std::max(b, 1024);
+  // evaluation batch: >= 1024 small images per forward; large images (VGG
+  // @224: ~50 MB of activations per image) evaluate at the training batch
+  const int eval_b = spec.input().H * spec.input().W > 64 * 64 ? b : std::max(b, 1024);
   GpuNet net(spec, dt, eval_b);
   {
     std::vector<float> p32(p64.begin(), p64.end());
@@ -140,9 +142,17 @@ int run_gpu_training(const CliArgs& a, Comm& comm, const char* program) {
   std::unique_ptr<float, hipError_t (*)(void*)> h_red_guard(h_red, hipHostFree);
   HIPCHK(hipMemset(d_step.p, 0, 8));
 
+  // Comm stream C from the high-priority pool: HIP spreads streams over
+  // GPU_MAX_HW_QUEUES hardware queues per priority, so a normal-priority C
+  // can share S's queue and serialise every all-reduce behind backward.
+  int prio_lo = 0, prio_hi = 0;
+  HIPCHK(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
   hipStream_t S, C;
-  HIPCHK(hipStreamCreateWithFlags(&S, hipStreamNonBlocking));
-  HIPCHK(hipStreamCreateWithFlags(&C, hipStreamNonBlocking));
+  auto make_streams = [&] {
+    HIPCHK(hipStreamCreateWithFlags(&S, hipStreamNonBlocking));
+    HIPCHK(hipStreamCreateWithPriority(&C, hipStreamNonBlocking, prio_hi));
+  };
+  make_streams();
   const bool coll = comm.collective();
   // identical weights on every rank (fixes D6: srand(rank), no broadcast)
   comm.broadcast_f32(net.params(), net.nparams(), 0, S);
@@ -214,8 +224,7 @@ int run_gpu_training(const CliArgs& a, Comm& comm, const char* program) {
         // a failed capture can leave the stream unusable: start from fresh streams
         (void)hipStreamDestroy(S);
         (void)hipStreamDestroy(C);
-        HIPCHK(hipStreamCreateWithFlags(&S, hipStreamNonBlocking));
-        HIPCHK(hipStreamCreateWithFlags(&C, hipStreamNonBlocking));
+        make_streams();
         if (rank == 0) std::fprintf(stderr, "note: hipGraph capture unavailable, running eagerly\n");
       }
     } else {

@@ -59,8 +59,17 @@ def init_process_group(backend: str, device: torch.device | None = None):
             s.bind(("127.0.0.1", 0))
             os.environ["MASTER_PORT"] = str(s.getsockname()[1])
     kw = {"timeout": comm_timeout()}
-    if backend == "nccl" and device is not None:
-        kw["device_id"] = device
+    if backend == "nccl":
+        if device is not None:
+            kw["device_id"] = device
+        # RCCL's stream from the high-priority pool: HIP maps streams onto
+        # GPU_MAX_HW_QUEUES (4) hardware queues per priority, and a
+        # normal-priority pool stream can land on the compute stream's queue,
+        # which serialises every all-reduce behind the backward kernels
+        # (measured: tools/probes/queue_probe.py, profiles/rccl_world1_r2.txt).
+        opts = dist.ProcessGroupNCCL.Options()
+        opts.is_high_priority_stream = True
+        kw["pg_options"] = opts
     dist.init_process_group(backend, **kw)
 
 

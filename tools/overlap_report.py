@@ -2,10 +2,13 @@
 """Comm/compute overlap from a rocprofv3 kernel trace (run_kernel_trace.csv).
 
 For every collective kernel (RCCL: name contains nccl / rccl / OneRank) it
-prints its queue/stream, its duration, and which kernels on OTHER queues ran
-concurrently with it (intersection of [start, end) intervals) — the evidence
-that a bucket's all-reduce runs on the comm stream while the compute stream
-continues with the earlier stages' backward.  Usage:
+prints its HIP stream and hardware queue, its duration, and which kernels on
+OTHER hardware queues ran concurrently with it (intersection of [start, end)
+intervals) — the evidence that a bucket's all-reduce runs on the comm stream
+while the compute stream continues with the earlier stages' backward.  (A
+replayed hipGraph reports one stream id for all its nodes; the executor runs
+independent branches on different hardware queues, so concurrency is judged
+by Queue_Id.)  Usage:
     overlap_report.py <trace dir> [max steps to print]
 """
 import csv
@@ -33,8 +36,8 @@ def main(d, max_show=6):
     rows = list(csv.DictReader(open(paths[0])))
     ks = []
     for r in rows:
-        q = r.get("Stream_Id") or r.get("Queue_Id") or "?"
-        ks.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), q, r.get("Queue_Id", "?"), r["Kernel_Name"]))
+        ks.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r.get("Queue_Id", "?"), r.get("Stream_Id", "?"),
+                   r["Kernel_Name"]))
     ks.sort()
     coll = [k for k in ks if is_coll(k[4])]
     print(f"trace: {paths[0]}")
@@ -42,10 +45,11 @@ def main(d, max_show=6):
     if not coll:
         return
     qs = sorted({k[2] for k in coll})
-    print(f"collective streams: {qs}; compute streams: {sorted({k[2] for k in ks if not is_coll(k[4])} )}")
+    print(f"collective hw queues: {qs}; compute hw queues: {sorted({k[2] for k in ks if not is_coll(k[4])})}")
     tot_c = sum(e - s for s, e, *_ in coll)
     ov_tot = 0
-    for i, (s, e, q, hq, n) in enumerate(coll):
+    shown = 0
+    for i, (s, e, q, hs, n) in enumerate(coll):
         over = [(max(s, s2), min(e, e2), n2, q2) for s2, e2, q2, hq2, n2 in ks if q2 != q and s2 < e and e2 > s]
         ov = 0
         # union of overlapping intervals
@@ -61,12 +65,13 @@ def main(d, max_show=6):
         if cur:
             ov += cur[1] - cur[0]
         ov_tot += ov
-        if i < max_show:
+        if shown < max_show and (ov > 0 or i + max_show >= len(coll)):
+            shown += 1
             names = sorted({short(n2) for *_, n2, q2 in over})
-            print(f"  [{i}] {short(n)} stream {q} (hw queue {hq}): {(e - s) / 1e3:.1f} us, "
+            print(f"  [{i}] {short(n)} hw queue {q} (stream {hs}): {(e - s) / 1e3:.1f} us, "
                   f"{100.0 * ov / max(1, e - s):.0f}% overlapped by: {', '.join(names) or '-'}")
     print(f"collective time {tot_c / 1e3:.1f} us total, {100.0 * ov_tot / max(1, tot_c):.1f}% of it concurrent "
-          f"with compute kernels on other streams")
+          f"with compute kernels on other hardware queues")
 
 
 if __name__ == "__main__":
