@@ -72,6 +72,9 @@ struct GpuNet::Stage {
   bool pipe_fwd = false, pipe_dx = false, pipe_dw = false;
   gpu::ConvPipeParams pf, pdx;
   gpu::ConvDwPipeParams pdw;
+  // single-channel first layer: row-chunked weight gradient (conv_rows.hip)
+  bool rows_dw = false;
+  gpu::ConvDwRowsParams prw;
 };
 
 static inline int r8(int x) { return (x + 7) & ~7; }
@@ -166,7 +169,15 @@ void GpuNet::plan_pipe(Stage& st, bool first) {
     st.pipe_dx = gpu::conv_pipe_plan(p) && p.layout == gpu::XL_C8 && st.CLd == ((st.C + 7) & ~7) &&
                  st.nchunks_d == p.nchunks;
   }
-  if (x_ok) {
+  if (first && st.inC == 1) {
+    gpu::ConvDwRowsParams& p = st.prw;
+    p.N = max_batch_; p.SH = st.inH; p.SW = st.inW; p.OH = st.OH; p.OW = st.OW; p.KS = st.KS; p.pad = st.pad;
+    p.Cout = st.C;
+    p.dmode = st.pooled ? gpu::PM_UNPOOL : gpu::PM_RELU;
+    p.DH = dyH; p.DW = dyW;
+    st.rows_dw = st.stride == 1 && (st.pooled || st.act == gpu::ACT_RELU) && gpu::conv_dw_rows_plan(p);
+  }
+  if (x_ok && !st.rows_dw) {
     gpu::ConvDwPipeParams& p = st.pdw;
     p.N = max_batch_; p.Cin = st.inC; p.OH = st.OH; p.OW = st.OW; p.cs = st.stride; p.KS = st.KS; p.Cout = st.C;
     p.x.mode = x_mode; p.x.SH = st.inH; p.x.SW = st.inW; p.x.SC = st.inC;
@@ -379,6 +390,67 @@ void GpuNet::build() {
   }
   packed_count_ = (int64_t)idx.size();
 
+  // ---- analytic maps of the same packed layouts (fused SGD + pack) ----
+  // Each weight stage's copies as (base, strides, flip) of its canonical
+  // (n, c, kh, kw) index; verified below against the table, entry by entry.
+  pack_.nstages = 0;
+  bool maps_ok = (int)stages_.size() <= gpu::kMaxPackStages;
+  if (const char* a = std::getenv("MCC_NO_FUSED_PACK")) maps_ok = maps_ok && std::atoi(a) == 0;  // A/B: table path
+  for (Stage* sp : stages_) {
+    if (!maps_ok) break;
+    const Stage& st = *sp;
+    gpu::PackStage& ps = pack_.st[pack_.nstages++];
+    ps.w_off = st.w_off; ps.nw = st.nw; ps.nmaps = 0;
+    auto add = [&](int64_t base, int sn, int sc, int skh, int skw, int flip) {
+      gpu::PackMap& m = ps.map[ps.nmaps++];
+      m.base = base; m.sn = sn; m.sc = sc; m.skh = skh; m.skw = skw; m.flip = flip;
+    };
+    if (st.kind == Stage::FC) {
+      ps.inC = st.Kin; ps.KS = 1;
+      add(st.pk_fwd, r8(st.Kin), 1, 0, 0, 0);
+      if (st.pk_dx >= 0) add(st.pk_dx, 1, st.out_ld, 0, 0, 0);
+    } else {
+      ps.inC = st.inC; ps.KS = st.KS;
+      const int KS = st.KS;
+      if (st.big) {
+        add(st.pk_fwd, st.kgem, 1, KS * st.inC, st.inC, 0);
+        if (st.pk_dx >= 0) add(st.pk_dx, 1, st.kgem_d, KS * st.C, st.C, 1);
+      } else if (st.pipe_fwd && st.pf.layout == gpu::XL_S1) {
+        add(st.pk_fwd, st.pf.kpad, 0, 8, 1, 0);
+        if (st.pf.pair) add(st.pk_fwd + 8 * (int64_t)st.pf.kpad + 1, st.pf.kpad, 0, 8, 1, 0);
+      } else {
+        const int CLx = st.cvec ? st.CL : st.inC;
+        add(st.pk_fwd, st.kpad, 1, KS * CLx, CLx, 0);
+        if (st.pk_dx >= 0) {
+          const int CLd = st.cvec_d ? st.CLd : st.C;
+          add(st.pk_dx, 1, st.kpad_d, KS * CLd, CLd, 1);
+        }
+      }
+    }
+  }
+  if (maps_ok) {
+    int64_t covered = 0;
+    for (int si = 0; si < pack_.nstages && maps_ok; ++si) {
+      const gpu::PackStage& ps = pack_.st[si];
+      const int KK = ps.KS * ps.KS;
+      for (int64_t j = 0; j < ps.nw && maps_ok; ++j) {
+        const int64_t n = j / ((int64_t)ps.inC * KK), r = j % ((int64_t)ps.inC * KK);
+        const int c = (int)(r / KK), kh = (int)(r % KK) / ps.KS, kw = (int)(r % KK) % ps.KS;
+        for (int m = 0; m < ps.nmaps; ++m) {
+          const gpu::PackMap& mp = ps.map[m];
+          const int h = mp.flip ? ps.KS - 1 - kh : kh, x = mp.flip ? ps.KS - 1 - kw : kw;
+          const int64_t pos = mp.base + n * mp.sn + (int64_t)c * mp.sc + (int64_t)h * mp.skh + (int64_t)x * mp.skw;
+          if (pos < 0 || pos >= packed_count_ || idx[pos] != ps.w_off + j) { maps_ok = false; break; }
+          ++covered;
+        }
+      }
+    }
+    int64_t used = 0;
+    for (int32_t v : idx) used += v >= 0;
+    maps_ok = maps_ok && covered == used;
+  }
+  fused_pack_ = maps_ok;
+
   // ---- arena: sizing pass then real pass ----
   const int Bm = max_batch_;
   size_t scratch = 0;
@@ -404,6 +476,7 @@ void GpuNet::build() {
       }
     } else if (st.kind == Stage::CONV) {
       scratch = std::max(scratch, (size_t)st.nx_dw * st.cout_pad * st.ncols_pad * 4);
+      if (st.rows_dw) scratch = std::max(scratch, gpu::conv_dw_rows_scratch_bytes(st.prw));
       if (st.pipe_dw) {
         const size_t nv = (size_t)st.pdw.cout_pad * st.pdw.ncols_pad;
         scratch = std::max(scratch, (st.pdw.grid + ceil_div(st.pdw.grid, 16)) * nv * 4);
@@ -431,7 +504,7 @@ void GpuNet::build() {
     logits_ld_ = r8(spec_.num_classes());
     logits_ = static_cast<float*>(arena_alloc(4 * (size_t)Bm * logits_ld_));
     packed_ = arena_alloc(es * (size_t)packed_count_);
-    pack_idx_ = static_cast<int32_t*>(arena_alloc(4 * (size_t)packed_count_));
+    pack_idx_ = fused_pack_ ? nullptr : static_cast<int32_t*>(arena_alloc(4 * (size_t)packed_count_));
     scratch_ = static_cast<float*>(arena_alloc(scratch_bytes_));
     col_ = col_bytes_ ? arena_alloc(col_bytes_) : nullptr;
     for (Stage* sp : stages_) {
@@ -452,13 +525,18 @@ void GpuNet::build() {
       HIP_OK(hipMemset(arena_, 0, arena_bytes_));
     }
   }
-  HIP_OK(hipMemcpy(pack_idx_, idx.data(), 4 * idx.size(), hipMemcpyHostToDevice));
+  if (!fused_pack_) HIP_OK(hipMemcpy(pack_idx_, idx.data(), 4 * idx.size(), hipMemcpyHostToDevice));
+  pack_.packed = packed_;
+  pack_.params = params_;
+  pack_.grads = grads_;
+  pack_.n = spec_.nparams;
 }
 
 std::string GpuNet::plan() const {
   std::ostringstream os;
   os << "GpuNet(" << spec_.name << ", " << dtype_name(dtype_) << ", max_batch=" << max_batch_
-     << ", arena=" << (arena_bytes_ >> 20) << " MiB)\n";
+     << ", arena=" << (arena_bytes_ >> 20) << " MiB, " << (fused_pack_ ? "fused sgd+pack" : "sgd + pack table")
+     << ")\n";
   for (size_t s = 0; s < stages_.size(); ++s) {
     const Stage& st = *stages_[s];
     if (st.kind == Stage::CONV) {
@@ -467,11 +545,12 @@ std::string GpuNet::plan() const {
          << (st.big ? (st.ig_fwd ? " igemm" : " im2col+gemm") : (st.cvec ? " lds-cvec" : " lds-scalar")) << " chunks=" << st.nchunks
          << " imgs=" << st.imgs_fwd << "/"
          << st.imgs_dx << "/" << st.imgs_dw;
-      if (st.pipe_fwd || st.pipe_dx || st.pipe_dw) {
+      if (st.pipe_fwd || st.pipe_dx || st.pipe_dw || st.rows_dw) {
         os << " pipe[";
         if (st.pipe_fwd) os << "fwd:" << (st.pf.layout == gpu::XL_S1 ? (st.pf.pair ? "s1p" : "s1") : "c8") << "x" << st.pf.imgs << "/g" << st.pf.grid << " ";
         if (st.pipe_dx) os << "dx:x" << st.pdx.imgs << "/g" << st.pdx.grid << " ";
         if (st.pipe_dw) os << "dw:x" << st.pdw.imgs << "/g" << st.pdw.grid;
+        if (st.rows_dw) os << "dw:rows x" << st.prw.imgs << "/g" << st.prw.grid;
         os << "]";
       }
       os << "\n";
@@ -539,7 +618,13 @@ void GpuNet::get_grads(float* host) const {
 }
 
 void GpuNet::pack(hipStream_t s) {
-  gpu::pack_gather(dtype_, packed_, params_, pack_idx_, packed_count_, s);
+  if (fused_pack_) {
+    gpu::SgdPackParams p = pack_;
+    p.update = false;
+    gpu::sgd_pack(dtype_, p, s);
+  } else {
+    gpu::pack_gather(dtype_, packed_, params_, pack_idx_, packed_count_, s);
+  }
 }
 
 void GpuNet::zero_stats(hipStream_t s) { HIP_OK(hipMemsetAsync(stats_, 0, 16, s)); }
@@ -800,7 +885,14 @@ void GpuNet::backward(int hi, int lo, hipStream_t s) {
         continue;
       }
       fork();
-      if (st.pipe_dw) {
+      if (st.rows_dw) {
+        gpu::ConvDwRowsParams w = st.prw;
+        w.N = B; w.ablate = ablate_;
+        w.x = images_; w.idx = idx_;
+        w.dy = st.grad_buf; w.aux_y = st.act_buf; w.aux_arg = st.arg_buf;
+        w.slab = scratch_;
+        gpu::conv_dw_rows(w, grads_ + st.w_off, grads_ + st.b_off, ws);
+      } else if (st.pipe_dw) {
         gpu::ConvDwPipeParams w = st.pdw;
         w.N = B; w.ablate = ablate_;
         if (si == 0) { w.x.src = images_; w.x.idx = idx_; }
@@ -818,9 +910,10 @@ void GpuNet::backward(int hi, int lo, hipStream_t s) {
         p.out = stages_[si - 1]->grad_buf;
         gpu::conv_pipe_forward(p, s);
       }
-      if (st.pipe_dw && (st.pipe_dx || si == 0)) continue;
+      const bool dw_done = st.pipe_dw || st.rows_dw;
+      if (dw_done && (st.pipe_dx || si == 0)) continue;
       // weight gradient
-      if (!st.pipe_dw) {
+      if (!dw_done) {
       gpu::ConvDwParams w;
       w.N = B; w.imgs = st.imgs_dw;
       w.nx = (int)std::min<int64_t>(ceil_div(B, st.imgs_dw), st.nx_dw);
@@ -932,6 +1025,14 @@ void GpuNet::ensure_momentum() {
 
 void GpuNet::sgd(float lr, float momentum, float weight_decay, hipStream_t s) {
   if (momentum != 0.f) ensure_momentum();
+  if (fused_pack_) {  // update + packed-copy refresh in one pass
+    gpu::SgdPackParams p = pack_;
+    p.update = true;
+    p.mom = momentum != 0.f ? mom_ : nullptr;
+    p.lr = lr; p.mu = momentum; p.wd = weight_decay;
+    gpu::sgd_pack(dtype_, p, s);
+    return;
+  }
   gpu::sgd_update(params_, grads_, momentum != 0.f ? mom_ : nullptr, spec_.nparams, lr, momentum, weight_decay, s);
   pack(s);
 }

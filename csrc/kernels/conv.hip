@@ -497,7 +497,8 @@ __global__ void __launch_bounds__(256) conv_fwd_kernel(ConvParams p) {
         }
         const size_t o = (obase + (rb >> 2)) * p.Cout + n;
         out[o] = from_f<T>(best);
-        p.out_arg[o] = (uint8_t)arg;
+        // ReLU-inactive window (pooled output <= 0): argmax byte 4, the backward routes nothing
+        p.out_arg[o] = (uint8_t)(ACT == ACT_RELU && !(to_f(from_f<T>(best)) > 0.f) ? 4 : arg);
       } else {
         if (rb + 4 <= M) {
 #pragma unroll

@@ -39,7 +39,7 @@ template <int MODE> struct ModeInfo;
 template <> struct ModeInfo<PM_U8S1> { static constexpr int W = 2, NI = 4; };
 template <> struct ModeInfo<PM_PLAIN> { static constexpr int W = 4, NI = 8; };
 template <> struct ModeInfo<PM_RELU> { static constexpr int W = 8, NI = 4; };
-template <> struct ModeInfo<PM_UNPOOL> { static constexpr int W = 10, NI = 4; };
+template <> struct ModeInfo<PM_UNPOOL> { static constexpr int W = 6, NI = 4; };  // 4 dY + 2 argmax words
 
 constexpr int mode_ni(int mode) { return mode == PM_PLAIN ? 8 : 4; }
 
@@ -153,8 +153,10 @@ struct Loader {
       } else {
         const size_t g = (size_t)n * img_src + soff[i];
         ld_chan(static_cast<const bf16*>(s.src) + g, s.RW, r[i]);
-        if constexpr (MODE == PM_RELU || MODE == PM_UNPOOL) ld_chan(static_cast<const bf16*>(s.aux_y) + g, s.RW, r[i] + 4);
-        if constexpr (MODE == PM_UNPOOL) ld_arg(s.aux_arg + g, s.RW, r[i] + 8);
+        if constexpr (MODE == PM_RELU) ld_chan(static_cast<const bf16*>(s.aux_y) + g, s.RW, r[i] + 4);
+        // PM_UNPOOL: the argmax byte is 4 for ReLU-inactive windows, so it
+        // carries the ReLU mask too and the layer output is not read
+        if constexpr (MODE == PM_UNPOOL) ld_arg(s.aux_arg + g, s.RW, r[i] + 4);
       }
     }
   }
@@ -186,16 +188,14 @@ struct Loader {
         for (int k = 0; k < 4; ++k) v[k] = relu_mask(r[i][k], r[i][4 + k]);
         st16(lds + dst[i], v);
       } else {  // PM_UNPOOL: dense write of the four window positions
-        uint32_t d[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) d[k] = relu_mask(r[i][k], r[i][4 + k]);
+        const uint32_t* d = r[i];
         const int dxo = s.up * s.CL, dyo = s.up * s.LWp * s.CL;
 #pragma unroll
         for (int pos = 0; pos < 4; ++pos) {
           uint32_t v[4];
 #pragma unroll
           for (int k = 0; k < 4; ++k) {
-            const uint32_t a = r[i][8 + (k >> 1)] >> (16 * (k & 1));  // bytes of channels 2k, 2k+1
+            const uint32_t a = r[i][4 + (k >> 1)] >> (16 * (k & 1));  // bytes of channels 2k, 2k+1
             const uint32_t lo = ((a & 0xffu) == (uint32_t)pos) ? 0x0000ffffu : 0u;
             const uint32_t hi = (((a >> 8) & 0xffu) == (uint32_t)pos) ? 0xffff0000u : 0u;
             v[k] = d[k] & (lo | hi);

@@ -231,7 +231,7 @@ __global__ void __launch_bounds__(256) dw_slab_final_kernel(const float* part, i
     const int rem = j - row * Cin * KK;
     const int ci = rem / KK, kp = rem - ci * KK;
     const int kh = kp / KS, kw = kp - kh * KS;
-    col = layout == XL_S1 ? kh * 8 + kw : kp * CL + ci;
+    col = layout == XL_S1 ? kh * 8 + kw : (layout == XL_ROWS ? kp : kp * CL + ci);
   } else {
     row = j - nW;
     col = kbias;
@@ -337,20 +337,28 @@ void conv_dw_pipe(const ConvDwPipeParams& pin, hipStream_t st) {
 #undef MCC_DW_TILES
 }
 
+void dw_slab_reduce(const float* slab, int nx, int cout_pad, int ncols_pad, float* part, int Cout, int Cin, int KS,
+                    int layout, int CL, int kbias, float* gw, float* gb, hipStream_t st) {
+  if (nx <= 0) return;
+  const int nv = cout_pad * ncols_pad;
+  const int xs_per = 64;
+  const int nxc = cdiv(nx, xs_per);
+  hipLaunchKernelGGL(dw_slab_sum_kernel, dim3((unsigned)cdiv(nv, 64), (unsigned)nxc), dim3(256), 0, st, slab, nx, nv,
+                     xs_per, part);
+  const int nout = Cout * Cin * KS * KS + Cout;
+  hipLaunchKernelGGL(dw_slab_final_kernel, dim3((unsigned)cdiv(nout, 256)), dim3(256), 0, st, part, nxc, nv, ncols_pad,
+                     kbias, Cout, Cin, KS, layout, CL, gw, gb);
+}
+
 void conv_dw_pipe_reduce(const ConvDwPipeParams& pin, float* gw, float* gb, hipStream_t st) {
   ConvDwPipeParams p = pin;
   const int ngroups = cdiv(p.N, p.imgs);
   const int nx = std::min(ngroups, std::min(pin.grid, kCUs * wgs_per_cu(p.lds, dw_wgs_cap())));
   if (nx <= 0) return;
   const int nv = p.cout_pad * p.ncols_pad;
-  const int xs_per = 64;
-  const int nxc = cdiv(nx, xs_per);
   float* part = p.slab + (size_t)pin.grid * nv;  // after the slabs (scratch sized by the planner's grid)
-  hipLaunchKernelGGL(dw_slab_sum_kernel, dim3((unsigned)cdiv(nv, 64), (unsigned)nxc), dim3(256), 0, st, p.slab, nx,
-                     nv, xs_per, part);
-  const int nout = p.Cout * p.Cin * p.KS * p.KS + p.Cout;
-  hipLaunchKernelGGL(dw_slab_final_kernel, dim3((unsigned)cdiv(nout, 256)), dim3(256), 0, st, part, nxc, nv,
-                     p.ncols_pad, p.kbias, p.Cout, p.Cin, p.KS, p.layout, p.x.CL, gw, gb);
+  dw_slab_reduce(p.slab, nx, p.cout_pad, p.ncols_pad, part, p.Cout, p.Cin, p.KS, p.layout, p.x.CL, p.kbias, gw, gb,
+                 st);
 }
 
 }  // namespace gpu

@@ -230,7 +230,8 @@ __global__ void __launch_bounds__(NT) conv_pipe_fwd_kernel(ConvPipeParams p) {
               const int o = win * p.Cout + c;
               MCC_DCHECK(o < p.imgs * out_img);
               outs[o] = (bf16)y;
-              args[o] = (uint8_t)arg;
+              // ReLU-inactive window: argmax byte 4 (the backward routes nothing, no y read)
+              args[o] = (uint8_t)(ACT == ACT_RELU && !((float)(bf16)y > 0.f) ? 4 : arg);
             }
           } else if (c < p.Cout) {
 #pragma unroll
@@ -262,8 +263,9 @@ __global__ void __launch_bounds__(NT) conv_pipe_fwd_kernel(ConvPipeParams p) {
           }
           const int o = (rb >> 2) * p.Cout + n;
           MCC_DCHECK(o < p.imgs * out_img);
-          outs[o] = (bf16)fmaxf(best + bv, 0.f);
-          args[o] = (uint8_t)arg;
+          const bf16 yb = (bf16)fmaxf(best + bv, 0.f);
+          outs[o] = yb;
+          args[o] = (uint8_t)((float)yb > 0.f ? arg : 4);  // 4: ReLU-inactive window
         } else {
 #pragma unroll
           for (int i = 0; i < 4; ++i) {

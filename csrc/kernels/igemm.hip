@@ -309,6 +309,11 @@ __global__ void __launch_bounds__(kIgT, 2) igemm_conv_kernel(IgemmParams p) {
       }
       const bf16x4 o = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
       const int orow = POOL ? (m >> 2) : m;
+      if (POOL && BIAS_ACT && p.act == ACT_RELU) {  // ReLU-inactive window: argmax byte 4
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (!((float)o[e] > 0.f)) arg = (arg & ~(0xffu << (8 * e))) | (4u << (8 * e));
+      }
       *reinterpret_cast<bf16x4*>(out + (size_t)orow * p.ldo + ch) = o;
       if (POOL) *reinterpret_cast<uint32_t*>(p.out_arg + (size_t)orow * p.N + ch) = arg;
     }

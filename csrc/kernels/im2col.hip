@@ -119,7 +119,7 @@ __global__ void __launch_bounds__(256) maxpool2_kernel(const T* __restrict__ in,
     for (int i = 1; i < 4; ++i)
       if (v[i] > best) { best = v[i]; a = i; }
     out[e] = from_f<T>(best);
-    arg[e] = (uint8_t)a;
+    arg[e] = (uint8_t)(to_f(from_f<T>(best)) > 0.f ? a : 4);  // input is post-ReLU: 4 = inactive window
   }
 }
 
@@ -157,6 +157,7 @@ __global__ void __launch_bounds__(256) maxpool2_vec_kernel(const bf16* __restric
       if ((float)v2[j] > best) { best = (float)v2[j]; a = 2; }
       if ((float)v3[j] > best) { best = (float)v3[j]; a = 3; }
       o[j] = (bf16)best;
+      if (!(best > 0.f)) a = 4;  // post-ReLU input: inactive window
       if (j < 4) a0 |= a << (8 * j); else a1 |= a << (8 * (j - 4));
     }
     store8(out + (size_t)r * C + c8 * 8, o);

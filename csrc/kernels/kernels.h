@@ -36,7 +36,7 @@ struct StageSrc {
   const void* src = nullptr;     // T* or uint8_t*
   const int32_t* idx = nullptr;  // IN_U8: optional per-image index
   const void* aux_y = nullptr;   // IN_RELU/IN_UNPOOL: layer output (T)
-  const uint8_t* aux_arg = nullptr;  // IN_UNPOOL: argmax (pos in 2x2 window)
+  const uint8_t* aux_arg = nullptr;  // IN_UNPOOL: argmax (pos in 2x2 window; 4 = ReLU-inactive window)
   int SH = 0, SW = 0, SC = 0;    // conv-grid dims of the source (pre-pool for UNPOOL)
   int PH = 0, PW = 0;            // IN_UNPOOL: pooled dims of src/aux tensors
   int off = 0, up = 1;
@@ -66,7 +66,9 @@ struct ConvParams {
   const void* wpk = nullptr;    // packed weights [round_up(Cout,16)][kpad], T
   const float* bias = nullptr;  // fp32 canonical bias [Cout]
   void* out = nullptr;          // T NHWC [N][OH'][OW'][Cout]
-  uint8_t* out_arg = nullptr;   // pool argmax [N][PH][PW][Cout]
+  uint8_t* out_arg = nullptr;   // pool argmax [N][PH][PW][Cout]: position 0..3 in the 2x2 window
+                                // (first max wins), or 4 where the pooled ReLU output is <= 0 —
+                                // the max-pool + ReLU backward then needs only dY and this byte
 };
 
 // Weight gradient of a conv_small layer: slab[x][co][col] partial sums over
@@ -117,7 +119,7 @@ enum PipeMode : int {
   PM_U8S1 = 0,    // u8 single-channel images -> four shifted bf16 copies (see below)
   PM_PLAIN = 1,   // bf16 NHWC
   PM_RELU = 2,    // bf16 NHWC masked by (aux_y > 0)
-  PM_UNPOOL = 3,  // pooled bf16 NHWC routed to the argmax of its 2x2 window, masked by (aux_y > 0)
+  PM_UNPOOL = 3,  // pooled bf16 NHWC routed to the argmax of its 2x2 window (argmax 4: ReLU-inactive, nothing routed)
 };
 enum PipeLayout : int {
   // Cin == 1: copy c (c = 0..3) holds tile[j + c] at j, so any 4 consecutive
@@ -125,6 +127,7 @@ enum PipeLayout : int {
   // (kernel row, 8 taps), two 8-byte reads per 8-wide K fragment.
   XL_S1 = 0,
   XL_C8 = 1,  // NHWC, channels padded to a multiple of 8: one 16-byte read per fragment
+  XL_ROWS = 2,  // conv_dw_rows: Cin == 1, tap-packed columns kh*KS + kw
 };
 
 struct PipeSrc {
@@ -193,6 +196,37 @@ bool conv_dw_pipe_plan(ConvDwPipeParams& p);
 void conv_dw_pipe(const ConvDwPipeParams& p, hipStream_t s);
 // Reduce the slabs of conv_dw_pipe into the canonical fp32 gradient.
 void conv_dw_pipe_reduce(const ConvDwPipeParams& p, float* gw, float* gb, hipStream_t s);
+// Deterministic two-level reduce of per-workgroup dW slabs [nx][cout_pad][ncols_pad]
+// (chunk partials in `part`, ceil(nx/64) * cout_pad * ncols_pad floats) into
+// gw[Cout][Cin][KS][KS] / gb[Cout]; `layout` names the slab column order.
+void dw_slab_reduce(const float* slab, int nx, int cout_pad, int ncols_pad, float* part, int Cout, int Cin, int KS,
+                    int layout, int CL, int kbias, float* gw, float* gb, hipStream_t s);
+
+// Row-chunked weight gradient of a single-channel (u8) stride-1 first layer
+// (conv_rows.hip): M = output channels, N = tap-packed kernel positions + a
+// ones column (bias), K = one 32-pixel output row; dZ staged channel-planar
+// with the max-pool / ReLU backward applied while staging, the input as four
+// shifted bf16 copies.  Persistent over image groups; fp32 slab per
+// workgroup, then dw_slab_reduce.
+struct ConvDwRowsParams {
+  int N = 0, SH = 0, SW = 0, OH = 0, OW = 0, KS = 1, pad = 0, Cout = 0;
+  const uint8_t* x = nullptr;        // u8 images [*][SH][SW]
+  const int32_t* idx = nullptr;      // optional per-image dataset index
+  int dmode = PM_UNPOOL;             // PM_UNPOOL (2x2/2 pool + ReLU) or PM_RELU
+  const void* dy = nullptr;          // bf16 NHWC [N][DH][DW][Cout]
+  const void* aux_y = nullptr;       // bf16 NHWC layer output (ReLU mask)
+  const uint8_t* aux_arg = nullptr;  // PM_UNPOOL argmax bytes
+  int DH = 0, DW = 0;                // dY grid (pooled for PM_UNPOOL)
+  float* slab = nullptr;             // scratch (conv_dw_rows_scratch_bytes)
+  // planner outputs
+  int A = 0, Pw = 0, LH = 0, CS = 0, ximg = 0, dplane = 0, dzimg = 0, KK = 0, ntiles = 0;
+  int m0 = 0, nblk = 0, imgs = 1, ngroups = 0, grid = 0;
+  size_t lds = 0;
+  int ablate = 0;  // diagnostics (MCC_ABLATE): 1 no staging, 2 no MFMA loop
+};
+bool conv_dw_rows_plan(ConvDwRowsParams& p);
+size_t conv_dw_rows_scratch_bytes(const ConvDwRowsParams& p);
+void conv_dw_rows(const ConvDwRowsParams& p, float* gw, float* gb, hipStream_t s);
 
 enum GemmEpi : int {
   EPI_BIAS_ACT = 0,  // C = act(acc + bias[n])  (T)
@@ -367,6 +401,38 @@ void sgd_update(float* params, const float* grads, float* mom, int64_t n, float 
                 hipStream_t s);
 // dst[i] = idx[i] >= 0 ? T(src[idx[i]]) : 0
 void pack_gather(DType t, void* dst, const float* src, const int32_t* idx, int64_t n, hipStream_t s);
+
+// Fused SGD (+momentum, weight decay) and packed-copy refresh in ONE pass over
+// the flat parameter buffer (reference Layer_update, cnn.c:303-314, followed
+// by the re-cast of every compute copy).  A weight stage's parameter j, in
+// canonical order (n, c, kh, kw) = OIHW or (n, k) for FC (KS = 1), lands in
+// each of its packed copies at
+//   base + n*sn + c*sc + kh'*skh + kw'*skw,   kh' = flip ? KS-1-kh : kh (same for kw)
+// so the copies are written straight from the updated value: no index table,
+// no second pass re-reading the parameters.
+struct PackMap {
+  int64_t base = 0;
+  int sn = 0, sc = 0, skh = 0, skw = 0, flip = 0;
+};
+struct PackStage {
+  int64_t w_off = 0, nw = 0;
+  int inC = 1, KS = 1, nmaps = 0;
+  uint64_t m_ckk = 0, m_kk = 0, m_ks = 0;  // division magic (set by sgd_pack)
+  PackMap map[3];
+};
+constexpr int kMaxPackStages = 14;
+struct SgdPackParams {
+  float* params = nullptr;
+  const float* grads = nullptr;
+  float* mom = nullptr;
+  int64_t n = 0;
+  float lr = 0.f, mu = 0.f, wd = 0.f;
+  bool update = true;  // false: refresh the packed copies only
+  void* packed = nullptr;
+  int nstages = 0;     // stages sorted by w_off
+  PackStage st[kMaxPackStages];
+};
+void sgd_pack(DType t, const SgdPackParams& p, hipStream_t s);
 void fill_f32(float* dst, float v, int64_t n, hipStream_t s);
 // Sampling with replacement (the reference draws rand() % N per sample,
 // cnn.c:455): idx[b] = lo + hash(seed, *step, b) % (hi - lo).  `step` lives in

@@ -350,6 +350,46 @@ __global__ void pack_kernel(T* __restrict__ dst, const float* __restrict__ src, 
   }
 }
 
+// q = n / d for n, d < 2^32 via m = ceil(2^64 / d) (d >= 2; d == 1: m = 0 = identity)
+__device__ __forceinline__ uint32_t fdiv(uint32_t n, uint64_t m) {
+  return m ? (uint32_t)__umul64hi((uint64_t)n, m) : n;
+}
+
+template <typename T, bool UPDATE>
+__global__ void __launch_bounds__(256) sgd_pack_kernel(SgdPackParams p) {
+  T* __restrict__ dst = static_cast<T*>(p.packed);
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  int s = 0;  // monotone per thread: i only grows
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < p.n; i += stride) {
+    float w = p.params[i];
+    if (UPDATE) {
+      float gi = p.grads[i];
+      if (p.wd != 0.f) gi += p.wd * w;
+      if (p.mom) {
+        const float v = p.mu * p.mom[i] + gi;
+        p.mom[i] = v;
+        gi = v;
+      }
+      w = w - p.lr * gi;
+      p.params[i] = w;
+    }
+    while (s < p.nstages && i >= p.st[s].w_off + p.st[s].nw) ++s;
+    if (s >= p.nstages || i < p.st[s].w_off) continue;  // a bias (no packed copy)
+    const PackStage& st = p.st[s];
+    const uint32_t j = (uint32_t)(i - st.w_off);
+    const uint32_t ckk = (uint32_t)(st.inC * st.KS * st.KS), kk = (uint32_t)(st.KS * st.KS);
+    const uint32_t n = fdiv(j, st.m_ckk), r = j - n * ckk;
+    const uint32_t c = fdiv(r, st.m_kk), r2 = r - c * kk;
+    const uint32_t kh = fdiv(r2, st.m_ks), kw = r2 - kh * (uint32_t)st.KS;
+    const T v = from_f<T>(w);
+    for (int m = 0; m < st.nmaps; ++m) {
+      const PackMap& mp = st.map[m];
+      const int h = mp.flip ? st.KS - 1 - (int)kh : (int)kh, x = mp.flip ? st.KS - 1 - (int)kw : (int)kw;
+      dst[mp.base + (int64_t)n * mp.sn + (int64_t)c * mp.sc + (int64_t)h * mp.skh + (int64_t)x * mp.skw] = v;
+    }
+  }
+}
+
 __global__ void fill_kernel(float* dst, float v, int64_t n) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) dst[i] = v;
@@ -446,6 +486,33 @@ void pack_gather(DType t, void* dst, const float* src, const int32_t* idx, int64
   else
     hipLaunchKernelGGL(pack_kernel<float>, dim3(grid_for(n)), dim3(256), 0, s, static_cast<float*>(dst), src, idx,
                        n);
+}
+
+static uint64_t div_magic(uint64_t d) {
+  if (d <= 1) return 0;
+  // ceil(2^64 / d) = floor((2^64 - 1) / d) + 1 for d not a power of two; exact either way below
+  const uint64_t q = ~0ull / d;
+  return q + 1;
+}
+
+void sgd_pack(DType t, const SgdPackParams& pin, hipStream_t s) {
+  if (pin.n <= 0) return;
+  MCC_CHECK(pin.nstages <= kMaxPackStages, "sgd_pack: too many weight stages");
+  SgdPackParams p = pin;
+  for (int i = 0; i < p.nstages; ++i) {
+    PackStage& st = p.st[i];
+    st.m_ckk = div_magic((uint64_t)st.inC * st.KS * st.KS);
+    st.m_kk = div_magic((uint64_t)st.KS * st.KS);
+    st.m_ks = div_magic((uint64_t)st.KS);
+  }
+  const dim3 grid(grid_for(p.n)), block(256);
+  if (t == DType::BF16) {
+    if (p.update) hipLaunchKernelGGL((sgd_pack_kernel<bf16, true>), grid, block, 0, s, p);
+    else hipLaunchKernelGGL((sgd_pack_kernel<bf16, false>), grid, block, 0, s, p);
+  } else {
+    if (p.update) hipLaunchKernelGGL((sgd_pack_kernel<float, true>), grid, block, 0, s, p);
+    else hipLaunchKernelGGL((sgd_pack_kernel<float, false>), grid, block, 0, s, p);
+  }
 }
 
 void sample_indices(int32_t* idx, int B, int64_t lo, int64_t hi, uint64_t seed, const uint64_t* step,

@@ -101,6 +101,45 @@ def test_sgd_and_pack_roundtrip(cuda):
     np.testing.assert_allclose(p.cpu().numpy(), params - 0.1 * g.cpu().numpy(), rtol=1e-6, atol=1e-6)
 
 
+def _sgd_steps(cuda, spec, dtype, B, steps=2):
+    C, H, W = spec.input_shape()
+    imgs, labels = mcc.synth_dataset(B, C, H, W, spec.num_classes(), seed=13)
+    net = mcc.GpuNet(spec, dtype, B)
+    net.set_params(mcc.init_params(spec, seed=6, mode="fast").astype(np.float32))
+    d_img = torch.from_numpy(imgs).to(cuda)
+    d_lab = torch.from_numpy(labels).to(cuda)
+    s = torch.cuda.current_stream().cuda_stream
+    for _ in range(steps):
+        net.forward(d_img.data_ptr(), 0, B, s)
+        net.loss(d_lab.data_ptr(), 0, 1.0 / B, True, s)
+        net.backward_all(s)
+        net.sgd(0.05, 0.9, 1e-3, s)
+    net.forward(d_img.data_ptr(), 0, B, s)  # reads the refreshed packed copies
+    torch.cuda.synchronize()
+    return net.plan(), net.get_params(), net.get_logits(B)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("model,dtype", [("lenet5", "bf16"), ("lenet5", "fp32"), ("ref", "bf16"), ("cifar3", "bf16"),
+                                         ("big", "bf16"), ("big", "fp32")])
+def test_fused_sgd_pack_matches_table(cuda, model, dtype, monkeypatch):
+    """One-pass SGD + packed-copy refresh (analytic per-stage maps, no index
+    table) vs the gather-table path (MCC_NO_FUSED_PACK=1): bit-identical
+    parameters after SGD with momentum + weight decay, and bit-identical
+    logits from the refreshed bf16/fp32 compute copies (every packed layout:
+    S1 pair, C8, flipped data-gradient copies, im2col, FC and FC^T)."""
+    spec = (mcc.parse_model_spec("input 3 72 72; conv 16 k3 s1 p1 relu; pool 2; conv 24 k3 s2 p1 relu; "
+                                 "fc 32 relu; fc 10 softmax", "big") if model == "big" else mcc.make_model(model))
+    B = 8 if model == "big" else 64
+    plan, p_fused, l_fused = _sgd_steps(cuda, spec, dtype, B)
+    assert "fused sgd+pack" in plan, plan
+    monkeypatch.setenv("MCC_NO_FUSED_PACK", "1")
+    plan2, p_tab, l_tab = _sgd_steps(cuda, spec, dtype, B)
+    assert "pack table" in plan2
+    np.testing.assert_array_equal(p_fused, p_tab)
+    np.testing.assert_array_equal(l_fused, l_tab)
+
+
 @pytest.mark.gpu
 def test_training_reduces_loss(cuda):
     spec = mcc.make_model("lenet5")
@@ -273,3 +312,46 @@ def test_max_batch_guard(cuda):
     spec = mcc.make_model("lenet5")
     with pytest.raises(Exception, match="32-bit activation indexing"):
         mcc.GpuNet(spec, "bf16", 1 << 20)
+
+
+def _lenet_grads(cuda, B, seed=7):
+    spec = mcc.make_model("lenet5")
+    imgs, labels = mcc.synth_dataset(B, 1, 28, 28, 10, seed=seed)
+    params = mcc.init_params(spec, seed=seed).astype(np.float32)
+    net = mcc.GpuNet(spec, "bf16", B)
+    net.set_params(params)
+    d_img = torch.from_numpy(imgs).to(cuda)
+    d_lab = torch.from_numpy(labels).to(cuda)
+    s = torch.cuda.current_stream().cuda_stream
+    net.forward(d_img.data_ptr(), 0, B, s)
+    net.loss(d_lab.data_ptr(), 0, 1.0 / B, True, s)
+    net.backward_all(s)
+    torch.cuda.synchronize()
+    return spec, net.plan(), net.get_grads()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B", [96, 4099])
+def test_rows_dw_matches_pipe_dw(cuda, B, monkeypatch):
+    """conv1 weight gradient on the row-chunked kernel (conv_rows.hip) vs the
+    pixel-major conv_dw_pipe kernel (MCC_NO_ROWS=1): identical bf16 operands,
+    only the fp32 summation order differs, so every output channel's
+    weights and bias agree to ~1e-5."""
+    spec, plan, g_rows = _lenet_grads(cuda, B)
+    assert "dw:rows" in plan, plan
+    monkeypatch.setenv("MCC_NO_ROWS", "1")
+    _, plan2, g_pipe = _lenet_grads(cuda, B)
+    assert "dw:rows" not in plan2
+    L = spec.layers()[1]
+    w0, nb = L["w_off"], L["nbiases"]
+    W = g_rows[w0 : w0 + L["nweights"]].reshape(nb, -1)
+    Wp = g_pipe[w0 : w0 + L["nweights"]].reshape(nb, -1)
+    for c in range(nb):
+        assert _relerr(W[c], Wp[c]) < 1e-4, (c, W[c], Wp[c])
+    bo = L["b_off"]
+    np.testing.assert_allclose(g_rows[bo : bo + nb], g_pipe[bo : bo + nb], rtol=1e-4, atol=1e-7)
+    # the other layers are untouched by the switch
+    rest = np.ones_like(g_rows, dtype=bool)
+    rest[w0 : w0 + L["nweights"]] = False
+    rest[bo : bo + nb] = False
+    np.testing.assert_array_equal(g_rows[rest], g_pipe[rest])
