@@ -23,13 +23,14 @@ HOSTHIP   := -D__HIP_PLATFORM_AMD__ -I$(ROCM)/include
 LDHIP     := -L$(ROCM)/lib -lamdhip64 -Wl,-rpath,$(ROCM)/lib
 
 OBJ       := build/obj
-CORE_SRC  := csrc/core/model.cpp csrc/core/cpu_net.cpp csrc/core/io.cpp
+CORE_SRC  := csrc/core/model.cpp csrc/core/cpu_net.cpp csrc/core/io.cpp csrc/core/cpu_kernels_base.cpp \
+             csrc/core/cpu_kernels_v3.cpp
 CORE_OBJ  := $(patsubst csrc/core/%.cpp,$(OBJ)/core/%.o,$(CORE_SRC))
 KERN_SRC  := $(wildcard csrc/kernels/*.hip)
 KERN_OBJ  := $(patsubst csrc/kernels/%.hip,$(OBJ)/kernels/%.o,$(KERN_SRC))
 ENG_SRC   := $(wildcard csrc/engine/*.cpp)
 ENG_OBJ   := $(patsubst csrc/engine/%.cpp,$(OBJ)/engine/%.o,$(ENG_SRC))
-HDRS      := $(wildcard csrc/include/mcc/*.h csrc/kernels/*.h csrc/apps/*.h)
+HDRS      := $(wildcard csrc/include/mcc/*.h csrc/kernels/*.h csrc/apps/*.h) csrc/core/cpu_kernels.inc
 
 MODULE    := mpi_cuda_cnn_amd/_C$(EXT)
 BINS      := build/bin/cnn build/bin/cnn_hip build/bin/cnn_dist build/bin/test_watchdog
@@ -43,6 +44,14 @@ module: $(MODULE)
 bins: $(BINS)
 
 $(OBJ)/core/%.o: csrc/core/%.cpp $(HDRS)
+	@mkdir -p $(dir $@)
+	$(CXX) $(CXXFLAGS) -c $< -o $@
+
+# the AVX2/FMA build of the CPU kernels (dispatched at run time)
+$(OBJ)/core/cpu_kernels_v3.o: csrc/core/cpu_kernels_v3.cpp csrc/core/cpu_kernels.inc $(HDRS)
+	@mkdir -p $(dir $@)
+	$(CXX) $(CXXFLAGS) -mavx2 -mfma -c $< -o $@
+$(OBJ)/core/cpu_kernels_base.o: csrc/core/cpu_kernels_base.cpp csrc/core/cpu_kernels.inc $(HDRS)
 	@mkdir -p $(dir $@)
 	$(CXX) $(CXXFLAGS) -c $< -o $@
 
@@ -96,7 +105,8 @@ asan: build/bin/cnn_asan
 build/bin/cnn_asan: csrc/apps/cnn.cpp $(CORE_SRC) $(HDRS)
 	@mkdir -p $(dir $@)
 	$(CXX) -O1 -g -std=c++17 $(INC) -fsanitize=address,undefined -fno-omit-frame-pointer \
-	  -fno-sanitize-recover=undefined -o $@ csrc/apps/cnn.cpp $(CORE_SRC) -lm
+	  -fno-sanitize-recover=undefined -o $@ csrc/apps/cnn.cpp $(filter-out %_v3.cpp,$(CORE_SRC)) \
+	  csrc/core/cpu_kernels_v3.cpp -mavx2 -mfma -lm
 
 # Device bounds checks (MCC_DCHECK in the pipelined conv kernels): a separate
 # module under build/checked/ (same Python package, checked _C); run e.g.

@@ -1,5 +1,6 @@
 // CPU reference executor.  See mcc/cpu_net.h for the reference mapping.
 #include "mcc/cpu_net.h"
+#include "mcc/cpu_kernels.h"
 
 #include <algorithm>
 #include <cmath>
@@ -83,6 +84,175 @@ CpuNet<T>::CpuNet(const ModelSpec& spec, bool ref_compat) : spec_(spec), ref_com
   acts_.resize(spec_.layers.size());
   errs_.resize(spec_.layers.size());
   pidx_.resize(spec_.layers.size());
+  col_.resize(spec_.layers.size());
+}
+
+// ------------------------------------------------------------ fast path ----
+// Default mode: batched layers over vectorised kernels (cpu_kernels.inc),
+// AVX2/FMA build when the CPU has it.
+
+template <typename T>
+const CpuKernels<T>& cpu_kernels() {
+  static const CpuKernels<T> k = [] {
+    const char* e = std::getenv("MCC_CPU_BASELINE");
+    const bool base = e && std::atoi(e) != 0;
+#if defined(__x86_64__) && defined(__GNUC__)
+    __builtin_cpu_init();
+    if (!base && __builtin_cpu_supports("avx2") && __builtin_cpu_supports("fma")) return cpu_v3::kernels<T>();
+#endif
+    return cpu_base::kernels<T>();
+  }();
+  return k;
+}
+template const CpuKernels<double>& cpu_kernels<double>();
+template const CpuKernels<float>& cpu_kernels<float>();
+
+template <typename T>
+void CpuNet<T>::conv_fwd_fast(size_t li, int B) {
+  const LayerSpec& L = spec_.layers[li];
+  const int Ci = L.inC, H = L.inH, Wd = L.inW, k = L.ks, C = L.C;
+  const int P = L.H * L.W;
+  const int64_t K = (int64_t)Ci * k * k, BP = (int64_t)B * P;
+  std::vector<T>& col = col_[li];
+  col.assign((size_t)(K * BP), T(0));
+  // im2col over the minibatch: col[(i, kh, kw)][b*P + oy*OW + ox]
+  for (int b = 0; b < B; ++b) {
+    const T* in = acts_[li - 1].data() + (size_t)b * L.in_nodes();
+    for (int i = 0; i < Ci; ++i)
+      for (int kh = 0; kh < k; ++kh)
+        for (int kw = 0; kw < k; ++kw) {
+          T* row = col.data() + ((int64_t)(i * k + kh) * k + kw) * BP + (int64_t)b * P;
+          for (int oy = 0; oy < L.H; ++oy) {
+            const int y = oy * L.stride - L.pad + kh;
+            if (y < 0 || y >= H) continue;
+            const T* src = in + ((size_t)i * H + y) * Wd;
+            for (int ox = 0; ox < L.W; ++ox) {
+              const int x = ox * L.stride - L.pad + kw;
+              if (x >= 0 && x < Wd) row[oy * L.W + ox] = src[x];
+            }
+          }
+        }
+  }
+  const T* W = params.data() + L.w_off;
+  const T* bias = params.data() + L.b_off;
+  tmp_.resize((size_t)C * BP);
+  for (int o = 0; o < C; ++o) std::fill(tmp_.begin() + (size_t)o * BP, tmp_.begin() + (size_t)(o + 1) * BP, bias[o]);
+  cpu_kernels<T>().gemm_acc(C, BP, K, W, K, col.data(), BP, tmp_.data(), BP);  // out_t += W col
+  // activation, back to [b][o][p]
+  for (int b = 0; b < B; ++b) {
+    T* out = acts_[li].data() + (size_t)b * L.nnodes();
+    for (int o = 0; o < C; ++o) {
+      const T* src = tmp_.data() + (size_t)o * BP + (size_t)b * P;
+      for (int q = 0; q < P; ++q) out[(size_t)o * P + q] = act_fwd(L.act, src[q]);
+    }
+  }
+}
+
+template <typename T>
+void CpuNet<T>::conv_bwd_fast(size_t li, int B, bool need_dx) {
+  const LayerSpec& L = spec_.layers[li];
+  const int Ci = L.inC, H = L.inH, Wd = L.inW, k = L.ks, C = L.C;
+  const int P = L.H * L.W;
+  const int64_t K = (int64_t)Ci * k * k, BP = (int64_t)B * P;
+  const T* W = params.data() + L.w_off;
+  T* gW = grads.data() + L.w_off;
+  T* gb = grads.data() + L.b_off;
+  // dz_t[o][b*P + q] = err * act'(y)
+  tmp_.resize((size_t)C * BP);
+  for (int b = 0; b < B; ++b) {
+    const T* y = acts_[li].data() + (size_t)b * L.nnodes();
+    const T* er = errs_[li].data() + (size_t)b * L.nnodes();
+    for (int o = 0; o < C; ++o)
+      for (int q = 0; q < P; ++q)
+        tmp_[(size_t)o * BP + (size_t)b * P + q] = er[(size_t)o * P + q] * act_grad(L.act, y[(size_t)o * P + q]);
+  }
+  for (int o = 0; o < C; ++o) {
+    T s = 0;
+    const T* d = tmp_.data() + (size_t)o * BP;
+    for (int64_t j = 0; j < BP; ++j) s += d[j];
+    gb[o] += s;
+  }
+  const CpuKernels<T>& kern = cpu_kernels<T>();
+  // gW[C][K] += dz_t[C][BP] col^T[BP][K]
+  tmp2_.resize((size_t)(K * BP));
+  kern.transpose(col_[li].data(), K, BP, tmp2_.data());
+  kern.gemm_acc(C, K, BP, tmp_.data(), BP, tmp2_.data(), K, gW, K);
+  if (!need_dx) return;
+  // dcol[K][BP] = W^T[K][C] dz_t[C][BP]
+  std::vector<T> wt((size_t)(K * C));
+  kern.transpose(W, C, K, wt.data());
+  tmp2_.assign((size_t)(K * BP), T(0));
+  kern.gemm_acc(K, BP, C, wt.data(), C, tmp_.data(), BP, tmp2_.data(), BP);
+  // col2im into the input error
+  for (int b = 0; b < B; ++b) {
+    T* pe = errs_[li - 1].data() + (size_t)b * L.in_nodes();
+    std::fill(pe, pe + L.in_nodes(), T(0));
+    for (int i = 0; i < Ci; ++i)
+      for (int kh = 0; kh < k; ++kh)
+        for (int kw = 0; kw < k; ++kw) {
+          const T* row = tmp2_.data() + ((int64_t)(i * k + kh) * k + kw) * BP + (int64_t)b * P;
+          for (int oy = 0; oy < L.H; ++oy) {
+            const int y = oy * L.stride - L.pad + kh;
+            if (y < 0 || y >= H) continue;
+            T* dst = pe + ((size_t)i * H + y) * Wd;
+            for (int ox = 0; ox < L.W; ++ox) {
+              const int x = ox * L.stride - L.pad + kw;
+              if (x >= 0 && x < Wd) dst[x] += row[oy * L.W + ox];
+            }
+          }
+        }
+  }
+}
+
+template <typename T>
+void CpuNet<T>::fc_fwd_fast(size_t li, int B) {
+  const LayerSpec& L = spec_.layers[li];
+  const T* W = params.data() + L.w_off;
+  const T* bias = params.data() + L.b_off;
+  const int64_t nin = L.in_nodes();
+  const int C = L.C;
+  // W^T [nin][C] so the inner loop runs over the outputs
+  tmp_.resize((size_t)(nin * C));
+  for (int o = 0; o < C; ++o)
+    for (int64_t i = 0; i < nin; ++i) tmp_[(size_t)(i * C + o)] = W[o * nin + i];
+  for (int b = 0; b < B; ++b) {
+    T* out = acts_[li].data() + (size_t)b * C;
+    for (int o = 0; o < C; ++o) out[o] = bias[o];
+  }
+  // out[B][C] += in[B][nin] W^T[nin][C]
+  cpu_kernels<T>().gemm_acc(B, C, nin, acts_[li - 1].data(), nin, tmp_.data(), C, acts_[li].data(), C);
+}
+
+template <typename T>
+void CpuNet<T>::fc_bwd_fast(size_t li, int B, bool need_dx) {
+  const LayerSpec& L = spec_.layers[li];
+  const bool last = li + 1 == spec_.layers.size();
+  const T* W = params.data() + L.w_off;
+  T* gW = grads.data() + L.w_off;
+  T* gb = grads.data() + L.b_off;
+  const int64_t nin = L.in_nodes();
+  const int C = L.C;
+  tmp_.resize((size_t)B * C);  // dnet[b][o]
+  for (int b = 0; b < B; ++b) {
+    const T* y = acts_[li].data() + (size_t)b * C;
+    const T* er = errs_[li].data() + (size_t)b * C;
+    for (int o = 0; o < C; ++o) tmp_[(size_t)b * C + o] = er[o] * (last ? T(1) : act_grad(L.act, y[o]));
+  }
+  for (int o = 0; o < C; ++o) {
+    T s = 0;
+    for (int b = 0; b < B; ++b) s += tmp_[(size_t)b * C + o];
+    gb[o] += s;
+  }
+  const CpuKernels<T>& kern = cpu_kernels<T>();
+  // gW[C][nin] += dnet^T[C][B] x[B][nin]
+  tmp2_.resize((size_t)B * C);
+  kern.transpose(tmp_.data(), B, C, tmp2_.data());
+  kern.gemm_acc(C, nin, B, tmp2_.data(), B, acts_[li - 1].data(), nin, gW, nin);
+  if (!need_dx) return;
+  // pe[B][nin] = dnet[B][C] W[C][nin]
+  T* pe = errs_[li - 1].data();
+  std::fill(pe, pe + (size_t)B * nin, T(0));
+  kern.gemm_acc(B, nin, C, tmp_.data(), C, W, nin, pe, nin);
 }
 
 template <typename T>
@@ -91,6 +261,8 @@ int64_t CpuNet<T>::widx(const LayerSpec& L, int o, int i, int kh, int kw) const 
   if (ref_compat_) return (int64_t)o * L.inC * k * k + kh * k + kw;  // defect D1, cnn.c:181,193
   return (((int64_t)o * L.inC + i) * k + kh) * k + kw;
 }
+// (the loop-nest conv paths below run in ref-compat mode only: the default
+// mode takes conv_fwd_fast / conv_bwd_fast)
 
 template <typename T>
 void CpuNet<T>::forward(const T* x, int B) {
@@ -113,6 +285,7 @@ void CpuNet<T>::forward(const T* x, int B) {
 
 template <typename T>
 void CpuNet<T>::conv_fwd(size_t li, int B) {
+  if (!ref_compat_) { conv_fwd_fast(li, B); return; }
   const LayerSpec& L = spec_.layers[li];
   const T* W = params.data() + L.w_off;
   const T* bias = params.data() + L.b_off;
@@ -120,23 +293,26 @@ void CpuNet<T>::conv_fwd(size_t li, int B) {
   for (int b = 0; b < B; ++b) {
     const T* in = acts_[li - 1].data() + (size_t)b * L.in_nodes();
     T* out = acts_[li].data() + (size_t)b * L.nnodes();
-    for (int o = 0; o < L.C; ++o)
+    // reference loop nest and summation order (cnn.c:175-210); weights
+    // indexed with the reference's shared slice (D1): every input channel
+    // reads W[o][0] (widx in ref-compat mode), hoisted out of the MAC loop
+    for (int o = 0; o < L.C; ++o) {
+      const T* wo = W + widx(L, o, 0, 0, 0);
       for (int oy = 0; oy < L.H; ++oy)
         for (int ox = 0; ox < L.W; ++ox) {
           T v = bias[o];
           const int y0 = oy * L.stride - L.pad, x0 = ox * L.stride - L.pad;
+          const int kh0 = std::max(0, -y0), kh1 = std::min(k, H - y0);
+          const int kw0 = std::max(0, -x0), kw1 = std::min(k, Wd - x0);
           for (int i = 0; i < Ci; ++i)
-            for (int kh = 0; kh < k; ++kh) {
-              const int y = y0 + kh;
-              if (y < 0 || y >= H) continue;
-              for (int kw = 0; kw < k; ++kw) {
-                const int xx = x0 + kw;
-                if (xx < 0 || xx >= Wd) continue;
-                v += in[((size_t)i * H + y) * Wd + xx] * W[widx(L, o, i, kh, kw)];
-              }
+            for (int kh = kh0; kh < kh1; ++kh) {
+              const T* src = in + ((size_t)i * H + y0 + kh) * Wd + x0;
+              const T* w = wo + kh * k;
+              for (int kw = kw0; kw < kw1; ++kw) v += src[kw] * w[kw];
             }
           out[((size_t)o * L.H + oy) * L.W + ox] = act_fwd(L.act, v);
         }
+    }
   }
 }
 
@@ -173,15 +349,17 @@ void CpuNet<T>::fc_fwd(size_t li, int B) {
   const T* bias = params.data() + L.b_off;
   const int64_t nin = L.in_nodes();
   const bool last = li + 1 == spec_.layers.size();
+  if (!ref_compat_) fc_fwd_fast(li, B);
   for (int b = 0; b < B; ++b) {
     const T* in = acts_[li - 1].data() + (size_t)b * nin;
     T* out = acts_[li].data() + (size_t)b * L.C;
-    for (int o = 0; o < L.C; ++o) {
-      T v = bias[o];
-      const T* w = W + (size_t)o * nin;
-      for (int64_t i = 0; i < nin; ++i) v += in[i] * w[i];
-      out[o] = v;
-    }
+    if (ref_compat_)
+      for (int o = 0; o < L.C; ++o) {
+        T v = bias[o];
+        const T* w = W + (size_t)o * nin;
+        for (int64_t i = 0; i < nin; ++i) v += in[i] * w[i];
+        out[o] = v;
+      }
     if (last) {
       // softmax with max subtraction (cnn.c:125-143); ref max starts at -1 (D10)
       T m = ref_compat_ ? T(-1) : out[0];
@@ -242,6 +420,7 @@ StepStats CpuNet<T>::backward(const int* labels, T scale) {
 
 template <typename T>
 void CpuNet<T>::fc_bwd(size_t li, int B, bool need_dx) {
+  if (!ref_compat_) { fc_bwd_fast(li, B, need_dx); return; }
   const LayerSpec& L = spec_.layers[li];
   const bool last = li + 1 == spec_.layers.size();
   const T* W = params.data() + L.w_off;
@@ -270,6 +449,7 @@ void CpuNet<T>::fc_bwd(size_t li, int B, bool need_dx) {
 
 template <typename T>
 void CpuNet<T>::conv_bwd(size_t li, int B, bool need_dx) {
+  if (!ref_compat_) { conv_bwd_fast(li, B, need_dx); return; }
   const LayerSpec& L = spec_.layers[li];
   const T* W = params.data() + L.w_off;
   T* gW = grads.data() + L.w_off;
@@ -281,28 +461,34 @@ void CpuNet<T>::conv_bwd(size_t li, int B, bool need_dx) {
     const T* er = errs_[li].data() + (size_t)b * L.nnodes();
     T* pe = need_dx ? errs_[li - 1].data() + (size_t)b * L.in_nodes() : nullptr;
     if (pe) std::fill(pe, pe + L.in_nodes(), T(0));
-    for (int o = 0; o < L.C; ++o)
+    // reference order (cnn.c:212-247), shared-slice weights (D1) hoisted
+    for (int o = 0; o < L.C; ++o) {
+      const T* wo = W + widx(L, o, 0, 0, 0);
+      T* go = gW + widx(L, o, 0, 0, 0);
       for (int oy = 0; oy < L.H; ++oy)
         for (int ox = 0; ox < L.W; ++ox) {
           const size_t oi = ((size_t)o * L.H + oy) * L.W + ox;
           const T d = er[oi] * act_grad(L.act, y[oi]);
           if (d == T(0)) continue;
           const int y0 = oy * L.stride - L.pad, x0 = ox * L.stride - L.pad;
+          const int kh0 = std::max(0, -y0), kh1 = std::min(k, H - y0);
+          const int kw0 = std::max(0, -x0), kw1 = std::min(k, Wd - x0);
           for (int i = 0; i < Ci; ++i)
-            for (int kh = 0; kh < k; ++kh) {
-              const int yy = y0 + kh;
-              if (yy < 0 || yy >= H) continue;
-              for (int kw = 0; kw < k; ++kw) {
-                const int xx = x0 + kw;
-                if (xx < 0 || xx >= Wd) continue;
-                const size_t ii = ((size_t)i * H + yy) * Wd + xx;
-                const int64_t wi = widx(L, o, i, kh, kw);
-                if (pe) pe[ii] += W[wi] * d;
-                gW[wi] += d * in[ii];
-              }
+            for (int kh = kh0; kh < kh1; ++kh) {
+              const size_t ii0 = ((size_t)i * H + y0 + kh) * Wd + x0;
+              const T* w = wo + kh * k;
+              T* g = go + kh * k;
+              if (pe)
+                for (int kw = kw0; kw < kw1; ++kw) {
+                  pe[ii0 + kw] += w[kw] * d;
+                  g[kw] += d * in[ii0 + kw];
+                }
+              else
+                for (int kw = kw0; kw < kw1; ++kw) g[kw] += d * in[ii0 + kw];
             }
           gb[o] += d;
         }
+    }
   }
 }
 

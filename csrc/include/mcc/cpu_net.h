@@ -63,6 +63,14 @@ class CpuNet {
   void zero_grads();
 
  private:
+  // Default mode runs batched, cache-blocked kernels (im2col over the whole
+  // minibatch + axpy-form GEMMs that vectorise; FC weights blocked to stay in
+  // L2 across the batch).  --ref-compat keeps the per-sample reference loop
+  // nests below, so its log stays byte-identical to cnn.c.
+  void conv_fwd_fast(size_t li, int B);
+  void conv_bwd_fast(size_t li, int B, bool need_dx);
+  void fc_fwd_fast(size_t li, int B);
+  void fc_bwd_fast(size_t li, int B, bool need_dx);
   void conv_fwd(size_t li, int B);
   void conv_bwd(size_t li, int B, bool need_dx);
   void pool_fwd(size_t li, int B);
@@ -77,6 +85,8 @@ class CpuNet {
   std::vector<std::vector<T>> acts_;   // per layer outputs [B][nnodes]
   std::vector<std::vector<T>> errs_;   // per layer dL/d(output) [B][nnodes]
   std::vector<std::vector<int>> pidx_; // maxpool argmax (flat input index)
+  std::vector<std::vector<T>> col_;    // fast path: im2col [K][B*P] of each conv layer (kept for backward)
+  std::vector<T> tmp_, tmp2_;          // fast path scratch
 };
 
 extern template class CpuNet<double>;

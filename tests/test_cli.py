@@ -97,6 +97,39 @@ def test_ref_compat_log_matches_reference_program(cnn_bin, data, tmp_path):
     assert ours.stderr == ref.stderr
 
 
+@pytest.mark.skipif(not os.path.exists(REF_SRC) or shutil.which("gcc") is None, reason="reference source absent")
+def test_cpu_path_beats_reference_program(cnn_bin, tmp_path_factory):
+    """BASELINE config 1 (the CPU path): the reference cnn.c built from source
+    with gcc -O2 vs `cnn --model ref` (single thread, batched cache-blocked
+    kernels), both whole-process on the same 2,000 / 500 synthetic set and
+    the reference's 10 epochs: ours must be at least 2x faster and as
+    accurate; --ref-compat (the reference's own loop order) must not be
+    slower than the reference."""
+    import time
+
+    d = str(tmp_path_factory.mktemp("cpuperf"))
+    files = []
+    for n, s, p in ((2000, 1, "train"), (500, 2, "test")):
+        files += list(_write_set(d, n, s, p))
+    files = [files[0], files[1], files[2], files[3]]
+    ref_bin = os.path.join(d, "cnn_ref")
+    subprocess.run(["gcc", "-O2", "-o", ref_bin, REF_SRC, "-lm"], check=True, capture_output=True)
+
+    def run(cmd):
+        t = time.perf_counter()
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=900)
+        assert r.returncode == 0, r.stderr[-500:]
+        return time.perf_counter() - t, int(r.stderr.strip().splitlines()[-1].split("=")[-1])
+
+    t_ref, c_ref = run([ref_bin] + files)
+    t_ours, c_ours = run([cnn_bin] + files + ["--model", "ref"])
+    t_compat, _ = run([cnn_bin] + files + ["--model", "ref", "--ref-compat"])
+    print(f"reference {t_ref:.1f} s, ours {t_ours:.1f} s ({t_ref / t_ours:.2f}x), ref-compat {t_compat:.1f} s")
+    assert c_ours >= c_ref - 5
+    assert t_ref / t_ours >= 2.0, (t_ref, t_ours)
+    assert t_compat <= 1.05 * t_ref, (t_ref, t_compat)
+
+
 def test_synthetic_data_source(cnn_bin):
     """--synthetic N: no IDX files needed (the GPU box has no MNIST); the
     generated pair of a split shares its seed, so the task stays learnable."""
