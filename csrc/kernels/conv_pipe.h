@@ -53,6 +53,16 @@ __device__ __forceinline__ void u8x4_bf16(uint32_t w, uint32_t& h0, uint32_t& h1
   h0 = pack2((float)(w & 0xffu) * s, (float)((w >> 8) & 0xffu) * s);
   h1 = pack2((float)((w >> 16) & 0xffu) * s, (float)(w >> 24) * s);
 }
+// four u8 pixels -> four bf16 holding the exact integers 0..255 (the f32 of
+// an integer below 256 has zero low half-word, so its high half IS the bf16)
+__device__ __forceinline__ void u8x4_int_bf16(uint32_t w, uint32_t& h0, uint32_t& h1) {
+  const uint32_t f0 = __builtin_bit_cast(uint32_t, (float)(w & 0xffu));
+  const uint32_t f1 = __builtin_bit_cast(uint32_t, (float)((w >> 8) & 0xffu));
+  const uint32_t f2 = __builtin_bit_cast(uint32_t, (float)((w >> 16) & 0xffu));
+  const uint32_t f3 = __builtin_bit_cast(uint32_t, (float)(w >> 24));
+  h0 = __builtin_amdgcn_perm(f1, f0, 0x07060302u);
+  h1 = __builtin_amdgcn_perm(f3, f2, 0x07060302u);
+}
 // (a.hi, b.lo) as a bf16 pair
 __device__ __forceinline__ uint32_t mid(uint32_t a, uint32_t b) { return __builtin_amdgcn_alignbit(b, a, 16); }
 

@@ -220,7 +220,7 @@ __global__ void __launch_bounds__(256) dw_slab_sum_kernel(const float* slab, int
 // Level 2: canonical gradient from the chunk partials.
 __global__ void __launch_bounds__(256) dw_slab_final_kernel(const float* part, int nxc, int nv, int ncols_pad,
                                                             int kbias, int Cout, int Cin, int KS, int layout,
-                                                            int CL, float* gw, float* gb) {
+                                                            int CL, float wscale, float* gw, float* gb) {
   const int KK = KS * KS;
   const int nW = Cout * Cin * KK;
   const int j = blockIdx.x * blockDim.x + threadIdx.x;
@@ -247,7 +247,7 @@ __global__ void __launch_bounds__(256) dw_slab_final_kernel(const float* part, i
   }
   for (; xc < nxc; ++xc) s0 += part[(size_t)xc * nv + v];
   const float s = (s0 + s1) + (s2 + s3);
-  if (j < nW) gw[j] = s;
+  if (j < nW) gw[j] = s * wscale;
   else gb[row] = s;
 }
 
@@ -338,7 +338,7 @@ void conv_dw_pipe(const ConvDwPipeParams& pin, hipStream_t st) {
 }
 
 void dw_slab_reduce(const float* slab, int nx, int cout_pad, int ncols_pad, float* part, int Cout, int Cin, int KS,
-                    int layout, int CL, int kbias, float* gw, float* gb, hipStream_t st) {
+                    int layout, int CL, int kbias, float* gw, float* gb, hipStream_t st, float wscale) {
   if (nx <= 0) return;
   const int nv = cout_pad * ncols_pad;
   const int xs_per = 64;
@@ -347,7 +347,7 @@ void dw_slab_reduce(const float* slab, int nx, int cout_pad, int ncols_pad, floa
                      xs_per, part);
   const int nout = Cout * Cin * KS * KS + Cout;
   hipLaunchKernelGGL(dw_slab_final_kernel, dim3((unsigned)cdiv(nout, 256)), dim3(256), 0, st, part, nxc, nv, ncols_pad,
-                     kbias, Cout, Cin, KS, layout, CL, gw, gb);
+                     kbias, Cout, Cin, KS, layout, CL, wscale, gw, gb);
 }
 
 void conv_dw_pipe_reduce(const ConvDwPipeParams& pin, float* gw, float* gb, hipStream_t st) {

@@ -38,9 +38,14 @@ __device__ __forceinline__ float swap8(float v) {
   return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x128, 0xf, 0xf, false));
 }
 
-template <int MODE, int EPI, int ACT, bool PAIR, int NT>
+// WR > 0 (one column tile, exactly WR K chunks): every lane keeps its B
+// fragments and K-group offsets in registers for the whole launch, so the
+// K loop reads only the A operand from LDS (half the LDS traffic and none of
+// the weight-row bank conflicts); two row tiles per item keep the register
+// budget at four waves per SIMD.
+template <int MODE, int EPI, int ACT, bool PAIR, int NT, int WR = 0>
 __global__ void __launch_bounds__(NT) conv_pipe_fwd_kernel(ConvPipeParams p) {
-  constexpr int MT = 4;
+  constexpr int MT = WR > 8 ? 2 : 4;
   constexpr bool S1 = MODE == PM_U8S1;
   constexpr bool pool = EPI == FE_POOL;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -105,6 +110,16 @@ __global__ void __launch_bounds__(NT) conv_pipe_fwd_kernel(ConvPipeParams p) {
 
   const int lane = tid & 63, wave = tid >> 6;
   const int r16 = lane & 15, g = lane >> 4;
+  bf16x8 wreg[WR > 0 ? WR : 1];
+  int kreg[WR > 0 ? WR : 1];
+  if constexpr (WR > 0) {
+    __syncthreads();  // weights and K table staged
+#pragma unroll
+    for (int q = 0; q < WR; ++q) {
+      wreg[q] = load8(ws + r16 * wld + 8 * g + q * 32);
+      kreg[q] = ktab[q * 4 + g];
+    }
+  }
   Div drpi;
   drpi.mh = p.rows_mh;
   drpi.ml = p.rows_ml;
@@ -171,6 +186,21 @@ __global__ void __launch_bounds__(NT) conv_pipe_fwd_kernel(ConvPipeParams p) {
         } else {
 #pragma unroll
           for (int t = 0; t < MT; ++t) acc[t] = mma(acc[t], a0[t], b0);
+        }
+      } else if constexpr (WR > 0) {
+        // fully unrolled K loop on register-resident weights; chunk q+1's A
+        // fragments are read while chunk q's MFMAs issue
+        bf16x8 a[MT], an[MT];
+        read_a(a, kreg[0]);
+#pragma unroll
+        for (int q = 0; q < WR; ++q) {
+          if (q + 1 < WR) read_a(an, kreg[q + 1]);
+#pragma unroll
+          for (int t = 0; t < MT; ++t) acc[t] = mma(acc[t], a[t], wreg[q]);
+          if (q + 1 < WR) {
+#pragma unroll
+            for (int t = 0; t < MT; ++t) a[t] = an[t];
+          }
         }
       } else {
         // one chunk of look-ahead: chunk q+1's fragments (and chunk q+2's
@@ -353,6 +383,19 @@ void conv_pipe_forward(const ConvPipeParams& pin, hipStream_t st) {
   const int nt = p.pair ? 512 : 256;
   const dim3 grid((unsigned)p.grid), block((unsigned)nt);
   auto go = [&](auto kern) { hipLaunchKernelGGL(kern, grid, block, p.lds, st, p); };
+  // register-resident weights for the LeNet-class shapes (one column tile,
+  // 7 or 13 K chunks): conv2 forward and conv2 data gradient
+  const int ntiles = cdiv(p.Cout, 16);
+  if (p.layout == XL_C8 && ntiles == 1 && !pipe_knob("MCC_NO_WREG", 0)) {
+    if (p.nchunks == 7 && p.in.mode == PM_PLAIN && p.epi == FE_POOL) {
+      go(conv_pipe_fwd_kernel<PM_PLAIN, FE_POOL, ACT_RELU, false, 256, 7>);
+      return;
+    }
+    if (p.nchunks == 13 && p.in.mode == PM_UNPOOL && p.epi == FE_PLAIN) {
+      go(conv_pipe_fwd_kernel<PM_UNPOOL, FE_PLAIN, ACT_NONE, false, 256, 13>);
+      return;
+    }
+  }
 #define MCC_PIPE_EPI(MODE)                                                                      \
   if (p.epi == FE_POOL) go(conv_pipe_fwd_kernel<MODE, FE_POOL, ACT_RELU, false, 256>);                      \
   else if (p.epi == FE_PLAIN) go(conv_pipe_fwd_kernel<MODE, FE_PLAIN, ACT_NONE, false, 256>);               \

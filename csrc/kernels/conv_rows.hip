@@ -18,9 +18,13 @@
 //      the 8 pixels of its row chunk as one 16-byte read;
 //   B: the input staged as four copies shifted by 0..3 elements, so the 8
 //      inputs X[oy+kh][8g+kw-pad ..+7] of lane (tap, g) are two aligned
-//      8-byte reads from copy (kw - pad + A) & 3.
-// Per chunk and wave: 1 + 2*NT LDS reads, NT MFMAs and a handful of address
-// adds (the chunk offset is wave-uniform).  The dZ staging applies the
+//      8-byte reads from copy (kw - pad + A) & 3; a fifth copy holds ones
+//      (the bias column reads it at the same chunk offset, no select).  The
+//      u8 pixels are staged as exact bf16 integers 0..255; the 1/255 input
+//      scale (cnn.c:457) is applied to the weight columns in the reduce.
+// Per chunk and wave: 1 + 2*NT LDS reads, NT MFMAs and 1 + 2*NT address adds
+// (every lane base is precomputed, the chunk offset is wave-uniform); the
+// chunk loop is unrolled by two with ping-pong fragment registers.  The dZ staging applies the
 // max-pool backward (the pooled gradient routed to its argmax, masked by
 // ReLU) while writing the planes, so dZ never exists in HBM.  Plane and copy
 // strides are chosen by a host-side search over the LDS bank map.
@@ -69,7 +73,6 @@ __global__ void __launch_bounds__(kT) conv_dw_rows_kernel(ConvDwRowsParams p) {
   const RowsDwLayout L = rows_dw_layout(p);
   bf16* xs = reinterpret_cast<bf16*>(smem + L.xs_off);
   bf16* dz = reinterpret_cast<bf16*>(smem + L.dz_off);
-  bf16* ones = reinterpret_cast<bf16*>(smem + L.ones_off);
   float* red = reinterpret_cast<float*>(smem);  // reused after the main loop
 
   const int tid = threadIdx.x;
@@ -78,20 +81,32 @@ __global__ void __launch_bounds__(kT) conv_dw_rows_kernel(ConvDwRowsParams p) {
   const int r16 = lane & 15, g = lane >> 4;
 
   zero_lds(reinterpret_cast<bf16*>(smem), L.ones_off / 2);
-  if (tid < 8) ones[tid] = (bf16)1.0f;
+  __syncthreads();
+  // the ones copy (copy 4) of every image slot: rows [0, OH), columns [0, 32)
+  for (int e = tid; e < p.imgs * p.OH * 4; e += kT) {
+    const int m = e / (p.OH * 4), r = e - m * p.OH * 4, y = r >> 2, c8 = (r & 3) * 8;
+    const uint32_t one2 = 0x3f803f80u;  // two bf16 1.0
+    bf16* d = xs + m * p.ximg + 4 * p.CS + y * p.Pw + c8;  // 8-byte aligned (Pw % 4 == 0)
+    st8(d, one2, one2);
+    st8(d + 4, one2, one2);
+  }
 
-  // ---- per-lane operand offsets (kernel-invariant) ----
+  // ---- per-lane operand byte offsets (kernel-invariant) ----
   const int c_l = r16 < p.Cout ? r16 : r16 % p.Cout;  // rows >= Cout: duplicate rows, discarded
-  const int a_lane = c_l * p.dplane + 8 * g;
-  int b_lane[NT];
-  bool b_one[NT];
+  const int a_lane = 2 * (L.dz_off / 2 + c_l * p.dplane + 8 * g);
+  int b_lo[NT], b_hi[NT];
 #pragma unroll
   for (int t = 0; t < NT; ++t) {
     const int n = t * 16 + r16;
-    b_one[t] = n >= p.KK;
     const int kh = n / p.KS, kw = n - kh * p.KS;
     const int sh = kw - p.pad + p.A, s = sh & 3;
-    b_lane[t] = b_one[t] ? 0 : s * p.CS + kh * p.Pw + (sh - s) + 8 * g;
+    // taps: shifted copy s; bias and padding columns: the ones copy
+    const int e = n < p.KK ? s * p.CS + kh * p.Pw + (sh - s) + 8 * g : 4 * p.CS + 8 * g;
+    b_lo[t] = 2 * e;
+    b_hi[t] = 2 * (e + 4);
+    // opaque to the optimiser: two ds_read_b64 (2 + 2 LDS cycles) instead
+    // of one fused ds_read2_b64 (8 cycles, MI355X_MICROARCH.md §LDS)
+    asm volatile("" : "+v"(b_hi[t]));
   }
 
   // ---- staging geometry (per thread, group-invariant) ----
@@ -180,8 +195,8 @@ __global__ void __launch_bounds__(kT) conv_dw_rows_kernel(ConvDwRowsParams p) {
     for (int i = 0; i < kNiX; ++i) {
       if (xim[i] < 0 || xim[i] >= nimg) continue;
       uint32_t h0, h1, h2, h3;
-      u8x4_bf16((xfl[i] & 1u) ? xw[i][0] : 0u, h0, h1);
-      u8x4_bf16((xfl[i] & 2u) ? xw[i][1] : 0u, h2, h3);
+      u8x4_int_bf16((xfl[i] & 1u) ? xw[i][0] : 0u, h0, h1);
+      u8x4_int_bf16((xfl[i] & 2u) ? xw[i][1] : 0u, h2, h3);
       bf16* b = xs + xdst[i];
       st8(b, h0, h1);
       st8(b + p.CS, mid(h0, h1), mid(h1, h2));
@@ -240,42 +255,45 @@ __global__ void __launch_bounds__(kT) conv_dw_rows_kernel(ConvDwRowsParams p) {
 
     // chunks q = (image, output row), wave-strided; offsets are wave-uniform
     const int nq = (p.ablate & 2) ? 0 : nimg * p.OH;
-    int q = wave, img = 0, oy = wave;
-    while (oy >= p.OH) { oy -= p.OH; ++img; }
+    const char* lds = smem;
     auto frag = [&](int im, int y, bf16x8& a, bf16x8 (&b)[NT]) {
-      a = load8(dz + im * p.dzimg + y * 32 + a_lane);
-      const int xo = im * p.ximg + y * p.Pw;
+      a = *reinterpret_cast<const bf16x8*>(lds + a_lane + 2 * (im * p.dzimg + y * 32));
+      const int xo = 2 * (im * p.ximg + y * p.Pw);
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
-        // element offsets from the LDS base (the ones vector sits past the tiles)
-        int o0 = b_one[t] ? (int)(L.ones_off / 2) : xo + b_lane[t];
-        int o1 = o0 + 4;
-        // opaque to the optimiser: two ds_read_b64 (2 + 2 LDS cycles) instead
-        // of one fused ds_read2_b64 (8 cycles, MI355X_MICROARCH.md §LDS)
-        asm volatile("" : "+v"(o1));
-        const bf16* base = reinterpret_cast<const bf16*>(smem);
-        const bf16x4 lo = *reinterpret_cast<const bf16x4*>(base + o0);
-        const bf16x4 hi = *reinterpret_cast<const bf16x4*>(base + o1);
+        const bf16x4 lo = *reinterpret_cast<const bf16x4*>(lds + b_lo[t] + xo);
+        const bf16x4 hi = *reinterpret_cast<const bf16x4*>(lds + b_hi[t] + xo);
         b[t] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
       }
     };
-    bf16x8 a, b[NT];
-    if (q < nq) frag(img, oy, a, b);
-    for (; q < nq; q += kT / 64) {
-      int imn = img, oyn = oy + kT / 64;
-      while (oyn >= p.OH) { oyn -= p.OH; ++imn; }
-      bf16x8 an, bn[NT];
-      const bool more = q + kT / 64 < nq;
-      if (more) frag(imn, oyn, an, bn);
+    // chunks wave, wave + 4, ...: (image, row) advanced incrementally
+    // (scalar, OH >= 4); unrolled by two with ping-pong fragments so no
+    // fragment is copied between registers
+    constexpr int NW = kT / 64;
+    const int cnt = nq > wave ? (nq - wave + NW - 1) / NW : 0;
+    int im = 0, y = wave;
+    auto step = [&](int& i, int& r) {
+      r += NW;
+      if (r >= p.OH) { r -= p.OH; ++i; }
+    };
+    bf16x8 a0, b0[NT], a1, b1[NT];
+    if (cnt > 0) frag(im, y, a0, b0);
+    int i = 0;
+    for (; i + 2 <= cnt; i += 2) {
+      int im1 = im, y1 = y;
+      step(im1, y1);
+      frag(im1, y1, a1, b1);
 #pragma unroll
-      for (int t = 0; t < NT; ++t) acc[t] = mma(acc[t], a, b[t]);
-      if (more) {
-        a = an;
+      for (int t = 0; t < NT; ++t) acc[t] = mma(acc[t], a0, b0[t]);
+      im = im1; y = y1;
+      step(im, y);
+      if (i + 2 < cnt) frag(im, y, a0, b0);
 #pragma unroll
-        for (int t = 0; t < NT; ++t) b[t] = bn[t];
-      }
-      img = imn;
-      oy = oyn;
+      for (int t = 0; t < NT; ++t) acc[t] = mma(acc[t], a1, b1[t]);
+    }
+    if (i < cnt) {
+#pragma unroll
+      for (int t = 0; t < NT; ++t) acc[t] = mma(acc[t], a0, b0[t]);
     }
   }
 
@@ -363,7 +381,7 @@ bool conv_dw_rows_plan(ConvDwRowsParams& p) {
       const int c = rows_b_conflicts(p, Pw, CS);
       if (c < best) { best = c; p.Pw = Pw; p.CS = CS; }
     }
-  p.ximg = (4 * p.CS + 7) & ~7;
+  p.ximg = (5 * p.CS + 7) & ~7;  // four shifted copies + the ones copy
   p.dplane = p.OH * 32 + 16;  // 16-element skew: conflict-free 16-byte A reads (host search, r2)
   p.dzimg = p.Cout * p.dplane;
   const int xper = p.SH * p.nblk, dper = p.DH * p.DW;
@@ -412,7 +430,7 @@ void conv_dw_rows(const ConvDwRowsParams& pin, float* gw, float* gb, hipStream_t
   // deterministic two-level reduce of the per-workgroup slabs
   const int ncols = p.ntiles * 16;
   dw_slab_reduce(p.slab, p.grid, 16, ncols, p.slab + (size_t)pin.grid * 16 * ncols, p.Cout, 1, p.KS, XL_ROWS, 1,
-                 p.KK, gw, gb, st);
+                 p.KK, gw, gb, st, 1.0f / 255.0f);  // the input was staged unscaled
 }
 
 }  // namespace gpu

@@ -199,8 +199,10 @@ void conv_dw_pipe_reduce(const ConvDwPipeParams& p, float* gw, float* gb, hipStr
 // Deterministic two-level reduce of per-workgroup dW slabs [nx][cout_pad][ncols_pad]
 // (chunk partials in `part`, ceil(nx/64) * cout_pad * ncols_pad floats) into
 // gw[Cout][Cin][KS][KS] / gb[Cout]; `layout` names the slab column order.
+// wscale multiplies the weight columns (not the bias), e.g. a 1/255 input scale
+// the kernel left out of its operand.
 void dw_slab_reduce(const float* slab, int nx, int cout_pad, int ncols_pad, float* part, int Cout, int Cin, int KS,
-                    int layout, int CL, int kbias, float* gw, float* gb, hipStream_t s);
+                    int layout, int CL, int kbias, float* gw, float* gb, hipStream_t s, float wscale = 1.f);
 
 // Row-chunked weight gradient of a single-channel (u8) stride-1 first layer
 // (conv_rows.hip): M = output channels, N = tap-packed kernel positions + a

@@ -334,9 +334,11 @@ def _lenet_grads(cuda, B, seed=7):
 @pytest.mark.parametrize("B", [96, 4099])
 def test_rows_dw_matches_pipe_dw(cuda, B, monkeypatch):
     """conv1 weight gradient on the row-chunked kernel (conv_rows.hip) vs the
-    pixel-major conv_dw_pipe kernel (MCC_NO_ROWS=1): identical bf16 operands,
-    only the fp32 summation order differs, so every output channel's
-    weights and bias agree to ~1e-5."""
+    pixel-major conv_dw_pipe kernel (MCC_NO_ROWS=1).  Same bf16 dZ; the
+    pixels differ only in rounding (conv_rows stages the exact integers
+    0..255 and applies 1/255 in fp32 at the end, conv_dw_pipe rounds x/255 to
+    bf16: <= 2^-9 relative per pixel), so every output channel agrees to a
+    few 1e-3 and the bias (no pixel operand) to ~1e-5."""
     spec, plan, g_rows = _lenet_grads(cuda, B)
     assert "dw:rows" in plan, plan
     monkeypatch.setenv("MCC_NO_ROWS", "1")
@@ -347,7 +349,7 @@ def test_rows_dw_matches_pipe_dw(cuda, B, monkeypatch):
     W = g_rows[w0 : w0 + L["nweights"]].reshape(nb, -1)
     Wp = g_pipe[w0 : w0 + L["nweights"]].reshape(nb, -1)
     for c in range(nb):
-        assert _relerr(W[c], Wp[c]) < 1e-4, (c, W[c], Wp[c])
+        assert _relerr(W[c], Wp[c]) < 4e-3, (c, W[c], Wp[c])
     bo = L["b_off"]
     np.testing.assert_allclose(g_rows[bo : bo + nb], g_pipe[bo : bo + nb], rtol=1e-4, atol=1e-7)
     # the other layers are untouched by the switch

