@@ -344,7 +344,7 @@ void GpuNet::build() {
           for (int kw = 0; kw < st.KS; ++kw) {
             const int32_t src = (int32_t)(st.w_off + ((int64_t)n * st.KS + kh) * st.KS + kw);
             idx[st.pk_fwd + (int64_t)n * st.pf.kpad + kh * 8 + kw] = src;
-            if (st.pf.pair) idx[st.pk_fwd + (int64_t)(8 + n) * st.pf.kpad + kh * 8 + kw + 1] = src;
+            if (st.pf.pair) idx[st.pk_fwd + (int64_t)(8 + n) * st.pf.kpad + kh * 8 + kw + st.pf.pair] = src;
           }
     } else if (st.kind == Stage::CONV) {
       const int KK = st.KS * st.KS;
@@ -417,7 +417,7 @@ void GpuNet::build() {
         if (st.pk_dx >= 0) add(st.pk_dx, 1, st.kgem_d, KS * st.C, st.C, 1);
       } else if (st.pipe_fwd && st.pf.layout == gpu::XL_S1) {
         add(st.pk_fwd, st.pf.kpad, 0, 8, 1, 0);
-        if (st.pf.pair) add(st.pk_fwd + 8 * (int64_t)st.pf.kpad + 1, st.pf.kpad, 0, 8, 1, 0);
+        if (st.pf.pair) add(st.pk_fwd + 8 * (int64_t)st.pf.kpad + st.pf.pair, st.pf.kpad, 0, 8, 1, 0);
       } else {
         const int CLx = st.cvec ? st.CL : st.inC;
         add(st.pk_fwd, st.kpad, 1, KS * CLx, CLx, 0);
@@ -547,7 +547,7 @@ std::string GpuNet::plan() const {
          << st.imgs_dx << "/" << st.imgs_dw;
       if (st.pipe_fwd || st.pipe_dx || st.pipe_dw || st.rows_dw) {
         os << " pipe[";
-        if (st.pipe_fwd) os << "fwd:" << (st.pf.layout == gpu::XL_S1 ? (st.pf.pair ? "s1p" : "s1") : "c8") << "x" << st.pf.imgs << "/g" << st.pf.grid << " ";
+        if (st.pipe_fwd) os << "fwd:" << (st.pf.layout == gpu::XL_S1 ? (st.pf.pair == 2 ? "s1w" : st.pf.pair ? "s1p" : "s1") : "c8") << "x" << st.pf.imgs << "/g" << st.pf.grid << " ";
         if (st.pipe_dx) os << "dx:x" << st.pdx.imgs << "/g" << st.pdx.grid << " ";
         if (st.pipe_dw) os << "dw:x" << st.pdw.imgs << "/g" << st.pdw.grid;
         if (st.rows_dw) os << "dw:rows x" << st.prw.imgs << "/g" << st.prw.grid;

@@ -234,11 +234,16 @@ __device__ __forceinline__ bf16x4 tr4_s1(const bf16* xs, int CS, int e) {
 // Output-pixel (row) -> tile offset of its first tap.  Pool: rows ordered by
 // 2x2 window so a 16-row tile holds four whole windows.
 __device__ void row_table(int* tab, int rows, bool pool, int OW, int cs, int ty0, int tx0, int LWp, int CL,
-                          bool pair = false) {
+                          int pair = 0) {
   const int PW = OW >> 1;
   for (int r = threadIdx.x; r < rows; r += blockDim.x) {
     int oy, ox;
-    if (pair && pool) {  // row = (window, top/bottom pixel pair)
+    if (pair == 2) {  // row = (base window (even column), position TL/TR/BL/BR)
+      const int bw = r >> 2, pos = r & 3, PB = PW >> 1;
+      const int ph = bw / PB, pm = bw - ph * PB;
+      oy = 2 * ph + (pos >> 1);
+      ox = 4 * pm + (pos & 1);
+    } else if (pair && pool) {  // row = (window, top/bottom pixel pair)
       const int win = r >> 1;
       const int ph = win / PW, pw = win - ph * PW;
       oy = 2 * ph + (r & 1);

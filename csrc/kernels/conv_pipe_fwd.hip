@@ -43,7 +43,7 @@ __device__ __forceinline__ float swap8(float v) {
 // K loop reads only the A operand from LDS (half the LDS traffic and none of
 // the weight-row bank conflicts); two row tiles per item keep the register
 // budget at four waves per SIMD.
-template <int MODE, int EPI, int ACT, bool PAIR, int NT, int WR = 0>
+template <int MODE, int EPI, int ACT, int PAIR, int NT, int WR = 0>
 __global__ void __launch_bounds__(NT) conv_pipe_fwd_kernel(ConvPipeParams p) {
   constexpr int MT = WR > 8 ? 2 : 4;
   constexpr bool S1 = MODE == PM_U8S1;
@@ -95,7 +95,7 @@ __global__ void __launch_bounds__(NT) conv_pipe_fwd_kernel(ConvPipeParams p) {
     }
     ktab[gi] = off;  // padding groups point at tap 0 (zero weights)
   }
-  row_table(ptab, rows_img, pool, p.OW, p.cs, p.ty0, p.tx0, s.LWp, S1 ? 1 : s.CL, PAIR);
+  row_table(ptab, rows_img, pool, p.OW, p.cs, p.ty0, p.tx0, s.LWp, S1 ? 1 : s.CL, PAIR);  // PAIR 2: window pairs
   if (S1) {  // bake the shifted-copy choice into the table (IMG and K offsets are multiples of 4)
     for (int r = tid; r < rows_img; r += NT) {
       const int b = ptab[r], c = b & 3;
@@ -226,7 +226,34 @@ __global__ void __launch_bounds__(NT) conv_pipe_fwd_kernel(ConvPipeParams p) {
         if (acc[0][0] == 1234.5f && acc[MT - 1][3] == -1.f) outs[0] = (bf16)0.f;
         continue;
       }
-      if constexpr (PAIR) {
+      if constexpr (PAIR == 2) {
+        // window pairs: rows 4g..4g+3 = the four positions (TL, TR, BL, BR)
+        // of base window bw; column r16 = channel (r16 & 7) of window bw
+        // (r16 < 8) or of its right neighbour (r16 >= 8): the 2x2 max-pool
+        // and its argmax are in-lane (no cross-lane exchange)
+        const int c = r16 & 7, sft = r16 >> 3;
+        const float bv = bias_s[r16];
+#pragma unroll
+        for (int t = 0; t < MT; ++t) {
+          const int bw = (mg * MT + t) * 4 + g;
+          float best = acc[t][0];
+          int arg = 0;
+#pragma unroll
+          for (int i = 1; i < 4; ++i) {
+            const bool gt = acc[t][i] > best;
+            best = gt ? acc[t][i] : best;
+            arg = gt ? i : arg;
+          }
+          if (c < p.Cout && 4 * bw < M) {
+            const bf16 yb = (bf16)fmaxf(best + bv, 0.f);
+            const int o = (2 * bw + sft) * p.Cout + c;
+            MCC_DCHECK(o < p.imgs * out_img);
+            outs[o] = yb;
+            args[o] = (uint8_t)((float)yb > 0.f ? arg : 4);  // 4: ReLU-inactive window
+          }
+        }
+        continue;
+      } else if constexpr (PAIR == 1) {
         // column r16 = channel (r16 & 7) of the left (r16 < 8) or right pixel
         const int c = r16 & 7;
         const bool right = r16 >= 8;
@@ -328,6 +355,10 @@ bool conv_pipe_plan(ConvPipeParams& p) {
   p.layout = s1 ? XL_S1 : XL_C8;
   p.pair = s1 && p.Cout <= 8 && p.KS <= 7 && p.cs == 1 && (p.OW & 1) == 0 &&
            (p.epi == FE_POOL || (p.epi == FE_ACT && (p.act == ACT_RELU || p.act == ACT_NONE)));
+  // window pairs (the second column half computes the next 2x2 window, taps
+  // shifted by two): the pool is in-lane, no DPP exchange
+  if (p.pair && p.epi == FE_POOL && p.KS <= 6 && (p.OW & 3) == 0 && (p.OH & 1) == 0 && !pipe_knob("MCC_NO_PAIR2", 0))
+    p.pair = 2;
   if (s1) {  // align the source columns to 4 (shift the conv origin accordingly)
     const int ox = s.offx < 4 ? 4 : (s.offx + 3) & ~3;
     p.tx0 += ox - s.offx;
@@ -388,24 +419,28 @@ void conv_pipe_forward(const ConvPipeParams& pin, hipStream_t st) {
   const int ntiles = cdiv(p.Cout, 16);
   if (p.layout == XL_C8 && ntiles == 1 && !pipe_knob("MCC_NO_WREG", 0)) {
     if (p.nchunks == 7 && p.in.mode == PM_PLAIN && p.epi == FE_POOL) {
-      go(conv_pipe_fwd_kernel<PM_PLAIN, FE_POOL, ACT_RELU, false, 256, 7>);
+      go(conv_pipe_fwd_kernel<PM_PLAIN, FE_POOL, ACT_RELU, 0, 256, 7>);
       return;
     }
     if (p.nchunks == 13 && p.in.mode == PM_UNPOOL && p.epi == FE_PLAIN) {
-      go(conv_pipe_fwd_kernel<PM_UNPOOL, FE_PLAIN, ACT_NONE, false, 256, 13>);
+      go(conv_pipe_fwd_kernel<PM_UNPOOL, FE_PLAIN, ACT_NONE, 0, 256, 13>);
       return;
     }
   }
 #define MCC_PIPE_EPI(MODE)                                                                      \
-  if (p.epi == FE_POOL) go(conv_pipe_fwd_kernel<MODE, FE_POOL, ACT_RELU, false, 256>);                      \
-  else if (p.epi == FE_PLAIN) go(conv_pipe_fwd_kernel<MODE, FE_PLAIN, ACT_NONE, false, 256>);               \
-  else if (p.act == ACT_RELU) go(conv_pipe_fwd_kernel<MODE, FE_ACT, ACT_RELU, false, 256>);                 \
-  else if (p.act == ACT_TANH) go(conv_pipe_fwd_kernel<MODE, FE_ACT, ACT_TANH, false, 256>);                 \
-  else go(conv_pipe_fwd_kernel<MODE, FE_ACT, ACT_NONE, false, 256>);
+  if (p.epi == FE_POOL) go(conv_pipe_fwd_kernel<MODE, FE_POOL, ACT_RELU, 0, 256>);                      \
+  else if (p.epi == FE_PLAIN) go(conv_pipe_fwd_kernel<MODE, FE_PLAIN, ACT_NONE, 0, 256>);               \
+  else if (p.act == ACT_RELU) go(conv_pipe_fwd_kernel<MODE, FE_ACT, ACT_RELU, 0, 256>);                 \
+  else if (p.act == ACT_TANH) go(conv_pipe_fwd_kernel<MODE, FE_ACT, ACT_TANH, 0, 256>);                 \
+  else go(conv_pipe_fwd_kernel<MODE, FE_ACT, ACT_NONE, 0, 256>);
+  if (p.pair == 2) {
+    go(conv_pipe_fwd_kernel<PM_U8S1, FE_POOL, ACT_RELU, 2, 512>);
+    return;
+  }
   if (p.pair) {
-    if (p.epi == FE_POOL) go(conv_pipe_fwd_kernel<PM_U8S1, FE_POOL, ACT_RELU, true, 512>);
-    else if (p.act == ACT_RELU) go(conv_pipe_fwd_kernel<PM_U8S1, FE_ACT, ACT_RELU, true, 512>);
-    else go(conv_pipe_fwd_kernel<PM_U8S1, FE_ACT, ACT_NONE, true, 512>);
+    if (p.epi == FE_POOL) go(conv_pipe_fwd_kernel<PM_U8S1, FE_POOL, ACT_RELU, 1, 512>);
+    else if (p.act == ACT_RELU) go(conv_pipe_fwd_kernel<PM_U8S1, FE_ACT, ACT_RELU, 1, 512>);
+    else go(conv_pipe_fwd_kernel<PM_U8S1, FE_ACT, ACT_NONE, 1, 512>);
     return;
   }
   switch (p.in.mode) {

@@ -165,7 +165,10 @@ struct ConvPipeParams {
   // XL_S1 with Cout <= 8: an MFMA row is a horizontal PAIR of output pixels;
   // columns 0..7 are the left pixel's channels, 8..15 the right one's (its
   // taps shifted by one inside the 8-wide K window).  Packed weights:
-  // [16][kpad], col n < 8: k = kh*8 + kw; col 8 + n: k = kh*8 + kw + 1.
+  // [16][kpad], col n < 8: k = kh*8 + kw; col 8 + n: k = kh*8 + kw + pair.
+  // pair == 2 (pooled, KS <= 6): rows are the four positions of a 2x2 window
+  // and columns 8.. compute the window two pixels to the right (taps shifted
+  // by two), so the max-pool is in-lane.
   int pair = 0;
   size_t lds = 0;
   uint32_t rows_mh = 0, rows_ml = 0;  // division magic for the GEMM rows per image (set at launch)

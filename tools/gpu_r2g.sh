@@ -12,4 +12,4 @@ for set in "SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_INSTS_VALU SQ_
   timeout -s KILL 90 rocprofv3 --kernel-trace --pmc $set -d $O/pmc$i -o run --output-format csv -- python $R/bench.py --steps 4 --warmup 2 --no-dist > $O/pmc$i.log 2>&1 || { tail -5 $O/pmc$i.log; exit 1; }
 done
 python $R/tools/pmc_summary.py $O/pmc1/run_counter_collection.csv $O/pmc2/run_counter_collection.csv > $O/pmc_summary.txt
-grep -A16 "conv_dw_rows\|conv_pipe_fwd_kernel<3" $O/pmc_summary.txt | head -60
+grep -A16 "conv_dw_rows\|conv_pipe_fwd_kernel<" $O/pmc_summary.txt | head -80
