@@ -108,21 +108,33 @@ __device__ __forceinline__ uint32_t relu_mask(uint32_t d, uint32_t y) {
 }
 
 // Per-thread staging of one image group: items e = tid + i*NT (i < NI).
-template <int MODE, int NT = kT>
+// INTU8 (PM_U8S1): the tile holds the exact integers 0..255 (the consumer
+// applies 1/255 in fp32), and the dataset indices of a group are gathered one
+// group ahead (load_idx) so the pixel loads never wait on the index gather.
+template <int MODE, int NT = kT, bool INTU8 = false>
 struct Loader {
   static constexpr int W = ModeInfo<MODE>::W, NI = ModeInfo<MODE>::NI;
   int im[NI];     // image within the group, -1: no item
-  int soff[NI];   // source offset within an image (bytes for u8, elements otherwise)
+  int soff[NI];   // source offset within an image (bytes for u8, elements otherwise);
+                  // U8S1: | bit0 first word of a row, bit1 last word of a row
   int dst[NI];    // LDS destination (elements)
-  uint32_t fl[NI];  // U8S1: bit0 first word of a row, bit1 last word of a row
+  int gim[NI];    // INTU8: dataset index of the item's image (next group to load)
   uint32_t r[NI][W];
+
+  __device__ __forceinline__ void load_idx(const PipeSrc& s, int img0, int N) {
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int n = min(img0 + max(im[i], 0), N - 1);
+      gim[i] = s.idx ? s.idx[n] : n;
+    }
+  }
 
   __device__ __forceinline__ void init(const PipeSrc& s, int imgs) {
     const int total = imgs * s.per_img;
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
       const int e = threadIdx.x + i * NT;
-      im[i] = -1; soff[i] = 0; dst[i] = 0; fl[i] = 0;
+      im[i] = -1; soff[i] = 0; dst[i] = 0;
 #pragma unroll
       for (int k = 0; k < W; ++k) r[i][k] = 0;
       if (e >= total) continue;
@@ -131,9 +143,8 @@ struct Loader {
       if constexpr (MODE == PM_U8S1) {
         const int wpr = s.SW >> 2;
         const int y = rem / wpr, w = rem - y * wpr;
-        soff[i] = y * s.SW + 4 * w;
+        soff[i] = y * s.SW + 4 * w + (w == 0 ? 1 : 0) + (w == wpr - 1 ? 2 : 0);
         dst[i] = m * s.IMG + (y + s.offy) * s.LWp + 4 * w + s.offx;
-        fl[i] = (w == 0 ? 1u : 0u) | (w == wpr - 1 ? 2u : 0u);
       } else {
         const int runs = s.SC / s.RW;
         const int pix = rem / runs, run = rem - pix * runs;
@@ -147,9 +158,20 @@ struct Loader {
     }
   }
 
-  // Issue the group's global loads (no waits here).
-  __device__ __forceinline__ void load(const PipeSrc& s, int img0, int N) {
+  // Issue the group's global loads (no waits here).  INTU8: unconditional
+  // loads of the prefetched indices, then the indices of group next_img0.
+  __device__ __forceinline__ void load(const PipeSrc& s, int img0, int N, int next_img0 = 0) {
     const size_t img_src = (size_t)s.SH * s.SW * s.SC;
+    if constexpr (INTU8) {
+#pragma unroll
+      for (int i = 0; i < NI; ++i) {
+        const uint8_t* p = static_cast<const uint8_t*>(s.src) + (size_t)gim[i] * img_src + (soff[i] & ~3);
+        r[i][0] = *reinterpret_cast<const uint32_t*>(p);
+        r[i][1] = *reinterpret_cast<const uint32_t*>(p + 4 - 2 * (soff[i] & 2));  // masked at the store
+      }
+      if (next_img0 < N) load_idx(s, next_img0, N);
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
       if (im[i] < 0) continue;
@@ -157,9 +179,9 @@ struct Loader {
       if (n >= N) continue;
       if constexpr (MODE == PM_U8S1) {
         const int gim = s.idx ? s.idx[n] : n;
-        const uint8_t* p = static_cast<const uint8_t*>(s.src) + (size_t)gim * img_src + soff[i];
+        const uint8_t* p = static_cast<const uint8_t*>(s.src) + (size_t)gim * img_src + (soff[i] & ~3);
         r[i][0] = *reinterpret_cast<const uint32_t*>(p);
-        r[i][1] = (fl[i] & 2u) ? 0u : *reinterpret_cast<const uint32_t*>(p + 4);
+        r[i][1] = (soff[i] & 2) ? 0u : *reinterpret_cast<const uint32_t*>(p + 4);
       } else {
         const size_t g = (size_t)n * img_src + soff[i];
         ld_chan(static_cast<const bf16*>(s.src) + g, s.RW, r[i]);
@@ -178,14 +200,19 @@ struct Loader {
       if (im[i] < 0 || im[i] >= nimg) continue;
       if constexpr (MODE == PM_U8S1) {
         uint32_t h0, h1, h2, h3;
-        u8x4_bf16(r[i][0], h0, h1);
-        u8x4_bf16(r[i][1], h2, h3);
+        if constexpr (INTU8) {
+          u8x4_int_bf16(r[i][0], h0, h1);
+          u8x4_int_bf16((soff[i] & 2) ? 0u : r[i][1], h2, h3);
+        } else {
+          u8x4_bf16(r[i][0], h0, h1);
+          u8x4_bf16(r[i][1], h2, h3);
+        }
         bf16* b = lds + dst[i];
         st8(b, h0, h1);
         st8(b + s.CS, mid(h0, h1), mid(h1, h2));
         st8(b + 2 * s.CS, h1, h2);
         st8(b + 3 * s.CS, mid(h1, h2), mid(h2, h3));
-        if (fl[i] & 1u) {  // the quad left of the row: (halo zeros, first pixels)
+        if (soff[i] & 1) {  // the quad left of the row: (halo zeros, first pixels)
           st8(b - 4 + s.CS, 0u, mid(0u, h0));
           st8(b - 4 + 2 * s.CS, 0u, h0);
           st8(b - 4 + 3 * s.CS, mid(0u, h0), mid(h0, h1));
@@ -225,6 +252,22 @@ __device__ __forceinline__ bf16x8 read_s1(const bf16* xs, int CS, int e) {
   const bf16x4 hi = *reinterpret_cast<const bf16x4*>(a + 4);
   return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
 }
+// XL_S1 fragment read at an 8-byte aligned element offset (shifted copy
+// already chosen): two 8-byte reads kept apart (fused, they would issue as
+// one ds_read2_b64: 8 LDS cycles and 32-bank instead of 64-bank service)
+__device__ __forceinline__ bf16x8 read_s1_pair(const bf16* xs, int e) {
+  int hb = 2 * e + 8;  // byte offset of the high half
+  asm volatile("" : "+v"(hb));
+  const bf16x4 lo = *reinterpret_cast<const bf16x4*>(xs + e);
+  const bf16x4 hi = *reinterpret_cast<const bf16x4*>(reinterpret_cast<const char*>(xs) + hb);
+  return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+// max of four floats without the NaN canonicalisation fmaxf adds (v_max3 + v_max)
+__device__ __forceinline__ float max4(float a, float b, float c, float d) {
+  float m;
+  asm("v_max3_f32 %0, %1, %2, %3\n\tv_max_f32 %0, %0, %4" : "=&v"(m) : "v"(a), "v"(b), "v"(c), "v"(d));
+  return m;
+}
 // XL_S1 transpose read (4 consecutive tile elements per lane)
 __device__ __forceinline__ bf16x4 tr4_s1(const bf16* xs, int CS, int e) {
   const int c = e & 3;
@@ -233,10 +276,12 @@ __device__ __forceinline__ bf16x4 tr4_s1(const bf16* xs, int CS, int e) {
 
 // Output-pixel (row) -> tile offset of its first tap.  Pool: rows ordered by
 // 2x2 window so a 16-row tile holds four whole windows.
+// Entries rows..rows_pad-1 (tile padding) repeat row 0.
 __device__ void row_table(int* tab, int rows, bool pool, int OW, int cs, int ty0, int tx0, int LWp, int CL,
-                          int pair = 0) {
+                          int pair = 0, int rows_pad = 0) {
   const int PW = OW >> 1;
-  for (int r = threadIdx.x; r < rows; r += blockDim.x) {
+  for (int rr = threadIdx.x; rr < max(rows, rows_pad); rr += blockDim.x) {
+    const int r = rr < rows ? rr : 0;
     int oy, ox;
     if (pair == 2) {  // row = (base window (even column), position TL/TR/BL/BR)
       const int bw = r >> 2, pos = r & 3, PB = PW >> 1;
@@ -261,7 +306,7 @@ __device__ void row_table(int* tab, int rows, bool pool, int OW, int cs, int ty0
       oy = r / OW;
       ox = r - oy * OW;
     }
-    tab[r] = ((oy * cs + ty0) * LWp + ox * cs + tx0) * CL;
+    tab[rr] = ((oy * cs + ty0) * LWp + ox * cs + tx0) * CL;
   }
 }
 
@@ -307,7 +352,7 @@ __host__ __device__ inline FwdLayout fwd_layout(const ConvPipeParams& p) {
   L.ws_off = o; o += align16((ntiles * 16 * (p.kpad + 8) + 32) * 2);  // +32: look-ahead read past the last row
   L.bias_off = o; o += ntiles * 16 * 4;
   L.ktab_off = o; o += align16((p.nchunks + 2) * 4 * 4);                 // +2 chunks of look-ahead (offset 0)
-  L.ptab_off = o; o += align16(rows_img * 4);
+  L.ptab_off = o; o += align16(((rows_img + 15) & ~15) * 4);  // tile padding (pair 2)
   L.outs_off = o; o += align16(p.imgs * out_img * 2);
   L.args_off = o; o += pool ? align16(p.imgs * out_img) : 0;
   L.total = o;

@@ -43,8 +43,10 @@ __device__ __forceinline__ float swap8(float v) {
 // K loop reads only the A operand from LDS (half the LDS traffic and none of
 // the weight-row bank conflicts); two row tiles per item keep the register
 // budget at four waves per SIMD.
+// (waves_per_eu(4): two 512-thread or four 256-thread workgroups per CU need
+// <= 128 VGPRs; at 129+ the CU holds half the waves)
 template <int MODE, int EPI, int ACT, int PAIR, int NT, int WR = 0>
-__global__ void __launch_bounds__(NT) conv_pipe_fwd_kernel(ConvPipeParams p) {
+__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WR > 0 ? 1 : 4))) conv_pipe_fwd_kernel(ConvPipeParams p) {
   constexpr int MT = WR > 8 ? 2 : 4;
   constexpr bool S1 = MODE == PM_U8S1;
   constexpr bool pool = EPI == FE_POOL;
@@ -95,27 +97,30 @@ __global__ void __launch_bounds__(NT) conv_pipe_fwd_kernel(ConvPipeParams p) {
     }
     ktab[gi] = off;  // padding groups point at tap 0 (zero weights)
   }
-  row_table(ptab, rows_img, pool, p.OW, p.cs, p.ty0, p.tx0, s.LWp, S1 ? 1 : s.CL, PAIR);  // PAIR 2: window pairs
+  const int rows_pad = PAIR == 2 ? (rows_img + 15) & ~15 : rows_img;
+  row_table(ptab, rows_img, pool, p.OW, p.cs, p.ty0, p.tx0, s.LWp, S1 ? 1 : s.CL, PAIR, rows_pad);  // PAIR 2: window pairs
   if (S1) {  // bake the shifted-copy choice into the table (IMG and K offsets are multiples of 4)
-    for (int r = tid; r < rows_img; r += NT) {
+    for (int r = tid; r < rows_pad; r += NT) {
       const int b = ptab[r], c = b & 3;
       ptab[r] = c * s.CS + b - c;
     }
   }
 
-  Loader<MODE, NT> ld;
+  // S1 (the dataset input): exact-integer tile, 1/255 applied in the epilogue
+  constexpr float xsc = S1 ? 1.f / 255.f : 1.f;
+  Loader<MODE, NT, S1> ld;
   ld.init(s, p.imgs);
-  int grp = blockIdx.x;
-  if (grp < p.ngroups) ld.load(s, grp * p.imgs, p.N);
+  if (S1) ld.load_idx(s, blockIdx.x * p.imgs, p.N);
 
-  const int lane = tid & 63, wave = tid >> 6;
+  const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r16 = lane & 15, g = lane >> 4;
-  bf16x8 wreg[WR > 0 ? WR : 1];
-  int kreg[WR > 0 ? WR : 1];
-  if constexpr (WR > 0) {
+  constexpr int NW = WR > 0 ? WR : (PAIR == 2 ? 2 : 1);
+  bf16x8 wreg[NW];
+  int kreg[NW];
+  if constexpr (WR > 0 || PAIR == 2) {
     __syncthreads();  // weights and K table staged
 #pragma unroll
-    for (int q = 0; q < WR; ++q) {
+    for (int q = 0; q < NW; ++q) {  // PAIR 2: nchunks <= 2 (the ws padding covers q = 1)
       wreg[q] = load8(ws + r16 * wld + 8 * g + q * 32);
       kreg[q] = ktab[q * 4 + g];
     }
@@ -124,14 +129,84 @@ __global__ void __launch_bounds__(NT) conv_pipe_fwd_kernel(ConvPipeParams p) {
   drpi.mh = p.rows_mh;
   drpi.ml = p.rows_ml;
 
-  for (; grp < p.ngroups; grp += gridDim.x) {
+  // Iteration k loads group blockIdx.x + k*gridDim.x and computes the one
+  // before it: ONE load site, so the prefetched registers stay in place until
+  // the store after the next barrier (a second site would merge the values
+  // through register moves that wait on the loads).
+  for (int k = 0;; ++k) {
+    const int lgrp = blockIdx.x + k * (int)gridDim.x, grp = lgrp - (int)gridDim.x;
+    if (grp >= p.ngroups) break;
     const int img0 = grp * p.imgs;
     const int nimg = min(p.imgs, p.N - img0);
-    __syncthreads();  // tiles free: previous compute and copy-out done (and setup, first time)
-    if (!(p.ablate & 1)) ld.store(s, xs, nimg);
-    __syncthreads();
-    if (!(p.ablate & 1) && grp + (int)gridDim.x < p.ngroups) ld.load(s, (grp + gridDim.x) * p.imgs, p.N);
+    if (k > 0) {
+      __syncthreads();  // tiles free: previous compute and copy-out done (and setup, first time)
+      if (!(p.ablate & 1)) ld.store(s, xs, nimg);
+      __syncthreads();
+    }
+    if (!(p.ablate & 1) && lgrp < p.ngroups) ld.load(s, lgrp * p.imgs, p.N, (lgrp + (int)gridDim.x) * p.imgs);
+    if (k == 0) continue;
 
+    if constexpr (PAIR == 2) {
+      // Window pairs on the single-channel input.  Tiles never straddle an
+      // image (rows padded to 16 per image), so a tile's image, its tile
+      // index and every bound are wave-uniform scalars; the lane's row offset
+      // is one table read.  Weights are register-resident (<= 2 K chunks).
+      const int tpi = rows_pad >> 4, ntl = nimg * tpi, nbw = rows_img >> 2;
+      for (int item = wave; item < ((p.ablate & 2) ? 0 : cdiv(ntl, MT)); item += NT / 64) {
+        int img[MT], ti[MT], base[MT];
+#pragma unroll
+        for (int t = 0; t < MT; ++t) {
+          const int T = min(item * MT + t, ntl - 1);
+          img[t] = drpi.div(T);
+          ti[t] = T - img[t] * tpi;
+          base[t] = img[t] * s.IMG + ptab[ti[t] * 16 + r16];
+        }
+        bf16x8 a0[MT], a1[MT];
+        f32x4 acc[MT];
+#pragma unroll
+        for (int t = 0; t < MT; ++t) {
+          a0[t] = read_s1_pair(xs, base[t] + kreg[0]);
+          acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+        if (p.nchunks > 1) {
+#pragma unroll
+          for (int t = 0; t < MT; ++t) a1[t] = read_s1_pair(xs, base[t] + kreg[1]);
+#pragma unroll
+          for (int t = 0; t < MT; ++t) acc[t] = mma(acc[t], a0[t], wreg[0]);
+#pragma unroll
+          for (int t = 0; t < MT; ++t) acc[t] = mma(acc[t], a1[t], wreg[1]);
+        } else {
+#pragma unroll
+          for (int t = 0; t < MT; ++t) acc[t] = mma(acc[t], a0[t], wreg[0]);
+        }
+        if (p.ablate & 4) {  // keep the accumulators live, skip the epilogue
+          if (acc[0][0] == 1234.5f && acc[MT - 1][3] == -1.f) outs[0] = (bf16)0.f;
+          continue;
+        }
+        // rows 4g..4g+3 = positions (TL, TR, BL, BR) of window pair bw;
+        // column r16 = channel (r16 & 7) of its left (r16 < 8) or right
+        // window: the 2x2 max-pool and its argmax are in-lane
+        const int c = r16 & 7, sft = r16 >> 3;
+        const float bv = bias_s[r16];
+        const int olane = (2 * g + sft) * p.Cout + c;  // + img*out_img + ti*8*Cout (scalar)
+#pragma unroll
+        for (int t = 0; t < MT; ++t) {
+          if (item * MT + t < ntl && c < p.Cout && g < nbw - ti[t] * 4) {
+            const float best = max4(acc[t][0], acc[t][1], acc[t][2], acc[t][3]);
+            // first maximum wins (as the reference's strict > scan)
+            int arg = 3;
+            arg = acc[t][2] == best ? 2 : arg;
+            arg = acc[t][1] == best ? 1 : arg;
+            arg = acc[t][0] == best ? 0 : arg;
+            const bf16 yb = (bf16)fmaxf(fmaf(best, xsc, bv), 0.f);
+            const int o = img[t] * out_img + ti[t] * 8 * p.Cout + olane;
+            MCC_DCHECK(o < p.imgs * out_img);
+            outs[o] = yb;
+            args[o] = (uint8_t)((float)yb > 0.f ? arg : 4);  // 4: ReLU-inactive window
+          }
+        }
+      }
+    } else {
     const int M = nimg * rows_img;
     const int mtiles = cdiv(M, 16), mgroups = cdiv(mtiles, MT);
     const int ko_s0 = ktab[g], ko_s1 = ktab[4 + g];  // XL_S1: at most two chunks, item-invariant
@@ -226,34 +301,7 @@ __global__ void __launch_bounds__(NT) conv_pipe_fwd_kernel(ConvPipeParams p) {
         if (acc[0][0] == 1234.5f && acc[MT - 1][3] == -1.f) outs[0] = (bf16)0.f;
         continue;
       }
-      if constexpr (PAIR == 2) {
-        // window pairs: rows 4g..4g+3 = the four positions (TL, TR, BL, BR)
-        // of base window bw; column r16 = channel (r16 & 7) of window bw
-        // (r16 < 8) or of its right neighbour (r16 >= 8): the 2x2 max-pool
-        // and its argmax are in-lane (no cross-lane exchange)
-        const int c = r16 & 7, sft = r16 >> 3;
-        const float bv = bias_s[r16];
-#pragma unroll
-        for (int t = 0; t < MT; ++t) {
-          const int bw = (mg * MT + t) * 4 + g;
-          float best = acc[t][0];
-          int arg = 0;
-#pragma unroll
-          for (int i = 1; i < 4; ++i) {
-            const bool gt = acc[t][i] > best;
-            best = gt ? acc[t][i] : best;
-            arg = gt ? i : arg;
-          }
-          if (c < p.Cout && 4 * bw < M) {
-            const bf16 yb = (bf16)fmaxf(best + bv, 0.f);
-            const int o = (2 * bw + sft) * p.Cout + c;
-            MCC_DCHECK(o < p.imgs * out_img);
-            outs[o] = yb;
-            args[o] = (uint8_t)((float)yb > 0.f ? arg : 4);  // 4: ReLU-inactive window
-          }
-        }
-        continue;
-      } else if constexpr (PAIR == 1) {
+      if constexpr (PAIR == 1) {
         // column r16 = channel (r16 & 7) of the left (r16 < 8) or right pixel
         const int c = r16 & 7;
         const bool right = r16 >= 8;
@@ -281,7 +329,7 @@ __global__ void __launch_bounds__(NT) conv_pipe_fwd_kernel(ConvPipeParams p) {
             if (tr > best) { best = tr; arg = 1; }
             if (bl > best) { best = bl; arg = 2; }
             if (br > best) { best = br; arg = 3; }
-            const float y = ACT == ACT_RELU ? fmaxf(best + bias_s[c], 0.f) : best + bias_s[c];
+            const float y = ACT == ACT_RELU ? fmaxf(fmaf(best, xsc, bias_s[c]), 0.f) : fmaf(best, xsc, bias_s[c]);
             const int win = (rb >> 1) + (right ? 1 : 0);
             if (c < p.Cout && 2 * win < M) {
               const int o = win * p.Cout + c;
@@ -293,7 +341,7 @@ __global__ void __launch_bounds__(NT) conv_pipe_fwd_kernel(ConvPipeParams p) {
           } else if (c < p.Cout) {
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-              const float x = acc[t][i] + bv;
+              const float x = fmaf(acc[t][i], xsc, bv);
               const float v = ACT == ACT_RELU ? fmaxf(x, 0.f) : (ACT == ACT_TANH ? tanhf(x) : x);
               if (rb + i < M) outs[(2 * (rb + i) + (r16 >> 3)) * p.Cout + c] = (bf16)v;
             }
@@ -320,19 +368,20 @@ __global__ void __launch_bounds__(NT) conv_pipe_fwd_kernel(ConvPipeParams p) {
           }
           const int o = (rb >> 2) * p.Cout + n;
           MCC_DCHECK(o < p.imgs * out_img);
-          const bf16 yb = (bf16)fmaxf(best + bv, 0.f);
+          const bf16 yb = (bf16)fmaxf(fmaf(best, xsc, bv), 0.f);
           outs[o] = yb;
           args[o] = (uint8_t)((float)yb > 0.f ? arg : 4);  // 4: ReLU-inactive window
         } else {
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
-            const float x = acc[t][i] + bv;
+            const float x = fmaf(acc[t][i], xsc, bv);
             const float v = ACT == ACT_RELU ? fmaxf(x, 0.f) : (ACT == ACT_TANH ? tanhf(x) : x);
             if (rb + i < M) outs[(rb + i) * p.Cout + n] = (bf16)v;
           }
         }
       }
     }
+    }  // PAIR != 2
     __syncthreads();
     if (p.ablate & 4) continue;
     char* gout = static_cast<char*>(p.out) + (size_t)img0 * out_img * 2;
@@ -402,7 +451,8 @@ void conv_pipe_forward(const ConvPipeParams& pin, hipStream_t st) {
   {
     const bool pool = p.epi == FE_POOL;
     const int rows_img = (pool ? (p.OH / 2) * (p.OW / 2) * 4 : p.OH * p.OW) / (p.pair ? 2 : 1);
-    const Div d = Div::host(rows_img);
+    // PAIR 2: the kernel divides tile indices by the (16-padded) tiles per image
+    const Div d = Div::host(p.pair == 2 ? (rows_img + 15) / 16 : rows_img);
     p.rows_mh = d.mh;
     p.rows_ml = d.ml;
   }
