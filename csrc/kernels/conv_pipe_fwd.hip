@@ -28,6 +28,10 @@
 //    per workgroup, reduced by a two-level deterministic sum.
 #include "conv_pipe.h"
 
+#include <cstdio>
+#include <utility>
+#include <vector>
+
 namespace mcc {
 namespace gpu {
 
@@ -393,7 +397,106 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WR > 0 
   }
 }
 
+// register-resident weights for the LeNet-class shapes (one column tile, 7
+// or 13 K chunks): conv2 forward and conv2 data gradient
+int fwd_wreg(const ConvPipeParams& p) {
+  if (p.layout != XL_C8 || cdiv(p.Cout, 16) != 1 || pipe_knob("MCC_NO_WREG", 0)) return 0;
+  if (p.nchunks == 7 && p.in.mode == PM_PLAIN && p.epi == FE_POOL) return 7;
+  if (p.nchunks == 13 && p.in.mode == PM_UNPOOL && p.epi == FE_PLAIN) return 13;
+  return 0;
+}
+
+// Bank-conflict cycles of the K-loop A-fragment reads over one full group
+// (the kernel's own row table, K table and tile walk, fed to the LDS bank
+// model), and the number of read instructions they belong to.
+std::pair<long, long> fwd_a_conflicts(const ConvPipeParams& p) {
+  const PipeSrc& s = p.in;
+  const bool S1 = p.layout == XL_S1, pool = p.epi == FE_POOL;
+  const int rows_img = (pool ? (p.OH / 2) * (p.OW / 2) * 4 : p.OH * p.OW) / (p.pair ? 2 : 1);
+  const int rows_pad = p.pair == 2 ? (rows_img + 15) & ~15 : rows_img;
+  std::vector<int> ptab(rows_pad);
+  for (int r = 0; r < rows_pad; ++r) {
+    const int b = row_offset(r < rows_img ? r : 0, pool, p.OW, p.cs, p.ty0, p.tx0, s.LWp, S1 ? 1 : s.CL, p.pair);
+    ptab[r] = S1 ? (b & 3) * s.CS + b - (b & 3) : b;
+  }
+  const int KK = p.KS * p.KS;
+  std::vector<int> ktab(p.nchunks * 4);
+  for (int gi = 0; gi < p.nchunks * 4; ++gi) {
+    int off = 0;
+    if (S1) {
+      if (gi < p.KS) off = gi * s.LWp;
+    } else {
+      const int CG = s.CL >> 3, kp = gi / CG, cg = gi - kp * CG;
+      if (kp < KK) off = ((kp / p.KS) * s.LWp + kp % p.KS) * s.CL + cg * 8;
+    }
+    ktab[gi] = off;
+  }
+  const int M = p.imgs * rows_img, tiles = p.pair == 2 ? p.imgs * (rows_pad / 16) : (M + 15) / 16;
+  long extra = 0, instrs = 0;
+  int a[64];
+  for (int T = 0; T < tiles; ++T) {
+    int base[16];
+    for (int r16 = 0; r16 < 16; ++r16) {
+      if (p.pair == 2) {
+        const int tpi = rows_pad / 16, img = T / tpi;
+        base[r16] = img * s.IMG + ptab[(T - img * tpi) * 16 + r16];
+      } else {
+        const int r = std::min(T * 16 + r16, M - 1), img = r / rows_img;
+        base[r16] = img * s.IMG + ptab[r - img * rows_img];
+      }
+    }
+    for (int q = 0; q < p.nchunks; ++q) {
+      for (int half = 0; half < (S1 ? 2 : 1); ++half) {  // S1: two 8-byte reads
+        for (int l = 0; l < 64; ++l) a[l] = (base[l & 15] + ktab[q * 4 + (l >> 4)]) / 2 + 2 * half;
+        extra += lds_conflicts(a, S1 ? LDS_B64 : LDS_B128);
+        ++instrs;
+      }
+    }
+  }
+  return {extra, instrs};
+}
+
 }  // namespace
+
+// Swizzle by padding: pick the tile row stride (and for XL_S1 the stride
+// between the shifted copies) with the fewest modelled bank conflicts per
+// A-fragment read, keeping the workgroups per CU (LDS budget) -- if need be
+// with up to a third fewer images per group.
+static void fwd_pick_strides(ConvPipeParams& p) {
+  PipeSrc& s = p.in;
+  const bool s1 = p.layout == XL_S1;
+  const int LW0 = s.LWp, CL = s1 ? 1 : s.CL, imgs0 = p.imgs;
+  // the register-resident-weight kernels (fwd_wreg) hold 3 workgroups per CU
+  // on VGPRs whatever the LDS allows
+  const int cap = fwd_wreg(p) ? std::min(3, fwd_wgs_cap()) : fwd_wgs_cap();
+  const int wgs = wgs_per_cu((size_t)fwd_layout(p).total, cap);
+  const auto e0 = fwd_a_conflicts(p);
+  double best = (double)e0.first / std::max(1L, e0.second);
+  ConvPipeParams bp = p;
+  const int step = s1 ? 4 : 1;
+  for (int im = imgs0; im >= std::max(1, (2 * imgs0 + 2) / 3); --im) {
+    for (int j = 0; j < 12; ++j) {
+      for (int m = 0; m < (s1 ? 8 : 1); ++m) {
+        ConvPipeParams q = p;
+        q.imgs = im;
+        q.in.LWp = LW0 + j * step;
+        q.in.IMG = p.LH * q.in.LWp * CL;
+        if (s1) q.in.CS = r8h(q.imgs * q.in.IMG + 8) + 8 * m;
+        const FwdLayout L = fwd_layout(q);
+        if ((size_t)L.total > kLdsPerCU || wgs_per_cu((size_t)L.total, cap) < wgs) continue;
+        const auto e = fwd_a_conflicts(q);
+        const double c = (double)e.first / std::max(1L, e.second);
+        // fewer images per group (more barriers) only for a clear gain
+        if (c < best - 1e-9 && (im == imgs0 || c < 0.5 * e0.first / std::max(1L, e0.second))) { best = c; bp = q; }
+      }
+    }
+  }
+  if (pipe_knob("MCC_BANK_LOG", 0))
+    fprintf(stderr, "conv_pipe fwd Cin=%d Cout=%d OH=%d mode=%d: LWp %d->%d imgs %d->%d CS %d, A-read conflict cycles/read %.2f -> %.2f\n",
+            p.Cin, p.Cout, p.OH, s.mode, LW0, bp.in.LWp, imgs0, bp.imgs, bp.in.CS,
+            (double)e0.first / std::max(1L, e0.second), best);
+  p = bp;
+}
 
 bool conv_pipe_plan(ConvPipeParams& p) {
   PipeSrc& s = p.in;
@@ -438,8 +541,9 @@ bool conv_pipe_plan(ConvPipeParams& p) {
     if ((size_t)fwd_layout(p).total <= fwd_lds_target() || imgs == 1) break;
   }
   if (imgs < 1) return false;
+  if ((size_t)fwd_layout(p).total > kLdsPerCU) return false;
+  if (!pipe_knob("MCC_NO_SWIZZLE", 0)) fwd_pick_strides(p);
   const FwdLayout L = fwd_layout(p);
-  if ((size_t)L.total > kLdsPerCU) return false;
   p.lds = (size_t)L.total;
   p.ngroups = cdiv(p.N, p.imgs);
   p.grid = std::min(p.ngroups, kCUs * wgs_per_cu(p.lds, fwd_wgs_cap()));
@@ -464,18 +568,10 @@ void conv_pipe_forward(const ConvPipeParams& pin, hipStream_t st) {
   const int nt = p.pair ? 512 : 256;
   const dim3 grid((unsigned)p.grid), block((unsigned)nt);
   auto go = [&](auto kern) { hipLaunchKernelGGL(kern, grid, block, p.lds, st, p); };
-  // register-resident weights for the LeNet-class shapes (one column tile,
-  // 7 or 13 K chunks): conv2 forward and conv2 data gradient
-  const int ntiles = cdiv(p.Cout, 16);
-  if (p.layout == XL_C8 && ntiles == 1 && !pipe_knob("MCC_NO_WREG", 0)) {
-    if (p.nchunks == 7 && p.in.mode == PM_PLAIN && p.epi == FE_POOL) {
-      go(conv_pipe_fwd_kernel<PM_PLAIN, FE_POOL, ACT_RELU, 0, 256, 7>);
-      return;
-    }
-    if (p.nchunks == 13 && p.in.mode == PM_UNPOOL && p.epi == FE_PLAIN) {
-      go(conv_pipe_fwd_kernel<PM_UNPOOL, FE_PLAIN, ACT_NONE, 0, 256, 13>);
-      return;
-    }
+  switch (fwd_wreg(p)) {
+    case 7: go(conv_pipe_fwd_kernel<PM_PLAIN, FE_POOL, ACT_RELU, 0, 256, 7>); return;
+    case 13: go(conv_pipe_fwd_kernel<PM_UNPOOL, FE_PLAIN, ACT_NONE, 0, 256, 13>); return;
+    default: break;
   }
 #define MCC_PIPE_EPI(MODE)                                                                      \
   if (p.epi == FE_POOL) go(conv_pipe_fwd_kernel<MODE, FE_POOL, ACT_RELU, 0, 256>);                      \
