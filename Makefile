@@ -117,5 +117,29 @@ checked:
 	  build/checked/mpi_cuda_cnn_amd/_C$(EXT)
 	cd mpi_cuda_cnn_amd && find . -name '*.py' -exec install -D -m 644 {} ../build/checked/mpi_cuda_cnn_amd/{} \;
 
+# Run targets (the reference Makefile's test_serial / test_mpi / test_cuda,
+# Makefile:38-51), on generated data unless DATA names the four IDX files:
+#   make run_serial                 CPU trainer (cnn)
+#   make run_mpi NP=8               CPU data-parallel over MPI (cnnmpi, if built)
+#   make run_hip                    one GPU (cnn_hip, hipGraph step)
+#   make run_dist NP=8              one process per GPU over RCCL (cnn_dist)
+#   make run_bench NP=8             bench.py under torch.distributed.run
+NP    ?= 2
+SYN   ?= 20000
+DATA  ?= --synthetic $(SYN)
+RUNFLAGS ?=
+.PHONY: run_serial run_mpi run_hip run_dist run_bench
+run_serial: build/bin/cnn
+	build/bin/cnn $(DATA) $(RUNFLAGS)
+run_mpi: build/bin/cnnmpi
+	$(dir $(MPICXX))mpiexec -n $(NP) build/bin/cnnmpi $(DATA) $(RUNFLAGS)
+run_hip: build/bin/cnn_hip
+	build/bin/cnn_hip $(DATA) $(RUNFLAGS)
+run_dist: build/bin/cnn_dist
+	$(PYTHON) -m mpi_cuda_cnn_amd.launch -n $(NP) build/bin/cnn_dist $(DATA) $(RUNFLAGS)
+run_bench: module
+	$(PYTHON) -m torch.distributed.run --nnodes=1 --nproc-per-node $(NP) --master-addr 127.0.0.1 \
+	  --master-port 29531 bench.py --gpus $(NP) $(RUNFLAGS)
+
 clean:
 	rm -rf build $(MODULE)

@@ -256,7 +256,8 @@ int run_gpu_training(const CliArgs& a, Comm& comm, const char* program) {
     if (!a.quiet && (mark < seen || it == steps - 1)) {
       // [mse sum of this rank, samples of this rank]; summed over ranks
       float* d = d_red.as<float>();
-      HIPCHK(hipMemcpyAsync(d, net.stats() + 1, 4, hipMemcpyDeviceToDevice, S));
+      gpu::stats_to_f32(net.stats(), d + 2, S);  // d[3] = this rank's mse sum
+      HIPCHK(hipMemcpyAsync(d, d + 3, 4, hipMemcpyDeviceToDevice, S));
       h_red[1] = (float)((seen - last_log) / world);
       HIPCHK(hipMemcpyAsync(d + 1, h_red + 1, 4, hipMemcpyHostToDevice, S));
       comm.allreduce_sum_f32(d, 2, S);
@@ -309,7 +310,8 @@ int run_gpu_training(const CliArgs& a, Comm& comm, const char* program) {
         for (int64_t j = i; j < i + nb; ++j)
           if (j % 1000 == 0) std::fprintf(stderr, "i=%lld\n", (long long)j);
       }
-      HIPCHK(hipMemcpyAsync(h_red, net.stats(), 16, hipMemcpyDeviceToHost, S));
+      gpu::stats_to_f32(net.stats(), d_red.as<float>(), S);
+      HIPCHK(hipMemcpyAsync(h_red, d_red.as<float>(), 12, hipMemcpyDeviceToHost, S));
       HIPCHK(hipStreamSynchronize(S));
       test_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t1).count();
       ncorrect = (int64_t)std::llround(h_red[2]);

@@ -121,6 +121,7 @@ py::capsule dlpack_wrap(uintptr_t p, int64_t numel, const std::string& dtype, in
   else if (dtype == "bfloat16") h->t.dl_tensor.dtype = DLDataType{4, 16, 1};
   else if (dtype == "uint8") h->t.dl_tensor.dtype = DLDataType{1, 8, 1};
   else if (dtype == "int32") h->t.dl_tensor.dtype = DLDataType{0, 32, 1};
+  else if (dtype == "int64") h->t.dl_tensor.dtype = DLDataType{0, 64, 1};
   else { delete h; throw Error("dlpack_wrap: unsupported dtype " + dtype); }
   h->t.dl_tensor.shape = h->shape;
   h->t.dl_tensor.strides = h->strides;
@@ -264,11 +265,13 @@ PYBIND11_MODULE(_C, m) {
            })
       .def("get_stats",
            [](const GpuNet& n) {
-             float h[4];
+             unsigned long long h[3];
              if (hipDeviceSynchronize() != hipSuccess) throw Error("hipDeviceSynchronize failed");
-             if (hipMemcpy(h, n.stats(), 16, hipMemcpyDeviceToHost) != hipSuccess) throw Error("hipMemcpy failed");
+             if (hipMemcpy(h, n.stats(), 24, hipMemcpyDeviceToHost) != hipSuccess) throw Error("hipMemcpy failed");
              py::dict d;
-             d["loss_sum"] = h[0]; d["mse_sum"] = h[1]; d["correct"] = h[2];
+             d["loss_sum"] = (double)h[0] / gpu::kStatScale;
+             d["mse_sum"] = (double)h[1] / gpu::kStatScale;
+             d["correct"] = (double)h[2];
              return d;
            })
       .def("forward",
@@ -386,7 +389,7 @@ PYBIND11_MODULE(_C, m) {
           p.M = M; p.N = N; p.logits = ptr<const float>(logits); p.ldl = ldl;
           p.labels = ptr<const uint8_t>(labels); p.labels_idx = ptr<const int32_t>(idx);
           p.dlogits = ptr<void>(dlogits); p.ldd = ldd; p.scale = scale;
-          p.stats = ptr<float>(stats); p.probs = ptr<float>(probs); p.pred = ptr<int32_t>(pred);
+          p.stats = ptr<unsigned long long>(stats); p.probs = ptr<float>(probs); p.pred = ptr<int32_t>(pred);
           gpu::softmax_xent(parse_dtype(dt), p, stream_of(s));
         },
         py::arg("dtype"), py::arg("M"), py::arg("N"), py::arg("logits"), py::arg("ldl"), py::arg("labels"),

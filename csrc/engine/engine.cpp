@@ -500,7 +500,7 @@ void GpuNet::build() {
     arena_used_ = 0;
     params_ = static_cast<float*>(arena_alloc(4 * (size_t)spec_.nparams));
     grads_ = static_cast<float*>(arena_alloc(4 * (size_t)spec_.nparams));
-    stats_ = static_cast<float*>(arena_alloc(64));
+    stats_ = static_cast<unsigned long long*>(arena_alloc(64));
     logits_ld_ = r8(spec_.num_classes());
     logits_ = static_cast<float*>(arena_alloc(4 * (size_t)Bm * logits_ld_));
     packed_ = arena_alloc(es * (size_t)packed_count_);
@@ -627,7 +627,7 @@ void GpuNet::pack(hipStream_t s) {
   }
 }
 
-void GpuNet::zero_stats(hipStream_t s) { HIP_OK(hipMemsetAsync(stats_, 0, 16, s)); }
+void GpuNet::zero_stats(hipStream_t s) { HIP_OK(hipMemsetAsync(stats_, 0, 32, s)); }
 
 void GpuNet::forward(const uint8_t* images, const int32_t* idx, int B, hipStream_t s) {
   MCC_CHECK(B > 0 && B <= max_batch_, "forward: batch exceeds max_batch");

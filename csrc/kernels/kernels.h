@@ -288,6 +288,12 @@ struct DwReduceParams {
   float beta = 0.f;
 };
 
+// Training statistics accumulate as fixed point (loss and mse per sample
+// are >= 0): value * kStatScale rounded, added with 64-bit integer atomics.
+constexpr double kStatScale = 4294967296.0;  // 2^32
+// stats[0..2] -> out[0..2] as floats (device side, for the drivers' logs)
+void stats_to_f32(const unsigned long long* stats, float* out, hipStream_t s);
+
 struct XentParams {
   int M = 0, N = 0;
   const float* logits = nullptr; int ldl = 0;
@@ -295,7 +301,9 @@ struct XentParams {
   const uint8_t* labels = nullptr;      // dataset labels (gathered by idx)
   void* dlogits = nullptr; int ldd = 0; // T
   float scale = 1.f;                    // dlogits = (p - y) * scale
-  float* stats = nullptr;               // [0]=loss sum [1]=mse sum [2]=correct
+  // [0]=loss sum [1]=mse sum (fixed point, kStatScale units) [2]=correct:
+  // integer atomics, so the sums are deterministic and the count exact
+  unsigned long long* stats = nullptr;
   float* probs = nullptr;               // optional fp32 probs [M][N] (eval)
   int32_t* pred = nullptr;              // optional argmax per sample
 };

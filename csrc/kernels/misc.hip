@@ -17,6 +17,19 @@ namespace gpu {
 
 namespace {
 
+// One workgroup's partial statistic into the fixed-point accumulator (the
+// workgroup sum is formed in a fixed order, so the total is deterministic).
+__device__ __forceinline__ void stat_add(unsigned long long* stats, int i, float t) {
+  const unsigned long long v = i == 2 ? (unsigned long long)(t + 0.5f)
+                                      : (unsigned long long)__double2ll_rn((double)t * kStatScale);
+  atomicAdd(stats + i, v);
+}
+
+__global__ void stats_to_f32_kernel(const unsigned long long* s, float* out) {
+  if (threadIdx.x < 3) out[threadIdx.x] = threadIdx.x == 2 ? (float)s[2] : (float)((double)s[threadIdx.x] / kStatScale);
+}
+
+
 // Softmax-cross-entropy forward + backward, one thread per sample.  For
 // N <= 16 classes (ldl % 4 == 0) the row is held in registers after 16-byte
 // loads; the three statistics are reduced per workgroup in LDS and leave as
@@ -85,7 +98,7 @@ __global__ void __launch_bounds__(256) softmax_xent_kernel(XentParams p) {
   __syncthreads();
   if (threadIdx.x < 3 && p.stats) {
     const float t = (red[threadIdx.x][0] + red[threadIdx.x][1]) + (red[threadIdx.x][2] + red[threadIdx.x][3]);
-    atomicAdd(p.stats + threadIdx.x, t);
+    stat_add(p.stats, threadIdx.x, t);
   }
 }
 
@@ -251,7 +264,7 @@ __global__ void __launch_bounds__(kHeadThreads) xent_head_kernel(XentHeadParams 
     float t = 0.f;
 #pragma unroll
     for (int w = 0; w < kHeadThreads / 64; ++w) t += red[tid][w];
-    atomicAdd(p.stats + tid, t);
+    stat_add(p.stats, tid, t);
   }
 }
 
@@ -313,7 +326,7 @@ __global__ void __launch_bounds__(256) softmax_xent_wide_kernel(XentParams p) {
   __syncthreads();
   if (threadIdx.x < 3 && p.stats) {
     const float t = (red[threadIdx.x][0] + red[threadIdx.x][1]) + (red[threadIdx.x][2] + red[threadIdx.x][3]);
-    atomicAdd(p.stats + threadIdx.x, t);
+    stat_add(p.stats, threadIdx.x, t);
   }
 }
 
@@ -549,6 +562,10 @@ void to_f32(DType t, float* dst, const void* src, int64_t n, hipStream_t s) {
   else
     hipLaunchKernelGGL(to_f32_kernel<float>, dim3(grid_for(n)), dim3(256), 0, s, dst, static_cast<const float*>(src),
                        n);
+}
+
+void stats_to_f32(const unsigned long long* stats, float* out, hipStream_t s) {
+  hipLaunchKernelGGL(stats_to_f32_kernel, dim3(1), dim3(64), 0, s, stats, out);
 }
 
 }  // namespace gpu

@@ -13,10 +13,45 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 
+class _RoundBF16(torch.autograd.Function):
+    """Round to bf16 in the forward AND the backward (a stored activation and
+    the gradient that flows back into it are both bf16 in the engine)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        return x.to(torch.bfloat16).to(x.dtype)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g.to(torch.bfloat16).to(g.dtype)
+
+
+class _RoundBF16Weight(torch.autograd.Function):
+    """bf16 compute copy of a parameter: rounded forward, gradient passed to
+    the fp32/fp64 master unchanged."""
+
+    @staticmethod
+    def forward(ctx, w):
+        return w.to(torch.bfloat16).to(w.dtype)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g
+
+
 class TorchReference(nn.Module):
-    def __init__(self, spec, dtype=torch.float32):
+    """``mimic_bf16``: the oracle of the bf16 engine's rounding points --
+    bf16 weight copies, every stored hidden activation (a conv fused with its
+    max-pool stores only the pooled value) and the gradient flowing back into
+    it rounded to bf16, fp64 everywhere else (accumulation, logits,
+    loss).  Fed the same rounded operands, the engine's per-channel errors
+    are then only its fp32 accumulation order, so tests can bound them
+    tightly per output channel."""
+
+    def __init__(self, spec, dtype=torch.float32, mimic_bf16=False):
         super().__init__()
         self.spec = spec
+        self.mimic_bf16 = mimic_bf16
         self.layer_info = spec.layers()
         mods = []
         for L in self.layer_info[1:]:
@@ -66,16 +101,24 @@ class TorchReference(nn.Module):
         for i, (L, m) in enumerate(zip(self.layer_info[1:], self.mods)):
             if L["kind"] == "fc" and x.dim() > 2:
                 x = x.reshape(x.shape[0], -1)
-            x = m(x)
+            if self.mimic_bf16 and L["kind"] in ("conv", "fc"):
+                w, b = _RoundBF16Weight.apply(m.weight), m.bias
+                x = (F.conv2d(x, w, b, m.stride, m.padding) if L["kind"] == "conv" else F.linear(x, w, b))
+            else:
+                x = m(x)
             if i == n - 1:
                 break
             act = L["act"]
-            if L["kind"] == "maxpool":
-                continue
-            if act == "relu":
-                x = F.relu(x)
-            elif act == "tanh":
-                x = torch.tanh(x)
+            if L["kind"] != "maxpool":
+                if act == "relu":
+                    x = F.relu(x)
+                elif act == "tanh":
+                    x = torch.tanh(x)
+            # a conv fused with the following max-pool stores only the pooled
+            # value (the max is taken on the unrounded sums)
+            nxt = self.layer_info[i + 2] if i + 2 < len(self.layer_info) else None
+            if self.mimic_bf16 and not (nxt is not None and nxt["kind"] == "maxpool"):
+                x = _RoundBF16.apply(x)
         return x
 
 

@@ -32,6 +32,9 @@ _ACT = {"none": _K.ACT_NONE, "relu": _K.ACT_RELU, "tanh": _K.ACT_TANH}
 _DT = {torch.bfloat16: "bf16", torch.float32: "fp32"}
 
 
+
+STAT_SCALE = float(2**32)  # loss / mse statistics: u64 fixed point (kernels.h kStatScale)
+
 def _check(*ts):
     for t in ts:
         if t is None:
@@ -133,10 +136,11 @@ def softmax_xent(logits: torch.Tensor, labels: torch.Tensor, scale: float = 1.0,
     lab = labels.to(torch.uint8).contiguous()
     ldd = _ld8(N)
     d = torch.empty(M, ldd, dtype=grad_dtype, device=logits.device)
-    stats = torch.zeros(4, dtype=torch.float32, device=logits.device)
+    stats = torch.zeros(4, dtype=torch.int64, device=logits.device)  # fixed point, see kStatScale
     _K.softmax_xent(_DT[grad_dtype], M, N, logits.data_ptr(), N, lab.data_ptr(), dlogits=d.data_ptr(), ldd=ldd,
                     scale=scale, stats=stats.data_ptr(), stream=_stream())
-    return d[:, :N], stats[0], stats[1], stats[2]
+    f = stats.to(torch.float64)
+    return d[:, :N], f[0] / STAT_SCALE, f[1] / STAT_SCALE, f[2]
 
 
 def sgd_(param: torch.Tensor, grad: torch.Tensor, mom: torch.Tensor | None = None, lr: float = 0.1,

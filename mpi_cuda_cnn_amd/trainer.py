@@ -49,7 +49,7 @@ class GpuTrainer:
         self.net.set_params(np.asarray(params, dtype=np.float32))
         self.params = _alias(self.net.params_ptr, n, "float32", self.device)
         self.grads = _alias(self.net.grads_ptr, n, "float32", self.device)
-        self.stats = _alias(self.net.stats_ptr, 4, "float32", self.device)
+        self.stats = _alias(self.net.stats_ptr, 4, "int64", self.device)  # u64 fixed point (get_stats decodes)
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         if dist.is_initialized():  # identical replicas (fixes D6: srand(rank), no broadcast)

@@ -114,7 +114,7 @@ def test_softmax_xent_kernel(cuda):
     logits = torch.randn(M, 16, device=cuda, generator=g) * 3
     labels = torch.randint(0, N, (M,), device=cuda, generator=g).to(torch.uint8)
     dl = torch.zeros(M, 16, device=cuda)
-    stats = torch.zeros(4, device=cuda)
+    stats = torch.zeros(4, dtype=torch.int64, device=cuda)  # u64 fixed point
     pred = torch.zeros(M, dtype=torch.int32, device=cuda)
     K_.softmax_xent("fp32", M, N, logits.data_ptr(), 16, labels.data_ptr(), dlogits=dl.data_ptr(), ldd=16,
                     scale=0.5, stats=stats.data_ptr(), pred=pred.data_ptr(), stream=_s())
@@ -124,8 +124,9 @@ def test_softmax_xent_kernel(cuda):
     y = torch.nn.functional.one_hot(labels.long(), N).float()
     torch.testing.assert_close(dl[:, :N], (p - y) * 0.5, atol=1e-5, rtol=1e-4)
     ce = torch.nn.functional.cross_entropy(lg, labels.long(), reduction="sum")
-    assert abs(stats[0].item() - ce.item()) < 1e-3 * ce.item()
-    assert abs(stats[1].item() - ((p - y) ** 2).mean(1).sum().item()) < 1e-3
+    st = stats.double().cpu() / torch.tensor([2.0**32, 2.0**32, 1.0, 1.0], dtype=torch.float64)
+    assert abs(st[0].item() - ce.item()) < 1e-3 * ce.item()
+    assert abs(st[1].item() - ((p - y) ** 2).mean(1).sum().item()) < 1e-3
     assert int(stats[2].item()) == int((lg.argmax(1) == labels.long()).sum().item())
     assert torch.equal(pred.long(), lg.argmax(1))
 
