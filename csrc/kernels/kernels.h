@@ -431,6 +431,7 @@ struct PackStage {
   int64_t w_off = 0, nw = 0;
   int inC = 1, KS = 1, nmaps = 0;
   uint64_t m_ckk = 0, m_kk = 0, m_ks = 0;  // division magic (set by sgd_pack)
+  int tile0 = -1;  // set by sgd_pack: first tile of a tiled (transposing) stage, -1 elementwise
   PackMap map[3];
 };
 constexpr int kMaxPackStages = 14;
@@ -443,6 +444,7 @@ struct SgdPackParams {
   bool update = true;  // false: refresh the packed copies only
   void* packed = nullptr;
   int nstages = 0;     // stages sorted by w_off
+  int ntiles = 0;      // set by sgd_pack: workgroups of the tiled stages (the rest run elementwise)
   PackStage st[kMaxPackStages];
 };
 void sgd_pack(DType t, const SgdPackParams& p, hipStream_t s);

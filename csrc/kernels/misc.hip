@@ -368,27 +368,88 @@ __device__ __forceinline__ uint32_t fdiv(uint32_t n, uint64_t m) {
   return m ? (uint32_t)__umul64hi((uint64_t)n, m) : n;
 }
 
+// Fused SGD (+ momentum, weight decay) and packed-copy refresh: one pass over
+// the fp32 master parameters writes the updated master, the momentum and
+// every packed compute copy (analytic per-stage maps, no index table).
+//
+// Conv stages of >= kPackTileMin weights run as (32 n x 32 c x KK) tiles:
+// the master reads/writes are contiguous (c, tap) runs of each n, the tile is
+// kept in LDS, and each copy is written with its unit-stride index (c for
+// the forward layouts, n for the data-gradient ones) across the lanes -- a
+// coalesced transpose instead of per-element scatters.  Everything else
+// (FC copies are row-major like the master, biases, tiny convs) runs
+// elementwise in the remaining workgroups.
+constexpr int kPackTN = 32, kPackTC = 32, kPackTCp = kPackTC + 2;
+constexpr int64_t kPackTileMin = 65536;
+constexpr int kPackMaxKK = 9;  // 3x3 and smaller (LDS: 9 x 32 x 34 elements)
+
+template <typename T, bool UPDATE>
+__device__ __forceinline__ float sgd_one(const SgdPackParams& p, int64_t i) {
+  float w = p.params[i];
+  if (UPDATE) {
+    float gi = p.grads[i];
+    if (p.wd != 0.f) gi += p.wd * w;
+    if (p.mom) {
+      const float v = p.mu * p.mom[i] + gi;
+      p.mom[i] = v;
+      gi = v;
+    }
+    w = w - p.lr * gi;
+    p.params[i] = w;
+  }
+  return w;
+}
+
 template <typename T, bool UPDATE>
 __global__ void __launch_bounds__(256) sgd_pack_kernel(SgdPackParams p) {
   T* __restrict__ dst = static_cast<T*>(p.packed);
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  int s = 0;  // monotone per thread: i only grows
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < p.n; i += stride) {
-    float w = p.params[i];
-    if (UPDATE) {
-      float gi = p.grads[i];
-      if (p.wd != 0.f) gi += p.wd * w;
-      if (p.mom) {
-        const float v = p.mu * p.mom[i] + gi;
-        p.mom[i] = v;
-        gi = v;
-      }
-      w = w - p.lr * gi;
-      p.params[i] = w;
+  if ((int)blockIdx.x < p.ntiles) {
+    __shared__ T tile[kPackMaxKK * kPackTN * kPackTCp];
+    // the tiled stages' tile ranges are contiguous and increasing
+    int s = 0;
+    for (; s < p.nstages; ++s) {
+      const PackStage& q = p.st[s];
+      if (q.tile0 < 0) continue;
+      const int Nq = (int)(q.nw / ((int64_t)q.inC * q.KS * q.KS));
+      if ((int)blockIdx.x < q.tile0 + cdiv(Nq, kPackTN) * cdiv(q.inC, kPackTC)) break;
     }
-    while (s < p.nstages && i >= p.st[s].w_off + p.st[s].nw) ++s;
-    if (s >= p.nstages || i < p.st[s].w_off) continue;  // a bias (no packed copy)
     const PackStage& st = p.st[s];
+    const int KK = st.KS * st.KS, C = st.inC;
+    const int N = (int)(st.nw / ((int64_t)C * KK));
+    const int tcs = (C + kPackTC - 1) / kPackTC;
+    const int t = (int)blockIdx.x - st.tile0, n0 = (t / tcs) * kPackTN, c0 = (t % tcs) * kPackTC;
+    const int nn = min(kPackTN, N - n0), cc = min(kPackTC, C - c0);
+    // phase 1: master update, (c, tap) runs of each n are contiguous
+    const int run = cc * KK;
+    for (int e = threadIdx.x; e < nn * run; e += blockDim.x) {
+      const int n = e / run, r = e - n * run;
+      const int c = r / KK, k = r - c * KK;
+      const int64_t i = st.w_off + ((int64_t)(n0 + n) * C + c0) * KK + r;
+      tile[(k * kPackTN + n) * kPackTCp + c] = from_f<T>(sgd_one<T, UPDATE>(p, i));
+    }
+    __syncthreads();
+    // phase 2: each copy along its unit-stride index
+    for (int m = 0; m < st.nmaps; ++m) {
+      const PackMap& mp = st.map[m];
+      const bool c_fast = mp.sc == 1;
+      const int inner = c_fast ? cc : nn, outer = c_fast ? nn : cc;
+      for (int e = threadIdx.x; e < KK * outer * inner; e += blockDim.x) {
+        const int k = e / (outer * inner), r = e - k * (outer * inner);
+        const int o = r / inner, q = r - o * inner;
+        const int n = c_fast ? o : q, c = c_fast ? q : o;
+        const int kh = k / st.KS, kw = k - kh * st.KS;
+        const int h = mp.flip ? st.KS - 1 - kh : kh, x = mp.flip ? st.KS - 1 - kw : kw;
+        dst[mp.base + (int64_t)(n0 + n) * mp.sn + (int64_t)(c0 + c) * mp.sc + (int64_t)h * mp.skh +
+            (int64_t)x * mp.skw] = tile[(k * kPackTN + n) * kPackTCp + c];
+      }
+    }
+    return;
+  }
+  // elementwise part: four consecutive parameters per thread (16-byte master
+  // and momentum accesses); an FC row segment's copy leaves as one 8/16-byte
+  // store, other packed elements one by one.  A group that straddles a
+  // region boundary (bias | weights | tiled weights) goes element by element.
+  auto pack_one = [&](const PackStage& st, int64_t i, float w) {
     const uint32_t j = (uint32_t)(i - st.w_off);
     const uint32_t ckk = (uint32_t)(st.inC * st.KS * st.KS), kk = (uint32_t)(st.KS * st.KS);
     const uint32_t n = fdiv(j, st.m_ckk), r = j - n * ckk;
@@ -400,6 +461,69 @@ __global__ void __launch_bounds__(256) sgd_pack_kernel(SgdPackParams p) {
       const int h = mp.flip ? st.KS - 1 - (int)kh : (int)kh, x = mp.flip ? st.KS - 1 - (int)kw : (int)kw;
       dst[mp.base + (int64_t)n * mp.sn + (int64_t)c * mp.sc + (int64_t)h * mp.skh + (int64_t)x * mp.skw] = v;
     }
+  };
+  // region of parameter i: 2*stage (the gap before it: biases) or 2*stage + 1 (its weights)
+  auto region = [&](int64_t i, int& ss) {
+    while (ss < p.nstages && i >= p.st[ss].w_off + p.st[ss].nw) ++ss;
+    return 2 * ss + ((ss < p.nstages && i >= p.st[ss].w_off) ? 1 : 0);
+  };
+  const int64_t stride = (int64_t)(gridDim.x - p.ntiles) * blockDim.x * 4;
+  int s = 0;  // monotone per thread: i only grows
+  for (int64_t i0 = ((int64_t)(blockIdx.x - p.ntiles) * blockDim.x + threadIdx.x) * 4; i0 < p.n; i0 += stride) {
+    int s3 = s;
+    const int r0 = region(i0, s), r3 = region(min(i0 + 3, p.n - 1), s3);
+    if (r0 == r3 && (r0 & 1) && p.st[s].tile0 >= 0) continue;  // done by the tiles
+    if (r0 != r3 || i0 + 3 >= p.n) {
+      for (int e = 0; e < 4 && i0 + e < p.n; ++e) {
+        int se = s;
+        const int re = region(i0 + e, se);
+        if ((re & 1) && p.st[se].tile0 >= 0) continue;
+        const float w = sgd_one<T, UPDATE>(p, i0 + e);
+        if (re & 1) pack_one(p.st[se], i0 + e, w);
+      }
+      continue;
+    }
+    float w[4];
+    {
+      const float4 w4 = *reinterpret_cast<const float4*>(p.params + i0);
+      w[0] = w4.x; w[1] = w4.y; w[2] = w4.z; w[3] = w4.w;
+    }
+    if (UPDATE) {
+      const float4 g4 = *reinterpret_cast<const float4*>(p.grads + i0);
+      float g[4] = {g4.x, g4.y, g4.z, g4.w};
+      if (p.wd != 0.f) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) g[e] += p.wd * w[e];
+      }
+      if (p.mom) {
+        const float4 v4 = *reinterpret_cast<const float4*>(p.mom + i0);
+        const float v[4] = {p.mu * v4.x + g[0], p.mu * v4.y + g[1], p.mu * v4.z + g[2], p.mu * v4.w + g[3]};
+        *reinterpret_cast<float4*>(p.mom + i0) = make_float4(v[0], v[1], v[2], v[3]);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) g[e] = v[e];
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) w[e] -= p.lr * g[e];
+      *reinterpret_cast<float4*>(p.params + i0) = make_float4(w[0], w[1], w[2], w[3]);
+    }
+    if (!(r0 & 1)) continue;  // biases: no packed copy
+    const PackStage& st = p.st[s];
+    if (st.KS == 1 && st.nmaps == 1 && st.map[0].sc == 1) {
+      const int64_t j0 = i0 - st.w_off;
+      const uint32_t n = fdiv((uint32_t)j0, st.m_ckk), c = (uint32_t)j0 - n * (uint32_t)st.inC;
+      const int64_t d = st.map[0].base + (int64_t)n * st.map[0].sn + c;
+      if (c + 3 < (uint32_t)st.inC && (d & 3) == 0) {  // one aligned row segment
+        if constexpr (sizeof(T) == 2) {
+          const bf16x4 v = {(bf16)w[0], (bf16)w[1], (bf16)w[2], (bf16)w[3]};
+          *reinterpret_cast<bf16x4*>(dst + d) = v;
+        } else {
+          *reinterpret_cast<float4*>(dst + d) = make_float4(w[0], w[1], w[2], w[3]);
+        }
+        continue;
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) pack_one(st, i0 + e, w[e]);
   }
 }
 
@@ -511,14 +635,29 @@ static uint64_t div_magic(uint64_t d) {
 void sgd_pack(DType t, const SgdPackParams& pin, hipStream_t s) {
   if (pin.n <= 0) return;
   MCC_CHECK(pin.nstages <= kMaxPackStages, "sgd_pack: too many weight stages");
+  MCC_CHECK(((reinterpret_cast<uintptr_t>(pin.params) | reinterpret_cast<uintptr_t>(pin.grads) |
+              reinterpret_cast<uintptr_t>(pin.mom) | reinterpret_cast<uintptr_t>(pin.packed)) & 15) == 0,
+            "sgd_pack: buffers must be 16-byte aligned");
   SgdPackParams p = pin;
+  p.ntiles = 0;
   for (int i = 0; i < p.nstages; ++i) {
     PackStage& st = p.st[i];
     st.m_ckk = div_magic((uint64_t)st.inC * st.KS * st.KS);
     st.m_kk = div_magic((uint64_t)st.KS * st.KS);
     st.m_ks = div_magic((uint64_t)st.KS);
+    // transposing copies of a large conv: tiles (see sgd_pack_kernel)
+    bool transposing = false;
+    for (int m = 0; m < st.nmaps; ++m) transposing = transposing || st.map[m].sc == 1 || st.map[m].sn == 1;
+    const int KK = st.KS * st.KS;
+    st.tile0 = -1;
+    if (st.nmaps > 0 && st.KS > 1 && KK <= kPackMaxKK && st.nw >= kPackTileMin && transposing &&
+        st.nw % ((int64_t)st.inC * KK) == 0) {
+      const int N = (int)(st.nw / ((int64_t)st.inC * KK));
+      st.tile0 = p.ntiles;
+      p.ntiles += cdiv(N, kPackTN) * cdiv(st.inC, kPackTC);
+    }
   }
-  const dim3 grid(grid_for(p.n)), block(256);
+  const dim3 grid((unsigned)(p.ntiles + (int)grid_for(p.n, 4))), block(256);
   if (t == DType::BF16) {
     if (p.update) hipLaunchKernelGGL((sgd_pack_kernel<bf16, true>), grid, block, 0, s, p);
     else hipLaunchKernelGGL((sgd_pack_kernel<bf16, false>), grid, block, 0, s, p);

@@ -128,16 +128,21 @@ def _sgd_steps(cuda, spec, dtype, B, steps=2):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("model,dtype", [("lenet5", "bf16"), ("lenet5", "fp32"), ("ref", "bf16"), ("cifar3", "bf16"),
-                                         ("big", "bf16"), ("big", "fp32")])
+                                         ("big", "bf16"), ("big", "fp32"), ("wide", "bf16"), ("wide", "fp32"),
+                                         ("vgg11", "bf16")])
 def test_fused_sgd_pack_matches_table(cuda, model, dtype, monkeypatch):
     """One-pass SGD + packed-copy refresh (analytic per-stage maps, no index
     table) vs the gather-table path (MCC_NO_FUSED_PACK=1): bit-identical
     parameters after SGD with momentum + weight decay, and bit-identical
     logits from the refreshed bf16/fp32 compute copies (every packed layout:
     S1 pair, C8, flipped data-gradient copies, im2col, FC and FC^T)."""
-    spec = (mcc.parse_model_spec("input 3 72 72; conv 16 k3 s1 p1 relu; pool 2; conv 24 k3 s2 p1 relu; "
-                                 "fc 32 relu; fc 10 softmax", "big") if model == "big" else mcc.make_model(model))
-    B = 8 if model == "big" else 64
+    # "wide": 3x3 convs of >= 64K weights with channel counts that are not
+    # multiples of the 32x32 tile (the tiled, transposing stage path)
+    specs = {"big": "input 3 72 72; conv 16 k3 s1 p1 relu; pool 2; conv 24 k3 s2 p1 relu; fc 32 relu; fc 10 softmax",
+             "wide": "input 3 40 40; conv 48 k3 s1 p1 relu; pool 2; conv 200 k3 s1 p1 relu; pool 2; "
+                     "conv 72 k3 s1 p1 relu; fc 32 relu; fc 10 softmax"}
+    spec = mcc.parse_model_spec(specs[model], model) if model in specs else mcc.make_model(model)
+    B = {"big": 8, "wide": 8, "vgg11": 2}.get(model, 64)
     plan, p_fused, l_fused = _sgd_steps(cuda, spec, dtype, B)
     assert "fused sgd+pack" in plan, plan
     monkeypatch.setenv("MCC_NO_FUSED_PACK", "1")
