@@ -336,9 +336,11 @@ __global__ void __launch_bounds__(kIgT, 2) igemm_dw_kernel(IgemmDwParams p) {
 
   const int ntm = cdiv(p.Cout, BM), ntn = cdiv(p.kf + 1, BN);
   const int ntiles = ntm * ntn;
+  // consecutive ids (one XCD after the remap) = different output tiles of
+  // the SAME pixel range: the dZ and X rows they stream are shared in L2
   const int id = xcd_remap(blockIdx.x, gridDim.x);
-  const int split = id % p.splitk, tile = id / p.splitk;
-  if (tile >= ntiles) return;
+  const int tile = id % ntiles, split = id / ntiles;
+  if (split >= p.splitk) return;
   const int tm = tile % ntm, tn = tile / ntm;
   const int co0 = tm * BM, k0 = tn * BN;
   const int nks = cdiv(p.M, BK);
@@ -351,15 +353,17 @@ __global__ void __launch_bounds__(kIgT, 2) igemm_dw_kernel(IgemmDwParams p) {
   const bf16* ones = reinterpret_cast<const bf16*>(kIgOnes);
 
   // per-thread staging geometry: row (pixel within the K-step) and the
-  // logical 16-byte slot (8 output channels / 8 im2col columns)
-  int d_row[J], d_col[J];
+  // logical 16-byte slot (8 output channels / 8 im2col columns).  The row's
+  // pixel (b, oy, ox) is decoded once and then advanced by BK pixels per
+  // K-step with carries (the K-steps of a split are staged in order), and
+  // every source is picked by selects: no per-step divisions, no branches.
+  int d_col[J], m_[J], b_[J], oy_[J], ox_[J];
   int x_ky[J], x_kx[J], x_c[J], x_kind[J];  // kind: 0 tap, 1 ones, 2 zero
 #pragma unroll
   for (int j = 0; j < J; ++j) {
     const int s = j * kIgT + tid;
     const int row = s >> 4;
     const int ls = (s & 15) ^ swz128(row);
-    d_row[j] = row;
     d_col[j] = co0 + ls * 8;
     const int k = k0 + ls * 8;
     if (k < p.kf) {
@@ -372,31 +376,39 @@ __global__ void __launch_bounds__(kIgT, 2) igemm_dw_kernel(IgemmDwParams p) {
       x_c[j] = 0; x_ky[j] = 0; x_kx[j] = 0;
       x_kind[j] = k == p.kf ? 1 : 2;
     }
+    const int m = ks0 * BK + row;
+    m_[j] = m;
+    b_[j] = mdiv(p.div_ohw, m);
+    const int rem = m - b_[j] * p.OH * p.OW;
+    oy_[j] = mdiv(p.div_ow, rem);
+    ox_[j] = rem - oy_[j] * p.OW;
   }
+  const uint64_t zero_u = reinterpret_cast<uint64_t>(zero), ones_u = reinterpret_cast<uint64_t>(ones);
 
-  auto stage = [&](int ks, int buf) {
+  auto stage = [&](int buf) {  // the next K-step of this split
     bf16* D = smem + buf * IMG;
     bf16* X = D + BK * BM;
-    const int mb = ks * BK;
 #pragma unroll
     for (int j = 0; j < J; ++j) {
-      const int m = mb + d_row[j];
-      const bool mok = m < p.M;
-      const bf16* dsrc = (mok && d_col[j] < p.Cout) ? dz + (size_t)m * p.ldz + d_col[j] : zero;  // piece may span the pad
+      const bool mok = m_[j] < p.M;
+      const uint64_t dz_u = reinterpret_cast<uint64_t>(dz + (size_t)m_[j] * p.ldz + d_col[j]);
+      const bf16* dsrc = reinterpret_cast<const bf16*>((mok && d_col[j] < p.Cout) ? dz_u : zero_u);  // piece may span the pad
       glds16(dsrc, D + (j * kIgT + wave * 64) * 8);
-      const bf16* xsrc = zero;
-      if (mok) {
-        if (x_kind[j] == 0) {
-          const int b = mdiv(p.div_ohw, m), rem = m - b * p.OH * p.OW;
-          const int oy = mdiv(p.div_ow, rem), ox = rem - oy * p.OW;
-          const int iy = oy * p.stride - p.pad + x_ky[j], ix = ox * p.stride - p.pad + x_kx[j];
-          if ((unsigned)iy < (unsigned)p.H && (unsigned)ix < (unsigned)p.W)
-            xsrc = in + (((size_t)b * p.H + iy) * p.W + ix) * p.C + x_c[j];
-        } else if (x_kind[j] == 1) {
-          xsrc = ones;
-        }
-      }
-      glds16(xsrc, X + (j * kIgT + wave * 64) * 8);
+      const int iy = oy_[j] * p.stride - p.pad + x_ky[j], ix = ox_[j] * p.stride - p.pad + x_kx[j];
+      const bool tap_ok = mok && x_kind[j] == 0 && (unsigned)iy < (unsigned)p.H && (unsigned)ix < (unsigned)p.W;
+      const int off = ((b_[j] * p.H + iy) * p.W + ix) * p.C + x_c[j];  // < 2^31 (host check); unused if !tap_ok
+      const uint64_t x_u = reinterpret_cast<uint64_t>(in) + 2 * (uint64_t)(uint32_t)off;
+      const uint64_t xs = tap_ok ? x_u : ((mok && x_kind[j] == 1) ? ones_u : zero_u);
+      glds16(reinterpret_cast<const bf16*>(xs), X + (j * kIgT + wave * 64) * 8);
+      // advance this row by BK pixels
+      m_[j] += BK;
+      ox_[j] += p.adv_x;
+      const int c1 = ox_[j] >= p.OW ? 1 : 0;
+      ox_[j] -= c1 * p.OW;
+      oy_[j] += p.adv_y + c1;
+      const int c2 = oy_[j] >= p.OH ? 1 : 0;
+      oy_[j] -= c2 * p.OH;
+      b_[j] += p.adv_b + c2;
     }
   };
 
@@ -415,11 +427,11 @@ __global__ void __launch_bounds__(kIgT, 2) igemm_dw_kernel(IgemmDwParams p) {
   };
 
   if (ks0 < ks1) {
-    stage(ks0, 0);
+    stage(0);
     __syncthreads();
     for (int ks = ks0; ks < ks1; ++ks) {
       const int buf = (ks - ks0) & 1;
-      if (ks + 1 < ks1) stage(ks + 1, buf ^ 1);
+      if (ks + 1 < ks1) stage(buf ^ 1);
       const bf16* D = smem + buf * IMG;
       const bf16* X = D + BK * BM;
 #pragma unroll
@@ -607,6 +619,12 @@ void igemm_dw(const IgemmDwParams& p0, float* gw, float* gb, float beta, hipStre
             "igemm_dw: bad permutation");
   p.div_ohw = magic(p.OH * p.OW);
   p.div_ow = magic(p.OW);
+  {  // +kIgBK output pixels as (ox, oy, b) increments with carries (igemm_dw_kernel)
+    const int q = kIgBK / p.OW;
+    p.adv_x = kIgBK % p.OW;
+    p.adv_y = q % p.OH;
+    p.adv_b = q / p.OH;
+  }
   const int nwg = cdiv(p.Cout, 128) * cdiv(p.kf + 1, 128) * p.splitk;
   p.direct = p.splitk == 1 && p.KS == 1 && p.perm_c == 0 && beta == 0.f;
   p.gw = gw;

@@ -388,6 +388,7 @@ struct IgemmDwParams {
   float* gw = nullptr;               // set at launch
   float* gb = nullptr;
   DivMagic div_ohw, div_ow;
+  int adv_x = 0, adv_y = 0, adv_b = 0;  // set at launch: +BK pixels as (ox, oy, b) increments
 };
 int igemm_dw_splitk(int M, int Cout, int kf);
 size_t igemm_dw_slab_bytes(int Cout, int kf, int splitk);
