@@ -75,6 +75,10 @@ struct GpuNet::Stage {
   // single-channel first layer: row-chunked weight gradient (conv_rows.hip)
   bool rows_dw = false;
   gpu::ConvDwRowsParams prw;
+  // fp32 small pooled convs: direct VALU kernels (conv_direct.hip) for the
+  // forward (direct_fwd) and, single-channel first layer, the weight gradient
+  bool direct_fwd = false, direct1 = false;
+  gpu::Conv1DirectParams pd1;
 };
 
 static inline int r8(int x) { return (x + 7) & ~7; }
@@ -286,6 +290,14 @@ void GpuNet::build() {
       }
       st.ig_pool = st.ig_fwd && st.pooled && st.OH % 2 == 0 && st.OW % 2 == 0;
       if (!st.big && dtype_ == DType::BF16 && !no_pipe_) plan_pipe(st, s == 0);
+      if (!st.big && dtype_ == DType::F32 && st.pooled && st.stride == 1 && !no_pipe_ &&
+          (s == 0 || st.inC > 1)) {
+        gpu::Conv1DirectParams& d = st.pd1;
+        d.N = max_batch_; d.H = st.inH; d.W = st.inW; d.Cin = st.inC; d.KS = st.KS; d.pad = st.pad; d.C = st.C;
+        d.OH = st.OH; d.OW = st.OW; d.PH = st.outH; d.PW = st.outW;
+        st.direct_fwd = gpu::conv_direct_fwd_supported(d);
+        st.direct1 = s == 0 && gpu::conv1_direct_dw_supported(d);
+      }
     } else {
       st.out_elems = st.Nout;
       st.out_ld = r8(st.Nout);
@@ -477,6 +489,7 @@ void GpuNet::build() {
     } else if (st.kind == Stage::CONV) {
       scratch = std::max(scratch, (size_t)st.nx_dw * st.cout_pad * st.ncols_pad * 4);
       if (st.rows_dw) scratch = std::max(scratch, gpu::conv_dw_rows_scratch_bytes(st.prw));
+      if (st.direct1) scratch = std::max(scratch, gpu::conv1_direct_slab_bytes(st.pd1));
       if (st.pipe_dw) {
         const size_t nv = (size_t)st.pdw.cout_pad * st.pdw.ncols_pad;
         scratch = std::max(scratch, (st.pdw.grid + ceil_div(st.pdw.grid, 16)) * nv * 4);
@@ -553,6 +566,7 @@ std::string GpuNet::plan() const {
         if (st.rows_dw) os << "dw:rows x" << st.prw.imgs << "/g" << st.prw.grid;
         os << "]";
       }
+      if (st.direct_fwd || st.direct1) os << " direct-f32[" << (st.direct_fwd ? "fwd" : "") << (st.direct1 ? " dw" : "") << "]";
       os << "\n";
     } else {
       os << "  [" << s << "] fc " << st.Kin << " -> " << st.Nout << (st.last ? " (logits)" : "")
@@ -669,6 +683,14 @@ void GpuNet::forward(const uint8_t* images, const int32_t* idx, int B, hipStream
       g.C = st.pooled ? st.conv_buf : st.act_buf; g.ldc = st.C;
       gpu::gemm(dtype_, g, s);
       if (st.pooled) gpu::maxpool2(dtype_, st.conv_buf, st.act_buf, st.arg_buf, B, st.OH, st.OW, st.C, s);
+    } else if (st.kind == Stage::CONV && st.direct_fwd) {
+      gpu::Conv1DirectParams p = st.pd1;
+      p.N = B;
+      if (si == 0) { p.x = images; p.idx = idx; }
+      else p.xf = static_cast<const float*>(stages_[si - 1]->act_buf);
+      p.w = params_ + st.w_off; p.bias = params_ + st.b_off;
+      p.out = static_cast<float*>(st.act_buf); p.out_arg = st.arg_buf;
+      gpu::conv_direct_forward(p, s);
     } else if (st.kind == Stage::CONV && st.pipe_fwd) {
       gpu::ConvPipeParams p = st.pf;
       p.N = B; p.ablate = ablate_;
@@ -885,7 +907,13 @@ void GpuNet::backward(int hi, int lo, hipStream_t s) {
         continue;
       }
       fork();
-      if (st.rows_dw) {
+      if (st.direct1) {
+        gpu::Conv1DirectParams w = st.pd1;
+        w.N = B; w.x = images_; w.idx = idx_;
+        w.dy = static_cast<const float*>(st.grad_buf); w.arg = st.arg_buf;
+        w.slab = scratch_;
+        gpu::conv1_direct_dw(w, grads_ + st.w_off, grads_ + st.b_off, ws);
+      } else if (st.rows_dw) {
         gpu::ConvDwRowsParams w = st.prw;
         w.N = B; w.ablate = ablate_;
         w.x = images_; w.idx = idx_;
@@ -910,7 +938,7 @@ void GpuNet::backward(int hi, int lo, hipStream_t s) {
         p.out = stages_[si - 1]->grad_buf;
         gpu::conv_pipe_forward(p, s);
       }
-      const bool dw_done = st.pipe_dw || st.rows_dw;
+      const bool dw_done = st.pipe_dw || st.rows_dw || st.direct1;
       if (dw_done && (st.pipe_dx || si == 0)) continue;
       // weight gradient
       if (!dw_done) {

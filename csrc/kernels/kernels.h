@@ -213,6 +213,29 @@ void dw_slab_reduce(const float* slab, int nx, int cout_pad, int ncols_pad, floa
 // with the max-pool / ReLU backward applied while staging, the input as four
 // shifted bf16 copies.  Persistent over image groups; fp32 slab per
 // workgroup, then dw_slab_reduce.
+// fp32 small conv with fused ReLU + 2x2/2 max-pool, direct VALU form
+// (conv_direct.hip): forward for the LeNet-class shapes (Cin 1 -> 6, 6 -> 16,
+// 5x5) and the single-channel layer's weight gradient.  Canonical fp32
+// weights [C][Cin][KS][KS] and bias are read directly (no packed copy).
+struct Conv1DirectParams {
+  int N = 0, H = 0, W = 0, Cin = 1, KS = 5, pad = 0, C = 0, OH = 0, OW = 0, PH = 0, PW = 0;
+  const uint8_t* x = nullptr;     // u8 images [.][H][W][Cin] (when xf is null)
+  const int32_t* idx = nullptr;   // optional per-image dataset index
+  const float* xf = nullptr;      // fp32 NHWC input [N][H][W][Cin] (a previous layer)
+  const float* w = nullptr;       // forward: canonical weights, bias
+  const float* bias = nullptr;
+  float* out = nullptr;           // forward: pooled [N][PH][PW][C]
+  uint8_t* out_arg = nullptr;     //          argmax (4: ReLU-inactive window)
+  const float* dy = nullptr;      // weight gradient: pooled output gradient [N][PH][PW][C]
+  const uint8_t* arg = nullptr;   //                  its argmax bytes
+  float* slab = nullptr;          //                  [grid][C][KS*KS + 1] partial sums
+};
+bool conv_direct_fwd_supported(const Conv1DirectParams& p);
+bool conv1_direct_dw_supported(const Conv1DirectParams& p);
+size_t conv1_direct_slab_bytes(const Conv1DirectParams& p);
+void conv_direct_forward(const Conv1DirectParams& p, hipStream_t s);
+void conv1_direct_dw(const Conv1DirectParams& p, float* gw, float* gb, hipStream_t s);
+
 struct ConvDwRowsParams {
   int N = 0, SH = 0, SW = 0, OH = 0, OW = 0, KS = 1, pad = 0, Cout = 0;
   const uint8_t* x = nullptr;        // u8 images [*][SH][SW]
