@@ -77,7 +77,7 @@ struct GpuNet::Stage {
   gpu::ConvDwRowsParams prw;
   // fp32 small pooled convs: direct VALU kernels (conv_direct.hip) for the
   // forward (direct_fwd) and, single-channel first layer, the weight gradient
-  bool direct_fwd = false, direct1 = false;
+  bool direct_fwd = false, direct1 = false, direct_dx = false;
   gpu::Conv1DirectParams pd1;
 };
 
@@ -297,6 +297,7 @@ void GpuNet::build() {
         d.OH = st.OH; d.OW = st.OW; d.PH = st.outH; d.PW = st.outW;
         st.direct_fwd = gpu::conv_direct_fwd_supported(d);
         st.direct1 = s == 0 && gpu::conv1_direct_dw_supported(d);
+        st.direct_dx = s > 0 && gpu::conv_direct_dx_supported(d);
       }
     } else {
       st.out_elems = st.Nout;
@@ -566,7 +567,8 @@ std::string GpuNet::plan() const {
         if (st.rows_dw) os << "dw:rows x" << st.prw.imgs << "/g" << st.prw.grid;
         os << "]";
       }
-      if (st.direct_fwd || st.direct1) os << " direct-f32[" << (st.direct_fwd ? "fwd" : "") << (st.direct1 ? " dw" : "") << "]";
+      if (st.direct_fwd || st.direct1 || st.direct_dx)
+        os << " direct-f32[" << (st.direct_fwd ? "fwd" : "") << (st.direct1 ? " dw" : "") << (st.direct_dx ? " dx" : "") << "]";
       os << "\n";
     } else {
       os << "  [" << s << "] fc " << st.Kin << " -> " << st.Nout << (st.last ? " (logits)" : "")
@@ -964,7 +966,12 @@ void GpuNet::backward(int hi, int lo, hipStream_t s) {
       gpu::conv_dw_reduce(r, ws);
       }
       // data gradient into the previous stage's output gradient
-      if (si > 0 && !st.pipe_dx) {
+      if (si > 0 && st.direct_dx) {
+        gpu::Conv1DirectParams p = st.pd1;
+        p.N = B; p.w = params_ + st.w_off;
+        p.dy = static_cast<const float*>(st.grad_buf); p.arg = st.arg_buf;
+        gpu::conv_direct_dx(p, static_cast<float*>(stages_[si - 1]->grad_buf), s);
+      } else if (si > 0 && !st.pipe_dx) {
         gpu::ConvParams p;
         p.N = B; p.imgs = st.imgs_dx;
         p.Cin = st.C; p.CL = st.CLd; p.cvec = st.cvec_d;

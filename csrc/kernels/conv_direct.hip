@@ -285,6 +285,93 @@ __global__ void __launch_bounds__(kDT) conv1_direct_dw_kernel(Conv1DirectParams 
   }
 }
 
+// Data gradient of a pooled 5x5 conv (stride 1, no padding): dX = full
+// correlation of dZ = unpool(dY, argmax) with the flipped weights.  Item =
+// (image, 2x2 block of dX pixels); its 6x6 dZ patch is exactly 3x3 pooling
+// windows (the block is 2-aligned and the halo KS-1 = 4 is even), so the
+// patch is decoded from the group's pooled dY / argmax in LDS (value at the
+// argmax position, zeros elsewhere; argmax 4 routes nothing) instead of
+// staging the 4x larger unpooled tensor.  Then 4*KS*KS FMAs per (input,
+// output channel) pair with scalar-loaded flipped weights, as the forward.
+constexpr int kDxImgs = 16;
+template <int KS, int CI, int CO>  // CI: dZ channels (forward Cout), CO: dX channels (forward Cin)
+__global__ void __launch_bounds__(kDT) conv_direct_dx_kernel(Conv1DirectParams p, const float* __restrict__ wgt,
+                                                           float* __restrict__ out) {
+  static_assert(KS == 5, "the 3x3-window patch decode assumes KS - 1 == 4");
+  extern __shared__ __attribute__((aligned(16))) float dys[];
+  const int PHW = p.PH * p.PW;  // pooled grid of dY
+  const int BH = p.H / 2, BW = p.W / 2, nb = BH * BW;  // 2x2 blocks of the dX grid (H x W)
+  uint8_t* args = reinterpret_cast<uint8_t*>(dys + kDxImgs * PHW * CI);
+  const int ngroups = (p.N + kDxImgs - 1) / kDxImgs;
+  for (int grp = blockIdx.x; grp < ngroups; grp += gridDim.x) {
+    const int img0 = grp * kDxImgs, nimg = min(kDxImgs, p.N - img0);
+    __syncthreads();
+    {
+      const int n4 = nimg * PHW * CI / 4;
+      const float4* g = reinterpret_cast<const float4*>(p.dy + (size_t)img0 * PHW * CI);
+      const uint32_t* ga = reinterpret_cast<const uint32_t*>(p.arg + (size_t)img0 * PHW * CI);
+      for (int i = threadIdx.x; i < n4; i += kDT) {
+        reinterpret_cast<float4*>(dys)[i] = g[i];
+        reinterpret_cast<uint32_t*>(args)[i] = ga[i];
+      }
+    }
+    __syncthreads();
+    for (int it = threadIdx.x; it < nimg * nb; it += kDT) {
+      const int m = it / nb, b = it - m * nb;
+      const int by = b / BW, bx = b - by * BW;
+      float acc[CO][4];
+#pragma unroll
+      for (int c = 0; c < CO; ++c) acc[c][0] = acc[c][1] = acc[c][2] = acc[c][3] = 0.f;
+      const float* dimg = dys + m * PHW * CI;
+      const uint8_t* aimg = args + m * PHW * CI;
+      for (int i = 0; i < CI; ++i) {
+        float P[KS + 1][KS + 1];
+#pragma unroll
+        for (int wr = 0; wr < 3; ++wr) {
+#pragma unroll
+          for (int wc = 0; wc < 3; ++wc) {
+            const int wy = by - 2 + wr, wx = bx - 2 + wc;
+            const bool ok = (unsigned)wy < (unsigned)p.PH && (unsigned)wx < (unsigned)p.PW;
+            const int o = ok ? (wy * p.PW + wx) * CI + i : 0;
+            const float g = ok ? dimg[o] : 0.f;
+            const int a = ok ? aimg[o] : 4;
+            P[2 * wr][2 * wc] = a == 0 ? g : 0.f;
+            P[2 * wr][2 * wc + 1] = a == 1 ? g : 0.f;
+            P[2 * wr + 1][2 * wc] = a == 2 ? g : 0.f;
+            P[2 * wr + 1][2 * wc + 1] = a == 3 ? g : 0.f;
+          }
+        }
+#pragma unroll
+        for (int c = 0; c < CO; ++c) {
+          // flipped weight of (dX channel c, dZ channel i, tap kh, kw) = w[i][c][KS-1-kh][KS-1-kw]
+          const float* wc = wgt + (i * CO + c) * KS * KS;
+#pragma unroll
+          for (int kh = 0; kh < KS; ++kh) {
+#pragma unroll
+            for (int kw = 0; kw < KS; ++kw) {
+              const float wv = wc[(KS - 1 - kh) * KS + (KS - 1 - kw)];
+              acc[c][0] = fmaf(wv, P[kh][kw], acc[c][0]);
+              acc[c][1] = fmaf(wv, P[kh][kw + 1], acc[c][1]);
+              acc[c][2] = fmaf(wv, P[kh + 1][kw], acc[c][2]);
+              acc[c][3] = fmaf(wv, P[kh + 1][kw + 1], acc[c][3]);
+            }
+          }
+        }
+      }
+      // dX pixels (2by + r, 2bx + q), CO channels each: two rows of 2*CO contiguous floats
+#pragma unroll
+      for (int r = 0; r < 2; ++r) {
+        float* d = out + (((size_t)(img0 + m) * p.H + 2 * by + r) * p.W + 2 * bx) * CO;
+#pragma unroll
+        for (int c = 0; c < CO; c += 2) {
+          *reinterpret_cast<float2*>(d + c) = make_float2(acc[c][2 * r], acc[c + 1][2 * r]);
+          *reinterpret_cast<float2*>(d + CO + c) = make_float2(acc[c][2 * r + 1], acc[c + 1][2 * r + 1]);
+        }
+      }
+    }
+  }
+}
+
 // One workgroup per column (c, k): 256 strided partial sums over the slabs,
 // then a fixed LDS tree.  k < KK: weight, k == KK: bias.
 __global__ void __launch_bounds__(256) conv1_direct_dw_reduce_kernel(Conv1DirectParams p, int nslab, float* gw,
@@ -321,6 +408,21 @@ bool conv_direct_fwd_supported(const Conv1DirectParams& p) {
                                    : (p.pad == 0 && t.TW == p.W && t.IMG % 4 == 0);
   return shape && stage_ok && p.OH % 2 == 0 && p.OW % 2 == 0 && p.OH == p.H + 2 * p.pad - p.KS + 1 &&
          p.OW == p.W + 2 * p.pad - p.KS + 1 && p.PH == p.OH / 2 && p.PW == p.OW / 2 && fwd_lds(p) <= 64 * 1024;
+}
+
+// dX geometry: p.H x p.W = the forward input (dX) grid, p.PH x p.PW = pooled dY
+bool conv_direct_dx_supported(const Conv1DirectParams& p) {
+  return p.KS == 5 && p.pad == 0 && p.Cin == 6 && p.C == 16 && p.OH == p.H - 4 && p.OW == p.W - 4 &&
+         p.H % 2 == 0 && p.W % 2 == 0 && p.PH == p.OH / 2 && p.PW == p.OW / 2 && (p.PH * p.PW * p.C) % 4 == 0 &&
+         (size_t)kDxImgs * p.PH * p.PW * p.C * 5 <= 64 * 1024;
+}
+
+void conv_direct_dx(const Conv1DirectParams& p, float* dx, hipStream_t s) {
+  MCC_CHECK(conv_direct_dx_supported(p) && p.w && p.dy && p.arg && dx, "conv_direct_dx: bad params");
+  const int ngroups = (p.N + kDxImgs - 1) / kDxImgs;
+  const dim3 grid((unsigned)std::max(1, std::min(ngroups, 256 * 4))), block(kDT);
+  const size_t lds = (size_t)kDxImgs * p.PH * p.PW * p.C * 5;
+  hipLaunchKernelGGL((conv_direct_dx_kernel<5, 16, 6>), grid, block, lds, s, p, p.w, dx);
 }
 
 bool conv1_direct_dw_supported(const Conv1DirectParams& p) {

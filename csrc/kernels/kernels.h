@@ -234,6 +234,10 @@ bool conv_direct_fwd_supported(const Conv1DirectParams& p);
 bool conv1_direct_dw_supported(const Conv1DirectParams& p);
 size_t conv1_direct_slab_bytes(const Conv1DirectParams& p);
 void conv_direct_forward(const Conv1DirectParams& p, hipStream_t s);
+// data gradient of the 6 -> 16 5x5 pooled conv into dX [N][H][W][Cin] from
+// the pooled dY / argmax (p.dy, p.arg) and the canonical weights p.w
+bool conv_direct_dx_supported(const Conv1DirectParams& p);
+void conv_direct_dx(const Conv1DirectParams& p, float* dx, hipStream_t s);
 void conv1_direct_dw(const Conv1DirectParams& p, float* gw, float* gb, hipStream_t s);
 
 struct ConvDwRowsParams {
