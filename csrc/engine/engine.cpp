@@ -60,6 +60,8 @@ struct GpuNet::Stage {
   // (the u8 input layer, C % 64 != 0, strided data gradients, fp32)
   bool ig_fwd = false, ig_dw = false, ig_dx = false;
   bool ig_dw0 = false;  // stage 0: im2col rows through the implicit-GEMM dW kernel
+  bool c0dw = false;    // stage 0, pooled 3x3: dW straight from pooled dY / argmax (conv0_dw.hip)
+  gpu::Conv0DwParams pc0;
   bool ig_pool = false; // forward max-pool fused into the implicit-GEMM epilogue
   // large FC layers (VGG heads): no W^T shadow (the data gradient reads the
   // forward copy K-major) and the weight gradient on the implicit-GEMM dW
@@ -283,6 +285,14 @@ void GpuNet::build() {
                   (int64_t)max_batch_ * st.OH * st.OW < (1ll << 31);
       // first layer forward: u8 gather through registers (K = KS*KS*inC small)
       if (st.ig_dw0 && st.KS * st.KS * st.inC <= 64) st.ig_fwd = true;
+      // first layer weight gradient straight from the pooled dY / argmax
+      if (st.ig_dw0 && st.ig_fwd && st.pooled && st.KS == 3 && st.stride == 1 && st.pad == 1 &&
+          !std::getenv("MCC_NO_C0DW")) {
+        gpu::Conv0DwParams& c = st.pc0;
+        c.B = max_batch_; c.H = st.OH; c.W = st.OW; c.C = st.inC; c.PH = st.outH; c.PW = st.outW; c.Cout = st.C;
+        st.c0dw = st.OH == st.inH && st.OW == st.inW && gpu::conv0_dw_supported(c);
+        if (st.c0dw) st.ig_dw0 = false;
+      }
       if (st.big && dtype_ == DType::BF16 && !no_igemm_ && s > 0) {
         st.ig_fwd = gpu::igemm_conv_supported(st.inC, st.C, st.KS);
         st.ig_dw = st.inC % 8 == 0;
@@ -473,7 +483,8 @@ void GpuNet::build() {
     if (st.kind == Stage::CONV && st.big) {
       const int KK = st.KS * st.KS;
       const int64_t rows = (int64_t)Bm * st.OH * st.OW;
-      if (!st.ig_fwd || !st.ig_dw) col_bytes_ = std::max(col_bytes_, es * (size_t)rows * st.kgem);
+      if (!st.ig_fwd || (!st.ig_dw && !st.c0dw)) col_bytes_ = std::max(col_bytes_, es * (size_t)rows * st.kgem);
+      if (st.c0dw) scratch = std::max(scratch, gpu::conv0_dw_slab_bytes(st.pc0));
       if (sp != stages_[0] && !st.ig_dx)
         col_bytes_ = std::max(col_bytes_, es * (size_t)Bm * st.inH * st.inW * st.kgem_d);
       if (st.ig_dw0) {
@@ -556,7 +567,8 @@ std::string GpuNet::plan() const {
     if (st.kind == Stage::CONV) {
       os << "  [" << s << "] conv " << st.inC << "x" << st.inH << "x" << st.inW << " -> " << st.C << "x" << st.OH << "x"
          << st.OW << (st.pooled ? " +maxpool" : "") << " k" << st.KS << "s" << st.stride << "p" << st.pad
-         << (st.big ? (st.ig_fwd ? " igemm" : " im2col+gemm") : (st.cvec ? " lds-cvec" : " lds-scalar")) << " chunks=" << st.nchunks
+         << (st.big ? (st.ig_fwd ? " igemm" : " im2col+gemm") : (st.cvec ? " lds-cvec" : " lds-scalar"))
+         << (st.c0dw ? " dw:pooled-direct" : "") << " chunks=" << st.nchunks
          << " imgs=" << st.imgs_fwd << "/"
          << st.imgs_dx << "/" << st.imgs_dw;
       if (st.pipe_fwd || st.pipe_dx || st.pipe_dw || st.rows_dw) {
@@ -796,7 +808,8 @@ void GpuNet::backward(int hi, int lo, hipStream_t s) {
     // large-image conv (col_ is shared by their dW and dX).  All dW work is
     // serialised on wstream_, so scratch_ (split-K slabs) stays single-user;
     // the dX kernels never touch scratch_.
-    const bool side = wstream_ && !(st.kind == Stage::CONV && st.big && !((st.ig_dw || st.ig_dw0) && (st.ig_dx || si == 0)));
+    const bool side = wstream_ && !(st.kind == Stage::CONV && st.big &&
+                                    !((st.ig_dw || st.ig_dw0 || st.c0dw) && (st.ig_dx || si == 0)));
     hipStream_t ws = s_main;
     if (!side && forked) {  // this stage's dW uses scratch_ on the main stream: drain the side stream first
       HIP_OK(hipEventRecord(join_ev_, wstream_));
@@ -818,6 +831,15 @@ void GpuNet::backward(int hi, int lo, hipStream_t s) {
       if (st.big) {
         const int KK = st.KS * st.KS;
         const int kf = KK * st.inC;
+        if (st.c0dw) {  // first layer: dW from the pooled dY / argmax directly (no dZ, no im2col)
+          fork();
+          gpu::Conv0DwParams c = st.pc0;
+          c.B = B; c.x = images_; c.idx = idx_;
+          c.dy = static_cast<const uint16_t*>(st.grad_buf); c.arg = st.arg_buf;
+          c.slab = scratch_;
+          gpu::conv0_dw(c, grads_ + st.w_off, grads_ + st.b_off, ws);
+          continue;
+        }
         // dZ = relu'/unpool(dY) at conv-output size
         gpu::grad_xform(dtype_, dy, st.dz_buf, B, s);
         fork();

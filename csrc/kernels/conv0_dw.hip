@@ -1,0 +1,200 @@
+// Weight gradient of the large-image FIRST conv layer (u8 input with few
+// channels, 3x3, stride 1, pad 1, fused ReLU + 2x2/2 max-pool): VGG-11's
+// conv1, bf16.
+//
+//   dW[co][c][ky][kx] = sum_px dZ[px][co] X(px, (ky,kx,c)),  db[co] = sum_px dZ[px][co]
+//   (reference math: Layer_feedBack_conv, cnn.c:212-247; OIHW as CUDAcnn.cu)
+//
+// The generic path for this layer materialised dZ = unpool(dY) at full
+// resolution (grad_xform: 1.6 GB written + read at B=256, 224^2, 64 channels)
+// and an im2col copy of the u8 input (0.8 GB), then ran the implicit-GEMM dW
+// over both: ~2 ms/step for a 46 GFLOP GEMM whose inputs are 0.6 GB.  Here the
+// GEMM operands are built in LDS straight from the pooled dY / argmax and the
+// u8 images, so the kernel reads each pooled gradient once:
+//
+//   * K = pixels, walked in pooled-window order: a K-step is 16 windows = 64
+//     pixels; the dZ^T tile [co][px] takes the window's dY at its argmax
+//     position and zeros at the other three (argmax 4 = ReLU-inactive: all
+//     zero), one 8-byte LDS store per (channel, window);
+//   * the X^T tile [k][px], k = (ky*3 + kx)*C + c plus a ones column (bias),
+//     is gathered from the u8 image (bf16 of x/255, as the forward stages it);
+//   * MFMA 16x16x32 bf16, each wave owns 16 output channels x 32 columns;
+//     the next K-step's loads are issued before the current MFMAs (register
+//     prefetch), LDS double-buffered, one barrier per step;
+//   * per-workgroup fp32 slabs, reduced over workgroups in a fixed order.
+#include "kernels.h"
+#include "mfma.h"
+
+#include <algorithm>
+
+namespace mcc {
+namespace gpu {
+
+namespace {
+
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+
+constexpr int kC0T = 256;      // threads: 4 waves x 16 output channels
+constexpr int kC0W = 16;       // pooled windows per K-step (64 pixels)
+constexpr int kC0K = 32;       // GEMM columns: KS*KS*C taps + ones column, padded
+constexpr int kC0Ld = 64 + 8;  // LDS row stride (bf16) of the [row][px] tiles
+
+__global__ void __launch_bounds__(kC0T) conv0_dw_kernel(Conv0DwParams p) {
+  __shared__ __attribute__((aligned(16))) bf16 Dt[2][64 * kC0Ld];     // dZ^T [co][px]
+  __shared__ __attribute__((aligned(16))) bf16 Xt[2][kC0K * kC0Ld];   // X^T [k][px]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r16 = lane & 15, g = lane >> 4;
+  const int PHW = p.PH * p.PW;
+  const int64_t nwin = (int64_t)p.B * PHW;
+  const int64_t nsteps = (nwin + kC0W - 1) / kC0W;
+  const int64_t per = (nsteps + gridDim.x - 1) / gridDim.x;
+  const int64_t s0 = (int64_t)blockIdx.x * per, s1 = nsteps < s0 + per ? nsteps : s0 + per;
+  const int kf = 9 * p.C;
+
+  // D staging: window w (0..15), four channels co4..co4+3
+  const int dw_ = tid >> 4, co4 = (tid & 15) * 4;
+  // X staging: pixel xp (0..63) of the step, columns 8*xq .. 8*xq+7
+  const int xp = tid >> 2, xq = tid & 3;
+  int kky[8], kkx[8], kc[8], kkind[8];  // kind 0 tap, 1 ones, 2 zero
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int k = 8 * xq + e;
+    const int tap = k / p.C;
+    kc[e] = k - tap * p.C;
+    kky[e] = tap / 3;
+    kkx[e] = tap - kky[e] * 3;
+    kkind[e] = k < kf ? 0 : (k == kf ? 1 : 2);
+  }
+
+  uint2 dv = make_uint2(0, 0);  // 4 bf16 of dY
+  uint32_t da = 0x04040404u;    // 4 argmax bytes
+  uint32_t xv[4];               // 8 bf16 of X
+  auto load = [&](int64_t step) {
+    {
+      const int64_t w = step * kC0W + dw_;
+      const bool ok = w < nwin && co4 < p.Cout;
+      const int64_t o = ok ? w * p.Cout + co4 : 0;
+      dv = ok ? *reinterpret_cast<const uint2*>(p.dy + o) : make_uint2(0, 0);
+      da = ok ? *reinterpret_cast<const uint32_t*>(p.arg + o) : 0x04040404u;
+    }
+    {
+      const int64_t w = step * kC0W + (xp >> 2);
+      const int pos = xp & 3;
+      const bool wok = w < nwin;
+      const int b = wok ? (int)(w / PHW) : 0;
+      const int rem = wok ? (int)(w - (int64_t)b * PHW) : 0;
+      const int wy = rem / p.PW, wx = rem - wy * p.PW;
+      const int y = 2 * wy + (pos >> 1), x = 2 * wx + (pos & 1);
+      const int img = p.idx ? p.idx[b] : b;
+      const uint8_t* src = p.x + (size_t)img * p.H * p.W * p.C;
+      float f[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int iy = y + kky[e] - 1, ix = x + kkx[e] - 1;
+        const bool in = wok && kkind[e] == 0 && (unsigned)iy < (unsigned)p.H && (unsigned)ix < (unsigned)p.W;
+        const int off = in ? (iy * p.W + ix) * p.C + kc[e] : 0;
+        const float v = (float)src[off] * (1.0f / 255.0f);
+        f[e] = in ? v : ((wok && kkind[e] == 1) ? 1.f : 0.f);
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const bf16x2 h = {(bf16)f[2 * e], (bf16)f[2 * e + 1]};
+        xv[e] = __builtin_bit_cast(uint32_t, h);
+      }
+    }
+  };
+  auto store = [&](int buf) {
+    bf16* D = Dt[buf];
+    const uint16_t v[4] = {(uint16_t)(dv.x & 0xffffu), (uint16_t)(dv.x >> 16), (uint16_t)(dv.y & 0xffffu),
+                           (uint16_t)(dv.y >> 16)};
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const uint32_t a = (da >> (8 * c)) & 0xffu;
+      const uint32_t lo = (a == 0 ? (uint32_t)v[c] : 0u) | (a == 1 ? (uint32_t)v[c] << 16 : 0u);
+      const uint32_t hi = (a == 2 ? (uint32_t)v[c] : 0u) | (a == 3 ? (uint32_t)v[c] << 16 : 0u);
+      *reinterpret_cast<uint2*>(D + (co4 + c) * kC0Ld + 4 * dw_) = make_uint2(lo, hi);
+    }
+    bf16* X = Xt[buf];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const uint32_t w2 = xv[e];
+      X[(8 * xq + 2 * e) * kC0Ld + xp] = __builtin_bit_cast(bf16, (uint16_t)(w2 & 0xffffu));
+      X[(8 * xq + 2 * e + 1) * kC0Ld + xp] = __builtin_bit_cast(bf16, (uint16_t)(w2 >> 16));
+    }
+  };
+
+  f32x4 acc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+  const int corow = wave * 16 + r16;  // A row (output channel) of this lane
+  if (s0 < s1) load(s0);
+  for (int64_t s = s0; s < s1; ++s) {
+    const int buf = (int)((s - s0) & 1);
+    store(buf);
+    __syncthreads();
+    if (s + 1 < s1) load(s + 1);
+    const bf16* D = Dt[buf];
+    const bf16* X = Xt[buf];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {  // 32 pixels each
+      const bf16x8 a = load8(D + corow * kC0Ld + 32 * h + 8 * g);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const bf16x8 b = load8(X + (16 * j + r16) * kC0Ld + 32 * h + 8 * g);
+        acc[j] = mma(acc[j], a, b);
+      }
+    }
+  }
+  // slab[wg][co][k]: lane holds rows (co) 4g..4g+3 of column r16 of tile j
+  float* slab = p.slab + (size_t)blockIdx.x * 64 * kC0K;
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) slab[(wave * 16 + 4 * g + i) * kC0K + 16 * j + r16] = acc[j][i];
+}
+
+// dW[co][c][ky][kx] (k = (ky*3 + kx)*C + c) and db[co] (k = 9C): a fixed-order
+// sum over the workgroup slabs, one workgroup per output column
+__global__ void __launch_bounds__(256) conv0_dw_reduce_kernel(Conv0DwParams p, int nslab, float* gw, float* gb) {
+  __shared__ float part[256];
+  const int col = blockIdx.x;  // co * kC0K + k
+  const int co = col / kC0K, k = col - co * kC0K;
+  const int kf = 9 * p.C;
+  float v = 0.f;
+  for (int s = threadIdx.x; s < nslab; s += 256) v += p.slab[(size_t)s * 64 * kC0K + col];
+  part[threadIdx.x] = v;
+  __syncthreads();
+  for (int hh = 128; hh > 0; hh >>= 1) {
+    if ((int)threadIdx.x < hh) part[threadIdx.x] += part[threadIdx.x + hh];
+    __syncthreads();
+  }
+  if (threadIdx.x != 0 || co >= p.Cout || k > kf) return;
+  if (k == kf) {
+    gb[co] = part[0];
+  } else {
+    const int tap = k / p.C, c = k - tap * p.C;
+    gw[((size_t)co * p.C + c) * 9 + tap] = part[0];
+  }
+}
+
+int conv0_dw_grid(const Conv0DwParams& p) {
+  const int64_t nsteps = ((int64_t)p.B * p.PH * p.PW + kC0W - 1) / kC0W;
+  return (int)std::max<int64_t>(1, std::min<int64_t>(nsteps, 256 * 8));
+}
+
+}  // namespace
+
+bool conv0_dw_supported(const Conv0DwParams& p) {
+  return p.C >= 1 && 9 * p.C + 1 <= kC0K && p.Cout >= 1 && p.Cout <= 64 && p.Cout % 4 == 0 && p.H % 2 == 0 &&
+         p.W % 2 == 0 && p.PH == p.H / 2 && p.PW == p.W / 2 && (int64_t)p.H * p.W * p.C < (1 << 30);
+}
+
+size_t conv0_dw_slab_bytes(const Conv0DwParams& p) { return (size_t)conv0_dw_grid(p) * 64 * kC0K * 4; }
+
+void conv0_dw(const Conv0DwParams& p, float* gw, float* gb, hipStream_t s) {
+  MCC_CHECK(conv0_dw_supported(p) && p.x && p.dy && p.arg && p.slab, "conv0_dw: bad params");
+  const int grid = conv0_dw_grid(p);
+  hipLaunchKernelGGL(conv0_dw_kernel, dim3((unsigned)grid), dim3(kC0T), 0, s, p);
+  hipLaunchKernelGGL(conv0_dw_reduce_kernel, dim3((unsigned)(p.Cout * kC0K)), dim3(256), 0, s, p, grid, gw, gb);
+}
+
+}  // namespace gpu
+}  // namespace mcc

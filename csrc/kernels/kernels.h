@@ -240,6 +240,21 @@ bool conv_direct_dx_supported(const Conv1DirectParams& p);
 void conv_direct_dx(const Conv1DirectParams& p, float* dx, hipStream_t s);
 void conv1_direct_dw(const Conv1DirectParams& p, float* gw, float* gb, hipStream_t s);
 
+// Weight gradient of a large-image first conv (u8 input, C <= 3, 3x3, stride
+// 1, pad 1, fused ReLU + 2x2/2 max-pool, Cout <= 64), bf16 (conv0_dw.hip):
+// GEMM operands built in LDS from the pooled dY / argmax and the u8 images.
+struct Conv0DwParams {
+  int B = 0, H = 0, W = 0, C = 0, PH = 0, PW = 0, Cout = 0;
+  const uint8_t* x = nullptr;     // u8 images [.][H][W][C]
+  const int32_t* idx = nullptr;   // optional per-image dataset index
+  const uint16_t* dy = nullptr;   // pooled output gradient, bf16 bits [B][PH][PW][Cout]
+  const uint8_t* arg = nullptr;   // argmax (4: ReLU-inactive window)
+  float* slab = nullptr;          // per-workgroup partials (conv0_dw_slab_bytes)
+};
+bool conv0_dw_supported(const Conv0DwParams& p);
+size_t conv0_dw_slab_bytes(const Conv0DwParams& p);
+void conv0_dw(const Conv0DwParams& p, float* gw, float* gb, hipStream_t s);
+
 struct ConvDwRowsParams {
   int N = 0, SH = 0, SW = 0, OH = 0, OW = 0, KS = 1, pad = 0, Cout = 0;
   const uint8_t* x = nullptr;        // u8 images [*][SH][SW]
