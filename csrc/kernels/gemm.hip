@@ -216,34 +216,34 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmParams p) {
   }
 }
 
-// Sum split-K partials: 4 independent accumulators per thread so the S loads
-// are in flight together.
-// Four lanes per output, each summing every 4th split-K partial with two
-// accumulators (the loads of ~S/4 partials are in flight together), then a
-// fixed-order shuffle reduction: deterministic, ~4x shorter dependency chain
-// than one lane per output.
+// Sum split-K partials.  L lanes per output (L = 4, 16 or 64 by the number
+// of partials S), each summing every L-th partial with two accumulators (the
+// loads of ~S/L partials are in flight together), then a fixed-order
+// shuffle reduction: deterministic, and the dependency chain is S/(2L) loads
+// instead of S (a 512-slab head reduce was 22 us on one lane per output).
+template <int L>
 __global__ void __launch_bounds__(256) dw_reduce_kernel(DwReduceParams p) {
   const int kc = p.kfeat + 1;
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int64_t j = t >> 2;
-  const int s4 = (int)(t & 3);
+  const int64_t j = t / L;
+  const int sl = (int)(t & (L - 1));
   const bool ok = j < (int64_t)p.Nout * kc;
   const int n = ok ? (int)(j / kc) : 0, k = ok ? (int)(j - (int64_t)n * kc) : 0;
   const float* src = p.part + (size_t)n * p.ldp + k;
   const size_t st = (size_t)p.partial_stride;
   float a0 = 0.f, a1 = 0.f;
   if (ok) {
-    int s = s4;
-    for (; s + 4 < p.S; s += 8) {
+    int s = sl;
+    for (; s + L < p.S; s += 2 * L) {
       a0 += src[(size_t)s * st];
-      a1 += src[(size_t)(s + 4) * st];
+      a1 += src[(size_t)(s + L) * st];
     }
-    for (; s < p.S; s += 4) a0 += src[(size_t)s * st];
+    for (; s < p.S; s += L) a0 += src[(size_t)s * st];
   }
   float acc = a0 + a1;
-  acc += __shfl_xor(acc, 1);
-  acc += __shfl_xor(acc, 2);
-  if (!ok || s4 != 0) return;
+#pragma unroll
+  for (int o = 1; o < L; o <<= 1) acc += __shfl_xor(acc, o);
+  if (!ok || sl != 0) return;
   float* dst;
   if (k < p.kfeat) {
     int kk = k;
@@ -345,7 +345,9 @@ void gemm_splitk_fwd(DType t, const GemmParams& p0, float* scratch, int splitk, 
 
 void dw_reduce(const DwReduceParams& p, hipStream_t s) {
   const int64_t n = (int64_t)p.Nout * (p.kfeat + 1);
-  hipLaunchKernelGGL(dw_reduce_kernel, dim3((unsigned)((4 * n + 255) / 256)), dim3(256), 0, s, p);
+  if (p.S >= 256) hipLaunchKernelGGL(dw_reduce_kernel<64>, dim3((unsigned)((64 * n + 255) / 256)), dim3(256), 0, s, p);
+  else if (p.S >= 64) hipLaunchKernelGGL(dw_reduce_kernel<16>, dim3((unsigned)((16 * n + 255) / 256)), dim3(256), 0, s, p);
+  else hipLaunchKernelGGL(dw_reduce_kernel<4>, dim3((unsigned)((4 * n + 255) / 256)), dim3(256), 0, s, p);
 }
 
 }  // namespace gpu
