@@ -48,7 +48,10 @@ __host__ __device__ inline size_t fc_lds(int N, int ldw, int K) {
   return (size_t)fc_welems(N, ldw, K) * 2 + (size_t)fc_npad(N) * 4 + (size_t)4 * 16 * kFcStageLd * 2;
 }
 
-template <int EPI, int ACT, int NCH>
+// P (persistent): large W (one or two workgroups per CU) is staged once per
+// workgroup and reused over several row blocks; small W keeps one row block
+// per workgroup (enough workgroups per CU to hide the A-fragment latency).
+template <int EPI, int ACT, int NCH, bool P>
 __global__ void __launch_bounds__(kFcThreads) fc_kernel(FcParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int ldk = p.ldw;
@@ -79,20 +82,27 @@ __global__ void __launch_bounds__(kFcThreads) fc_kernel(FcParams p) {
   }
 
   // ---- this wave's A fragments, straight from HBM into registers.  K need
-  // not be a multiple of 8: producers leave the leading-dim padding at 0 ----
-  const int row0 = blockIdx.x * kFcRows + wave * 16;
-  const int arow = row0 + r16;
+  // not be a multiple of 8: producers leave the leading-dim padding at 0.
+  // Persistent: the workgroup keeps W and walks row blocks blockIdx.x,
+  // +gridDim.x, ... (W is staged once per CU instead of once per 64 rows) ----
   const bf16* A = static_cast<const bf16*>(p.A);
+  const int nrb = (p.M + kFcRows - 1) / kFcRows;
   bf16x8 a[NCH];
+  auto load_a = [&](int rb) {
+    const int arow = rb * kFcRows + wave * 16 + r16;
 #pragma unroll
-  for (int q = 0; q < NCH; ++q) {
-    const int k = q * 32 + 8 * g;
-    if (arow < p.M && k < p.K) a[q] = load8(A + (size_t)arow * p.lda + k);
-    else a[q] = bf16x8{};
-  }
+    for (int q = 0; q < NCH; ++q) {
+      const int k = q * 32 + 8 * g;
+      if (arow < p.M && k < p.K) a[q] = load8(A + (size_t)arow * p.lda + k);
+      else a[q] = bf16x8{};
+    }
+  };
+  load_a(blockIdx.x);
   if (dbg && lane == 0) dbg[1] = (long long)__builtin_amdgcn_s_memrealtime();
   __syncthreads();  // also drains the DMA (vmcnt)
   if (dbg && lane == 0) dbg[2] = (long long)__builtin_amdgcn_s_memrealtime();
+  for (int rb = blockIdx.x; rb < (P ? nrb : (int)blockIdx.x + 1); rb += gridDim.x) {
+  const int row0 = rb * kFcRows + wave * 16;
 
   auto epilogue = [&](const f32x4& acc, int tile, int slot) {
     const int col = tile * 16 + r16;
@@ -166,6 +176,8 @@ __global__ void __launch_bounds__(kFcThreads) fc_kernel(FcParams p) {
     }
     __builtin_amdgcn_wave_barrier();
   }
+  if (P && rb + (int)gridDim.x < nrb) load_a(rb + gridDim.x);
+  }  // row blocks
   if (dbg && lane == 0) dbg[3] = (long long)__builtin_amdgcn_s_memrealtime();
 }
 
@@ -186,19 +198,24 @@ void fc_forward(const FcParams& p, hipStream_t s) {
                 (p.epi == EPI_LOGITS || p.ldc % 8 == 0),
             "fc_forward: leading dims must be multiples of 8 covering K");
   if (p.M <= 0) return;
-  const dim3 grid((unsigned)cdiv(p.M, kFcRows)), block(kFcThreads);
   const size_t lds = fc_lds(p.N, p.ldw, p.K);
+  // persistent (as many workgroups as the LDS lets every CU hold) when W
+  // limits the CU to one or two workgroups
+  const int per_cu = std::max(1, std::min(8, (int)((160 * 1024) / (lds + 1024))));
+  const bool persist = per_cu <= 2;
+  const dim3 grid((unsigned)(persist ? std::min(cdiv(p.M, kFcRows), 256 * per_cu) : cdiv(p.M, kFcRows))),
+      block(kFcThreads);
   MCC_CHECK(lds <= 160 * 1024, "fc_forward: weights do not fit in LDS");
   const int nchb = fc_nchb(p.K);
   auto go = [&](auto kern) { hipLaunchKernelGGL(kern, grid, block, lds, s, p); };
   auto by_nch = [&](auto tag) {
     constexpr int EPI = decltype(tag)::epi, ACT = decltype(tag)::act;
     switch (nchb) {
-      case 1: go(fc_kernel<EPI, ACT, 1>); break;
-      case 2: go(fc_kernel<EPI, ACT, 2>); break;
-      case 4: go(fc_kernel<EPI, ACT, 4>); break;
-      case 8: go(fc_kernel<EPI, ACT, 8>); break;
-      default: go(fc_kernel<EPI, ACT, 16>); break;
+      case 1: (persist ? go(fc_kernel<EPI, ACT, 1, true>) : go(fc_kernel<EPI, ACT, 1, false>)); break;
+      case 2: (persist ? go(fc_kernel<EPI, ACT, 2, true>) : go(fc_kernel<EPI, ACT, 2, false>)); break;
+      case 4: (persist ? go(fc_kernel<EPI, ACT, 4, true>) : go(fc_kernel<EPI, ACT, 4, false>)); break;
+      case 8: (persist ? go(fc_kernel<EPI, ACT, 8, true>) : go(fc_kernel<EPI, ACT, 8, false>)); break;
+      default: (persist ? go(fc_kernel<EPI, ACT, 16, true>) : go(fc_kernel<EPI, ACT, 16, false>)); break;
     }
   };
   switch (p.epi) {
