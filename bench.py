@@ -55,6 +55,11 @@ def main():
     ap.add_argument("--momentum", type=float, default=0.9)
     ap.add_argument("--no-dist", action="store_true",
                     help="N=1 only: no process group, no collectives (A/B against the RCCL path)")
+    ap.add_argument("--graph", choices=["auto", "on", "off"], default="auto",
+                    help="replay the whole step (sampler, fwd, loss, bwd, bucketed RCCL all-reduce, SGD) "
+                         "from a HIP graph; auto = on at N=1 (bit-equal to eager: tests/test_gpu_rccl.py) "
+                         "with a fallback to per-kernel launches if capture fails, off at N>1 (multi-rank "
+                         "capture of the collectives is not verifiable on a one-GPU box)")
     args = ap.parse_args()
 
     import torch
@@ -98,15 +103,42 @@ def main():
         init="fast",
         bucket_bytes=int(args.bucket_mb * (1 << 20)),
     )
-    gen = torch.Generator(device=dev)
-    gen.manual_seed(rank)
+    # device minibatch sampler (rand() % N semantics, cnn.c:455): indices and
+    # its step counter live on the GPU, so a graph replay draws a fresh batch
+    K = mcc._C.kernels
+    idx_buf = torch.empty(B, dtype=torch.int32, device=dev)
+    counter = torch.zeros(1, dtype=torch.int64, device=dev)
+    seed = 0x5EED0000 + rank
 
-    def step():
-        idx = torch.randint(0, args.dataset, (B,), device=dev, dtype=torch.int32, generator=gen)
-        tr.step(d_img, d_lab, idx)
+    def step_launch():
+        s = torch.cuda.current_stream(dev).cuda_stream
+        K.sample_indices(idx_buf.data_ptr(), B, 0, args.dataset, seed, counter.data_ptr(), s)
+        tr.step(d_img, d_lab, idx_buf)
+        K.advance_counter(counter.data_ptr(), s)
 
+    step = step_launch
+    graph_note = "per-kernel launches" + (" (--graph off)" if args.graph == "off" else "")
+    coll_graph = None
     tr.zero_stats()
-    for _ in range(args.warmup):
+    step_launch()  # eager first: code objects loaded, RCCL communicator warmed up
+    torch.cuda.synchronize()
+    if args.graph == "on" or (args.graph == "auto" and world == 1):
+        from mpi_cuda_cnn_amd.trainer import capture_step
+
+        issued_before = tr.sync.issued
+        g, why = capture_step(step_launch)
+        ok = torch.tensor([1 if g is not None else 0], device=dev, dtype=torch.int32)
+        if dist.is_initialized():  # every rank replays or none does (collectives inside)
+            dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        if int(ok.item()) == 1:
+            coll_graph = tr.sync.issued - issued_before
+            step = g.replay
+            graph_note = "hip graph: whole step captured once (torch.cuda.CUDAGraph), replayed per step"
+        else:
+            if args.graph == "on":
+                raise RuntimeError(f"--graph on: capture failed: {why}")
+            graph_note = f"off (capture failed: {why})"
+    for _ in range(max(0, args.warmup - 1)):
         step()
     torch.cuda.synchronize()
     if dist.is_initialized():
@@ -122,7 +154,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    coll_per_step = (tr.sync.issued - issued0) / max(1, args.steps)
+    coll_per_step = (tr.sync.issued - issued0) / max(1, args.steps) if coll_graph is None else coll_graph
     if dist.is_initialized():
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -156,6 +188,7 @@ def main():
                               f"bucket(s) <= {args.bucket_mb} MiB, async on RCCL's stream, joined before SGD"
                               if coll_per_step else "none (--no-dist)"),
                 "train_loss_last": round(st["loss_sum"] / (B * args.steps), 4),
+                "launch": graph_note,
             },
         }
         print(json.dumps(out), flush=True)

@@ -376,6 +376,16 @@ PYBIND11_MODULE(_C, m) {
         py::arg("B"), py::arg("H"), py::arg("W"), py::arg("C"), py::arg("Cout"), py::arg("KS"), py::arg("stride"),
         py::arg("pad"), py::arg("dz"), py::arg("ldz"), py::arg("input"), py::arg("slab"), py::arg("slab_stride"),
         py::arg("splitk"), py::arg("gw"), py::arg("gb"), py::arg("beta") = 0.f, py::arg("stream") = 0);
+  // device minibatch sampler (rand() % N semantics, cnn.c:455) with the step
+  // counter in device memory: graph-capturable (a replay draws fresh indices)
+  k.def("sample_indices",
+        [](uintptr_t idx, int B, int64_t lo, int64_t hi, uint64_t seed, uintptr_t step, uintptr_t s) {
+          gpu::sample_indices(ptr<int32_t>(idx), B, lo, hi, seed, ptr<const uint64_t>(step), stream_of(s));
+        },
+        py::arg("idx"), py::arg("B"), py::arg("lo"), py::arg("hi"), py::arg("seed"), py::arg("step"),
+        py::arg("stream") = 0);
+  k.def("advance_counter", [](uintptr_t step, uintptr_t s) { gpu::advance_counter(ptr<uint64_t>(step), stream_of(s)); },
+        py::arg("step"), py::arg("stream") = 0);
   k.def("sgd_update",
         [](uintptr_t p, uintptr_t g, uintptr_t v, int64_t n, float lr, float mu, float wd, uintptr_t s) {
           gpu::sgd_update(ptr<float>(p), ptr<const float>(g), ptr<float>(v), n, lr, mu, wd, stream_of(s));

@@ -89,3 +89,24 @@ class GpuTrainer:
 
     def state_dict(self) -> np.ndarray:
         return self.net.get_params()
+
+
+def capture_step(fn):
+    """Capture ``fn()`` -- a training step that launches everything on the
+    current stream (engine kernels, the device sampler, the bucketed RCCL
+    all-reduces) -- into a HIP graph via ``torch.cuda.CUDAGraph`` and return
+    ``(graph, None)``; ``(None, reason)`` if capture is not possible here.
+
+    A replay re-issues every kernel and collective of the step with the
+    captured pointers: callers keep their buffers (batch indices, sampler
+    counter) alive and fixed.  Run ``fn`` eagerly at least once before (code
+    objects loaded, RCCL communicator set up)."""
+    g = torch.cuda.CUDAGraph()
+    try:
+        with torch.cuda.graph(g):
+            fn()
+    except Exception as e:  # capture unsupported by a component: caller falls back to eager
+        torch.cuda.synchronize()
+        return None, f"{type(e).__name__}: {str(e)[:120]}"
+    return g, None
+

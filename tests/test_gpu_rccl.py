@@ -110,3 +110,66 @@ def test_cnn_dist_rccl_world1_bit_equal(idx_files, tmp_path):
     np.testing.assert_array_equal(p_g, p_e)  # graph replay == eager
     np.testing.assert_array_equal(p_g, p_p)  # --profile (event-timed phases) == graph
     assert js_g["ncorrect"] >= 0.9 * js_g["ntests"]
+
+
+def _graph_worker(rank, out):
+    """Eager steps vs one eager step + HIP-graph replays of the captured step
+    (bench.py --graph), both under the world-1 RCCL group, same init."""
+    import torch.distributed as dist
+
+    from mpi_cuda_cnn_amd.parallel.ddp import init_process_group
+    from mpi_cuda_cnn_amd.trainer import GpuTrainer, capture_step
+
+    os.environ.pop("MASTER_PORT", None)
+    os.environ.update(RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    init_process_group("nccl", dev)
+    spec = mcc.make_model("lenet5")
+    imgs, labels = mcc.synth_dataset(4096, 1, 28, 28, 10, seed=9)
+    d_img, d_lab = torch.from_numpy(imgs).to(dev), torch.from_numpy(labels).to(dev)
+    K = mcc._C.kernels
+    res = []
+    for graphed in (False, True):
+        tr = GpuTrainer(spec, dtype="bf16", batch=B, device=0, lr=LR, momentum=MOM,
+                        params=mcc.init_params(spec, seed=3, mode="fast"), bucket_bytes=BUCKET)
+        idx = torch.empty(B, dtype=torch.int32, device=dev)
+        ctr = torch.zeros(1, dtype=torch.int64, device=dev)
+
+        def launch():
+            s = torch.cuda.current_stream().cuda_stream
+            K.sample_indices(idx.data_ptr(), B, 0, 4096, 77, ctr.data_ptr(), s)
+            tr.step(d_img, d_lab, idx)
+            K.advance_counter(ctr.data_ptr(), s)
+
+        launch()
+        torch.cuda.synchronize()
+        if graphed:
+            g, why = capture_step(launch)
+            assert g is not None, why
+            for _ in range(STEPS):
+                g.replay()
+        else:
+            for _ in range(STEPS):
+                launch()
+        torch.cuda.synchronize()
+        res.append((tr.state_dict(), int(ctr.item()), tr.sync.issued, len(tr.sync.buckets)))
+    (pe, ce, ie, nb), (pg, cg, ig, _) = res
+    np.save(os.path.join(out, "pe.npy"), pe)
+    np.save(os.path.join(out, "pg.npy"), pg)
+    np.save(os.path.join(out, "meta.npy"), np.array([ce, cg, ie, ig, nb]))
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_python_graph_replay_bit_equal(cuda, tmp_path):
+    """bench.py's graph mode: a captured step (device sampler, engine kernels,
+    bucketed RCCL all-reduces, fused SGD) replayed K times gives BIT-equal
+    weights to K eager steps, and every replay really advances the sampler."""
+    mp.spawn(_graph_worker, args=(str(tmp_path),), nprocs=1, join=True)
+    pe, pg = np.load(tmp_path / "pe.npy"), np.load(tmp_path / "pg.npy")
+    ce, cg, ie, ig, nb = np.load(tmp_path / "meta.npy")
+    assert ce == cg == STEPS + 1, (ce, cg)
+    assert ie == (STEPS + 1) * nb and ig == 2 * nb, (ie, ig, nb)  # eager: every step; graph: eager + capture
+    assert not np.array_equal(pe, mcc.init_params(mcc.make_model("lenet5"), seed=3, mode="fast"))
+    np.testing.assert_array_equal(pe, pg)
