@@ -417,7 +417,7 @@ __host__ __device__ inline DwLayout dw_layout(const ConvDwPipeParams& p) {
   L.ones_off = o; o += 16;
   L.stage = o;
   const int ntw = dw_ntw(p.cout_pad / 16, p.ncols_pad / 16);
-  L.red = p.cout_pad * ntw * 16 * 4;
+  L.red = p.cout_pad * ntw * 16 * 4 * (p.wsplit ? 4 : 1);
   L.total = L.stage > L.red ? L.stage : L.red;
   return L;
 }

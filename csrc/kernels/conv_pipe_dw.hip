@@ -10,7 +10,7 @@ namespace gpu {
 
 namespace {
 
-template <int XM, int DM, int MTW, int NTW>
+template <int XM, int DM, int MTW, int NTW, bool WS = false>
 __global__ void __launch_bounds__(kT) conv_dw_pipe_kernel(ConvDwPipeParams p) {
   constexpr bool S1 = XM == PM_U8S1;
   constexpr bool PIPE_B = NTW <= 4;  // few column tiles: prefetch B too (else the tiles give the ILP)
@@ -39,7 +39,8 @@ __global__ void __launch_bounds__(kT) conv_dw_pipe_kernel(ConvDwPipeParams p) {
   bool kone[NTW];
 #pragma unroll
   for (int t = 0; t < NTW; ++t) {
-    const int c4 = (blockIdx.y * NTW + t) * 16 + 4 * pp;  // first of this lane's 4 columns
+    // first of this lane's 4 columns (WS: this wave's own tiles)
+    const int c4 = ((WS ? blockIdx.y * 4 + wave : blockIdx.y) * NTW + t) * 16 + 4 * pp;
     koff[t] = 0;
     kone[t] = c4 == p.kbias;
     if (S1) {
@@ -124,7 +125,8 @@ __global__ void __launch_bounds__(kT) conv_dw_pipe_kernel(ConvDwPipeParams p) {
     const int nq = (p.ablate & 2) ? 0 : cdiv(npix, 32);
     // fragment k -> pixel: lane group g reads rows 4g..4g+3 (and +16).
     // Pipelined one pixel chunk deep (pixbase is padded by one chunk).
-    int qc = wave;
+    constexpr int QS = WS ? 1 : kT / 64;  // chunk step: WS waves walk every chunk
+    int qc = WS ? 0 : wave;
     int pix1 = qc * 32 + 4 * g + q;
     int pb1 = 0, pb2 = 0;
     bf16x8 a[MTW], b[NTW];
@@ -137,8 +139,8 @@ __global__ void __launch_bounds__(kT) conv_dw_pipe_kernel(ConvDwPipeParams p) {
         for (int t = 0; t < NTW; ++t) b[t] = read_b(pb1, pb2, t);
       }
     }
-    for (; qc < nq; qc += kT / 64) {
-      const int qn = qc + kT / 64;
+    for (; qc < nq; qc += QS) {
+      const int qn = qc + QS;
       const int pixn = qn * 32 + 4 * g + q;
       const bool more = qn < nq;
       const int pbn1 = more ? pixbase[pixn] : 0, pbn2 = more ? pixbase[pixn + 16] : 0;
@@ -170,8 +172,18 @@ __global__ void __launch_bounds__(kT) conv_dw_pipe_kernel(ConvDwPipeParams p) {
     }
   }
   // combine the waves in a fixed order: red[MTW*16 rows][NTW*16 cols]
-  const int rcols = NTW * 16;
-  for (int w = 0; w < kT / 64; ++w) {
+  // (WS: each wave owns its NTW*16 columns of red[MTW*16][4*NTW*16])
+  const int rcols = (WS ? 4 : 1) * NTW * 16;
+  if constexpr (WS) {
+    __syncthreads();  // red aliases the staged tiles
+#pragma unroll
+    for (int m = 0; m < MTW; ++m)
+#pragma unroll
+      for (int t = 0; t < NTW; ++t)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) red[(m * 16 + 4 * g + i) * rcols + (wave * NTW + t) * 16 + r16] = acc[m][t][i];
+  }
+  for (int w = 0; w < (WS ? 0 : kT / 64); ++w) {
     __syncthreads();
     if (wave == w) {
 #pragma unroll
@@ -288,6 +300,12 @@ bool conv_dw_pipe_plan(ConvDwPipeParams& p) {
   // the im2col operand), computed by the same MFMAs
   p.kbias = s1 ? p.KS * 8 : KK * CL;
   p.ncols_pad = r16h(p.kbias + 1);
+  // wide outputs (>= 4 row tiles) split the column tiles over the waves when
+  // there are enough of them (4 waves x NTW)
+  {
+    const int mtw = p.cout_pad / 16, nct = p.ncols_pad / 16;
+    p.wsplit = mtw >= 4 && nct >= 2 * dw_ntw(mtw, nct) && !pipe_knob("MCC_NO_DW_WSPLIT", 0) ? 1 : 0;
+  }
   const int nix = mode_ni(x.mode) * kT / std::max(1, x.per_img);
   const int nid = mode_ni(d.mode) * kT / std::max(1, d.per_img);
   int imgs = std::max(1, std::min(16, std::min(nix, nid)));
@@ -314,7 +332,7 @@ void conv_dw_pipe(const ConvDwPipeParams& pin, hipStream_t st) {
   const int mtw = p.cout_pad / 16;
   const int ncol_tiles = p.ncols_pad / 16;
   const int ntw = dw_ntw(mtw, ncol_tiles);
-  const dim3 grid((unsigned)p.grid, (unsigned)cdiv(ncol_tiles, ntw)), block(kT);
+  const dim3 grid((unsigned)p.grid, (unsigned)cdiv(ncol_tiles, ntw * (p.wsplit ? 4 : 1))), block(kT);
   auto go = [&](auto kern) { hipLaunchKernelGGL(kern, grid, block, p.lds, st, p); };
 #define MCC_DW_TILES(XM, DM)                                     \
   if (mtw <= 1) {                                                \
@@ -325,7 +343,10 @@ void conv_dw_pipe(const ConvDwPipeParams& pin, hipStream_t st) {
     else if (ntw == 13) go(conv_dw_pipe_kernel<XM, DM, 1, 13>);  \
     else go(conv_dw_pipe_kernel<XM, DM, 1, 16>);                 \
   } else if (mtw <= 2) go(conv_dw_pipe_kernel<XM, DM, 2, 8>);   \
-  else if (mtw <= 4) go(conv_dw_pipe_kernel<XM, DM, 4, 4>);     \
+  else if (mtw <= 4) {                                           \
+    if (p.wsplit) go(conv_dw_pipe_kernel<XM, DM, 4, 4, true>);   \
+    else go(conv_dw_pipe_kernel<XM, DM, 4, 4>);                  \
+  } else if (p.wsplit) go(conv_dw_pipe_kernel<XM, DM, 8, 2, true>); \
   else go(conv_dw_pipe_kernel<XM, DM, 8, 2>);
 #define MCC_DW_DM(XM)                                            \
   if (p.dy.mode == PM_UNPOOL) { MCC_DW_TILES(XM, PM_UNPOOL) }    \

@@ -146,37 +146,36 @@ __global__ void __launch_bounds__(kIgT, 2) igemm_conv_kernel(IgemmParams p) {
     const int s = j * kIgT + tid;
     const int row = s >> 3;
     a_seg[j] = ((s & 7) ^ swz64(row)) * 8;
-    a_img[j] = in8;
+    // decoded for a clamped row (branch-free: the U8 sample-index loads of
+    // all four rows issue together), then invalidated by a select
     const int m = m0 + row;
-    if (m < p.M) {
-      int b, oy, ox;
-      if (POOL) {  // m = ((b*PH + py)*PW + px)*4 + pos
-        const int q = m >> 2, pos = m & 3;
-        b = mdiv(p.div_ohw, q);  // div_ohw = PH*PW here
-        const int rq = q - b * (p.OH >> 1) * (p.OW >> 1);
-        const int py = mdiv(p.div_ow, rq), px = rq - py * (p.OW >> 1);  // div_ow = PW
-        oy = 2 * py + (pos >> 1);
-        ox = 2 * px + (pos & 1);
-      } else {
-        b = mdiv(p.div_ohw, m);
-        const int rem = m - b * p.OH * p.OW;
-        oy = mdiv(p.div_ow, rem);
-        ox = rem - oy * p.OW;
-      }
-      a_iy[j] = oy * p.stride - p.pad;
-      a_ix[j] = ox * p.stride - p.pad;
-      if (U8) {  // image base in a 64-bit pointer (large image sets), pixel offset in a_base
-        const int img = p.idx ? p.idx[b] : b;
-        a_img[j] = in8 + (size_t)img * p.H * p.W * p.C;
-        a_base[j] = (a_iy[j] * p.W + a_ix[j]) * p.C;
-      } else {
-        a_base[j] = ((b * p.H + a_iy[j]) * p.W + a_ix[j]) * p.C;
-      }
+    const int mc = m < p.M ? m : p.M - 1;
+    int b, oy, ox;
+    if (POOL) {  // m = ((b*PH + py)*PW + px)*4 + pos
+      const int q = mc >> 2, pos = mc & 3;
+      b = mdiv(p.div_ohw, q);  // div_ohw = PH*PW here
+      const int rq = q - b * (p.OH >> 1) * (p.OW >> 1);
+      const int py = mdiv(p.div_ow, rq), px = rq - py * (p.OW >> 1);  // div_ow = PW
+      oy = 2 * py + (pos >> 1);
+      ox = 2 * px + (pos & 1);
     } else {
-      a_iy[j] = -(1 << 20);  // fails every bounds test
-      a_ix[j] = 0;
-      a_base[j] = 0;
+      b = mdiv(p.div_ohw, mc);
+      const int rem = mc - b * p.OH * p.OW;
+      oy = mdiv(p.div_ow, rem);
+      ox = rem - oy * p.OW;
     }
+    const int iy = oy * p.stride - p.pad, ix = ox * p.stride - p.pad;
+    if (U8) {  // image base in a 64-bit pointer (large image sets), pixel offset in a_base
+      const int img = p.idx ? p.idx[b] : b;
+      a_img[j] = in8 + (size_t)img * p.H * p.W * p.C;
+      a_base[j] = (iy * p.W + ix) * p.C;
+    } else {
+      a_img[j] = in8;
+      a_base[j] = ((b * p.H + iy) * p.W + ix) * p.C;
+    }
+    a_iy[j] = m < p.M ? iy : -(1 << 20);  // fails every bounds test
+    a_ix[j] = ix;
+    if (m >= p.M) a_base[j] = 0;
   }
   const bf16* b_ptr[BJ];
   int b_k[BJ];
@@ -196,21 +195,31 @@ __global__ void __launch_bounds__(kIgT, 2) igemm_conv_kernel(IgemmParams p) {
     bf16* Bw = A + BM * kIgBK;
     if constexpr (U8) {
       const float sc = 1.0f / 255.0f;
+      uint8_t raw[AJ][8];
+      uint32_t inb[AJ] = {};
 #pragma unroll
       for (int j = 0; j < AJ; ++j) {
-        bf16x8 v;
         const int4 t0 = *reinterpret_cast<const int4*>(ktab + k0 + a_seg[j]);
         const int4 t1 = *reinterpret_cast<const int4*>(ktab + k0 + a_seg[j] + 4);
         const int tv[8] = {t0.x, t0.y, t0.z, t0.w, t1.x, t1.y, t1.z, t1.w};
+        // every byte load is unconditional (padding taps read byte 0 of the
+        // image and are zeroed by a select): a guarded load compiles to a
+        // branch + vmcnt(0) per element, 32 serialised memory latencies
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          float f = 0.f;
           const int t = tv[e];
           const int iy = a_iy[j] + ((t >> 4) & 15), ix = a_ix[j] + (t & 15);
-          if (t >= 0 && (unsigned)iy < (unsigned)p.H && (unsigned)ix < (unsigned)p.W)
-            f = (float)a_img[j][a_base[j] + (t >> 8)] * sc;
-          v[e] = (bf16)f;
+          const bool in = t >= 0 && (unsigned)iy < (unsigned)p.H && (unsigned)ix < (unsigned)p.W;
+          raw[j][e] = a_img[j][in ? a_base[j] + (t >> 8) : 0];
+          inb[j] |= (uint32_t)in << e;
         }
+      }
+      // all 32 loads are in flight before the first conversion
+#pragma unroll
+      for (int j = 0; j < AJ; ++j) {
+        bf16x8 v;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = (bf16)((inb[j] >> e & 1u) ? (float)raw[j][e] * sc : 0.f);
         store8(A + (j * kIgT + tid) * 8, v);
       }
     } else {

@@ -192,6 +192,10 @@ struct ConvDwPipeParams {
   // planner outputs
   int layout = XL_C8, imgs = 1, ngroups = 0, grid = 0, LH = 0;
   int cout_pad = 0, drow = 0, kbias = 0, ncols_pad = 0, ppad = 0;
+  // wsplit: the 4 waves own different column tiles and each walks every
+  // pixel chunk (wide-Cout layers: the staged group is shared by 4x more
+  // columns; otherwise the waves split the pixel chunks of the same tiles)
+  int wsplit = 0;
   size_t lds = 0;
   int ablate = 0;  // diagnostics: 1 no staging, 2 no MFMA loop
 };
