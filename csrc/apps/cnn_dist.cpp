@@ -170,9 +170,6 @@ struct RcclComm : Comm {
   void allreduce_sum_f32(float* buf, int64_t n, hipStream_t s) override {
     NCCLCHK(ncclAllReduce(buf, buf, (size_t)n, ncclFloat32, ncclSum, comm_, s));
   }
-  void allreduce_avg_f32(float* buf, int64_t n, hipStream_t s) override {
-    NCCLCHK(ncclAllReduce(buf, buf, (size_t)n, ncclFloat32, ncclAvg, comm_, s));
-  }
   void allreduce_max_f64(double* buf, int64_t n, hipStream_t s) override {
     NCCLCHK(ncclAllReduce(buf, buf, (size_t)n, ncclFloat64, ncclMax, comm_, s));
   }

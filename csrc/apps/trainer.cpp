@@ -167,10 +167,11 @@ int run_gpu_training(const CliArgs& a, Comm& comm, const char* program) {
   hipEvent_t ev_join;
   for (auto& e : ev_b) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   HIPCHK(hipEventCreateWithFlags(&ev_join, hipEventDisableTiming));
-  // The loss is scaled by 1/b (this rank's batch) and the bucket all-reduce
-  // averages over ranks (ncclAvg), so the update uses the global-batch mean.
-  // (At one rank RCCL still runs its one-rank reduce kernel on stream C.)
-  const float grad_scale = 1.0f / (float)b;
+  // The loss is scaled by 1/(b*world) and the bucket all-reduce sums over
+  // ranks, so the update uses the global-batch mean.  (ncclAvg is a
+  // pre-multiplied sum in RCCL: at one rank it still streams the whole bucket
+  // through a "oneRankReduce" kernel, while an in-place one-rank SUM is elided.)
+  const float grad_scale = 1.0f / ((float)b * (float)world);
   PhaseTimer timer(a.profile);
 
   auto step = [&](bool timed) {
@@ -186,7 +187,7 @@ int run_gpu_training(const CliArgs& a, Comm& comm, const char* program) {
         // continues with the earlier stages' backward
         HIPCHK(hipEventRecord(ev_b[k], S));
         HIPCHK(hipStreamWaitEvent(C, ev_b[k], 0));
-        comm.allreduce_avg_f32(net.grads() + buckets[k].off, buckets[k].count, C);
+        comm.allreduce_sum_f32(net.grads() + buckets[k].off, buckets[k].count, C);
       }
     }
     if (timed) timer.mark(2, S);

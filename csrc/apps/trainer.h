@@ -32,8 +32,6 @@ struct Comm {
     if (hipEventSynchronize(ev) != hipSuccess) throw Error("hipEventSynchronize failed");
   }
   virtual void allreduce_sum_f32(float* buf, int64_t n, hipStream_t s) = 0;
-  // mean over ranks (the gradient buckets: RCCL scales inside the collective)
-  virtual void allreduce_avg_f32(float* buf, int64_t n, hipStream_t s) = 0;
   virtual void allreduce_max_f64(double* buf, int64_t n, hipStream_t s) = 0;
   virtual void broadcast_f32(float* buf, int64_t n, int root, hipStream_t s) = 0;
   virtual void barrier() = 0;
@@ -46,7 +44,6 @@ struct LocalComm : Comm {
   const char* name() const override { return "local"; }
   bool collective() const override { return false; }
   void allreduce_sum_f32(float*, int64_t, hipStream_t) override {}
-  void allreduce_avg_f32(float*, int64_t, hipStream_t) override {}
   void allreduce_max_f64(double*, int64_t, hipStream_t) override {}
   void broadcast_f32(float*, int64_t, int, hipStream_t) override {}
   void barrier() override {}

@@ -347,7 +347,8 @@ PYBIND11_MODULE(_C, m) {
   k.def("igemm_conv_supported", &gpu::igemm_conv_supported);
   k.def("igemm_conv",
         [](int B, int H, int W, int C, int N, int KS, int stride, int pad, uintptr_t in, uintptr_t w, int ldw,
-           uintptr_t bias, bool bias_act, int act, uintptr_t out, int ldo, uintptr_t s) {
+           uintptr_t bias, bool bias_act, int act, uintptr_t out, int ldo, uintptr_t out_arg, int tile,
+           uintptr_t s) {
           gpu::IgemmParams p;
           p.B = B; p.H = H; p.W = W; p.C = C; p.N = N; p.KS = KS; p.stride = stride; p.pad = pad;
           p.OH = (H + 2 * pad - KS) / stride + 1; p.OW = (W + 2 * pad - KS) / stride + 1;
@@ -355,27 +356,30 @@ PYBIND11_MODULE(_C, m) {
           p.in = ptr<void>(in); p.w = ptr<void>(w); p.ldw = ldw;
           p.bias = ptr<float>(bias); p.epi_bias_act = bias_act; p.act = act;
           p.out = ptr<void>(out); p.ldo = ldo;
+          p.pool = out_arg != 0; p.out_arg = ptr<uint8_t>(out_arg); p.tile = tile;
           gpu::igemm_conv(p, stream_of(s));
         },
         py::arg("B"), py::arg("H"), py::arg("W"), py::arg("C"), py::arg("N"), py::arg("KS"), py::arg("stride"),
         py::arg("pad"), py::arg("input"), py::arg("w"), py::arg("ldw"), py::arg("bias") = 0,
         py::arg("bias_act") = true, py::arg("act") = 0, py::arg("out") = 0, py::arg("ldo") = 0,
-        py::arg("stream") = 0);
-  k.def("igemm_dw_splitk", &gpu::igemm_dw_splitk);
+        py::arg("out_arg") = 0, py::arg("tile") = -1, py::arg("stream") = 0);
+  k.def("igemm_dw_splitk", &gpu::igemm_dw_splitk, py::arg("M"), py::arg("Cout"), py::arg("kf"), py::arg("tile") = -1);
   k.def("igemm_dw",
         [](int B, int H, int W, int C, int Cout, int KS, int stride, int pad, uintptr_t dz, int ldz, uintptr_t in,
-           uintptr_t slab, int64_t slab_stride, int splitk, uintptr_t gw, uintptr_t gb, float beta, uintptr_t s) {
+           uintptr_t slab, int64_t slab_stride, int splitk, uintptr_t gw, uintptr_t gb, float beta, int tile,
+           uintptr_t s) {
           gpu::IgemmDwParams p;
           p.B = B; p.H = H; p.W = W; p.C = C; p.Cout = Cout; p.KS = KS; p.stride = stride; p.pad = pad;
           p.OH = (H + 2 * pad - KS) / stride + 1; p.OW = (W + 2 * pad - KS) / stride + 1;
           p.M = B * p.OH * p.OW; p.kf = KS * KS * C;
           p.dz = ptr<void>(dz); p.ldz = ldz; p.in = ptr<void>(in);
-          p.slab = ptr<float>(slab); p.slab_stride = slab_stride; p.splitk = splitk;
+          p.slab = ptr<float>(slab); p.slab_stride = slab_stride; p.splitk = splitk; p.tile = tile;
           gpu::igemm_dw(p, ptr<float>(gw), ptr<float>(gb), beta, stream_of(s));
         },
         py::arg("B"), py::arg("H"), py::arg("W"), py::arg("C"), py::arg("Cout"), py::arg("KS"), py::arg("stride"),
         py::arg("pad"), py::arg("dz"), py::arg("ldz"), py::arg("input"), py::arg("slab"), py::arg("slab_stride"),
-        py::arg("splitk"), py::arg("gw"), py::arg("gb"), py::arg("beta") = 0.f, py::arg("stream") = 0);
+        py::arg("splitk"), py::arg("gw"), py::arg("gb"), py::arg("beta") = 0.f, py::arg("tile") = -1,
+        py::arg("stream") = 0);
   // device minibatch sampler (rand() % N semantics, cnn.c:455) with the step
   // counter in device memory: graph-capturable (a replay draws fresh indices)
   k.def("sample_indices",

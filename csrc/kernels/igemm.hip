@@ -330,6 +330,327 @@ __global__ void __launch_bounds__(kIgT, 2) igemm_conv_kernel(IgemmParams p) {
 }
 
 // ---------------------------------------------------------------------------
+// forward / data gradient on 256-pixel x BC-channel tiles, phase-pipelined
+// ---------------------------------------------------------------------------
+// The 128x128 kernel above streams 32 KiB of operands per 2.1 MFLOP K-step
+// and drains every LDS-DMA at each __syncthreads: on the VGG layers it runs
+// at ~30% of the bf16 MFMA peak, bound by the per-CU fetch rate.  Here one
+// 512-thread workgroup per CU owns a 256 x BC tile (2x / 1.5x the flops per
+// staged byte) and keeps up to three quarter-tiles of DMA in flight across
+// its barriers (cdna_hip_programming.md §5 "The 256² 8-phase template"):
+//   LDS   2 buffers x [A0 | A1 | B0 | B1], A = weight halves (BC/2 channel
+//         rows), B = pixel halves (128 rows), each row 64 k (128 B, swz64);
+//   waves 2 (channels) x 4 (pixels); wave (wr, wc) owns channels
+//         hA*BC/2 + wr*BC/4 + [0, BC/4) and pixels hB*128 + wc*32 + [0, 32)
+//         of each quadrant (hA, hB);
+//   phase p0 (A0,B0)  p1 (A0,B1)  p2 (A1,B1)  p3 (A1,B0): the A/B register
+//         subtiles are read once per K-tile (p0: A0+B0, p1: B1, p2: A1), and
+//         phase p stages quarter p of the NEXT K-tile (A0', B0', B1', A1'),
+//         so the counted wait before phase p's barrier retires exactly the
+//         quarter that phase reads (one barrier later, rule "read a staged
+//         buffer one phase after the wait that retires it").
+// Raw s_barrier + counted vmcnt: __syncthreads() would emit vmcnt(0) and drain
+// the prefetch (guide §5 "Pipelining across barriers").
+template <int N> __device__ __forceinline__ void vm_wait();
+#define MCC_VM_WAIT(n) \
+  template <> __device__ __forceinline__ void vm_wait<n>() { asm volatile("s_waitcnt vmcnt(" #n ")" ::: "memory"); }
+MCC_VM_WAIT(0) MCC_VM_WAIT(1) MCC_VM_WAIT(2) MCC_VM_WAIT(3) MCC_VM_WAIT(4) MCC_VM_WAIT(6)
+#undef MCC_VM_WAIT
+__device__ __forceinline__ void raw_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+constexpr int kBigT = 512;
+constexpr int kBigBP = 256;
+
+// K loop of the 256-tile kernels.  Quadrant order (A0,B0) (A0,B1) (A1,B1)
+// (A1,B0); phase q reads its new register subtile (rd q: 0 = A0+B0, 1 = B1,
+// 2 = A1), stages quarter q of the next K-tile (st q: A0', B0', B1', A1') and
+// runs its MFMAs (mm q).  GA / GB = glds per thread per A / B quarter.
+// PP = false: one barrier per phase, all waves in step (reads, then MFMAs).
+// PP = true (ping-pong): each phase is [reads + stage] barrier [MFMAs]
+// barrier, and wave group 1 (waves 4-7: one wave per SIMD) runs one barrier
+// behind group 0, so on every SIMD one wave's MFMA cluster overlaps the other
+// wave's LDS reads, DMA issue and address math (guide §5, 8-phase template:
+// staggered groups, s_setprio around the MFMA clusters).  The quarter read in
+// phase P is retired by every wave before barrier 2P-1 (group 0: after its
+// MFMAs of P-1; group 1: after its stage of P-1), which both groups' reads of
+// P follow ("read a staged buffer one barrier after the wait").
+template <bool PP, int GA, int GB, class RD, class ST, class MM>
+__device__ __forceinline__ void pipe_loop(int nk, bool grp1, RD&& rd, ST&& st, MM&& mm) {
+  st(0, 0); st(0, 1); st(0, 2); st(0, 3);
+  if constexpr (!PP) {
+    for (int kt = 0; kt < nk; ++kt) {
+      const bool nx = kt + 1 < nk;
+      vm_wait<GA + GB>();  // A0, B0 landed (B1, A1 in flight)
+      raw_barrier();
+      rd(kt, 0);
+      if (nx) st(kt + 1, 0);
+      mm(0);
+      if (nx) vm_wait<2 * GA>(); else vm_wait<GA>();  // B1 (A1, A0' in flight)
+      raw_barrier();
+      rd(kt, 1);
+      if (nx) st(kt + 1, 1);
+      mm(1);
+      if (nx) vm_wait<GA + GB>(); else vm_wait<0>();  // A1 (A0', B0' in flight)
+      raw_barrier();
+      rd(kt, 2);
+      if (nx) st(kt + 1, 2);
+      mm(2);
+      if (nx) st(kt + 1, 3);
+      mm(3);
+    }
+  } else {
+    auto mf = [&](int q) {
+      __builtin_amdgcn_s_setprio(1);
+      mm(q);
+      __builtin_amdgcn_s_setprio(0);
+    };
+    vm_wait<GA + GB>();
+    raw_barrier();
+    if (grp1) raw_barrier();  // stagger
+    for (int kt = 0; kt < nk; ++kt) {
+      const bool nx = kt + 1 < nk;
+      // p0: retire B1 for p1 (A1, A0' may stay in flight)
+      rd(kt, 0);
+      if (nx) st(kt + 1, 0);
+      if (grp1) { if (nx) vm_wait<2 * GA>(); else vm_wait<GA>(); }
+      raw_barrier();
+      mf(0);
+      if (!grp1) { if (nx) vm_wait<2 * GA>(); else vm_wait<GA>(); }
+      raw_barrier();
+      // p1: retire A1 for p2 (A0', B0' may stay in flight)
+      rd(kt, 1);
+      if (nx) st(kt + 1, 1);
+      if (grp1) { if (nx) vm_wait<GA + GB>(); else vm_wait<0>(); }
+      raw_barrier();
+      mf(1);
+      if (!grp1) { if (nx) vm_wait<GA + GB>(); else vm_wait<0>(); }
+      raw_barrier();
+      // p2: p3 reads nothing
+      rd(kt, 2);
+      if (nx) st(kt + 1, 2);
+      raw_barrier();
+      mf(2);
+      raw_barrier();
+      // p3: retire A0', B0' for the next p0 (B1', A1' may stay in flight)
+      if (nx) st(kt + 1, 3);
+      if (grp1 && nx) vm_wait<GA + GB>();
+      raw_barrier();
+      mf(3);
+      if (!grp1 && nx) vm_wait<GA + GB>();
+      raw_barrier();
+    }
+    if (!grp1) raw_barrier();  // balance the stagger
+  }
+}
+
+template <int BC, bool BIAS_ACT, bool POOL, bool PP>
+__global__ void __launch_bounds__(kBigT, 1) igemm_big_kernel(IgemmParams p) {
+  constexpr int BK = kIgBK;
+  constexpr int HA = BC / 2, HB = kBigBP / 2;    // rows per A / B half
+  constexpr int GA = HA * 8 / kBigT, GB = HB * 8 / kBigT;  // glds per thread per half
+  constexpr int QA = HA * BK, QB = HB * BK;        // elements per half image
+  constexpr int BUF = 2 * QA + 2 * QB;             // [A0][A1][B0][B1]
+  constexpr int FA = HA / 2 / 16;                  // channel fragments per wave per half
+  static_assert(GA >= 1 && GB == 2 && FA >= 1, "tile shape");
+  __shared__ __attribute__((aligned(16))) bf16 smem[2 * BUF];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r16 = lane & 15, g = lane >> 4;
+  const int wr = wave >> 2, wc = wave & 3;
+
+  const int ntn = cdiv(p.N, BC);
+  const int tile = xcd_remap(blockIdx.x, gridDim.x);
+  const int tn = tile % ntn, tm = tile / ntn;  // neighbours share the pixel tile
+  const int m0 = tm * kBigBP, n0 = tn * BC;
+  const bf16* in = static_cast<const bf16*>(p.in);
+  const bf16* w = static_cast<const bf16*>(p.w);
+  const bf16* zero = reinterpret_cast<const bf16*>(kIgZero);
+
+  // pixel pieces: half h, j < GB -> row (j*512 + tid) >> 3 of the half
+  int a_iy[2][GB], a_ix[2][GB], a_off[2][GB];
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int j = 0; j < GB; ++j) {
+      const int s = j * kBigT + tid;
+      const int row = s >> 3;
+      const int seg = ((s & 7) ^ swz64(row)) * 8;
+      const int m = m0 + h * HB + row;
+      const int mc = m < p.M ? m : p.M - 1;
+      int b, oy, ox;
+      if (POOL) {  // m = ((b*PH + py)*PW + px)*4 + pos
+        const int q = mc >> 2, pos = mc & 3;
+        b = mdiv(p.div_ohw, q);
+        const int rq = q - b * (p.OH >> 1) * (p.OW >> 1);
+        const int py = mdiv(p.div_ow, rq), px = rq - py * (p.OW >> 1);
+        oy = 2 * py + (pos >> 1);
+        ox = 2 * px + (pos & 1);
+      } else {
+        b = mdiv(p.div_ohw, mc);
+        const int rem = mc - b * p.OH * p.OW;
+        oy = mdiv(p.div_ow, rem);
+        ox = rem - oy * p.OW;
+      }
+      const int iy = oy * p.stride - p.pad, ix = ox * p.stride - p.pad;
+      a_iy[h][j] = m < p.M ? iy : -(1 << 20);  // fails every bounds test
+      a_ix[h][j] = ix;
+      a_off[h][j] = m < p.M ? ((b * p.H + iy) * p.W + ix) * p.C + seg : 0;
+    }
+  // weight pieces: half h, j < GA -> channel row (j*512 + tid) >> 3 of the half
+  const bf16* w_ptr[2][GA];
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int j = 0; j < GA; ++j) {
+      const int s = j * kBigT + tid;
+      const int row = s >> 3;
+      const int n = n0 + h * HA + row;
+      w_ptr[h][j] = n < p.N ? w + (size_t)n * p.ldw + ((s & 7) ^ swz64(row)) * 8 : nullptr;
+    }
+
+  auto stage_a = [&](int kt, int h) {
+    bf16* dst = smem + (kt & 1) * BUF + h * QA;
+    const int k0 = kt * BK;
+#pragma unroll
+    for (int j = 0; j < GA; ++j)
+      glds16(w_ptr[h][j] ? w_ptr[h][j] + k0 : zero, dst + (j * kBigT + wave * 64) * 8);
+  };
+  auto stage_b = [&](int kt, int h) {
+    bf16* dst = smem + (kt & 1) * BUF + 2 * QA + h * QB;
+    const int k0 = kt * BK;
+    const int tap = k0 / p.C;  // uniform; C % 64 == 0
+    const int c0 = k0 - tap * p.C;
+    const int ky = tap / p.KS, kx = tap - ky * p.KS;
+    const int toff = (ky * p.W + kx) * p.C + c0;
+#pragma unroll
+    for (int j = 0; j < GB; ++j) {
+      const int iy = a_iy[h][j] + ky, ix = a_ix[h][j] + kx;
+      const bool ok = (unsigned)iy < (unsigned)p.H && (unsigned)ix < (unsigned)p.W;
+      glds16(ok ? in + (a_off[h][j] + toff) : zero, dst + (j * kBigT + wave * 64) * 8);
+    }
+  };
+
+  f32x4 acc[2][FA][2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int f = 0; f < FA; ++f)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int e = 0; e < 2; ++e) acc[a][f][b][e] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  bf16x8 fa[FA][2], fb0[2][2], fb1[2][2];  // [frag][k half of the 64-deep step]
+  auto read_a = [&](const bf16* img, int h) {
+#pragma unroll
+    for (int f = 0; f < FA; ++f) {
+      const int row = wr * (HA / 2) + f * 16 + r16;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+        fa[f][ks] = load8(img + h * QA + row * BK + (((4 * ks + g) ^ swz64(row)) << 3));
+    }
+  };
+  auto read_b = [&](const bf16* img, int h, bf16x8 (&fb)[2][2]) {
+#pragma unroll
+    for (int f = 0; f < 2; ++f) {
+      const int row = wc * 32 + f * 16 + r16;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+        fb[f][ks] = load8(img + 2 * QA + h * QB + row * BK + (((4 * ks + g) ^ swz64(row)) << 3));
+    }
+  };
+  auto mfma_q = [&](int ha, int hb, const bf16x8 (&fb)[2][2]) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int f = 0; f < FA; ++f)
+#pragma unroll
+        for (int e = 0; e < 2; ++e) acc[ha][f][hb][e] = mma(acc[ha][f][hb][e], fa[f][ks], fb[e][ks]);
+  };
+
+  const int nk = p.K / BK;  // host: K % 64 == 0
+  pipe_loop<PP, GA, GB>(
+      nk, wr == 1,
+      [&](int kt, int q) {
+        const bf16* img = smem + (kt & 1) * BUF;
+        if (q == 0) { read_a(img, 0); read_b(img, 0, fb0); }
+        else if (q == 1) read_b(img, 1, fb1);
+        else read_a(img, 1);
+      },
+      [&](int kt, int q) {
+        if (q == 0) stage_a(kt, 0);
+        else if (q == 1) stage_b(kt, 0);
+        else if (q == 2) stage_b(kt, 1);
+        else stage_a(kt, 1);
+      },
+      [&](int q) {
+        if (q == 0) mfma_q(0, 0, fb0);
+        else if (q == 1) mfma_q(0, 1, fb1);
+        else if (q == 2) mfma_q(1, 1, fb1);
+        else mfma_q(1, 0, fb0);
+      });
+
+  // ---- epilogue: lane holds channels 4g..4g+3 of pixel r16 per fragment ----
+  bf16* out = static_cast<bf16*>(p.out);
+#pragma unroll
+  for (int ha = 0; ha < 2; ++ha)
+#pragma unroll
+    for (int f = 0; f < FA; ++f) {
+      const int ch = n0 + ha * HA + wr * (HA / 2) + f * 16 + 4 * g;
+      const bool chok = ch < p.N;
+      float bv[4] = {0.f, 0.f, 0.f, 0.f};
+      if (BIAS_ACT && p.bias && chok) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) bv[e] = p.bias[ch + e];
+      }
+#pragma unroll
+      for (int hb = 0; hb < 2; ++hb)
+#pragma unroll
+        for (int e2 = 0; e2 < 2; ++e2) {
+          const int m = m0 + hb * HB + wc * 32 + e2 * 16 + r16;
+          float v[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = acc[ha][f][hb][e2][e];
+          uint32_t arg = 0;
+          if constexpr (POOL) {  // every lane of the quad takes part in the exchange
+            const int pos = r16 & 3;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              int a = pos;
+              float o = qswap1(v[e]);
+              int oa = qswap1i(a);
+              if (o > v[e] || (o == v[e] && oa < a)) { v[e] = o; a = oa; }
+              o = qswap2(v[e]);
+              oa = qswap2i(a);
+              if (o > v[e] || (o == v[e] && oa < a)) { v[e] = o; a = oa; }
+              arg |= (uint32_t)a << (8 * e);
+            }
+          }
+          if (!chok || m >= p.M) continue;
+          if (POOL && (r16 & 3) != 0) continue;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            v[e] += bv[e];
+            if (BIAS_ACT) v[e] = act_apply(p.act, v[e]);
+          }
+          const bf16x4 o = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+          const int orow = POOL ? (m >> 2) : m;
+          if (POOL && BIAS_ACT && p.act == ACT_RELU) {  // ReLU-inactive window: argmax byte 4
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              if (!((float)o[e] > 0.f)) arg = (arg & ~(0xffu << (8 * e))) | (4u << (8 * e));
+          }
+          *reinterpret_cast<bf16x4*>(out + (size_t)orow * p.ldo + ch) = o;
+          if (POOL) *reinterpret_cast<uint32_t*>(p.out_arg + (size_t)orow * p.N + ch) = arg;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // weight gradient (split-K over pixels)
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(kIgT, 2) igemm_dw_kernel(IgemmDwParams p) {
@@ -549,6 +870,263 @@ __global__ void __launch_bounds__(256) igemm_dw_reduce_kernel(IgemmDwParams p, f
   *dst = beta != 0.f ? beta * *dst + v : v;
 }
 
+// ---------------------------------------------------------------------------
+// weight gradient on BA-channel x 256-column tiles, phase-pipelined
+// ---------------------------------------------------------------------------
+// Same schedule as igemm_big_kernel (4 phases per 64-pixel K-step, quarter
+// tiles staged one K-step ahead, counted vmcnt + raw barriers), with the
+// weight-gradient operands: A = dZ [64 pixels][BA/2 channels] halves, B =
+// im2col(X) [64 pixels][128 columns] halves, both read transposed
+// (ds_read_b64_tr_b16).  The bias column is not a GEMM column here (with
+// kf % 256 == 0 it would cost a whole extra tile column): the k0 == 0 tiles
+// add db = dZ^T 1 with one extra MFMA against a ones fragment per (phase,
+// channel fragment), spread over the four pixel-column waves.
+// 128-byte rows (BA = 128): 32-byte chunk c of row r sits at c ^ h(r),
+// h(r) = ((r >> 1) & 1) | ((r >> 3) & 1) << 1 -> the 8 rows of one
+// transposed read land on 8 distinct 32-byte bank ranges (as swz128 does for
+// 256-byte rows).
+__device__ __forceinline__ int swz_tr64(int row) { return 2 * (((row >> 1) & 1) | (((row >> 3) & 1) << 1)); }
+
+template <int BA, bool PP>
+__global__ void __launch_bounds__(kBigT, 1) igemm_dwbig_kernel(IgemmDwParams p) {
+  constexpr int BK = 64;
+  constexpr int CA = BA / 2, CB = 128;            // columns per A / B half
+  constexpr int SA = CA / 8, SB = CB / 8;         // 16-byte slots per row
+  constexpr int GA = BK * SA / kBigT, GB = BK * SB / kBigT;
+  constexpr int QA = BK * CA, QB = BK * CB;
+  constexpr int BUF = 2 * QA + 2 * QB;
+  constexpr int FA = CA / 2 / 16;                 // channel fragments per wave per half
+  static_assert(GA >= 1 && GB == 2 && FA >= 1, "tile shape");
+  __shared__ __attribute__((aligned(16))) bf16 smem[2 * BUF];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r16 = lane & 15, g = lane >> 4;
+  const int q = r16 >> 2, pp = r16 & 3;
+  const int wr = wave >> 2, wc = wave & 3;
+
+  const int ntm = cdiv(p.Cout, BA), ntn = cdiv(p.kf, 2 * CB);
+  const int ntiles = ntm * ntn;
+  const int id = xcd_remap(blockIdx.x, gridDim.x);
+  const int tile = id % ntiles, split = id / ntiles;
+  if (split >= p.splitk) return;
+  const int tm = tile % ntm, tn = tile / ntm;
+  const int co0 = tm * BA, k0 = tn * 2 * CB;
+  const int nks = cdiv(p.M, BK);
+  const int per = cdiv(nks, p.splitk);
+  const int ks0 = split * per, ks1 = min(nks, ks0 + per);
+
+  const bf16* dz = static_cast<const bf16*>(p.dz);
+  const bf16* in = static_cast<const bf16*>(p.in);
+  const uint64_t zero_u = reinterpret_cast<uint64_t>(kIgZero);
+  auto swa = [](int row) { return SA == 16 ? swz128(row) : swz_tr64(row); };
+
+  // dZ pieces: row (pixel in the K-step) and channel offset in the half, per j
+  // (host: Cout % BA == 0, so every channel column of the tile exists)
+  int da_row[GA], da_col[GA];
+#pragma unroll
+  for (int j = 0; j < GA; ++j) {
+    const int s = j * kBigT + tid;
+    const int row = s / SA;
+    da_row[j] = row;
+    da_col[j] = co0 + ((s % SA) ^ swa(row)) * 8;
+  }
+  // X pieces: pixel row j (decoded once, advanced per K-step with carries),
+  // tap/channel per (half, j) packed as c << 8 | ky << 4 | kx (-1: k >= kf)
+  int m_[GB], b_[GB], oy_[GB], ox_[GB];
+  int x_tap[2][GB];
+#pragma unroll
+  for (int j = 0; j < GB; ++j) {
+    const int s = j * kBigT + tid;
+    const int row = s >> 4;
+    const int m = ks0 * BK + row;
+    m_[j] = m;
+    b_[j] = mdiv(p.div_ohw, m);
+    const int rem = m - b_[j] * p.OH * p.OW;
+    oy_[j] = mdiv(p.div_ow, rem);
+    ox_[j] = rem - oy_[j] * p.OW;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int k = k0 + h * CB + ((s & 15) ^ swz128(row)) * 8;
+      if (k < p.kf) {
+        const int tap = k / p.C, c = k - tap * p.C;
+        const int ky = tap / p.KS, kx = tap - ky * p.KS;
+        x_tap[h][j] = (c << 8) | (ky << 4) | kx;
+      } else {
+        x_tap[h][j] = -1;
+      }
+    }
+  }
+
+  auto stage_a = [&](int ks, int h) {
+    bf16* dst = smem + ((ks - ks0) & 1) * BUF + h * QA;
+#pragma unroll
+    for (int j = 0; j < GA; ++j) {
+      const int m = ks * BK + da_row[j];
+      const bool ok = m < p.M;
+      const uint64_t src = reinterpret_cast<uint64_t>(dz + (size_t)m * p.ldz + da_col[j] + h * CA);
+      glds16(reinterpret_cast<const bf16*>(ok ? src : zero_u), dst + (j * kBigT + wave * 64) * 8);
+    }
+  };
+  auto stage_b = [&](int ks, int h) {  // pixel geometry currently decoded for K-step ks
+    bf16* dst = smem + ((ks - ks0) & 1) * BUF + 2 * QA + h * QB;
+#pragma unroll
+    for (int j = 0; j < GB; ++j) {
+      const int t = x_tap[h][j];
+      const int iy = oy_[j] * p.stride - p.pad + ((t >> 4) & 15), ix = ox_[j] * p.stride - p.pad + (t & 15);
+      const bool ok = t >= 0 && m_[j] < p.M && (unsigned)iy < (unsigned)p.H && (unsigned)ix < (unsigned)p.W;
+      const int off = ((b_[j] * p.H + iy) * p.W + ix) * p.C + (t >> 8);  // < 2^31 (host check); unused if !ok
+      const uint64_t src = reinterpret_cast<uint64_t>(in) + 2 * (uint64_t)(uint32_t)off;
+      glds16(reinterpret_cast<const bf16*>(ok ? src : zero_u), dst + (j * kBigT + wave * 64) * 8);
+    }
+  };
+  auto advance = [&]() {
+#pragma unroll
+    for (int j = 0; j < GB; ++j) {
+      m_[j] += BK;
+      ox_[j] += p.adv_x;
+      const int c1 = ox_[j] >= p.OW ? 1 : 0;
+      ox_[j] -= c1 * p.OW;
+      oy_[j] += p.adv_y + c1;
+      const int c2 = oy_[j] >= p.OH ? 1 : 0;
+      oy_[j] -= c2 * p.OH;
+      b_[j] += p.adv_b + c2;
+    }
+  };
+
+  f32x4 acc[2][FA][2][2], accb[2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a) {
+    accb[a] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int f = 0; f < FA; ++f)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int e = 0; e < 2; ++e) acc[a][f][b][e] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  const bool bias_wave = k0 == 0 && wc < FA;  // wave-uniform
+  bf16x8 ones;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) ones[e] = (bf16)1.0f;
+
+  // transposed fragment: 4 consecutive pixel rows of 16 columns per call
+  auto tr = [&](const bf16* img, int ncols, int kr, int col0) {
+    const int row = kr + q;
+    const int col = col0 + 4 * pp;
+    const int sw = ncols == 128 ? swz128(row) : swz_tr64(row);
+    return tr4(img + row * ncols + (((col >> 3) ^ sw) << 3) + (col & 7));
+  };
+  bf16x8 fa[FA][2], fb0[2][2], fb1[2][2];
+  auto read_a = [&](const bf16* img, int h) {
+#pragma unroll
+    for (int f = 0; f < FA; ++f)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const int kr = 32 * ks + 8 * g, c0 = wr * (CA / 2) + f * 16;
+        const bf16x4 lo = tr(img + h * QA, CA, kr, c0), hi = tr(img + h * QA, CA, kr + 4, c0);
+        fa[f][ks] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+      }
+  };
+  auto read_b = [&](const bf16* img, int h, bf16x8 (&fb)[2][2]) {
+#pragma unroll
+    for (int e = 0; e < 2; ++e)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const int kr = 32 * ks + 8 * g, c0 = wc * 32 + e * 16;
+        const bf16* base = img + 2 * QA + h * QB;
+        const bf16x4 lo = tr(base, CB, kr, c0), hi = tr(base, CB, kr + 4, c0);
+        fb[e][ks] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+      }
+  };
+  auto mfma_q = [&](int ha, int hb, const bf16x8 (&fb)[2][2]) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int f = 0; f < FA; ++f)
+#pragma unroll
+        for (int e = 0; e < 2; ++e) acc[ha][f][hb][e] = mma(acc[ha][f][hb][e], fa[f][ks], fb[e][ks]);
+  };
+  auto mfma_bias = [&](int ha) {
+    if (!bias_wave) return;
+#pragma unroll
+    for (int f = 0; f < FA; ++f)
+      if (f == wc)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) accb[ha] = mma(accb[ha], fa[f][ks], ones);
+  };
+
+  if (ks0 < ks1)
+    pipe_loop<PP, GA, GB>(
+        ks1 - ks0, wr == 1,
+        [&](int t, int q) {
+          const bf16* img = smem + (t & 1) * BUF;
+          if (q == 0) { read_a(img, 0); read_b(img, 0, fb0); }
+          else if (q == 1) read_b(img, 1, fb1);
+          else read_a(img, 1);
+        },
+        [&](int t, int q) {  // the B quarters use the decoded pixels of K-step t, advanced after B1
+          if (q == 0) stage_a(ks0 + t, 0);
+          else if (q == 1) stage_b(ks0 + t, 0);
+          else if (q == 2) { stage_b(ks0 + t, 1); advance(); }
+          else stage_a(ks0 + t, 1);
+        },
+        [&](int q) {
+          if (q == 0) { mfma_q(0, 0, fb0); mfma_bias(0); }
+          else if (q == 1) mfma_q(0, 1, fb1);
+          else if (q == 2) mfma_q(1, 1, fb1);
+          else { mfma_q(1, 0, fb0); mfma_bias(1); }
+        });
+
+  if (p.direct) {
+    // one split, KS == 1, canonical order: write the gradient in place (the
+    // 16 lanes of a group cover 16 consecutive k of one row: 64-byte runs)
+    const int kreal = p.kreal > 0 ? p.kreal : p.kf;
+#pragma unroll
+    for (int ha = 0; ha < 2; ++ha) {
+#pragma unroll
+      for (int f = 0; f < FA; ++f) {
+        const int co = co0 + ha * CA + wr * (CA / 2) + f * 16 + 4 * g;
+#pragma unroll
+        for (int hb = 0; hb < 2; ++hb)
+#pragma unroll
+          for (int e = 0; e < 2; ++e) {
+            const int k = k0 + hb * CB + wc * 32 + e * 16 + r16;
+            if (k < kreal)
+#pragma unroll
+              for (int i = 0; i < 4; ++i) p.gw[(size_t)(co + i) * kreal + k] = acc[ha][f][hb][e][i];
+          }
+      }
+      if (bias_wave && r16 == 0) {
+        const int co = co0 + ha * CA + wr * (CA / 2) + wc * 16 + 4 * g;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) p.gb[co + i] = accb[ha][i];  // gb: 4-byte alignment only
+      }
+    }
+    return;
+  }
+  // slab[split][k][co]: lane holds co 4g..4g+3 of column k = r16
+  float* slab = p.slab + (size_t)split * p.slab_stride;
+#pragma unroll
+  for (int ha = 0; ha < 2; ++ha) {
+#pragma unroll
+    for (int f = 0; f < FA; ++f) {
+      const int co = co0 + ha * CA + wr * (CA / 2) + f * 16 + 4 * g;
+      if (co >= p.Cout) continue;
+#pragma unroll
+      for (int hb = 0; hb < 2; ++hb)
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          const int k = k0 + hb * CB + wc * 32 + e * 16 + r16;
+          if (k < p.kf) *reinterpret_cast<f32x4*>(slab + (size_t)k * p.Cout + co) = acc[ha][f][hb][e];
+        }
+    }
+    if (bias_wave && r16 == 0) {  // every column of the ones product is db
+      const int co = co0 + ha * CA + wr * (CA / 2) + wc * 16 + 4 * g;
+      if (co < p.Cout) *reinterpret_cast<f32x4*>(slab + (size_t)p.kf * p.Cout + co) = accb[ha];
+    }
+  }
+}
+
 template <int BN, bool BA, bool POOL, bool U8>
 void launch_conv(const IgemmParams& p, hipStream_t s) {
   const int nwg = cdiv(p.M, kIgBM) * cdiv(p.N, BN);
@@ -556,6 +1134,17 @@ void launch_conv(const IgemmParams& p, hipStream_t s) {
 }
 
 }  // namespace
+
+static int igemm_env_mode();
+// MCC_IGEMM_PP=1: the staggered ping-pong schedule instead of lockstep phases
+// (measured slower on VGG-11: 18.41 vs 17.66 ms/step, tools/gpu_r2i.sh)
+static bool igemm_pp_mode() {
+  static const bool m = [] {
+    const char* e = getenv("MCC_IGEMM_PP");
+    return e ? atoi(e) != 0 : false;
+  }();
+  return m;
+}
 
 bool igemm_conv_supported(int C, int N, int KS) {
   return C % 64 == 0 && N % 8 == 0 && (KS * KS * C) % kIgBK == 0;
@@ -595,6 +1184,29 @@ void igemm_conv(const IgemmParams& p0, hipStream_t s) {
     }
     return;
   }
+  // 256-pixel tiles for the wide layers (MCC_IGEMM_BIG=0: 128x128 kernel
+  // only; =128: 256x128 tiles only)
+  const int big_mode = p.tile >= 0 ? p.tile : igemm_env_mode();
+  // auto: 256x256 tiles where N % 256 == 0 (the 128-channel variant measured
+  // slower than the 128x128 kernel on VGG conv2 / conv3-dX: tools/gpu_r2i.sh)
+  if ((big_mode == 1 && p.N % 256 == 0) || ((big_mode == 128 || big_mode == 256) && p.N % 128 == 0)) {
+    const bool c256 = p.N % 256 == 0 && big_mode != 128;
+    const int nwg = cdiv(p.M, kBigBP) * (p.N / (c256 ? 256 : 128));
+#define MCC_BIG(BC, BA, PL)                                                                              \
+  do {                                                                                                   \
+    if (igemm_pp_mode())                                                                                 \
+      hipLaunchKernelGGL((igemm_big_kernel<BC, BA, PL, true>), dim3((unsigned)nwg), dim3(kBigT), 0, s, p);  \
+    else                                                                                                 \
+      hipLaunchKernelGGL((igemm_big_kernel<BC, BA, PL, false>), dim3((unsigned)nwg), dim3(kBigT), 0, s, p); \
+  } while (0)
+    if (c256) {
+      if (p.pool) MCC_BIG(256, true, true); else if (ba) MCC_BIG(256, true, false); else MCC_BIG(256, false, false);
+    } else {
+      if (p.pool) MCC_BIG(128, true, true); else if (ba) MCC_BIG(128, true, false); else MCC_BIG(128, false, false);
+    }
+#undef MCC_BIG
+    return;
+  }
   if (p.pool) {
     if (p.N <= 64) launch_conv<64, true, true, false>(p, s); else launch_conv<128, true, true, false>(p, s);
   } else if (p.N <= 64) {
@@ -604,9 +1216,38 @@ void igemm_conv(const IgemmParams& p0, hipStream_t s) {
   }
 }
 
-int igemm_dw_splitk(int M, int Cout, int kf) {
-  const int tiles = cdiv(Cout, 128) * cdiv(kf + 1, 128);
+static int igemm_env_mode() {
+  static const int m = [] {
+    const char* e = getenv("MCC_IGEMM_BIG");
+    return e ? atoi(e) : 1;
+  }();
+  return m;
+}
+
+// weight-gradient tile: 0 = 128x128 kernel, 128 / 256 = igemm_dwbig_kernel<BA>
+static int dw_big_ba(int Cout, int kf, int tile) {
+  const int mode = tile >= 0 ? tile : igemm_env_mode();
+  if (mode == 0 || Cout % 128 != 0 || kf < 256 || kf >= (1 << 23)) return 0;  // kernel packs c << 8
+  if (mode == 1) return Cout % 256 == 0 ? 256 : 0;  // auto: the 128-channel variant lost to 128x128 (conv2)
+  return (Cout % 256 == 0 && mode != 128) ? 256 : 128;
+}
+
+int igemm_dw_splitk(int M, int Cout, int kf, int tile) {
   const int nks = cdiv(M, kIgBK);
+  const int ba = dw_big_ba(Cout, kf, tile);
+  if (ba) {
+    // one 512-thread workgroup per CU: pick the split count that fills whole
+    // rounds of 256 workgroups (>= 8 K-steps per split)
+    const int tiles = (Cout / ba) * cdiv(kf, 256);
+    const int cap = std::max(1, nks / 8);
+    for (int r = 1; r <= 8; ++r) {
+      const int sk = std::min(cap, (256 * r) / tiles);
+      if (sk >= 1 && (double)tiles * sk >= 0.85 * 256 * r) return sk;
+      if (sk >= cap) return std::max(1, sk);
+    }
+    return std::max(1, std::min(cap, 2048 / tiles));
+  }
+  const int tiles = cdiv(Cout, 128) * cdiv(kf + 1, 128);
   int sk = std::max(1, 1024 / tiles);         // ~4 workgroups per CU in flight
   sk = std::min(sk, std::max(1, nks / 4));    // >= 4 K-steps per slice
   return std::min(sk, 1024);
@@ -634,12 +1275,25 @@ void igemm_dw(const IgemmDwParams& p0, float* gw, float* gb, float beta, hipStre
     p.adv_y = q % p.OH;
     p.adv_b = q / p.OH;
   }
-  const int nwg = cdiv(p.Cout, 128) * cdiv(p.kf + 1, 128) * p.splitk;
-  p.direct = p.splitk == 1 && p.KS == 1 && p.perm_c == 0 && beta == 0.f;
   p.gw = gw;
   p.gb = gb;
-  hipLaunchKernelGGL(igemm_dw_kernel, dim3((unsigned)nwg), dim3(kIgT), 0, s, p);
-  if (p.direct) return;
+  const int ba = dw_big_ba(p.Cout, p.kf, p.tile);
+  if (ba) {
+    MCC_CHECK(p.KS < 16, "igemm_dw: 256-column kernel packs ky, kx in 4 bits");
+    p.direct = p.splitk == 1 && p.KS == 1 && p.perm_c == 0 && beta == 0.f;
+    const int nwg = (p.Cout / ba) * cdiv(p.kf, 256) * p.splitk;
+    const bool pp = igemm_pp_mode();
+    if (ba == 256 && pp) hipLaunchKernelGGL((igemm_dwbig_kernel<256, true>), dim3((unsigned)nwg), dim3(kBigT), 0, s, p);
+    else if (ba == 256) hipLaunchKernelGGL((igemm_dwbig_kernel<256, false>), dim3((unsigned)nwg), dim3(kBigT), 0, s, p);
+    else if (pp) hipLaunchKernelGGL((igemm_dwbig_kernel<128, true>), dim3((unsigned)nwg), dim3(kBigT), 0, s, p);
+    else hipLaunchKernelGGL((igemm_dwbig_kernel<128, false>), dim3((unsigned)nwg), dim3(kBigT), 0, s, p);
+    if (p.direct) return;
+  } else {
+    const int nwg = cdiv(p.Cout, 128) * cdiv(p.kf + 1, 128) * p.splitk;
+    p.direct = p.splitk == 1 && p.KS == 1 && p.perm_c == 0 && beta == 0.f;
+    hipLaunchKernelGGL(igemm_dw_kernel, dim3((unsigned)nwg), dim3(kIgT), 0, s, p);
+    if (p.direct) return;
+  }
   const int64_t total4 = (int64_t)(p.kf + 1) * p.Cout / 4;  // Cout % 8 == 0
   hipLaunchKernelGGL(igemm_dw_reduce_kernel, dim3((unsigned)((total4 + 15) / 16)), dim3(256), 0, s, p, gw, gb, beta);
 }

@@ -410,6 +410,8 @@ struct IgemmParams {
   uint8_t* out_arg = nullptr;
   bool u8 = false;                   // input = u8 image set (first layer), scaled 1/255
   const int32_t* idx = nullptr;      // u8: optional per-sample image index
+  int tile = -1;                     // -1 auto (MCC_IGEMM_BIG, default on), 0: 128x128 kernel,
+                                     // 128 / 256: 256-pixel x 128 / 256-channel kernel where legal
   DivMagic div_ohw, div_ow;
 };
 bool igemm_conv_supported(int C, int N, int KS);
@@ -435,8 +437,10 @@ struct IgemmDwParams {
   float* gb = nullptr;
   DivMagic div_ohw, div_ow;
   int adv_x = 0, adv_y = 0, adv_b = 0;  // set at launch: +BK pixels as (ox, oy, b) increments
+  int tile = -1;                     // -1 auto (MCC_IGEMM_BIG), 0: 128x128 kernel, 128 / 256: BA x 256
+                                     // phase-pipelined kernel (igemm_dw_splitk must see the same value)
 };
-int igemm_dw_splitk(int M, int Cout, int kf);
+int igemm_dw_splitk(int M, int Cout, int kf, int tile = -1);
 size_t igemm_dw_slab_bytes(int Cout, int kf, int splitk);
 void igemm_dw(const IgemmDwParams& p, float* gw, float* gb, float beta, hipStream_t s);
 

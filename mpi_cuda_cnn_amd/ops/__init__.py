@@ -165,8 +165,12 @@ def pack_conv_weight(w: torch.Tensor) -> torch.Tensor:
 
 
 def conv2d_nhwc(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None = None, stride: int = 1, pad: int = 0,
-                act: str = "none") -> torch.Tensor:
-    """y = act(conv2d(x, w, b)) on channels-last bf16: x [B, H, W, C] (C % 64 == 0), w OIHW -> y [B, OH, OW, O]."""
+                act: str = "none", pool: bool = False, tile: int = -1):
+    """y = act(conv2d(x, w, b)) on channels-last bf16: x [B, H, W, C] (C % 64 == 0), w OIHW -> y [B, OH, OW, O].
+
+    pool=True fuses a 2x2/2 max-pool (returns (y_pooled, argmax bytes [B, OH/2, OW/2, O])).
+    tile selects the kernel (igemm.hip): -1 auto, 0 the 128x128 kernel, 128 / 256 the
+    256-pixel x 128 / 256-channel phase-pipelined kernel (where O allows it)."""
     _check(x, b)
     if x.dtype != torch.bfloat16:
         raise RuntimeError("conv2d_nhwc: bf16 activations")
@@ -176,15 +180,19 @@ def conv2d_nhwc(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None = None,
         raise RuntimeError("conv2d_nhwc: needs square kernels, C % 64 == 0 and O % 8 == 0")
     wp = pack_conv_weight(w)
     OH, OW = _conv_geom(H, W, KS, stride, pad)
-    y = torch.empty(B, OH, OW, O, dtype=torch.bfloat16, device=x.device)
+    if pool and (OH % 2 or OW % 2):
+        raise RuntimeError("conv2d_nhwc: the fused pool needs even output dims")
+    PH, PW = (OH // 2, OW // 2) if pool else (OH, OW)
+    y = torch.empty(B, PH, PW, O, dtype=torch.bfloat16, device=x.device)
+    arg = torch.empty(B, PH, PW, O, dtype=torch.uint8, device=x.device) if pool else None
     bias = b.float().contiguous() if b is not None else None
     _K.igemm_conv(B, H, W, C, O, KS, stride, pad, x.data_ptr(), wp.data_ptr(), wp.shape[1],
                   bias=bias.data_ptr() if bias is not None else 0, bias_act=True, act=_ACT[act], out=y.data_ptr(),
-                  ldo=O, stream=_stream())
-    return y
+                  ldo=O, out_arg=arg.data_ptr() if pool else 0, tile=tile, stream=_stream())
+    return (y, arg) if pool else y
 
 
-def conv2d_dgrad_nhwc(dy: torch.Tensor, w: torch.Tensor, pad: int = 0) -> torch.Tensor:
+def conv2d_dgrad_nhwc(dy: torch.Tensor, w: torch.Tensor, pad: int = 0, tile: int = -1) -> torch.Tensor:
     """dx of a stride-1 conv: dy [B, OH, OW, O] bf16 (O % 64 == 0), w OIHW -> dx [B, H, W, I]."""
     _check(dy)
     B, OH, OW, O = dy.shape
@@ -196,12 +204,15 @@ def conv2d_dgrad_nhwc(dy: torch.Tensor, w: torch.Tensor, pad: int = 0) -> torch.
     H, W = _conv_geom(OH, OW, KS, 1, pd)
     dx = torch.empty(B, H, W, I, dtype=torch.bfloat16, device=dy.device)
     _K.igemm_conv(B, OH, OW, O, I, KS, 1, pd, dy.data_ptr(), wf.data_ptr(), wf.shape[1], bias_act=False,
-                  out=dx.data_ptr(), ldo=I, stream=_stream())
+                  out=dx.data_ptr(), ldo=I, tile=tile, stream=_stream())
     return dx
 
 
-def conv2d_wgrad_nhwc(dy: torch.Tensor, x: torch.Tensor, KS: int, stride: int = 1, pad: int = 0, splitk: int = 0):
-    """(dW [O, I, KS, KS] fp32, db [O] fp32) for dy [B, OH, OW, O], x [B, H, W, I] bf16 NHWC."""
+def conv2d_wgrad_nhwc(dy: torch.Tensor, x: torch.Tensor, KS: int, stride: int = 1, pad: int = 0, splitk: int = 0,
+                      tile: int = -1):
+    """(dW [O, I, KS, KS] fp32, db [O] fp32) for dy [B, OH, OW, O], x [B, H, W, I] bf16 NHWC.
+
+    tile: -1 auto, 0 the 128x128 kernel, 128 / 256 the phase-pipelined O-tile x 256 kernel (O % 128 == 0)."""
     _check(dy, x)
     B, H, W, C = x.shape
     O = dy.shape[3]
@@ -211,12 +222,12 @@ def conv2d_wgrad_nhwc(dy: torch.Tensor, x: torch.Tensor, KS: int, stride: int = 
     kf = KS * KS * C
     M = B * OH * OW
     if splitk <= 0:
-        splitk = _K.igemm_dw_splitk(M, O, kf)
+        splitk = _K.igemm_dw_splitk(M, O, kf, tile)
     slab = torch.empty(splitk, kf + 1, O, dtype=torch.float32, device=x.device)
     gw = torch.empty(O, C, KS, KS, dtype=torch.float32, device=x.device)
     gb = torch.empty(O, dtype=torch.float32, device=x.device)
     _K.igemm_dw(B, H, W, C, O, KS, stride, pad, dy.data_ptr(), O, x.data_ptr(), slab.data_ptr(), (kf + 1) * O,
-                splitk, gw.data_ptr(), gb.data_ptr(), stream=_stream())
+                splitk, gw.data_ptr(), gb.data_ptr(), tile=tile, stream=_stream())
     return gw, gb
 
 

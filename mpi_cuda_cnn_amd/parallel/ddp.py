@@ -11,10 +11,12 @@ the wrong buffer (cnnmpi.c:487-498, defects D4/D5) with:
   stages' backward kernels are enqueued: RCCL runs it on its own HIP stream
   (ordered after the producing kernels by an event) while the compute stream
   continues with the earlier stages' backward — comm/compute overlap on xGMI;
-* with RCCL ("nccl") the collective is AVG (ncclAvg: RCCL scales inside the
-  reduction) and the loss gradient is scaled by 1/(local batch); with gloo
-  (no AVG) the loss is pre-scaled by 1/(global batch) and the op is SUM —
-  either way the update uses the global-batch mean gradient;
+* the collective is SUM and the loss gradient is pre-scaled by 1/(global
+  batch), so the update uses the global-batch mean gradient.  (ncclAvg would
+  scale inside the reduction, but RCCL implements it as a pre-multiplied sum
+  that, at one rank, still launches a full read+write "oneRankReduce" pass
+  over the buffer: 0.96 ms per VGG-11 step for nothing; an in-place one-rank
+  SUM is elided by RCCL while the same call path still runs.)
 * initial weights are broadcast from rank 0 (fixes D6: ``srand(rank)``).
 
 Bucket size: xGMI is point-to-point (7 links x ~153 GB/s per MI355X); a ring
@@ -84,8 +86,7 @@ class BucketedAllReduce:
         self.group = group
         self.active = dist.is_initialized()
         self.world = dist.get_world_size(group) if self.active else 1
-        self.avg = self.active and dist.get_backend(group) == "nccl"
-        self.op = dist.ReduceOp.AVG if self.avg else dist.ReduceOp.SUM
+        self.op = dist.ReduceOp.SUM
         self.buckets = [tuple(b) for b in net.buckets(int(bucket_bytes))]
         self.issued = 0  # collectives issued so far (introspection / tests)
         covered = sum(b[3] for b in self.buckets)
@@ -93,7 +94,7 @@ class BucketedAllReduce:
 
     def loss_scale(self, local_batch: int) -> float:
         """Gradient scale for the loss of `local_batch` samples on this rank."""
-        return 1.0 / (local_batch if self.avg else local_batch * self.world)
+        return 1.0 / (local_batch * self.world)
 
     def backward(self, stream_handle: int):
         """Run the engine backward bucket by bucket, launching each bucket's

@@ -91,3 +91,106 @@ def test_igemm_rejects_unsupported(cuda):
         ops.conv2d_nhwc(x, w)
     with pytest.raises(RuntimeError):
         ops.conv2d_nhwc(x.cpu(), w.cpu())
+
+
+# 256-pixel phase-pipelined kernel (igemm_big_kernel): every tile variant vs
+# fp32 F.conv2d and vs the 128x128 kernel; pixel counts that leave partial
+# 256-row tiles (and a whole grid smaller than one tile), fused pool.
+BIG_CASES = [
+    # B, H, W, C, O, KS, stride, pad
+    (2, 30, 26, 128, 256, 3, 1, 1),   # M = 1560: partial last tile
+    (1, 14, 14, 512, 512, 3, 1, 1),   # M = 196 < 256
+    (2, 28, 28, 64, 128, 3, 1, 1),    # BC = 128 only
+    (3, 20, 12, 256, 384, 3, 1, 1),   # N % 256 != 0 -> 128-channel tiles
+    (2, 19, 17, 128, 256, 3, 2, 1),   # strided
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B,H,W,C,O,KS,stride,pad", BIG_CASES)
+@pytest.mark.parametrize("tile", [128, 256])
+def test_igemm_big_forward(cuda, B, H, W, C, O, KS, stride, pad, tile):
+    g = torch.Generator(device=cuda).manual_seed(B * 31 + C + O + tile)
+    x = _rand((B, H, W, C), g, cuda)
+    w = _rand((O, C, KS, KS), g, cuda, (2.0 / (C * KS * KS)) ** 0.5)
+    w[:, :, 0, KS - 1] *= 3.0
+    b = torch.randn(O, generator=g, device=cuda) * 0.1
+    y = ops.conv2d_nhwc(x, w, b, stride=stride, pad=pad, act="relu", tile=tile)
+    ref = F.relu(F.conv2d(x.float().permute(0, 3, 1, 2), w.float(), b, stride=stride, padding=pad)).permute(0, 2, 3, 1)
+    assert _relerr(y, ref) < 1e-2
+    torch.testing.assert_close(y.float(), ref, atol=3e-2, rtol=2e-2)
+    # same fp32 accumulation order per fragment as the 128x128 kernel: equal bits
+    y0 = ops.conv2d_nhwc(x, w, b, stride=stride, pad=pad, act="relu", tile=0)
+    assert torch.equal(y, y0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("tile", [0, 128, 256])
+def test_igemm_big_pool(cuda, tile):
+    B, H, W, C, O = 3, 22, 18, 128, 256
+    g = torch.Generator(device=cuda).manual_seed(5 + tile)
+    x = _rand((B, H, W, C), g, cuda)
+    w = _rand((O, C, 3, 3), g, cuda, (2.0 / (C * 9)) ** 0.5)
+    b = torch.randn(O, generator=g, device=cuda) * 0.1
+    y, arg = ops.conv2d_nhwc(x, w, b, stride=1, pad=1, act="relu", pool=True, tile=tile)
+    z = ops.conv2d_nhwc(x, w, b, stride=1, pad=1, act="relu", tile=tile)  # pre-pool, same kernel family
+    zr = z.float().reshape(B, H // 2, 2, W // 2, 2, O).permute(0, 1, 3, 5, 2, 4).reshape(B, H // 2, W // 2, O, 4)
+    assert torch.equal(y.float(), zr.max(-1).values)
+    live = y.float() > 0
+    a = arg.long()
+    assert bool((a[live] < 4).all())
+    # the argmax names a position holding the max (ties after bf16 rounding may pick either)
+    picked = zr.gather(-1, a.clamp(max=3).unsqueeze(-1)).squeeze(-1)
+    assert torch.equal(picked[live], y.float()[live])
+    assert bool((a[~live] == 4).all())  # ReLU-inactive windows: byte 4
+    if tile:
+        y0, arg0 = ops.conv2d_nhwc(x, w, b, stride=1, pad=1, act="relu", pool=True, tile=0)
+        assert torch.equal(y, y0) and torch.equal(arg, arg0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B,H,W,C,O", [(2, 28, 28, 128, 128), (1, 14, 14, 512, 512), (2, 15, 13, 256, 256)])
+def test_igemm_big_dgrad(cuda, B, H, W, C, O):
+    g = torch.Generator(device=cuda).manual_seed(11 + B + C)
+    dy = _rand((B, H, W, O), g, cuda)
+    w = _rand((O, C, 3, 3), g, cuda, (1.0 / (O * 9)) ** 0.5)
+    w[:, :, 2, 0] *= 2.0
+    ref = torch.nn.grad.conv2d_input((B, C, H, W), w.float(), dy.float().permute(0, 3, 1, 2), padding=1)
+    ref = ref.permute(0, 2, 3, 1)
+    dx0 = ops.conv2d_dgrad_nhwc(dy, w, pad=1, tile=0)
+    for tile in (128, 256):
+        dx = ops.conv2d_dgrad_nhwc(dy, w, pad=1, tile=tile)
+        assert _relerr(dx, ref) < 1e-2
+        assert torch.equal(dx, dx0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B,H,W,C,O,KS,stride,pad", [
+    (2, 30, 26, 128, 256, 3, 1, 1),   # kf = 1152: partial last 256-column tile
+    (1, 14, 14, 512, 512, 3, 1, 1),   # M = 196: partial K-step
+    (2, 28, 28, 64, 128, 3, 1, 1),    # 128-channel tiles (128-byte transposed rows)
+    (3, 20, 12, 256, 384, 3, 1, 1),   # O % 256 != 0
+    (2, 19, 17, 128, 256, 3, 2, 1),   # strided
+    (4, 8, 8, 512, 256, 1, 1, 0),     # 1x1, one split: direct write (FC-style)
+])
+@pytest.mark.parametrize("tile", [128, 256])
+def test_igemm_big_wgrad(cuda, B, H, W, C, O, KS, stride, pad, tile):
+    g = torch.Generator(device=cuda).manual_seed(3 + H + O + tile)
+    OH, OW = (H + 2 * pad - KS) // stride + 1, (W + 2 * pad - KS) // stride + 1
+    x = _rand((B, H, W, C), g, cuda)
+    dy = _rand((B, OH, OW, O), g, cuda, 0.1)
+    xr = x.float().permute(0, 3, 1, 2)
+    dyr = dy.float().permute(0, 3, 1, 2)
+    ref_w = torch.nn.grad.conv2d_weight(xr, (O, C, KS, KS), dyr, stride=stride, padding=pad)
+    ref_b = dyr.sum((0, 2, 3))
+    gw, gb = ops.conv2d_wgrad_nhwc(dy, x, KS, stride=stride, pad=pad, tile=tile)
+    assert _relerr(gw, ref_w) < 1e-3
+    assert _relerr(gb, ref_b) < 1e-3
+    # per output channel: a wrong channel fragment cannot hide in the whole-tensor norm
+    cw = ((gw - ref_w).flatten(1).norm(dim=1) / ref_w.flatten(1).norm(dim=1).clamp_min(1e-12))
+    assert float(cw.max()) < 3e-3
+    assert float(((gb - ref_b).abs() / ref_b.abs().clamp_min(1e-3)).max()) < 1e-2
+    gw2, gb2 = ops.conv2d_wgrad_nhwc(dy, x, KS, stride=stride, pad=pad, tile=tile)
+    assert torch.equal(gw, gw2) and torch.equal(gb, gb2)
+    gw1, gb1 = ops.conv2d_wgrad_nhwc(dy, x, KS, stride=stride, pad=pad, splitk=1, tile=tile)
+    assert _relerr(gw1, ref_w) < 1e-3 and _relerr(gb1, ref_b) < 1e-3
