@@ -188,12 +188,91 @@ __global__ void __launch_bounds__(kIgT, 2) igemm_conv_kernel(IgemmParams p) {
     b_ptr[j] = n < p.N ? w + (size_t)n * p.ldw + b_k[j] : nullptr;
   }
 
+  // U8 runs (p.u8_runs: C = 3, 3x3, pad 1, stride 1, 4-byte aligned rows):
+  // pixel row tid (< BM) of the tile gathers its im2col row as three 9-byte
+  // image-row runs (k = ky*9 + kx*3 + c), each from three aligned dword loads
+  // and two byte-aligns, instead of 32 single-byte loads (27 taps + 5
+  // padding); threads BM..2BM-1 write the all-zero K slots 4..7 of row
+  // tid - BM.  Dwords outside the image row read as 0, which is exactly the
+  // zero padding of the kx = 0 / kx = 2 taps at the left / right border.
+  const uint8_t* r_row0 = in8;
+  int r_iy = -(1 << 20), r_dv = 0, r_sh = 0;
+  if (U8 && p.u8_runs && tid < BM) {
+    const int m = m0 + tid;
+    if (m < p.M) {
+      int b, oy, ox;
+      if (POOL) {
+        const int q = m >> 2, pos = m & 3;
+        b = mdiv(p.div_ohw, q);
+        const int rq = q - b * (p.OH >> 1) * (p.OW >> 1);
+        const int py = mdiv(p.div_ow, rq), px = rq - py * (p.OW >> 1);
+        oy = 2 * py + (pos >> 1);
+        ox = 2 * px + (pos & 1);
+      } else {
+        b = mdiv(p.div_ohw, m);
+        const int rem = m - b * p.OH * p.OW;
+        oy = mdiv(p.div_ow, rem);
+        ox = rem - oy * p.OW;
+      }
+      const int img = p.idx ? p.idx[b] : b;
+      r_row0 = in8 + (size_t)img * p.H * p.W * 3;
+      r_iy = oy - 1;
+      const int o = 3 * (ox - 1);  // byte offset of tap kx = 0 in its row (-3 at the left border)
+      r_dv = o & ~3;
+      r_sh = o - r_dv;
+    }
+  }
+
   const int nk = cdiv(p.K, kIgBK);  // !U8: host guarantees K % 64 == 0 and C % 64 == 0
   auto stage = [&](int kt, int buf) {
     const int k0 = kt * kIgBK;
     bf16* A = smem + buf * IMG;
     bf16* Bw = A + BM * kIgBK;
     if constexpr (U8) {
+    if (p.u8_runs) {
+      const float sc = 1.0f / 255.0f;
+      const int rb = 3 * p.W;  // row bytes
+      if (tid < BM) {
+        uint32_t qd[3][3];
+#pragma unroll
+        for (int ky = 0; ky < 3; ++ky) {
+          const int iy = r_iy + ky;
+          const bool rok = (unsigned)iy < (unsigned)p.H;
+          const uint8_t* row = r_row0 + (size_t)(rok ? iy : 0) * rb;
+#pragma unroll
+          for (int i = 0; i < 3; ++i) {
+            const int d = r_dv + 4 * i;
+            const bool ok = rok && d >= 0 && d <= rb - 4;
+            qd[ky][i] = *reinterpret_cast<const uint32_t*>(row + (ok ? d : 0));  // unconditional (no branch + vmcnt(0))
+            qd[ky][i] = ok ? qd[ky][i] : 0u;
+          }
+        }
+        bf16x8 v[4];
+#pragma unroll
+        for (int ky = 0; ky < 3; ++ky) {
+          const uint32_t w0 = __builtin_amdgcn_alignbyte(qd[ky][1], qd[ky][0], r_sh);
+          const uint32_t w1 = __builtin_amdgcn_alignbyte(qd[ky][2], qd[ky][1], r_sh);
+          const uint32_t w2 = __builtin_amdgcn_alignbyte(0u, qd[ky][2], r_sh);
+          const uint32_t wb[3] = {w0, w1, w2};
+#pragma unroll
+          for (int j = 0; j < 9; ++j) {
+            const int k = ky * 9 + j;
+            v[k >> 3][k & 7] = (bf16)((float)((wb[j >> 2] >> (8 * (j & 3))) & 0xffu) * sc);
+          }
+        }
+#pragma unroll
+        for (int k = 27; k < 32; ++k) v[k >> 3][k & 7] = (bf16)0.f;
+#pragma unroll
+        for (int ls = 0; ls < 4; ++ls) store8(A + tid * kIgBK + ((ls ^ swz64(tid)) << 3), v[ls]);
+      } else {
+        const int row = tid - BM;
+        bf16x8 z;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) z[e] = (bf16)0.f;
+#pragma unroll
+        for (int ls = 4; ls < 8; ++ls) store8(A + row * kIgBK + ((ls ^ swz64(row)) << 3), z);
+      }
+    } else {
       const float sc = 1.0f / 255.0f;
       uint8_t raw[AJ][8];
       uint32_t inb[AJ] = {};
@@ -222,6 +301,7 @@ __global__ void __launch_bounds__(kIgT, 2) igemm_conv_kernel(IgemmParams p) {
         for (int e = 0; e < 8; ++e) v[e] = (bf16)((inb[j] >> e & 1u) ? (float)raw[j][e] * sc : 0.f);
         store8(A + (j * kIgT + tid) * 8, v);
       }
+    }
     } else {
       const int tap = k0 / p.C;  // wave-uniform
       const int c0 = k0 - tap * p.C;
@@ -1177,6 +1257,10 @@ void igemm_conv(const IgemmParams& p0, hipStream_t s) {
   const bool ba = p.epi_bias_act;
   if (p.u8) {
     MCC_CHECK(p.N > 64 || p.N % 8 == 0, "igemm_conv(u8): N");
+    const char* runs_env = getenv("MCC_U8_RUNS");  // =0: single-byte staging (A/B; read per launch)
+    const bool runs_ok = runs_env ? atoi(runs_env) != 0 : true;
+    p.u8_runs = runs_ok && p.C == 3 && p.KS == 3 && p.pad == 1 && p.stride == 1 && p.W >= 6 && (p.W * 3) % 4 == 0 &&
+                reinterpret_cast<uintptr_t>(p.in) % 4 == 0;
     if (p.pool) {
       if (p.N <= 64) launch_conv<64, true, true, true>(p, s); else launch_conv<128, true, true, true>(p, s);
     } else {

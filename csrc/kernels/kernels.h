@@ -410,6 +410,7 @@ struct IgemmParams {
   uint8_t* out_arg = nullptr;
   bool u8 = false;                   // input = u8 image set (first layer), scaled 1/255
   const int32_t* idx = nullptr;      // u8: optional per-sample image index
+  bool u8_runs = false;              // set at launch: u8 C=3 3x3 pad-1 im2col rows from dword runs
   int tile = -1;                     // -1 auto (MCC_IGEMM_BIG, default on), 0: 128x128 kernel,
                                      // 128 / 256: 256-pixel x 128 / 256-channel kernel where legal
   DivMagic div_ohw, div_ow;

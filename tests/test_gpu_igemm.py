@@ -194,3 +194,40 @@ def test_igemm_big_wgrad(cuda, B, H, W, C, O, KS, stride, pad, tile):
     assert torch.equal(gw, gw2) and torch.equal(gb, gb2)
     gw1, gb1 = ops.conv2d_wgrad_nhwc(dy, x, KS, stride=stride, pad=pad, splitk=1, tile=tile)
     assert _relerr(gw1, ref_w) < 1e-3 and _relerr(gb1, ref_b) < 1e-3
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("hw", [80, 66])  # 66: rows not dword-aligned -> byte path in both
+def test_u8_first_layer_runs_match_bytes(cuda, monkeypatch, hw):
+    """First-layer u8 staging from dword image-row runs (C=3, 3x3, pad 1) vs
+    the single-byte gather: bit-identical logits and gradients through the
+    engine (same bf16 rounding of byte/255), incl. the left/right/top/bottom
+    zero padding and a sample-index gather."""
+    import numpy as np
+    import mpi_cuda_cnn_amd as mcc
+
+    spec = mcc.parse_model_spec(f"input 3 {hw} {hw}; conv 64 k3 s1 p1 relu; pool 2; conv 64 k3 s1 p1 relu; "
+                                "fc 32 relu; fc 10 softmax", "u8runs")
+    B = 6
+    imgs, labels = mcc.synth_dataset(3 * B, 3, hw, hw, 10, seed=4)
+    imgs = np.random.default_rng(1).integers(0, 256, imgs.shape, dtype=np.uint8)  # every byte position matters
+    params = mcc.init_params(spec, seed=3).astype(np.float32)
+    d_img = torch.from_numpy(imgs).to(cuda)
+    d_lab = torch.from_numpy(labels).to(cuda)
+    idx = torch.tensor([5, 0, 17, 3, 3, 9], dtype=torch.int32, device=cuda)
+    s = torch.cuda.current_stream().cuda_stream
+    out = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("MCC_U8_RUNS", mode)
+        net = mcc.GpuNet(spec, "bf16", B)
+        net.set_params(params)
+        net.zero_stats(s)
+        net.forward(d_img.data_ptr(), idx.data_ptr(), B, s)
+        net.loss(d_lab.data_ptr(), idx.data_ptr(), 1.0 / B, True, s)
+        net.backward_all(s)
+        torch.cuda.synchronize()
+        out[mode] = (net.plan(), net.get_logits(B), net.get_grads())
+        del net
+    assert "igemm" in out["1"][0], out["1"][0]
+    np.testing.assert_array_equal(out["1"][1], out["0"][1])
+    np.testing.assert_array_equal(out["1"][2], out["0"][2])
