@@ -25,11 +25,14 @@ sys.path.insert(0, ROOT)
 BASELINE_IMG_S = 2510.0  # best reference number (8-rank MPI CPU)
 METRIC = "images/sec (whole node), LeNet-5 MNIST-shaped, at 1/2/4/8 MI355X"
 # Per-GPU batch sized for 288 GB HBM3E: LeNet-5 throughput keeps rising with
-# batch (profiles/lenet5_batch_sweep_r1g.txt: 36.7 M img/s at 16,384 ->
-# 45.3 M at 65,536 -> 47.3 M at 131,072) as the persistent conv kernels'
-# per-step prologue/tail and the launch chain amortise; 65,536 is the knee.
+# batch as the persistent conv kernels' per-step prologue/tail and the launch
+# chain amortise (round 1: 36.7 M img/s at 16,384 -> 45.3 M at 65,536 -> 47.3 M
+# at 131,072, profiles/lenet5_batch_sweep_r1g.txt; round 2 kernels: 59.1 M at
+# 65,536 -> 64.9 M at 131,072, profiles/batch_sweep_r2.txt).  131,072 is the
+# largest power of two under the engine's 32-bit activation-index bound
+# (B * 16 padded channels * 28 * 28 < 2^31).
 # CIFAR-3conv: 1.88 M img/s at 4,096 -> 2.58 M at 16,384 (profiles/bench_models_r1g.jsonl).
-DEFAULT_BATCH = {"lenet5": 65536, "ref": 65536, "cifar3": 16384, "vgg11": 256}
+DEFAULT_BATCH = {"lenet5": 131072, "ref": 65536, "cifar3": 16384, "vgg11": 256}
 # models whose step is faster with the dW side stream (engine.cpp, measured A/B)
 SIDE_STREAM = {"cifar3"}
 
@@ -46,7 +49,7 @@ def main():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--model", default="lenet5")
-    ap.add_argument("--batch-per-gpu", type=int, default=0, help="default: per-model (16384 for LeNet-5)")
+    ap.add_argument("--batch-per-gpu", type=int, default=0, help="default: per-model (131072 for LeNet-5)")
     ap.add_argument("--dtype", default="bf16")
     ap.add_argument("--dataset", type=int, default=0,
                     help="synthetic samples resident per GPU (default 65536; 8 batches for large images)")
@@ -88,7 +91,7 @@ def main():
         os.environ.setdefault("MCC_SIDE_STREAM", "1")
     B = args.batch_per_gpu or DEFAULT_BATCH.get(args.model, 1024)
     if not args.dataset:
-        args.dataset = 65536 if H * W <= 32 * 32 else max(256, 8 * B)
+        args.dataset = max(65536, B) if H * W <= 32 * 32 else max(256, 8 * B)
     imgs, labels = mcc.synth_dataset(args.dataset, C, H, W, spec.num_classes(), seed=1234 + rank)
     d_img = torch.from_numpy(imgs).to(dev)
     d_lab = torch.from_numpy(labels).to(dev)

@@ -45,7 +45,8 @@ __global__ void __launch_bounds__(kC0T) conv0_dw_kernel(Conv0DwParams p) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r16 = lane & 15, g = lane >> 4;
   const int PHW = p.PH * p.PW;
-  const int64_t nwin = (int64_t)p.B * PHW;
+  const int64_t nwin = (int64_t)p.B * PHW;  // < 2^24 (conv0_dw_supported): exact magic division
+  const Div d_phw(PHW), d_pw(p.PW);
   const int64_t nsteps = (nwin + kC0W - 1) / kC0W;
   const int64_t per = (nsteps + gridDim.x - 1) / gridDim.x;
   const int64_t s0 = (int64_t)blockIdx.x * per, s1 = nsteps < s0 + per ? nsteps : s0 + per;
@@ -81,9 +82,10 @@ __global__ void __launch_bounds__(kC0T) conv0_dw_kernel(Conv0DwParams p) {
       const int64_t w = step * kC0W + (xp >> 2);
       const int pos = xp & 3;
       const bool wok = w < nwin;
-      const int b = wok ? (int)(w / PHW) : 0;
-      const int rem = wok ? (int)(w - (int64_t)b * PHW) : 0;
-      const int wy = rem / p.PW, wx = rem - wy * p.PW;
+      const int wi = wok ? (int)w : 0;  // 64-bit divisions here were ~200 VALU per K-step
+      const int b = d_phw.div(wi);
+      const int rem = wi - b * PHW;
+      const int wy = d_pw.div(rem), wx = rem - wy * p.PW;
       const int y = 2 * wy + (pos >> 1), x = 2 * wx + (pos & 1);
       const int img = p.idx ? p.idx[b] : b;
       const uint8_t* src = p.x + (size_t)img * p.H * p.W * p.C;
@@ -184,7 +186,8 @@ int conv0_dw_grid(const Conv0DwParams& p) {
 
 bool conv0_dw_supported(const Conv0DwParams& p) {
   return p.C >= 1 && 9 * p.C + 1 <= kC0K && p.Cout >= 1 && p.Cout <= 64 && p.Cout % 4 == 0 && p.H % 2 == 0 &&
-         p.W % 2 == 0 && p.PH == p.H / 2 && p.PW == p.W / 2 && (int64_t)p.H * p.W * p.C < (1 << 30);
+         p.W % 2 == 0 && p.PH == p.H / 2 && p.PW == p.W / 2 && (int64_t)p.H * p.W * p.C < (1 << 30) &&
+         (int64_t)p.B * p.PH * p.PW < (1 << 24);
 }
 
 size_t conv0_dw_slab_bytes(const Conv0DwParams& p) { return (size_t)conv0_dw_grid(p) * 64 * kC0K * 4; }
