@@ -115,6 +115,7 @@ GpuNet::GpuNet(const ModelSpec& spec, DType dtype, int max_batch, int device)
   if (const char* a = std::getenv("MCC_NO_PIPE")) no_pipe_ = std::atoi(a) != 0;  // A/B against conv_small
   if (const char* a = std::getenv("MCC_NO_FC")) no_fc_ = std::atoi(a) != 0;      // A/B against the tiled GEMM
   if (const char* a = std::getenv("MCC_NO_IGEMM")) no_igemm_ = std::atoi(a) != 0;  // A/B against im2col + GEMM
+  if (const char* a = std::getenv("MCC_IGEMM_SMALL")) igemm_small_ = std::atoi(a) != 0;  // wide small-image convs
   if (const char* a = std::getenv("MCC_NO_HEAD")) no_head_ = std::atoi(a) != 0;    // A/B against softmax_xent + FC backward
   // dW side stream: opt-in (MCC_SIDE_STREAM=1).  Measured on MI355X (one GPU,
   // bench.py): CIFAR-3conv 2.27 -> 2.17 ms/step, but LeNet-5 0.452 -> 0.502 and
@@ -278,6 +279,14 @@ void GpuNet::build() {
       const int64_t lds_cap = 120 * 1024;
       st.big = st.OH * st.OW > 4096 || st.cout_pad > 128 || (int64_t)img_b > lds_cap ||
                (int64_t)LHd * LWd * st.CLd * (int64_t)es > lds_cap || (int64_t)dw_img_b > lds_cap;
+      // small images with wide channels (C % 64, Cout % 8, stride 1) go to the
+      // 128x128 / 256-tile MFMA kernels (MCC_IGEMM_SMALL=0: the whole-image LDS
+      // kernels).  CIFAR-3conv conv3 (64 -> 128): 3.91 -> 4.32 M img/s; conv2
+      // (32 -> 64) measured slower on igemm (3.83 M), so C % 64 only.
+      if (!st.big && igemm_small_ && s > 0 && dtype_ == DType::BF16 && !no_igemm_ && st.stride == 1 &&
+          st.inC % 64 == 0 && st.C % 64 == 0 &&
+          gpu::igemm_conv_supported(st.inC, st.C, st.KS) && gpu::igemm_conv_supported(st.C, st.inC, st.KS))
+        st.big = true;
       st.kgem = r8(KK * st.inC);
       st.kgem_d = r8(KK * st.C);
       if (st.big) MCC_CHECK(st.C % 8 == 0, "im2col conv path needs Cout % 8 == 0");

@@ -223,7 +223,7 @@ __global__ void __launch_bounds__(kIgT, 2) igemm_conv_kernel(IgemmParams p) {
     }
   }
 
-  const int nk = cdiv(p.K, kIgBK);  // !U8: host guarantees K % 64 == 0 and C % 64 == 0
+  const int nk = cdiv(p.K, kIgBK);  // !U8: C % 32 == 0; pieces at k >= K read the zero page
   auto stage = [&](int kt, int buf) {
     const int k0 = kt * kIgBK;
     bf16* A = smem + buf * IMG;
@@ -303,21 +303,27 @@ __global__ void __launch_bounds__(kIgT, 2) igemm_conv_kernel(IgemmParams p) {
       }
     }
     } else {
-      const int tap = k0 / p.C;  // wave-uniform
+      // C % 32 == 0: a 64-deep K-step spans at most two taps (the second from
+      // the piece's channel wrap; C = 32: slots 4..7), both wave-uniform
+      const int tap = k0 / p.C;
       const int c0 = k0 - tap * p.C;
       const int ky = tap / p.KS, kx = tap - ky * p.KS;
-      const int toff = (ky * p.W + kx) * p.C + c0;
+      const int ky1 = kx + 1 < p.KS ? ky : ky + 1, kx1 = kx + 1 < p.KS ? kx + 1 : 0;
+      const int toff = (ky * p.W + kx) * p.C;
+      const int toff1 = (ky1 * p.W + kx1) * p.C - p.C;  // channel index c0 + seg - C
 #pragma unroll
       for (int j = 0; j < AJ; ++j) {
-        const int iy = a_iy[j] + ky, ix = a_ix[j] + kx;
-        const bool ok = (unsigned)iy < (unsigned)p.H && (unsigned)ix < (unsigned)p.W;
-        const bf16* src = ok ? in + (a_base[j] + toff + a_seg[j]) : zero;
+        const int c = c0 + a_seg[j];
+        const bool wrap = c >= p.C;
+        const int iy = a_iy[j] + (wrap ? ky1 : ky), ix = a_ix[j] + (wrap ? kx1 : kx);
+        const bool ok = k0 + a_seg[j] < p.K && (unsigned)iy < (unsigned)p.H && (unsigned)ix < (unsigned)p.W;
+        const bf16* src = ok ? in + (a_base[j] + (wrap ? toff1 : toff) + c) : zero;
         glds16(src, A + (j * kIgT + wave * 64) * 8);
       }
     }
 #pragma unroll
     for (int j = 0; j < BJ; ++j) {
-      const bf16* src = (b_ptr[j] && (!U8 || k0 + b_k[j] < p.ldw)) ? b_ptr[j] + k0 : zero;
+      const bf16* src = (b_ptr[j] && k0 + b_k[j] < p.K) ? b_ptr[j] + k0 : zero;
       glds16(src, Bw + (j * kIgT + wave * 64) * 8);
     }
   };
@@ -1227,7 +1233,9 @@ static bool igemm_pp_mode() {
 }
 
 bool igemm_conv_supported(int C, int N, int KS) {
-  return C % 64 == 0 && N % 8 == 0 && (KS * KS * C) % kIgBK == 0;
+  // 128x128 kernel: C % 32 (a K-step spans <= 2 taps; K padded to 64 with
+  // zero pieces); the 256-tile kernels additionally need C % 64 (igemm_conv)
+  return C % 32 == 0 && N % 8 == 0 && KS <= 16;
 }
 
 void igemm_conv(const IgemmParams& p0, hipStream_t s) {
@@ -1237,7 +1245,7 @@ void igemm_conv(const IgemmParams& p0, hipStream_t s) {
                   (int64_t)p.KS * p.W * p.C < (1 << 22),
               "igemm_conv(u8): bad shapes");
   } else {
-    MCC_CHECK(igemm_conv_supported(p.C, p.N, p.KS), "igemm_conv: needs C % 64 == 0 and N % 8 == 0");
+    MCC_CHECK(igemm_conv_supported(p.C, p.N, p.KS), "igemm_conv: needs C % 32 == 0 and N % 8 == 0");
   }
   MCC_CHECK(p.K == p.KS * p.KS * p.C, "igemm_conv: K must be KS*KS*C");
   MCC_CHECK(p.M == p.B * p.OH * p.OW && p.M > 0, "igemm_conv: M must be B*OH*OW");
@@ -1273,7 +1281,8 @@ void igemm_conv(const IgemmParams& p0, hipStream_t s) {
   const int big_mode = p.tile >= 0 ? p.tile : igemm_env_mode();
   // auto: 256x256 tiles where N % 256 == 0 (the 128-channel variant measured
   // slower than the 128x128 kernel on VGG conv2 / conv3-dX: tools/gpu_r2i.sh)
-  if ((big_mode == 1 && p.N % 256 == 0) || ((big_mode == 128 || big_mode == 256) && p.N % 128 == 0)) {
+  if (p.C % 64 == 0 &&
+      ((big_mode == 1 && p.N % 256 == 0) || ((big_mode == 128 || big_mode == 256) && p.N % 128 == 0))) {
     const bool c256 = p.N % 256 == 0 && big_mode != 128;
     const int nwg = cdiv(p.M, kBigBP) * (p.N / (c256 ? 256 : 128));
 #define MCC_BIG(BC, BA, PL)                                                                              \

@@ -166,7 +166,7 @@ def pack_conv_weight(w: torch.Tensor) -> torch.Tensor:
 
 def conv2d_nhwc(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None = None, stride: int = 1, pad: int = 0,
                 act: str = "none", pool: bool = False, tile: int = -1):
-    """y = act(conv2d(x, w, b)) on channels-last bf16: x [B, H, W, C] (C % 64 == 0), w OIHW -> y [B, OH, OW, O].
+    """y = act(conv2d(x, w, b)) on channels-last bf16: x [B, H, W, C] (C % 32 == 0), w OIHW -> y [B, OH, OW, O].
 
     pool=True fuses a 2x2/2 max-pool (returns (y_pooled, argmax bytes [B, OH/2, OW/2, O])).
     tile selects the kernel (igemm.hip): -1 auto, 0 the 128x128 kernel, 128 / 256 the
@@ -177,7 +177,7 @@ def conv2d_nhwc(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None = None,
     B, H, W, C = x.shape
     O, I, KS, KS2 = w.shape
     if I != C or KS != KS2 or not _K.igemm_conv_supported(C, O, KS):
-        raise RuntimeError("conv2d_nhwc: needs square kernels, C % 64 == 0 and O % 8 == 0")
+        raise RuntimeError("conv2d_nhwc: needs square kernels, C % 32 == 0 and O % 8 == 0")
     wp = pack_conv_weight(w)
     OH, OW = _conv_geom(H, W, KS, stride, pad)
     if pool and (OH % 2 or OW % 2):
@@ -193,12 +193,12 @@ def conv2d_nhwc(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None = None,
 
 
 def conv2d_dgrad_nhwc(dy: torch.Tensor, w: torch.Tensor, pad: int = 0, tile: int = -1) -> torch.Tensor:
-    """dx of a stride-1 conv: dy [B, OH, OW, O] bf16 (O % 64 == 0), w OIHW -> dx [B, H, W, I]."""
+    """dx of a stride-1 conv: dy [B, OH, OW, O] bf16 (O % 32 == 0), w OIHW -> dx [B, H, W, I]."""
     _check(dy)
     B, OH, OW, O = dy.shape
     Oc, I, KS, _ = w.shape
     if Oc != O or not _K.igemm_conv_supported(O, I, KS):
-        raise RuntimeError("conv2d_dgrad_nhwc: needs O % 64 == 0 and I % 8 == 0")
+        raise RuntimeError("conv2d_dgrad_nhwc: needs O % 32 == 0 and I % 8 == 0")
     wf = w.flip(2, 3).permute(1, 2, 3, 0).reshape(I, KS * KS * O).to(torch.bfloat16).contiguous()
     pd = KS - 1 - pad
     H, W = _conv_geom(OH, OW, KS, 1, pd)

@@ -21,6 +21,9 @@ CASES = [
     (4, 13, 11, 64, 64, 3, 1, 1),
     (2, 17, 19, 128, 72, 3, 2, 1),
     (2, 9, 9, 64, 136, 5, 1, 0),
+    (3, 16, 16, 32, 64, 3, 1, 1),    # C = 32: a K-step spans two taps, K = 288 (tail K-step half zero)
+    (2, 14, 14, 32, 48, 5, 1, 2),    # C = 32, 5x5: K = 800
+    (2, 12, 10, 96, 40, 3, 1, 1),    # C = 96: channel wrap at c0 = 64
 ]
 
 
@@ -48,7 +51,7 @@ def test_igemm_forward(cuda, B, H, W, C, O, KS, stride, pad):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("B,H,W,C,O,KS,stride,pad", [c for c in CASES if c[6] == 1 and c[4] % 64 == 0])
+@pytest.mark.parametrize("B,H,W,C,O,KS,stride,pad", [c for c in CASES if c[6] == 1 and c[4] % 32 == 0])
 def test_igemm_dgrad(cuda, B, H, W, C, O, KS, stride, pad):
     g = torch.Generator(device=cuda).manual_seed(7 + B + C)
     OH, OW = (H + 2 * pad - KS) + 1, (W + 2 * pad - KS) + 1
