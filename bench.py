@@ -121,6 +121,11 @@ def main():
         tr.step(d_img, d_lab, idx_buf)
         K.advance_counter(counter.data_ptr(), s)
 
+    # host-side rank agreement (capture consensus, the barriers around the
+    # timed loop, the MAX of the per-rank times) only where there are ranks
+    # to agree with: at world 1 a barrier / MAX is the identity, and no eager
+    # collective then follows the graph capture (see ddp.init_process_group)
+    multi = dist.is_initialized() and world > 1
     step = step_launch
     graph_note = "per-kernel launches" + (" (--graph off)" if args.graph == "off" else "")
     coll_graph = None
@@ -133,7 +138,7 @@ def main():
         issued_before = tr.sync.issued
         g, why = capture_step(step_launch)
         ok = torch.tensor([1 if g is not None else 0], device=dev, dtype=torch.int32)
-        if dist.is_initialized():  # every rank replays or none does (collectives inside)
+        if multi:  # every rank replays or none does (collectives inside)
             dist.all_reduce(ok, op=dist.ReduceOp.MIN)
         if int(ok.item()) == 1:
             coll_graph = tr.sync.issued - issued_before
@@ -146,7 +151,7 @@ def main():
     for _ in range(max(0, args.warmup - 1)):
         step()
     torch.cuda.synchronize()
-    if dist.is_initialized():
+    if multi:
         dist.barrier()
     torch.cuda.synchronize()
     tr.zero_stats()
@@ -155,12 +160,12 @@ def main():
     for _ in range(args.steps):
         step()
     torch.cuda.synchronize()
-    if dist.is_initialized():
+    if multi:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     coll_per_step = (tr.sync.issued - issued0) / max(1, args.steps) if coll_graph is None else coll_graph
-    if dist.is_initialized():
+    if multi:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())

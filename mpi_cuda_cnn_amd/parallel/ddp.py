@@ -62,6 +62,12 @@ def init_process_group(backend: str, device: torch.device | None = None):
             os.environ["MASTER_PORT"] = str(s.getsockname()[1])
     kw = {"timeout": comm_timeout()}
     if backend == "nccl":
+        # No recycled HIP events between collectives: with the cache on, the
+        # events of collectives captured into a HIP graph (bench.py --graph)
+        # return to the cache "last recorded in a capturing stream", a later
+        # eager collective inherits one, and the process-group watchdog's
+        # query of it fails (hipErrorCapturedEvent -> abort; seen 1 in 7 runs).
+        os.environ.setdefault("TORCH_NCCL_CUDA_EVENT_CACHE", "0")
         if device is not None:
             kw["device_id"] = device
         # RCCL's stream from the high-priority pool: HIP maps streams onto
