@@ -54,6 +54,7 @@ struct GpuNet::Stage {
   // large-image conv (explicit im2col + MFMA GEMM) when the image tile does
   // not fit the whole-image LDS kernels
   bool big = false;
+  bool generic = false;  // tanh conv / pool after a non-ReLU conv: im2col or igemm path + grad_xform
   int kgem = 0, kgem_d = 0;      // im2col row strides (fwd/dW, data grad)
   // implicit-GEMM kernels (igemm.hip) per direction of a large-image conv;
   // the explicit im2col + GEMM path remains for what they do not cover
@@ -210,11 +211,16 @@ void GpuNet::build() {
       st->C = l.C; st->OH = l.H; st->OW = l.W;
       st->KS = l.ks; st->stride = l.stride; st->pad = l.pad;
       st->outH = l.H; st->outW = l.W;
-      MCC_CHECK(l.act == Act::ReLU || l.act == Act::None, "GPU conv supports relu/none activations");
+      MCC_CHECK(l.act == Act::ReLU || l.act == Act::None || l.act == Act::Tanh,
+                "GPU conv supports relu/tanh/none activations");
+      // the pipelined / whole-image kernels fold the ReLU mask into their
+      // staging; tanh convs and pools after a non-ReLU conv take the
+      // implicit-GEMM / im2col path, whose separate grad_xform pass applies
+      // act' (and the unpool) for any activation
+      st->generic = l.act != Act::ReLU && !(l.act == Act::None && !(i + 1 < L.size() && L[i + 1].kind == LayerKind::MaxPool));
       if (i + 1 < L.size() && L[i + 1].kind == LayerKind::MaxPool) {
         const LayerSpec& pl = L[i + 1];
-        MCC_CHECK(pl.ks == 2 && pl.stride == 2, "GPU engine fuses only 2x2/2 max-pools");
-        MCC_CHECK(l.act == Act::ReLU, "fused max-pool needs a ReLU conv");
+        MCC_CHECK(pl.ks == 2 && pl.stride == 2, "GPU engine fuses only 2x2/2 max-pools (after a conv)");
         st->pooled = true;
         st->outH = pl.H; st->outW = pl.W;
         ++i;
@@ -227,7 +233,7 @@ void GpuNet::build() {
       if (l.inH * l.inW > 1) { st->permC = l.inC; st->permHW = l.inH * l.inW; }
     } else {
       delete st;
-      throw Error("GPU engine: max-pool must directly follow a ReLU conv");
+      throw Error("GPU engine: max-pool must directly follow a conv");
     }
     stages_.push_back(st);
   }
@@ -278,7 +284,8 @@ void GpuNet::build() {
       // whole-image LDS kernels if one image fits comfortably; else im2col + GEMM
       const int64_t lds_cap = 120 * 1024;
       st.big = st.OH * st.OW > 4096 || st.cout_pad > 128 || (int64_t)img_b > lds_cap ||
-               (int64_t)LHd * LWd * st.CLd * (int64_t)es > lds_cap || (int64_t)dw_img_b > lds_cap;
+               (int64_t)LHd * LWd * st.CLd * (int64_t)es > lds_cap || (int64_t)dw_img_b > lds_cap || st.generic;
+      MCC_CHECK(!st.generic || st.C % 8 == 0, "GPU engine: tanh convs / pools after a non-ReLU conv need Cout % 8 == 0");
       // small images with wide channels (C % 64, Cout % 8, stride 1) go to the
       // 128x128 / 256-tile MFMA kernels (MCC_IGEMM_SMALL=0: the whole-image LDS
       // kernels).  CIFAR-3conv conv3 (64 -> 128): 3.91 -> 4.32 M img/s; conv2
@@ -295,7 +302,7 @@ void GpuNet::build() {
       // first layer forward: u8 gather through registers (K = KS*KS*inC small)
       if (st.ig_dw0 && st.KS * st.KS * st.inC <= 64) st.ig_fwd = true;
       // first layer weight gradient straight from the pooled dY / argmax
-      if (st.ig_dw0 && st.ig_fwd && st.pooled && st.KS == 3 && st.stride == 1 && st.pad == 1 &&
+      if (st.ig_dw0 && st.ig_fwd && st.pooled && st.act == gpu::ACT_RELU && st.KS == 3 && st.stride == 1 && st.pad == 1 &&
           !std::getenv("MCC_NO_C0DW")) {
         gpu::Conv0DwParams& c = st.pc0;
         c.B = max_batch_; c.H = st.OH; c.W = st.OW; c.C = st.inC; c.PH = st.outH; c.PW = st.outW; c.Cout = st.C;
@@ -688,7 +695,8 @@ void GpuNet::forward(const uint8_t* images, const int32_t* idx, int B, hipStream
       g.pool = st.ig_pool; g.out_arg = st.arg_buf;
       if (si == 0) { g.u8 = true; g.in = images; g.idx = idx; }
       gpu::igemm_conv(g, s);
-      if (st.pooled && !st.ig_pool) gpu::maxpool2(dtype_, st.conv_buf, st.act_buf, st.arg_buf, B, st.OH, st.OW, st.C, s);
+      if (st.pooled && !st.ig_pool)
+        gpu::maxpool2(dtype_, st.conv_buf, st.act_buf, st.arg_buf, B, st.OH, st.OW, st.C, s, st.act == gpu::ACT_RELU);
     } else if (st.kind == Stage::CONV && st.big) {
       // im2col (input transform fused) -> GEMM with bias+ReLU epilogue -> 2x2 max-pool
       gpu::Im2colParams ic;
@@ -705,7 +713,8 @@ void GpuNet::forward(const uint8_t* images, const int32_t* idx, int B, hipStream
       g.epi = gpu::EPI_BIAS_ACT; g.act = st.act; g.bias = params_ + st.b_off;
       g.C = st.pooled ? st.conv_buf : st.act_buf; g.ldc = st.C;
       gpu::gemm(dtype_, g, s);
-      if (st.pooled) gpu::maxpool2(dtype_, st.conv_buf, st.act_buf, st.arg_buf, B, st.OH, st.OW, st.C, s);
+      if (st.pooled)
+        gpu::maxpool2(dtype_, st.conv_buf, st.act_buf, st.arg_buf, B, st.OH, st.OW, st.C, s, st.act == gpu::ACT_RELU);
     } else if (st.kind == Stage::CONV && st.direct_fwd) {
       gpu::Conv1DirectParams p = st.pd1;
       p.N = B;
@@ -834,7 +843,9 @@ void GpuNet::backward(int hi, int lo, hipStream_t s) {
     };
     if (st.kind == Stage::CONV) {
       gpu::StageSrc dy;
-      dy.mode = st.pooled ? gpu::IN_UNPOOL : (st.act == gpu::ACT_RELU ? gpu::IN_RELU : gpu::IN_PLAIN);
+      dy.mode = st.pooled ? gpu::IN_UNPOOL
+                          : (st.act == gpu::ACT_RELU ? gpu::IN_RELU : st.act == gpu::ACT_TANH ? gpu::IN_TANH : gpu::IN_PLAIN);
+      dy.act = st.act;
       dy.src = st.grad_buf; dy.aux_y = st.act_buf; dy.aux_arg = st.arg_buf;
       dy.SH = st.OH; dy.SW = st.OW; dy.SC = st.C; dy.PH = st.outH; dy.PW = st.outW;
       if (st.big) {

@@ -37,7 +37,13 @@ __device__ __forceinline__ float src_value(const StageSrc& s, int n, int sy, int
       if (py >= s.PH || px >= s.PW) return 0.f;
       const size_t i = (((size_t)n * s.PH + py) * s.PW + px) * s.SC + c;
       if (s.aux_arg[i] != (((sy & 1) << 1) | (sx & 1))) return 0.f;
-      return to_f(static_cast<const T*>(s.aux_y)[i]) > 0.f ? to_f(static_cast<const T*>(s.src)[i]) : 0.f;
+      const float y = to_f(static_cast<const T*>(s.aux_y)[i]), d = to_f(static_cast<const T*>(s.src)[i]);
+      return s.act == ACT_RELU ? (y > 0.f ? d : 0.f) : d * act_grad_y(s.act, y);
+    }
+    case IN_TANH: {
+      const size_t i = (((size_t)n * s.SH + sy) * s.SW + sx) * s.SC + c;
+      const float y = to_f(static_cast<const T*>(s.aux_y)[i]);
+      return to_f(static_cast<const T*>(s.src)[i]) * (1.f - y * y);
     }
     default:
       return to_f(static_cast<const T*>(s.src)[(((size_t)n * s.SH + sy) * s.SW + sx) * s.SC + c]);
@@ -104,7 +110,8 @@ __global__ void __launch_bounds__(256) im2col_kernel(Im2colParams p) {
 
 template <typename T>
 __global__ void __launch_bounds__(256) maxpool2_kernel(const T* __restrict__ in, T* __restrict__ out,
-                                                       uint8_t* __restrict__ arg, int N, int H, int W, int C) {
+                                                       uint8_t* __restrict__ arg, int N, int H, int W, int C,
+                                                       bool post_relu) {
   const int PH = H >> 1, PW = W >> 1;
   const int64_t total = (int64_t)N * PH * PW * C;
   for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
@@ -119,7 +126,7 @@ __global__ void __launch_bounds__(256) maxpool2_kernel(const T* __restrict__ in,
     for (int i = 1; i < 4; ++i)
       if (v[i] > best) { best = v[i]; a = i; }
     out[e] = from_f<T>(best);
-    arg[e] = (uint8_t)(to_f(from_f<T>(best)) > 0.f ? a : 4);  // input is post-ReLU: 4 = inactive window
+    arg[e] = (uint8_t)(!post_relu || to_f(from_f<T>(best)) > 0.f ? a : 4);  // post-ReLU: 4 = inactive window
   }
 }
 
@@ -138,7 +145,8 @@ __global__ void __launch_bounds__(256) grad_xform_kernel(StageSrc s, T* __restri
 // bf16, C % 8 == 0: one thread per (pixel, 8 channels), 16-byte moves,
 // 32-bit index math (host checks the element count).
 __global__ void __launch_bounds__(256) maxpool2_vec_kernel(const bf16* __restrict__ in, bf16* __restrict__ out,
-                                                           uint8_t* __restrict__ arg, int N, int H, int W, int C) {
+                                                           uint8_t* __restrict__ arg, int N, int H, int W, int C,
+                                                           bool post_relu) {
   const int PH = H >> 1, PW = W >> 1, C8 = C >> 3;
   const int total = N * PH * PW * C8;
   for (int e = blockIdx.x * blockDim.x + threadIdx.x; e < total; e += gridDim.x * blockDim.x) {
@@ -157,7 +165,7 @@ __global__ void __launch_bounds__(256) maxpool2_vec_kernel(const bf16* __restric
       if ((float)v2[j] > best) { best = (float)v2[j]; a = 2; }
       if ((float)v3[j] > best) { best = (float)v3[j]; a = 3; }
       o[j] = (bf16)best;
-      if (!(best > 0.f)) a = 4;  // post-ReLU input: inactive window
+      if (post_relu && !(best > 0.f)) a = 4;  // post-ReLU input: inactive window
       if (j < 4) a0 |= a << (8 * j); else a1 |= a << (8 * (j - 4));
     }
     store8(out + (size_t)r * C + c8 * 8, o);
@@ -235,25 +243,27 @@ void im2col(DType t, const Im2colParams& p, hipStream_t s) {
   else hipLaunchKernelGGL(im2col_kernel<float>, dim3(grid_cap(n)), dim3(256), 0, s, p);
 }
 
-void maxpool2(DType t, const void* in, void* out, uint8_t* arg, int N, int H, int W, int C, hipStream_t s) {
+void maxpool2(DType t, const void* in, void* out, uint8_t* arg, int N, int H, int W, int C, hipStream_t s,
+              bool post_relu) {
   const int64_t n = (int64_t)N * (H / 2) * (W / 2) * C;
   if (t == DType::BF16 && C % 8 == 0 && (int64_t)N * H * W * C < (1ll << 31)) {
     hipLaunchKernelGGL(maxpool2_vec_kernel, dim3(grid_cap(n / 8)), dim3(256), 0, s, static_cast<const bf16*>(in),
-                       static_cast<bf16*>(out), arg, N, H, W, C);
+                       static_cast<bf16*>(out), arg, N, H, W, C, post_relu);
     return;
   }
   if (t == DType::BF16)
     hipLaunchKernelGGL(maxpool2_kernel<bf16>, dim3(grid_cap(n)), dim3(256), 0, s, static_cast<const bf16*>(in),
-                       static_cast<bf16*>(out), arg, N, H, W, C);
+                       static_cast<bf16*>(out), arg, N, H, W, C, post_relu);
   else
     hipLaunchKernelGGL(maxpool2_kernel<float>, dim3(grid_cap(n)), dim3(256), 0, s, static_cast<const float*>(in),
-                       static_cast<float*>(out), arg, N, H, W, C);
+                       static_cast<float*>(out), arg, N, H, W, C, post_relu);
 }
 
 void grad_xform(DType t, const StageSrc& src, void* dz, int N, hipStream_t s) {
   const int64_t n = (int64_t)N * src.SH * src.SW * src.SC;
   if (t == DType::BF16 && src.SC % 8 == 0 && n < (1ll << 31) &&
-      (src.mode == IN_RELU || (src.mode == IN_UNPOOL && src.PH == src.SH / 2 && src.PW == src.SW / 2))) {
+      (src.mode == IN_RELU ||
+       (src.mode == IN_UNPOOL && src.act == ACT_RELU && src.PH == src.SH / 2 && src.PW == src.SW / 2))) {
     hipLaunchKernelGGL(grad_xform_vec_kernel, dim3(grid_cap(n / 8)), dim3(256), 0, s, src, static_cast<bf16*>(dz), N);
     return;
   }

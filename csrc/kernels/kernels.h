@@ -21,7 +21,9 @@ enum InMode : int {
   IN_PLAIN = 0,   // src is T NHWC
   IN_U8 = 1,      // src is u8 NHWC images (optionally gathered by idx), scaled 1/255
   IN_RELU = 2,    // value = (aux_y > 0) ? src : 0          (ReLU backward, no pool)
-  IN_UNPOOL = 3,  // value = (argmax == pos && aux_y > 0) ? src_pooled : 0  (2x2 maxpool + ReLU backward)
+  IN_UNPOOL = 3,  // value = (argmax == pos) ? act'(aux_y) * src_pooled : 0  (2x2 maxpool + act backward, act in
+                  // StageSrc::act; ReLU: argmax 4 also marks an inactive window)
+  IN_TANH = 4,    // value = (1 - aux_y^2) * src                 (tanh backward, no pool)
 };
 
 enum ActKind : int { ACT_NONE = 0, ACT_RELU = 1, ACT_TANH = 2 };
@@ -40,6 +42,7 @@ struct StageSrc {
   int SH = 0, SW = 0, SC = 0;    // conv-grid dims of the source (pre-pool for UNPOOL)
   int PH = 0, PW = 0;            // IN_UNPOOL: pooled dims of src/aux tensors
   int off = 0, up = 1;
+  int act = 1;                   // IN_UNPOOL: activation of the pooled conv (ActKind; default ReLU)
 };
 
 // Implicit-GEMM conv over small images staged whole in LDS ("conv_small").
@@ -383,7 +386,8 @@ struct Im2colParams {
   void* out = nullptr;
 };
 void im2col(DType t, const Im2colParams& p, hipStream_t s);
-void maxpool2(DType t, const void* in, void* out, uint8_t* arg, int N, int H, int W, int C, hipStream_t s);
+void maxpool2(DType t, const void* in, void* out, uint8_t* arg, int N, int H, int W, int C, hipStream_t s,
+              bool post_relu = true);
 // dz[n][y][x][c] = transform(src) at the conv-output grid (SH x SW x SC)
 void grad_xform(DType t, const StageSrc& src, void* dz, int N, hipStream_t s);
 

@@ -469,3 +469,46 @@ def test_bf16_grads_per_channel_vs_rounded_oracle(cuda, model):
     print("\n".join(report + [plan]))
     assert lerr < PER_CHANNEL_TOL["logit"], report[0]
     assert not bad, "\n".join(bad)
+
+
+GENERIC_SPECS = {
+    # tanh conv + pool (u8 first layer), pool after a linear conv, tanh FC
+    "tanhpool": "input 1 28 28; conv 8 k5 s1 p2 tanh; pool 2; conv 16 k3 s1 p1 none; pool 2; fc 32 tanh; fc 10 softmax",
+    # tanh conv without a pool feeding a strided ReLU conv on the regular kernels
+    "tanhplain": "input 3 20 20; conv 16 k3 s1 p1 tanh; conv 32 k3 s2 p1 relu; fc 10 softmax",
+}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+@pytest.mark.parametrize("name", sorted(GENERIC_SPECS))
+def test_generic_activation_convs_match_torch(cuda, name, dtype):
+    """Conv layers the pipelined kernels do not cover (tanh activations, a
+    max-pool after a non-ReLU conv) run on the implicit-GEMM / im2col path
+    with act' and the unpool applied by grad_xform: one step vs the fp64
+    PyTorch oracle (the CPU executor accepts the same specs)."""
+    spec = mcc.parse_model_spec(GENERIC_SPECS[name], name)
+    C, H, W = spec.input_shape()
+    B = 24
+    imgs, labels = mcc.synth_dataset(B, C, H, W, spec.num_classes(), seed=5)
+    params = mcc.init_params(spec, seed=2).astype(np.float32)
+    net = mcc.GpuNet(spec, dtype, B)
+    net.set_params(params)
+    d_img = torch.from_numpy(imgs).to(cuda)
+    d_lab = torch.from_numpy(labels).to(cuda)
+    s = torch.cuda.current_stream().cuda_stream
+    net.zero_stats(s)
+    net.forward(d_img.data_ptr(), 0, B, s)
+    net.loss(d_lab.data_ptr(), 0, 1.0 / B, True, s)
+    net.backward_all(s)
+    torch.cuda.synchronize()
+    logits, grads = net.get_logits(B), net.get_grads()
+    ref_logits, ref_grads, _ = _oracle(spec, params, imgs, labels)
+    tol = {"fp32": (1e-4, 1e-3), "bf16": (3e-2, 8e-2)}[dtype]
+    assert _relerr(logits, ref_logits) < tol[0], "logits mismatch"
+    for L in spec.layers():
+        if L["nweights"] == 0:
+            continue
+        for off, n, what in ((L["w_off"], L["nweights"], "W"), (L["b_off"], L["nbiases"], "b")):
+            err = _relerr(grads[off : off + n], ref_grads[off : off + n])
+            assert err < tol[1], f"{name} {dtype} {L['kind']} {what} grad rel err {err:.3e}"
