@@ -54,7 +54,8 @@ struct GpuNet::Stage {
   // large-image conv (explicit im2col + MFMA GEMM) when the image tile does
   // not fit the whole-image LDS kernels
   bool big = false;
-  bool generic = false;  // tanh conv / pool after a non-ReLU conv: im2col or igemm path + grad_xform
+  bool generic = false;  // tanh conv / pool after a non-ReLU conv / non-2x2 pool: im2col or igemm path + grad_xform
+  int pk = 2, ps = 2;    // pooled: window / stride
   int kgem = 0, kgem_d = 0;      // im2col row strides (fwd/dW, data grad)
   // implicit-GEMM kernels (igemm.hip) per direction of a large-image conv;
   // the explicit im2col + GEMM path remains for what they do not cover
@@ -220,8 +221,10 @@ void GpuNet::build() {
       st->generic = l.act != Act::ReLU && !(l.act == Act::None && !(i + 1 < L.size() && L[i + 1].kind == LayerKind::MaxPool));
       if (i + 1 < L.size() && L[i + 1].kind == LayerKind::MaxPool) {
         const LayerSpec& pl = L[i + 1];
-        MCC_CHECK(pl.ks == 2 && pl.stride == 2, "GPU engine fuses only 2x2/2 max-pools (after a conv)");
+        MCC_CHECK(pl.ks <= 15, "GPU engine: max-pool windows up to 15x15");
         st->pooled = true;
+        st->pk = pl.ks; st->ps = pl.stride;
+        if (pl.ks != 2 || pl.stride != 2) st->generic = true;  // standalone k x k / s pool + gather unpool
         st->outH = pl.H; st->outW = pl.W;
         ++i;
       }
@@ -302,7 +305,8 @@ void GpuNet::build() {
       // first layer forward: u8 gather through registers (K = KS*KS*inC small)
       if (st.ig_dw0 && st.KS * st.KS * st.inC <= 64) st.ig_fwd = true;
       // first layer weight gradient straight from the pooled dY / argmax
-      if (st.ig_dw0 && st.ig_fwd && st.pooled && st.act == gpu::ACT_RELU && st.KS == 3 && st.stride == 1 && st.pad == 1 &&
+      if (st.ig_dw0 && st.ig_fwd && st.pooled && st.pk == 2 && st.ps == 2 && st.act == gpu::ACT_RELU && st.KS == 3 &&
+          st.stride == 1 && st.pad == 1 &&
           !std::getenv("MCC_NO_C0DW")) {
         gpu::Conv0DwParams& c = st.pc0;
         c.B = max_batch_; c.H = st.OH; c.W = st.OW; c.C = st.inC; c.PH = st.outH; c.PW = st.outW; c.Cout = st.C;
@@ -314,7 +318,7 @@ void GpuNet::build() {
         st.ig_dw = st.inC % 8 == 0;
         st.ig_dx = st.stride == 1 && gpu::igemm_conv_supported(st.C, st.inC, st.KS);
       }
-      st.ig_pool = st.ig_fwd && st.pooled && st.OH % 2 == 0 && st.OW % 2 == 0;
+      st.ig_pool = st.ig_fwd && st.pooled && st.pk == 2 && st.ps == 2 && st.OH % 2 == 0 && st.OW % 2 == 0;
       if (!st.big && dtype_ == DType::BF16 && !no_pipe_) plan_pipe(st, s == 0);
       if (!st.big && dtype_ == DType::F32 && st.pooled && st.stride == 1 && !no_pipe_ &&
           (s == 0 || st.inC > 1)) {
@@ -673,6 +677,14 @@ void GpuNet::pack(hipStream_t s) {
 
 void GpuNet::zero_stats(hipStream_t s) { HIP_OK(hipMemsetAsync(stats_, 0, 32, s)); }
 
+// standalone max-pool of a conv stage's output (conv_buf -> act_buf, argmax)
+void GpuNet::pool_fwd(Stage& st, int B, hipStream_t s) {
+  if (st.pk == 2 && st.ps == 2)
+    gpu::maxpool2(dtype_, st.conv_buf, st.act_buf, st.arg_buf, B, st.OH, st.OW, st.C, s, st.act == gpu::ACT_RELU);
+  else
+    gpu::maxpool(dtype_, st.conv_buf, st.act_buf, st.arg_buf, B, st.OH, st.OW, st.C, st.pk, st.ps, s);
+}
+
 void GpuNet::forward(const uint8_t* images, const int32_t* idx, int B, hipStream_t s) {
   MCC_CHECK(B > 0 && B <= max_batch_, "forward: batch exceeds max_batch");
   B_ = B;
@@ -695,8 +707,7 @@ void GpuNet::forward(const uint8_t* images, const int32_t* idx, int B, hipStream
       g.pool = st.ig_pool; g.out_arg = st.arg_buf;
       if (si == 0) { g.u8 = true; g.in = images; g.idx = idx; }
       gpu::igemm_conv(g, s);
-      if (st.pooled && !st.ig_pool)
-        gpu::maxpool2(dtype_, st.conv_buf, st.act_buf, st.arg_buf, B, st.OH, st.OW, st.C, s, st.act == gpu::ACT_RELU);
+      if (st.pooled && !st.ig_pool) pool_fwd(st, B, s);
     } else if (st.kind == Stage::CONV && st.big) {
       // im2col (input transform fused) -> GEMM with bias+ReLU epilogue -> 2x2 max-pool
       gpu::Im2colParams ic;
@@ -713,8 +724,7 @@ void GpuNet::forward(const uint8_t* images, const int32_t* idx, int B, hipStream
       g.epi = gpu::EPI_BIAS_ACT; g.act = st.act; g.bias = params_ + st.b_off;
       g.C = st.pooled ? st.conv_buf : st.act_buf; g.ldc = st.C;
       gpu::gemm(dtype_, g, s);
-      if (st.pooled)
-        gpu::maxpool2(dtype_, st.conv_buf, st.act_buf, st.arg_buf, B, st.OH, st.OW, st.C, s, st.act == gpu::ACT_RELU);
+      if (st.pooled) pool_fwd(st, B, s);
     } else if (st.kind == Stage::CONV && st.direct_fwd) {
       gpu::Conv1DirectParams p = st.pd1;
       p.N = B;
@@ -846,6 +856,7 @@ void GpuNet::backward(int hi, int lo, hipStream_t s) {
       dy.mode = st.pooled ? gpu::IN_UNPOOL
                           : (st.act == gpu::ACT_RELU ? gpu::IN_RELU : st.act == gpu::ACT_TANH ? gpu::IN_TANH : gpu::IN_PLAIN);
       dy.act = st.act;
+      dy.pk = st.pk; dy.ps = st.ps;
       dy.src = st.grad_buf; dy.aux_y = st.act_buf; dy.aux_arg = st.arg_buf;
       dy.SH = st.OH; dy.SW = st.OW; dy.SC = st.C; dy.PH = st.outH; dy.PW = st.outW;
       if (st.big) {

@@ -33,12 +33,18 @@ __device__ __forceinline__ float src_value(const StageSrc& s, int n, int sy, int
       return to_f(static_cast<const T*>(s.aux_y)[i]) > 0.f ? to_f(static_cast<const T*>(s.src)[i]) : 0.f;
     }
     case IN_UNPOOL: {
-      const int py = sy >> 1, px = sx >> 1;
-      if (py >= s.PH || px >= s.PW) return 0.f;
-      const size_t i = (((size_t)n * s.PH + py) * s.PW + px) * s.SC + c;
-      if (s.aux_arg[i] != (((sy & 1) << 1) | (sx & 1))) return 0.f;
-      const float y = to_f(static_cast<const T*>(s.aux_y)[i]), d = to_f(static_cast<const T*>(s.src)[i]);
-      return s.act == ACT_RELU ? (y > 0.f ? d : 0.f) : d * act_grad_y(s.act, y);
+      // every window (py, px) holding (sy, sx) whose argmax is this position
+      // (one window for a 2x2/2 pool; overlapping pools sum, in window order)
+      float acc = 0.f;
+      const int py0 = sy >= s.pk ? (sy - s.pk) / s.ps + 1 : 0, px0 = sx >= s.pk ? (sx - s.pk) / s.ps + 1 : 0;
+      for (int py = py0; py <= sy / s.ps && py < s.PH; ++py)
+        for (int px = px0; px <= sx / s.ps && px < s.PW; ++px) {
+          const size_t i = (((size_t)n * s.PH + py) * s.PW + px) * s.SC + c;
+          if (s.aux_arg[i] != (sy - py * s.ps) * s.pk + (sx - px * s.ps)) continue;
+          const float y = to_f(static_cast<const T*>(s.aux_y)[i]), d = to_f(static_cast<const T*>(s.src)[i]);
+          acc += s.act == ACT_RELU ? (y > 0.f ? d : 0.f) : d * act_grad_y(s.act, y);
+        }
+      return acc;
     }
     case IN_TANH: {
       const size_t i = (((size_t)n * s.SH + sy) * s.SW + sx) * s.SC + c;
@@ -127,6 +133,27 @@ __global__ void __launch_bounds__(256) maxpool2_kernel(const T* __restrict__ in,
       if (v[i] > best) { best = v[i]; a = i; }
     out[e] = from_f<T>(best);
     arg[e] = (uint8_t)(!post_relu || to_f(from_f<T>(best)) > 0.f ? a : 4);  // post-ReLU: 4 = inactive window
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) maxpool_kernel(const T* __restrict__ in, T* __restrict__ out,
+                                                      uint8_t* __restrict__ arg, int N, int H, int W, int C, int k,
+                                                      int st, int PH, int PW) {
+  const int64_t total = (int64_t)N * PH * PW * C;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    const int c = (int)(e % C);
+    const int64_t r = e / C;
+    const int px = (int)(r % PW), py = (int)((r / PW) % PH), n = (int)(r / ((int64_t)PW * PH));
+    float best = 0.f;
+    int a = -1;
+    for (int dy = 0; dy < k; ++dy)
+      for (int dx = 0; dx < k; ++dx) {
+        const float v = to_f(in[(((size_t)n * H + py * st + dy) * W + px * st + dx) * C + c]);
+        if (a < 0 || v > best) { best = v; a = dy * k + dx; }
+      }
+    out[e] = from_f<T>(best);
+    arg[e] = (uint8_t)a;
   }
 }
 
@@ -259,11 +286,24 @@ void maxpool2(DType t, const void* in, void* out, uint8_t* arg, int N, int H, in
                        static_cast<float*>(out), arg, N, H, W, C, post_relu);
 }
 
+void maxpool(DType t, const void* in, void* out, uint8_t* arg, int N, int H, int W, int C, int k, int stride,
+             hipStream_t s) {
+  MCC_CHECK(k >= 1 && k <= 15 && stride >= 1 && H >= k && W >= k, "maxpool: bad window");
+  const int PH = (H - k) / stride + 1, PW = (W - k) / stride + 1;
+  const int64_t n = (int64_t)N * PH * PW * C;
+  if (t == DType::BF16)
+    hipLaunchKernelGGL(maxpool_kernel<bf16>, dim3(grid_cap(n)), dim3(256), 0, s, static_cast<const bf16*>(in),
+                       static_cast<bf16*>(out), arg, N, H, W, C, k, stride, PH, PW);
+  else
+    hipLaunchKernelGGL(maxpool_kernel<float>, dim3(grid_cap(n)), dim3(256), 0, s, static_cast<const float*>(in),
+                       static_cast<float*>(out), arg, N, H, W, C, k, stride, PH, PW);
+}
+
 void grad_xform(DType t, const StageSrc& src, void* dz, int N, hipStream_t s) {
   const int64_t n = (int64_t)N * src.SH * src.SW * src.SC;
   if (t == DType::BF16 && src.SC % 8 == 0 && n < (1ll << 31) &&
-      (src.mode == IN_RELU ||
-       (src.mode == IN_UNPOOL && src.act == ACT_RELU && src.PH == src.SH / 2 && src.PW == src.SW / 2))) {
+      (src.mode == IN_RELU || (src.mode == IN_UNPOOL && src.act == ACT_RELU && src.pk == 2 && src.ps == 2 &&
+                               src.PH == src.SH / 2 && src.PW == src.SW / 2))) {
     hipLaunchKernelGGL(grad_xform_vec_kernel, dim3(grid_cap(n / 8)), dim3(256), 0, s, src, static_cast<bf16*>(dz), N);
     return;
   }

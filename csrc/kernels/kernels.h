@@ -43,6 +43,7 @@ struct StageSrc {
   int PH = 0, PW = 0;            // IN_UNPOOL: pooled dims of src/aux tensors
   int off = 0, up = 1;
   int act = 1;                   // IN_UNPOOL: activation of the pooled conv (ActKind; default ReLU)
+  int pk = 2, ps = 2;            // IN_UNPOOL: pool window / stride (argmax = dy * pk + dx in the window)
 };
 
 // Implicit-GEMM conv over small images staged whole in LDS ("conv_small").
@@ -388,6 +389,9 @@ struct Im2colParams {
 void im2col(DType t, const Im2colParams& p, hipStream_t s);
 void maxpool2(DType t, const void* in, void* out, uint8_t* arg, int N, int H, int W, int C, hipStream_t s,
               bool post_relu = true);
+// k x k / stride max-pool (floor mode, first max wins, argmax = dy * k + dx; k <= 15)
+void maxpool(DType t, const void* in, void* out, uint8_t* arg, int N, int H, int W, int C, int k, int stride,
+             hipStream_t s);
 // dz[n][y][x][c] = transform(src) at the conv-output grid (SH x SW x SC)
 void grad_xform(DType t, const StageSrc& src, void* dz, int N, hipStream_t s);
 

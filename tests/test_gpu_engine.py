@@ -476,6 +476,10 @@ GENERIC_SPECS = {
     "tanhpool": "input 1 28 28; conv 8 k5 s1 p2 tanh; pool 2; conv 16 k3 s1 p1 none; pool 2; fc 32 tanh; fc 10 softmax",
     # tanh conv without a pool feeding a strided ReLU conv on the regular kernels
     "tanhplain": "input 3 20 20; conv 16 k3 s1 p1 tanh; conv 32 k3 s2 p1 relu; fc 10 softmax",
+    # overlapping 3x3/2 and 2x2/1 max-pools after ReLU convs (gather unpool sums the windows)
+    "pool32": "input 1 28 28; conv 8 k3 s1 p1 relu; pool 3 2; conv 16 k3 s1 p1 relu; pool 2 1; fc 10 softmax",
+    # non-overlapping 3x3/3 pool after a tanh conv (floor mode: 25 -> 8)
+    "pool33": "input 3 25 25; conv 16 k3 s1 p1 tanh; pool 3 3; fc 16 relu; fc 10 softmax",
 }
 
 
@@ -484,9 +488,10 @@ GENERIC_SPECS = {
 @pytest.mark.parametrize("name", sorted(GENERIC_SPECS))
 def test_generic_activation_convs_match_torch(cuda, name, dtype):
     """Conv layers the pipelined kernels do not cover (tanh activations, a
-    max-pool after a non-ReLU conv) run on the implicit-GEMM / im2col path
-    with act' and the unpool applied by grad_xform: one step vs the fp64
-    PyTorch oracle (the CPU executor accepts the same specs)."""
+    max-pool after a non-ReLU conv, k x k / s pools other than 2x2/2) run on
+    the implicit-GEMM / im2col path with act' and the (gather) unpool applied
+    by grad_xform: one step vs the fp64 PyTorch oracle (the CPU executor
+    accepts the same specs)."""
     spec = mcc.parse_model_spec(GENERIC_SPECS[name], name)
     C, H, W = spec.input_shape()
     B = 24
