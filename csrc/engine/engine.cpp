@@ -54,6 +54,7 @@ struct GpuNet::Stage {
   // large-image conv (explicit im2col + MFMA GEMM) when the image tile does
   // not fit the whole-image LDS kernels
   bool big = false;
+  bool dz_fused = false;  // big ReLU stage whose dZ the next stage's dX epilogue writes
   bool generic = false;  // tanh conv / pool after a non-ReLU conv / non-2x2 pool: im2col or igemm path + grad_xform
   int pk = 2, ps = 2;    // pooled: window / stride
   int kgem = 0, kgem_d = 0;      // im2col row strides (fwd/dW, data grad)
@@ -351,6 +352,32 @@ void GpuNet::build() {
                    st.in_ld % 8 == 0 && st.in_ld >= st.Kin && (int64_t)st.Nout * st.Kin >= 8192;
   }
 
+  // ---- data gradient straight into dZ (no grad_xform pass) ----
+  // A big stage whose input is a ReLU big conv writes that stage's dZ in its
+  // implicit-GEMM data-gradient epilogue: dX * (y > 0) for an unpooled conv
+  // (VGG-11 conv3/5/7), optionally the 2x2 unpool by the stored argmax for a
+  // pooled one (conv2/4/6); the separate grad_xform pass re-reads dX (and y /
+  // argmax) and re-writes dZ.
+  {
+    // 0: off, 1: ReLU mask + unpool, 2 (default): ReLU mask only -- the
+    // unpool epilogue's four scattered 8-byte stores per fragment cost more
+    // in the dX kernel than the grad_xform pass they replace (VGG-11 B=512:
+    // off 15.61k, mask-only 15.77k, mask+unpool 15.46k img/s)
+    const char* e = std::getenv("MCC_DZ_FUSE");
+    const int mode = e ? std::atoi(e) : 2;
+    const bool on = mode != 0;
+    for (size_t s = 1; on && s < stages_.size(); ++s) {
+      Stage& cur = *stages_[s];
+      Stage& pv = *stages_[s - 1];
+      const bool unpool_ok = pv.pooled && pv.pk == 2 && pv.ps == 2 && pv.OH % 2 == 0 && pv.OW % 2 == 0 &&
+                             pv.outH * 2 == pv.OH && pv.outW * 2 == pv.OW;
+      // (not for a conv0_dw first layer: its weight gradient reads the pooled dY itself)
+      pv.dz_fused = cur.kind == Stage::CONV && cur.big && cur.ig_dx && pv.kind == Stage::CONV && pv.big && !pv.c0dw &&
+                    (!pv.pooled || (unpool_ok && mode != 2)) && pv.act == gpu::ACT_RELU && dtype_ == DType::BF16 &&
+                    pv.C == cur.inC;
+    }
+  }
+
   // ---- packed weight table ----
   std::vector<int32_t> idx;
   auto reserve = [&](int64_t n) {
@@ -588,7 +615,8 @@ std::string GpuNet::plan() const {
       os << "  [" << s << "] conv " << st.inC << "x" << st.inH << "x" << st.inW << " -> " << st.C << "x" << st.OH << "x"
          << st.OW << (st.pooled ? " +maxpool" : "") << " k" << st.KS << "s" << st.stride << "p" << st.pad
          << (st.big ? (st.ig_fwd ? " igemm" : " im2col+gemm") : (st.cvec ? " lds-cvec" : " lds-scalar"))
-         << (st.c0dw ? " dw:pooled-direct" : "") << " chunks=" << st.nchunks
+         << (st.c0dw ? " dw:pooled-direct" : "") << (st.dz_fused ? " dz<-next-dx" : "")
+         << (st.generic ? " generic" : "") << " chunks=" << st.nchunks
          << " imgs=" << st.imgs_fwd << "/"
          << st.imgs_dx << "/" << st.imgs_dw;
       if (st.pipe_fwd || st.pipe_dx || st.pipe_dw || st.rows_dw) {
@@ -872,7 +900,7 @@ void GpuNet::backward(int hi, int lo, hipStream_t s) {
           continue;
         }
         // dZ = relu'/unpool(dY) at conv-output size
-        gpu::grad_xform(dtype_, dy, st.dz_buf, B, s);
+        if (!st.dz_fused) gpu::grad_xform(dtype_, dy, st.dz_buf, B, s);  // else written by the next stage's dX
         fork();
         if (st.ig_dw0) {
           // stage 0 (u8 input, few channels): the explicit im2col rows as a 1x1
@@ -942,6 +970,12 @@ void GpuNet::backward(int hi, int lo, hipStream_t s) {
           d.w = static_cast<const char*>(packed_) + es * st.pk_dx; d.ldw = st.kgem_d;
           d.epi_bias_act = false;
           d.out = stages_[si - 1]->grad_buf; d.ldo = st.inC;
+          if (stages_[si - 1]->dz_fused) {  // dZ of the ReLU stage below: masked / unpooled in the epilogue
+            const Stage& pv = *stages_[si - 1];
+            d.out = pv.dz_buf;
+            if (pv.pooled) d.unpool_arg = pv.arg_buf;
+            else d.relu_mask = pv.act_buf;
+          }
           gpu::igemm_conv(d, s);
         } else if (si > 0) {
           // dX = im2col(zero-inserted dZ) x flipped W^T

@@ -402,6 +402,26 @@ __global__ void __launch_bounds__(kIgT, 2) igemm_conv_kernel(IgemmParams p) {
         v[e] += bv[e];
         if (BIAS_ACT) v[e] = act_apply(p.act, v[e]);
       }
+      if (!BIAS_ACT && p.unpool_arg) {  // dX straight to the unpooled dZ of a 2x2-pooled ReLU layer
+        const int b = mdiv(p.div_ohw, m);
+        const int rem = m - b * p.OH * p.OW;
+        const int py = mdiv(p.div_ow, rem), px = rem - py * p.OW;
+        const uint32_t a4 = *reinterpret_cast<const uint32_t*>(p.unpool_arg + (size_t)m * p.N + ch);
+        bf16* base = out + (((size_t)b * 2 * p.OH + 2 * py) * 2 * p.OW + 2 * px) * p.ldo + ch;
+      #pragma unroll
+        for (int q = 0; q < 4; ++q) {  // argmax 4 (ReLU-inactive window): all four zero
+          bf16x4 oq;
+      #pragma unroll
+          for (int e = 0; e < 4; ++e) oq[e] = ((a4 >> (8 * e)) & 0xffu) == (uint32_t)q ? (bf16)v[e] : (bf16)0.f;
+          *reinterpret_cast<bf16x4*>(base + ((size_t)(q >> 1) * 2 * p.OW + (q & 1)) * p.ldo) = oq;
+        }
+        continue;
+      }
+      if (!BIAS_ACT && p.relu_mask) {  // data gradient straight to dZ of a ReLU layer: dX * (y > 0)
+        const bf16x4 y = *reinterpret_cast<const bf16x4*>(static_cast<const bf16*>(p.relu_mask) + (size_t)m * p.ldo + ch);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = (float)y[e] > 0.f ? v[e] : 0.f;
+      }
       const bf16x4 o = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
       const int orow = POOL ? (m >> 2) : m;
       if (POOL && BIAS_ACT && p.act == ACT_RELU) {  // ReLU-inactive window: argmax byte 4
@@ -722,6 +742,26 @@ __global__ void __launch_bounds__(kBigT, 1) igemm_big_kernel(IgemmParams p) {
           for (int e = 0; e < 4; ++e) {
             v[e] += bv[e];
             if (BIAS_ACT) v[e] = act_apply(p.act, v[e]);
+          }
+          if (!BIAS_ACT && p.unpool_arg) {  // dX straight to the unpooled dZ of a 2x2-pooled ReLU layer
+            const int b = mdiv(p.div_ohw, m);
+            const int rem = m - b * p.OH * p.OW;
+            const int py = mdiv(p.div_ow, rem), px = rem - py * p.OW;
+            const uint32_t a4 = *reinterpret_cast<const uint32_t*>(p.unpool_arg + (size_t)m * p.N + ch);
+            bf16* base = out + (((size_t)b * 2 * p.OH + 2 * py) * 2 * p.OW + 2 * px) * p.ldo + ch;
+          #pragma unroll
+            for (int q = 0; q < 4; ++q) {  // argmax 4 (ReLU-inactive window): all four zero
+              bf16x4 oq;
+          #pragma unroll
+              for (int e = 0; e < 4; ++e) oq[e] = ((a4 >> (8 * e)) & 0xffu) == (uint32_t)q ? (bf16)v[e] : (bf16)0.f;
+              *reinterpret_cast<bf16x4*>(base + ((size_t)(q >> 1) * 2 * p.OW + (q & 1)) * p.ldo) = oq;
+            }
+            continue;
+          }
+          if (!BIAS_ACT && p.relu_mask) {  // data gradient straight to dZ of a ReLU layer
+            const bf16x4 y = *reinterpret_cast<const bf16x4*>(static_cast<const bf16*>(p.relu_mask) + (size_t)m * p.ldo + ch);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = (float)y[e] > 0.f ? v[e] : 0.f;
           }
           const bf16x4 o = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
           const int orow = POOL ? (m >> 2) : m;
@@ -1250,6 +1290,8 @@ void igemm_conv(const IgemmParams& p0, hipStream_t s) {
   MCC_CHECK(p.K == p.KS * p.KS * p.C, "igemm_conv: K must be KS*KS*C");
   MCC_CHECK(p.M == p.B * p.OH * p.OW && p.M > 0, "igemm_conv: M must be B*OH*OW");
   MCC_CHECK(p.ldw >= p.K && p.ldw % 8 == 0 && p.ldo >= p.N && p.ldo % 4 == 0, "igemm_conv: bad leading dims");
+  MCC_CHECK((!p.relu_mask && !p.unpool_arg) || (!p.epi_bias_act && !p.pool && !(p.relu_mask && p.unpool_arg)),
+            "igemm_conv: relu_mask / unpool_arg are data-gradient epilogues (one of them)");
   MCC_CHECK((int64_t)(p.u8 ? 1 : p.B) * p.H * p.W * p.C < (1ll << 31), "igemm_conv: input exceeds 2^31");
   MCC_CHECK(p.OH == (p.H + 2 * p.pad - p.KS) / p.stride + 1 && p.OW == (p.W + 2 * p.pad - p.KS) / p.stride + 1,
             "igemm_conv: output geometry mismatch");

@@ -419,6 +419,10 @@ struct IgemmParams {
   bool u8 = false;                   // input = u8 image set (first layer), scaled 1/255
   const int32_t* idx = nullptr;      // u8: optional per-sample image index
   bool u8_runs = false;              // set at launch: u8 C=3 3x3 pad-1 im2col rows from dword runs
+  const void* relu_mask = nullptr;   // bf16; data gradient only: out = dX * (relu_mask > 0), same layout as out
+                                     // (writes the next-lower ReLU layer's dZ directly: no grad_xform pass)
+  const uint8_t* unpool_arg = nullptr;  // data gradient only: 2x2/2 argmax bytes [M][N] of the layer below;
+                                     // out = its unpooled dZ [B][2*OH][2*OW][ldo] (argmax 4: inactive window)
   int tile = -1;                     // -1 auto (MCC_IGEMM_BIG, default on), 0: 128x128 kernel,
                                      // 128 / 256: 256-pixel x 128 / 256-channel kernel where legal
   DivMagic div_ohw, div_ow;

@@ -517,3 +517,39 @@ def test_generic_activation_convs_match_torch(cuda, name, dtype):
         for off, n, what in ((L["w_off"], L["nweights"], "W"), (L["b_off"], L["nbiases"], "b")):
             err = _relerr(grads[off : off + n], ref_grads[off : off + n])
             assert err < tol[1], f"{name} {dtype} {L['kind']} {what} grad rel err {err:.3e}"
+
+
+@pytest.mark.gpu
+def test_dz_fused_into_next_dgrad_bit_equal(cuda, monkeypatch):
+    """ReLU big convs get their dZ from the next stage's implicit-GEMM
+    data-gradient epilogue -- dX * (y > 0), or the 2x2 unpool by the stored
+    argmax for a pooled conv -- instead of a grad_xform pass (MCC_DZ_FUSE=0:
+    the pass): bit-identical logits and gradients (masking / routing commute
+    with the bf16 rounding of dX)."""
+    spec = mcc.parse_model_spec("input 3 72 72; conv 64 k3 s1 p1 relu; conv 64 k3 s1 p1 relu; pool 2; "
+                                "conv 128 k3 s1 p1 relu; conv 128 k3 s1 p1 relu; pool 2; fc 10 softmax", "dzfuse")
+    C, H, W = spec.input_shape()
+    B = 6
+    imgs, labels = mcc.synth_dataset(B, C, H, W, spec.num_classes(), seed=8)
+    params = mcc.init_params(spec, seed=4).astype(np.float32)
+    d_img = torch.from_numpy(imgs).to(cuda)
+    d_lab = torch.from_numpy(labels).to(cuda)
+    s = torch.cuda.current_stream().cuda_stream
+    out = {}
+    for mode in ("1", "2", "0"):
+        monkeypatch.setenv("MCC_DZ_FUSE", mode)
+        net = mcc.GpuNet(spec, "bf16", B)
+        net.set_params(params)
+        net.zero_stats(s)
+        net.forward(d_img.data_ptr(), 0, B, s)
+        net.loss(d_lab.data_ptr(), 0, 1.0 / B, True, s)
+        net.backward_all(s)
+        torch.cuda.synchronize()
+        out[mode] = (net.plan(), net.get_logits(B), net.get_grads())
+        del net
+    assert out["1"][0].count("dz<-next-dx") == 3, out["1"][0]  # conv1, conv2 (pooled: unpool), conv3
+    assert out["2"][0].count("dz<-next-dx") == 2, out["2"][0]  # conv1, conv3 (ReLU mask only, the default)
+    assert "dz<-next-dx" not in out["0"][0]
+    for m in ("1", "2"):
+        np.testing.assert_array_equal(out[m][1], out["0"][1])
+        np.testing.assert_array_equal(out[m][2], out["0"][2])
