@@ -68,7 +68,8 @@ def _load_idx(path, spec):
 
 def _log(rank, msg):
     if rank == 0:
-        print(msg, file=sys.stderr, flush=True)
+        sys.stderr.write(f"{msg}\n")  # one write per line (see the shard line)
+        sys.stderr.flush()
 
 
 def main(argv=None) -> int:
@@ -141,7 +142,10 @@ def _train(a, world, rank, local_rank, use_gpu) -> int:
     tr_img = tr_img.reshape(N, H, W, C)
     lo, hi = N // world * rank, N // world * (rank + 1)
     if world > 1:
-        print(f"{rank} {lo} {hi}", file=sys.stderr, flush=True)
+        # one write per line: ranks share the stderr pipe, and print() writes
+        # the text and the newline separately (lines interleaved under load)
+        sys.stderr.write(f"{rank} {lo} {hi}\n")
+        sys.stderr.flush()
     b = max(1, a.batch // world)
     B = b * world  # effective global batch (SGD mean, sample count, img/s)
     total = a.epochs * N
