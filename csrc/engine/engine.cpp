@@ -55,6 +55,7 @@ struct GpuNet::Stage {
   // not fit the whole-image LDS kernels
   bool big = false;
   bool dz_fused = false;  // big ReLU stage whose dZ the next stage's dX epilogue writes
+  bool fc_fbwd = false;   // small FC: dX + dW in one fused pass (fc_bwd.hip)
   bool generic = false;  // tanh conv / pool after a non-ReLU conv / non-2x2 pool: im2col or igemm path + grad_xform
   int pk = 2, ps = 2;    // pooled: window / stride
   int kgem = 0, kgem_d = 0;      // im2col row strides (fwd/dW, data grad)
@@ -378,6 +379,20 @@ void GpuNet::build() {
     }
   }
 
+  // ---- small FC layers: data + weight gradient in one pass (MCC_FC_FBWD=1) ----
+  // Off by default: measured 50 us + a 15 us slab reduce for LeNet-5's 120 -> 84
+  // layer at B = 131072, vs 54 us for the split-K dW + reduce + FC dX kernels
+  // (one wave per SIMD, LDS-staged 2-byte epilogue; tools/gpu_r2w.sh).
+  {
+    const char* e = std::getenv("MCC_FC_FBWD");
+    const bool on = (e && std::atoi(e) != 0) && dtype_ == DType::BF16 && !no_fc_;
+    for (size_t s = 1; on && s < stages_.size(); ++s) {
+      Stage& st = *stages_[s];
+      st.fc_fbwd = st.kind == Stage::FC && !st.last && gpu::fc_small_bwd_supported(st.Nout, st.Kin) &&
+                   st.in_ld % 8 == 0 && st.out_ld % 8 == 0 && st.ldp >= st.Kin + 1 && st.permC == 0;
+    }
+  }
+
   // ---- packed weight table ----
   std::vector<int32_t> idx;
   auto reserve = [&](int64_t n) {
@@ -527,6 +542,8 @@ void GpuNet::build() {
   col_bytes_ = 0;
   for (Stage* sp : stages_) {
     const Stage& st = *sp;
+    if (st.kind == Stage::FC && st.fc_fbwd)
+      scratch = std::max(scratch, (size_t)gpu::fc_small_bwd_grid(Bm) * st.Nout * st.ldp * 4);
     if (st.kind == Stage::CONV && st.big) {
       const int KK = st.KS * st.KS;
       const int64_t rows = (int64_t)Bm * st.OH * st.OW;
@@ -632,7 +649,7 @@ std::string GpuNet::plan() const {
       os << "\n";
     } else {
       os << "  [" << s << "] fc " << st.Kin << " -> " << st.Nout << (st.last ? " (logits)" : "")
-         << (st.permC ? " nhwc-flatten" : "") << "\n";
+         << (st.permC ? " nhwc-flatten" : "") << (st.fc_fbwd ? " fused-bwd" : "") << "\n";
     }
   }
   return os.str();
@@ -865,7 +882,8 @@ void GpuNet::backward(int hi, int lo, hipStream_t s) {
     // serialised on wstream_, so scratch_ (split-K slabs) stays single-user;
     // the dX kernels never touch scratch_.
     const bool side = wstream_ && !(st.kind == Stage::CONV && st.big &&
-                                    !((st.ig_dw || st.ig_dw0 || st.c0dw) && (st.ig_dx || si == 0)));
+                                    !((st.ig_dw || st.ig_dw0 || st.c0dw) && (st.ig_dx || si == 0))) &&
+                      !(st.kind == Stage::FC && st.fc_fbwd);
     hipStream_t ws = s_main;
     if (!side && forked) {  // this stage's dW uses scratch_ on the main stream: drain the side stream first
       HIP_OK(hipEventRecord(join_ev_, wstream_));
@@ -1076,6 +1094,25 @@ void GpuNet::backward(int hi, int lo, hipStream_t s) {
     } else {
       const Stage& pv = *stages_[si - 1];
       if (st.head && head_done_) continue;  // done by loss() (xent_head)
+      if (st.fc_fbwd) {  // dX and dW/db in one pass (main stream: it owns scratch_ here)
+        gpu::FcBwdParams f;
+        f.M = B; f.N = st.Nout; f.K = st.Kin;
+        f.dz = st.grad_buf; f.ldz = st.out_ld;
+        f.x = pv.act_buf; f.ldx = st.in_ld;
+        f.w = params_ + st.w_off;
+        f.act = pv.kind == Stage::FC ? pv.act : gpu::ACT_NONE;  // conv masks are applied by its staging
+        f.dx = pv.grad_buf; f.lddx = st.in_ld;
+        f.slab = scratch_; f.ldp = st.ldp;
+        MCC_CHECK((size_t)gpu::fc_small_bwd_grid(B) * st.Nout * st.ldp * 4 <= scratch_bytes_, "fc fused bwd scratch");
+        gpu::fc_small_bwd(f, s);
+        gpu::DwReduceParams r;
+        r.S = gpu::fc_small_bwd_grid(B); r.Nout = st.Nout; r.kfeat = st.Kin; r.ldp = st.ldp; r.part = scratch_;
+        r.partial_stride = (int64_t)st.Nout * st.ldp;
+        r.gw = grads_ + st.w_off; r.gb = grads_ + st.b_off;
+        r.permC = 0; r.permHW = 0;
+        gpu::dw_reduce(r, s);
+        continue;
+      }
       fork();
       if (st.fc_igdw) {
         gpu::IgemmDwParams w;

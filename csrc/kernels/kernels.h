@@ -328,6 +328,25 @@ void fc_forward(const FcParams& p, hipStream_t s);
 
 // Reduce split-K partials of a weight gradient into the canonical grad:
 // gw[n*Kc + perm(k)] (k < kfeat), gb[n] (k == kfeat).
+// Fused backward of a small FC layer (fc_bwd.hip): dX = act'(X) * (dZ W) and
+// per-workgroup dW/db slabs [grid][N][ldp] (column K = bias) in one pass.
+struct FcBwdParams {
+  int M = 0, N = 0, K = 0;           // rows, outputs (<= 96), inputs (< 128, % 8)
+  const void* dz = nullptr;          // bf16 [M][ldz] pre-activation gradient of this layer
+  int ldz = 0;
+  const void* x = nullptr;           // bf16 [M][ldx] layer input (the previous layer's output)
+  int ldx = 0;
+  const float* w = nullptr;          // [N][K] fp32 master weights (rounded to bf16 in LDS)
+  int act = 0;                       // activation of the previous layer (act' from X)
+  void* dx = nullptr;                // bf16 [M][lddx]
+  int lddx = 0;
+  float* slab = nullptr;             // [fc_small_bwd_grid(M)][N][ldp]
+  int ldp = 0;
+};
+bool fc_small_bwd_supported(int N, int K);
+int fc_small_bwd_grid(int M);
+void fc_small_bwd(const FcBwdParams& p, hipStream_t s);
+
 struct DwReduceParams {
   int S = 1, Nout = 0, kfeat = 0, ldp = 0;
   const float* part = nullptr;  // [S][Nout][ldp]

@@ -553,3 +553,36 @@ def test_dz_fused_into_next_dgrad_bit_equal(cuda, monkeypatch):
     for m in ("1", "2"):
         np.testing.assert_array_equal(out[m][1], out["0"][1])
         np.testing.assert_array_equal(out[m][2], out["0"][2])
+
+
+@pytest.mark.gpu
+def test_fc_fused_bwd_matches_unfused(cuda, monkeypatch):
+    """Small FC layers (LeNet-5 120 -> 84) run dX and dW/db in one fused pass
+    (fc_bwd.hip); MCC_FC_FBWD=0 runs the split-K dW GEMM + reduce and the FC
+    data-gradient kernel.  Same step up to fp32 summation order."""
+    spec = mcc.make_model("lenet5")
+    B = 200  # not a multiple of the 64-row block
+    imgs, labels = mcc.synth_dataset(B, 1, 28, 28, 10, seed=6)
+    params = mcc.init_params(spec, seed=5).astype(np.float32)
+    d_img = torch.from_numpy(imgs).to(cuda)
+    d_lab = torch.from_numpy(labels).to(cuda)
+    s = torch.cuda.current_stream().cuda_stream
+    out = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("MCC_FC_FBWD", mode)
+        net = mcc.GpuNet(spec, "bf16", B)
+        net.set_params(params)
+        net.zero_stats(s)
+        net.forward(d_img.data_ptr(), 0, B, s)
+        net.loss(d_lab.data_ptr(), 0, 1.0 / B, True, s)
+        net.backward_all(s)
+        torch.cuda.synchronize()
+        out[mode] = (net.plan(), net.get_grads())
+        del net
+    assert "fused-bwd" in out["1"][0] and "fused-bwd" not in out["0"][0], out["1"][0]
+    for L in spec.layers():
+        if L["nweights"] == 0:
+            continue
+        for off, n, what in ((L["w_off"], L["nweights"], "W"), (L["b_off"], L["nbiases"], "b")):
+            err = _relerr(out["1"][1][off : off + n], out["0"][1][off : off + n])
+            assert err < 1e-2, f"{L['kind']} {what} fused vs unfused rel err {err:.3e}"
