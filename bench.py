@@ -65,6 +65,9 @@ def main():
                          "from a HIP graph; auto = on at N=1 (bit-equal to eager: tests/test_gpu_rccl.py) "
                          "with a fallback to per-kernel launches if capture fails, off at N>1 (multi-rank "
                          "capture of the collectives is not verifiable on a one-GPU box)")
+    ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
+                    help="nccl (= RCCL, the measured path) or gloo: a rehearsal of the multi-rank bench logic "
+                         "with more ranks than GPUs (ranks share GPUs round-robin; not a performance number)")
     args = ap.parse_args()
 
     import torch
@@ -75,14 +78,19 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and rank == 0:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    ndev = torch.cuda.device_count()  # (counting does not initialise the GPU)
+    if args.dist_backend == "nccl" and world > ndev:
+        raise SystemExit(f"bench: {world} ranks but {ndev} GPU(s): RCCL needs one GPU per rank (--dist-backend gloo "
+                         "rehearses more ranks than GPUs)")
+    dev_idx = local_rank % max(1, ndev)
+    torch.cuda.set_device(dev_idx)
+    dev = torch.device("cuda", dev_idx)
     if world > 1 or not args.no_dist:
         # RCCL process group at every N, 1 included: the N=1 step runs the
         # same broadcast + bucketed all-reduce on RCCL's stream as N=8
         from mpi_cuda_cnn_amd.parallel.ddp import init_process_group
 
-        init_process_group("nccl", dev)
+        init_process_group(args.dist_backend, dev)
 
     import mpi_cuda_cnn_amd as mcc
     from mpi_cuda_cnn_amd.trainer import GpuTrainer
@@ -101,7 +109,7 @@ def main():
         spec,
         dtype=args.dtype,
         batch=B,
-        device=local_rank,
+        device=dev_idx,
         seed=0,
         lr=args.lr,
         momentum=args.momentum,
@@ -194,7 +202,7 @@ def main():
                 "batch_per_gpu": B,
                 "input_shape": f"{C}x{H}x{W}",
                 "optimizer": f"sgd lr={args.lr} momentum={args.momentum}",
-                "allreduce": (f"rccl: {coll_per_step:g} all-reduce(s)/step over {len(tr.sync.buckets)} "
+                "allreduce": (f"{'rccl' if args.dist_backend == 'nccl' else 'gloo (rehearsal)'}: {coll_per_step:g} all-reduce(s)/step over {len(tr.sync.buckets)} "
                               f"bucket(s) <= {args.bucket_mb} MiB, async on RCCL's stream, joined before SGD"
                               if coll_per_step else "none (--no-dist)"),
                 "train_loss_last": round(st["loss_sum"] / (B * args.steps), 4),

@@ -104,3 +104,23 @@ def test_exit_codes_gpu_programs(idx_files):
     for prog in ("cnn_hip", "cnn_dist"):
         assert _run([os.path.join(ROOT, "build/bin", prog)]).returncode == 100
         assert _run([os.path.join(ROOT, "build/bin", prog), "/nonexistent"] + idx_files[1:]).returncode == 111
+
+
+@pytest.mark.gpu
+def test_bench_two_ranks_gloo_rehearsal():
+    """bench.py's multi-rank logic as the driver launches it (torch.distributed.run,
+    one JSON line from rank 0, barriers + MAX of the rank times, n_gpus = world),
+    rehearsed with two gloo ranks sharing the box's one GPU (RCCL needs a GPU per
+    rank; the 8-GPU RCCL run is the driver's)."""
+    import json
+
+    r = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+              "--master-addr=127.0.0.1", f"--master-port={_free_port()}", "bench.py", "--gpus", "2",
+              "--steps", "3", "--warmup", "2", "--batch-per-gpu", "4096", "--dist-backend", "gloo"],
+             cwd=ROOT, env=dict(os.environ, MASTER_ADDR="127.0.0.1"))
+    assert r.returncode == 0, r.stderr
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["steps"] == 3 and d["config"]["global_batch"] == 8192, d
+    assert d["config"]["parallelism"] == "dp2" and d["value"] > 0, d
