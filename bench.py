@@ -35,8 +35,10 @@ METRIC = "images/sec (whole node), LeNet-5 MNIST-shaped, at 1/2/4/8 MI355X"
 # round 2: 3.64 M at 16,384 -> 3.91 M at 32,768 (65,536 exceeds the 32-bit bound).
 # VGG-11: 15.0 k img/s at 256 -> 15.8 k at 512.
 DEFAULT_BATCH = {"lenet5": 131072, "ref": 65536, "cifar3": 32768, "vgg11": 512}
-# models whose step is faster with the dW side stream (engine.cpp, measured A/B)
-SIDE_STREAM = {"cifar3"}
+# models whose step is faster with the dW side stream (engine.cpp, measured A/B): none with the
+# round-2 kernels (CIFAR-3conv at 32768: 4.38 M img/s without, 4.27 M with; LeNet-5 / VGG-11 / ref
+# also faster without, profiles/side_stream_ab_r2.txt)
+SIDE_STREAM: set = set()
 
 
 def metric_for(model):
