@@ -460,7 +460,7 @@ __global__ void __launch_bounds__(kIgT, 2) igemm_conv_kernel(IgemmParams p) {
 template <int N> __device__ __forceinline__ void vm_wait();
 #define MCC_VM_WAIT(n) \
   template <> __device__ __forceinline__ void vm_wait<n>() { asm volatile("s_waitcnt vmcnt(" #n ")" ::: "memory"); }
-MCC_VM_WAIT(0) MCC_VM_WAIT(1) MCC_VM_WAIT(2) MCC_VM_WAIT(3) MCC_VM_WAIT(4) MCC_VM_WAIT(6)
+MCC_VM_WAIT(0) MCC_VM_WAIT(1) MCC_VM_WAIT(2) MCC_VM_WAIT(3) MCC_VM_WAIT(4)
 #undef MCC_VM_WAIT
 __device__ __forceinline__ void raw_barrier() {
   asm volatile("" ::: "memory");
