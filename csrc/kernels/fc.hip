@@ -52,8 +52,21 @@ __host__ __device__ inline size_t fc_lds(int N, int ldw, int K) {
 // workgroup and reused over several row blocks; small W keeps one row block
 // per workgroup (enough workgroups per CU to hide the A-fragment latency).
 template <int EPI, int ACT, int NCH, bool P>
-__global__ void __launch_bounds__(kFcThreads) fc_kernel(FcParams p) {
+__global__ void __launch_bounds__(kFcThreads) fc_kernel(FcParams p0) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  // column split: this workgroup's W rows / bias / aux / output columns
+  FcParams p = p0;
+  int cols = p.ldc;  // stored columns (up to the leading dim: its padding is written as 0)
+  if (p.nsub > 0) {
+    const int n0 = (int)blockIdx.y * p.nsub;
+    p.N = min(p.nsub, p.N - n0);
+    p.W = static_cast<const bf16*>(p.W) + (size_t)n0 * p.ldw;
+    if (p.bias) p.bias += n0;
+    if (p.aux) p.aux = static_cast<const bf16*>(p.aux) + n0;
+    if (p.C) p.C = static_cast<bf16*>(p.C) + n0;
+    if (p.Cf) p.Cf += n0;
+    cols = blockIdx.y + 1 < gridDim.y ? p.nsub : p.ldc - n0;
+  }
   const int ldk = p.ldw;
   const int npad = fc_npad(p.N);
   const int wel = fc_welems(p.N, p.ldw, p.K);
@@ -165,7 +178,7 @@ __global__ void __launch_bounds__(kFcThreads) fc_kernel(FcParams p) {
     // wave-private tile -> 16 rows x (tn*16) columns, 16-byte stores (ldc % 8 == 0)
     __builtin_amdgcn_wave_barrier();
     const int c0 = t0 * 16;
-    const int ncols = min(tn * 16, p.ldc - c0);  // up to the leading dim (padding columns written as 0)
+    const int ncols = min(tn * 16, cols - c0);  // up to the leading dim (padding columns written as 0)
     bf16* C = static_cast<bf16*>(p.C);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {  // 16 rows x 16 vectors of 8 columns, 4 per lane
@@ -198,16 +211,30 @@ void fc_forward(const FcParams& p, hipStream_t s) {
                 (p.epi == EPI_LOGITS || p.ldc % 8 == 0),
             "fc_forward: leading dims must be multiples of 8 covering K");
   if (p.M <= 0) return;
-  const size_t lds = fc_lds(p.N, p.ldw, p.K);
+  FcParams pl = p;
+  // a W that leaves room for only ONE workgroup per CU (LeNet-5 FC1 forward
+  // and data gradient: 96 KB) is split by columns over blockIdx.y: half of W
+  // per workgroup, several workgroups per CU to hide the A / store latency
+  // (MCC_FC_SPLIT=1; default: one workgroup holds all of W)
+  const char* split_env = std::getenv("MCC_FC_SPLIT");
+  const bool split_ok = (split_env && std::atoi(split_env) != 0) && p.epi != EPI_LOGITS;
+  int nsplit = 1;
+  if (split_ok && p.N >= 64 && (160 * 1024) / (fc_lds(p.N, p.ldw, p.K) + 1024) <= 1) {
+    pl.nsub = (cdiv(p.N, 2) + 15) & ~15;
+    nsplit = cdiv(p.N, pl.nsub);
+  }
+  const int nmax = pl.nsub ? pl.nsub : p.N;
+  const size_t lds = fc_lds(nmax, p.ldw, p.K);
   // persistent (as many workgroups as the LDS lets every CU hold) when W
   // limits the CU to one or two workgroups
   const int per_cu = std::max(1, std::min(8, (int)((160 * 1024) / (lds + 1024))));
   const bool persist = per_cu <= 2;
-  const dim3 grid((unsigned)(persist ? std::min(cdiv(p.M, kFcRows), 256 * per_cu) : cdiv(p.M, kFcRows))),
+  const dim3 grid((unsigned)(persist ? std::min(cdiv(p.M, kFcRows), 256 * per_cu) : cdiv(p.M, kFcRows)),
+                  (unsigned)nsplit),
       block(kFcThreads);
   MCC_CHECK(lds <= 160 * 1024, "fc_forward: weights do not fit in LDS");
   const int nchb = fc_nchb(p.K);
-  auto go = [&](auto kern) { hipLaunchKernelGGL(kern, grid, block, lds, s, p); };
+  auto go = [&](auto kern) { hipLaunchKernelGGL(kern, grid, block, lds, s, pl); };
   auto by_nch = [&](auto tag) {
     constexpr int EPI = decltype(tag)::epi, ACT = decltype(tag)::act;
     switch (nchb) {

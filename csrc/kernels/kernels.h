@@ -322,6 +322,7 @@ struct FcParams {
   float* Cf = nullptr;
   long long* dbg = nullptr;  // diagnostics: per-wave phase timestamps [grid][4 waves][4]
   int ablate = 0;            // diagnostics: 1 skip the output copy, 2 skip the MFMAs
+  int nsub = 0;              // set at launch: column split (blockIdx.y owns columns [y*nsub, +nsub))
 };
 bool fc_supported(int N, int K);
 void fc_forward(const FcParams& p, hipStream_t s);
