@@ -215,9 +215,12 @@ void fc_forward(const FcParams& p, hipStream_t s) {
   // a W that leaves room for only ONE workgroup per CU (LeNet-5 FC1 forward
   // and data gradient: 96 KB) is split by columns over blockIdx.y: half of W
   // per workgroup, several workgroups per CU to hide the A / store latency
-  // (MCC_FC_SPLIT=1; default: one workgroup holds all of W)
+  // (MCC_FC_SPLIT: 0 never, 1 forward and data gradient, 2 data gradient only)
   const char* split_env = std::getenv("MCC_FC_SPLIT");
-  const bool split_ok = (split_env && std::atoi(split_env) != 0) && p.epi != EPI_LOGITS;
+  // default: data gradient only (LeNet-5 FC1 dX 48.8 -> 43.2 us; the forward
+  // measured slower split, 37.6 -> 43.7 us: tools/gpu_r3e.sh)
+  const int split_mode = split_env ? std::atoi(split_env) : 2;  // 0 off, 1 all, 2 data gradient
+  const bool split_ok = p.epi != EPI_LOGITS && (split_mode == 1 || (split_mode == 2 && p.epi == EPI_DACT));
   int nsplit = 1;
   if (split_ok && p.N >= 64 && (160 * 1024) / (fc_lds(p.N, p.ldw, p.K) + 1024) <= 1) {
     pl.nsub = (cdiv(p.N, 2) + 15) & ~15;
