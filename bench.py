@@ -33,8 +33,9 @@ METRIC = "images/sec (whole node), LeNet-5 MNIST-shaped, at 1/2/4/8 MI355X"
 # (B * 16 padded channels * 28 * 28 < 2^31).
 # CIFAR-3conv: 1.88 M img/s at 4,096 -> 2.58 M at 16,384 (profiles/bench_models_r1g.jsonl);
 # round 2: 3.64 M at 16,384 -> 3.91 M at 32,768 (65,536 exceeds the 32-bit bound).
-# VGG-11: 15.0 k img/s at 256 -> 15.8 k at 512.
-DEFAULT_BATCH = {"lenet5": 131072, "ref": 65536, "cifar3": 32768, "vgg11": 512}
+# VGG-11: 15.0 k img/s at 256 -> 15.7 k at 512 -> 16.26 k at 640 (640 x 64 x 224^2 is 95.7 % of the
+# 32-bit activation bound; the 224^2 x 64 pre-pool conv1 tensor is never materialised).
+DEFAULT_BATCH = {"lenet5": 131072, "ref": 65536, "cifar3": 32768, "vgg11": 640}
 # models whose step is faster with the dW side stream (engine.cpp, measured A/B): none with the
 # round-2 kernels (CIFAR-3conv at 32768: 4.38 M img/s without, 4.27 M with; LeNet-5 / VGG-11 / ref
 # also faster without, profiles/side_stream_ab_r2.txt)
