@@ -115,21 +115,30 @@ __global__ void __launch_bounds__(256) softmax_xent_kernel(XentParams p) {
 constexpr int kHeadRows = 128;
 constexpr int kHeadThreads = 512;
 constexpr int kHeadLd = kHeadRows + 8;  // bf16 row stride of the transposed images (16-byte aligned)
-constexpr int kHeadLds = 16 * 128 * 4 + 16 * kHeadLd * 2 + 128 * kHeadLd * 2;
+// LDS sized by the input width (16 * NT columns, NT = ceil((Kin + 1) / 16)):
+// LeNet-5's 84 -> 10 head needs 36.6 KB, four workgroups per CU, so the
+// 1024 workgroups of a 131072-row batch run in one round (a fixed 128-column
+// layout took 47.6 KB: three per CU, two rounds; 33.2 -> 31.5 us,
+// profiles/xent_head_lds_ab_r2.txt)
+__host__ __device__ constexpr int head_nt(int Kin) { return (Kin + 1 + 15) >> 4; }
+__host__ __device__ constexpr int head_lds(int Kin) {
+  return 16 * (16 * head_nt(Kin)) * 4 + 16 * kHeadLd * 2 + 16 * head_nt(Kin) * kHeadLd * 2;
+}
 
 __global__ void __launch_bounds__(kHeadThreads) xent_head_kernel(XentHeadParams hp) {
-  __shared__ __attribute__((aligned(16))) char smem[kHeadLds];
+  extern __shared__ __attribute__((aligned(16))) char smem[];
   __shared__ float red[3][kHeadThreads / 64];
   const XentParams& p = hp.x;
+  const int N = p.N, Kin = hp.Kin;
+  const int NT = head_nt(Kin), kw = 16 * NT;  // Ws row stride (floats) = HT rows
   float* Ws = reinterpret_cast<float*>(smem);
-  bf16* E = reinterpret_cast<bf16*>(smem + 16 * 128 * 4);
+  bf16* E = reinterpret_cast<bf16*>(smem + 16 * kw * 4);
   bf16* HT = E + 16 * kHeadLd;
   const int tid = threadIdx.x;
   const int r = tid >> 2, q = tid & 3;
-  const int N = p.N, Kin = hp.Kin;
   // weights rounded through bf16, as the packed compute copy of the FC path
-  for (int i = tid; i < 16 * 128; i += kHeadThreads) {
-    const int n = i >> 7, k = i & 127;
+  for (int i = tid; i < 16 * kw; i += kHeadThreads) {
+    const int n = i / kw, k = i - n * kw;
     Ws[i] = (n < N && k < Kin) ? (float)(bf16)hp.w[(size_t)n * Kin + k] : 0.f;
   }
   const int row = blockIdx.x * kHeadRows + r;
@@ -196,7 +205,6 @@ __global__ void __launch_bounds__(kHeadThreads) xent_head_kernel(XentHeadParams 
   const bf16* hrow = static_cast<const bf16*>(hp.h) + (size_t)row * hp.ldh;
   bf16* drow = static_cast<bf16*>(hp.dh) + (size_t)row * hp.ldh;
   const int K8 = (Kin + 7) & ~7;
-  const int NT = (Kin + 1 + 15) >> 4;
   for (int k0 = 8 * q; k0 < K8; k0 += 32) {
     bf16x8 hv;
     if (live) hv = load8(hrow + k0);
@@ -208,8 +216,8 @@ __global__ void __launch_bounds__(kHeadThreads) xent_head_kernel(XentHeadParams 
 #pragma unroll
     for (int n = 0; n < 16; ++n) {
       if (n >= N) break;
-      const f32x4 w0 = *reinterpret_cast<const f32x4*>(Ws + n * 128 + k0);
-      const f32x4 w1 = *reinterpret_cast<const f32x4*>(Ws + n * 128 + k0 + 4);
+      const f32x4 w0 = *reinterpret_cast<const f32x4*>(Ws + n * kw + k0);
+      const f32x4 w1 = *reinterpret_cast<const f32x4*>(Ws + n * kw + k0 + 4);
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         acc[i] += e[n] * w0[i];
@@ -587,7 +595,7 @@ void xent_head(const XentHeadParams& p, hipStream_t s) {
   MCC_CHECK(p.h && p.dh && p.w && p.slab && p.ldp >= p.Kin + 1 && (reinterpret_cast<uintptr_t>(p.h) & 15) == 0 &&
                 (reinterpret_cast<uintptr_t>(p.dh) & 15) == 0,
             "xent_head: bad buffers");
-  hipLaunchKernelGGL(xent_head_kernel, dim3((unsigned)xent_head_slabs(p.x.M)), dim3(kHeadThreads), 0, s, p);
+  hipLaunchKernelGGL(xent_head_kernel, dim3((unsigned)xent_head_slabs(p.x.M)), dim3(kHeadThreads), head_lds(p.Kin), s, p);
 }
 
 void softmax_xent(DType t, const XentParams& p, hipStream_t s) {

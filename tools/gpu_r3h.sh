@@ -1,10 +1,9 @@
 #!/bin/bash
-# 13-chunk FC instantiation (LeNet-5 FC1 K=400): numerics + A/B against the previous build (git stash-free:
-# the A/B arm is the same binary with MCC_FC_NCH16=... not available, so compare to the recorded 65.1-65.3 M)
+# xent head LDS sized by input width: numerics + bench + timeline
 set -o pipefail
 cd "$(dirname "$0")/.."
 R=$PWD
-O=$R/gpurun_out/r3h
+O=$R/gpurun_out/${OUT:-r3h}
 mkdir -p $O
 timeout -k 10 400 python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_engine.py -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest.log 2>&1 \
   || { grep -E "FAIL|Error|assert" $O/pytest.log | head -30; tail -30 $O/pytest.log; exit 1; }
@@ -17,4 +16,4 @@ done
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv -- python3 $R/bench.py --steps 8 --warmup 2 > $O/prof.log 2>&1 || { tail $O/prof.log; exit 1; }
 python3 $R/tools/step_timeline.py $O/prof/run_kernel_trace.csv > $O/timeline.txt
-grep -E "fc_|step" $O/timeline.txt | cut -c1-110
+grep -E "fc_|xent|dw_reduce_kernel|step" $O/timeline.txt | cut -c1-110
