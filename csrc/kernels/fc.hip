@@ -24,8 +24,9 @@ namespace gpu {
 
 namespace {
 
-constexpr int kFcThreads = 256;
-constexpr int kFcRows = 64;       // rows per workgroup (16 per wave)
+constexpr int kFcThreads = 512;  // 8 waves: 256 measured 7.8 us/step slower over LeNet-5's five FC kernels (profiles/fc_waves_ab_r2.txt)
+constexpr int kFcWaves = kFcThreads / 64;
+constexpr int kFcRows = 16 * kFcWaves;  // rows per workgroup (16 per wave)
 constexpr int kFcMaxChunks = 16;  // K <= 512
 constexpr int kFcGroupTiles = 8;  // column tiles per staged output group (128 columns)
 constexpr int kFcStageLd = kFcGroupTiles * 16 + 8;
@@ -45,7 +46,7 @@ __host__ __device__ inline int fc_welems(int N, int ldw, int K) {
   return ((fc_npad(N) * ldw + fc_nchb(K) * 32 + 7) & ~7);
 }
 __host__ __device__ inline size_t fc_lds(int N, int ldw, int K) {
-  return (size_t)fc_welems(N, ldw, K) * 2 + (size_t)fc_npad(N) * 4 + (size_t)4 * 16 * kFcStageLd * 2;
+  return (size_t)fc_welems(N, ldw, K) * 2 + (size_t)fc_npad(N) * 4 + (size_t)kFcWaves * 16 * kFcStageLd * 2;
 }
 
 // P (persistent): large W (one or two workgroups per CU) is staged once per
@@ -75,7 +76,7 @@ __global__ void __launch_bounds__(kFcThreads) fc_kernel(FcParams p0) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r16 = lane & 15, g = lane >> 4;
   bf16* stg = reinterpret_cast<bf16*>(smem + (size_t)wel * 2 + (size_t)npad * 4) + wave * 16 * kFcStageLd;
-  long long* dbg = p.dbg ? p.dbg + ((size_t)blockIdx.x * 4 + wave) * 4 : nullptr;
+  long long* dbg = p.dbg ? p.dbg + ((size_t)blockIdx.x * kFcWaves + wave) * 4 : nullptr;
   if (dbg && lane == 0) dbg[0] = (long long)__builtin_amdgcn_s_memrealtime();
 
   // ---- W -> LDS: the packed [N][ldw] block is contiguous, so it moves as
