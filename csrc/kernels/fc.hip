@@ -218,9 +218,12 @@ void fc_forward(const FcParams& p, hipStream_t s) {
   // per workgroup, several workgroups per CU to hide the A / store latency
   // (MCC_FC_SPLIT: 0 never, 1 forward and data gradient, 2 data gradient only)
   const char* split_env = std::getenv("MCC_FC_SPLIT");
-  // default: data gradient only (LeNet-5 FC1 dX 48.8 -> 43.2 us; the forward
-  // measured slower split, 37.6 -> 43.7 us: tools/gpu_r3e.sh)
-  const int split_mode = split_env ? std::atoi(split_env) : 2;  // 0 off, 1 all, 2 data gradient
+  // default: never.  With 4-wave workgroups the data-gradient split paid
+  // (LeNet-5 FC1 dX 48.8 -> 43.2 us) but the forward did not (37.6 -> 43.7 us);
+  // with 8-wave workgroups one whole-W workgroup per CU already streams A with
+  // 8 waves and the split loses both ways (dX 39.6 -> 45.0 us, forward
+  // 34.9 -> 47.7 us: profiles/fc_split_ab_r2.txt)
+  const int split_mode = split_env ? std::atoi(split_env) : 0;  // 0 off, 1 all, 2 data gradient
   const bool split_ok = p.epi != EPI_LOGITS && (split_mode == 1 || (split_mode == 2 && p.epi == EPI_DACT));
   int nsplit = 1;
   if (split_ok && p.N >= 64 && (160 * 1024) / (fc_lds(p.N, p.ldw, p.K) + 1024) <= 1) {
