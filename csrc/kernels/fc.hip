@@ -117,6 +117,10 @@ __global__ void __launch_bounds__(kFcThreads) fc_kernel(FcParams p0) {
   if (dbg && lane == 0) dbg[2] = (long long)__builtin_amdgcn_s_memrealtime();
   for (int rb = blockIdx.x; rb < (P ? nrb : (int)blockIdx.x + 1); rb += gridDim.x) {
   const int row0 = rb * kFcRows + wave * 16;
+  // 16-byte act' operand loads (rows 16-byte aligned, the leading dim's
+  // padding readable; otherwise per-element loads in the epilogue)
+  const bool vaux = EPI == EPI_DACT && ACT != ACT_NONE && (p.ldaux & 7) == 0 && p.ldaux >= p0.ldc &&
+                    (reinterpret_cast<uintptr_t>(p.aux) & 15) == 0;
 
   auto epilogue = [&](const f32x4& acc, int tile, int slot) {
     const int col = tile * 16 + r16;
@@ -130,7 +134,10 @@ __global__ void __launch_bounds__(kFcThreads) fc_kernel(FcParams p0) {
         v = ACT == ACT_RELU ? fmaxf(v, 0.f) : (ACT == ACT_TANH ? tanhf(v) : v);
       } else if (EPI == EPI_DACT) {
         if (ACT != ACT_NONE && cv && row < p.M) {
-          const float y = (float)static_cast<const bf16*>(p.aux)[(size_t)row * p.ldaux + col];
+          // the forward activation: pre-staged in this lane's own stage slot
+          // (overwritten below with the result), or a 2-byte load
+          const float y = vaux ? (float)stg[(4 * g + i) * kFcStageLd + slot * 16 + r16]
+                               : (float)static_cast<const bf16*>(p.aux)[(size_t)row * p.ldaux + col];
           v *= ACT == ACT_RELU ? (y > 0.f ? 1.f : 0.f) : (1.f - y * y);
         }
       }
@@ -145,6 +152,23 @@ __global__ void __launch_bounds__(kFcThreads) fc_kernel(FcParams p0) {
   const int ntiles = npad >> 4;
   for (int t0 = 0; t0 < ntiles; t0 += kFcGroupTiles) {
     const int tn = min(kFcGroupTiles, ntiles - t0);
+    if (EPI == EPI_DACT && ACT != ACT_NONE && vaux) {
+      // act' operand of the group: 16 rows x (tn*16) columns of the forward
+      // activation as coalesced 16-byte loads into the wave's stage tile,
+      // issued before the MFMAs (one 2-byte load per output element exposed
+      // its latency in every epilogue)
+      const int ncols = min(tn * 16, cols - t0 * 16);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int v = lane + 64 * j;
+        const int r = v >> 4, c = (v & 15) * 8;
+        const int row = row0 + r;
+        bf16x8 y = {};
+        if (c < ncols && row < p.M) y = load8(static_cast<const bf16*>(p.aux) + (size_t)row * p.ldaux + t0 * 16 + c);
+        store8(stg + r * kFcStageLd + c, y);
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
     for (int tt = 0; tt < tn; tt += 2) {
       // two column tiles per pass: independent accumulator chains, all B
       // fragment reads unconditional (rows zero-padded to NCH*32) so they
