@@ -380,6 +380,32 @@ PYBIND11_MODULE(_C, m) {
         py::arg("pad"), py::arg("dz"), py::arg("ldz"), py::arg("input"), py::arg("slab"), py::arg("slab_stride"),
         py::arg("splitk"), py::arg("gw"), py::arg("gb"), py::arg("beta") = 0.f, py::arg("tile") = -1,
         py::arg("stream") = 0);
+  // LeNet-5 conv block (lenet.hip): raw launches for the kernel unit tests
+  k.def("lenet_forward",
+        [](int B, uintptr_t x, uintptr_t idx, uintptr_t w1, uintptr_t b1, uintptr_t w2, uintptr_t b2, uintptr_t y1,
+           uintptr_t a1, uintptr_t y2, uintptr_t a2, uintptr_t s) {
+          gpu::LenetFwdParams p;
+          p.B = B; p.x = ptr<const uint8_t>(x); p.idx = ptr<const int32_t>(idx);
+          p.w1 = ptr<const float>(w1); p.b1 = ptr<const float>(b1); p.w2 = ptr<const float>(w2); p.b2 = ptr<const float>(b2);
+          p.y1 = ptr<void>(y1); p.a1 = ptr<uint8_t>(a1); p.y2 = ptr<void>(y2); p.a2 = ptr<uint8_t>(a2);
+          gpu::lenet_forward(p, stream_of(s));
+        },
+        py::arg("B"), py::arg("x"), py::arg("idx"), py::arg("w1"), py::arg("b1"), py::arg("w2"), py::arg("b2"),
+        py::arg("y1"), py::arg("a1"), py::arg("y2"), py::arg("a2"), py::arg("stream") = 0);
+  k.def("lenet_backward",
+        [](int B, uintptr_t x, uintptr_t idx, uintptr_t w2, uintptr_t dy2, uintptr_t a2, uintptr_t y1, uintptr_t a1,
+           uintptr_t slab, uintptr_t gw1, uintptr_t gb1, uintptr_t gw2, uintptr_t gb2, uintptr_t s) {
+          gpu::LenetBwdParams p;
+          p.B = B; p.x = ptr<const uint8_t>(x); p.idx = ptr<const int32_t>(idx); p.w2 = ptr<const float>(w2);
+          p.dy2 = ptr<const void>(dy2); p.a2 = ptr<const uint8_t>(a2); p.y1 = ptr<const void>(y1);
+          p.a1 = ptr<const uint8_t>(a1); p.slab = ptr<float>(slab);
+          p.gw1 = ptr<float>(gw1); p.gb1 = ptr<float>(gb1); p.gw2 = ptr<float>(gw2); p.gb2 = ptr<float>(gb2);
+          gpu::lenet_backward(p, stream_of(s));
+        },
+        py::arg("B"), py::arg("x"), py::arg("idx"), py::arg("w2"), py::arg("dy2"), py::arg("a2"), py::arg("y1"),
+        py::arg("a1"), py::arg("slab"), py::arg("gw1"), py::arg("gb1"), py::arg("gw2"), py::arg("gb2"),
+        py::arg("stream") = 0);
+  k.def("lenet_slab_bytes", &gpu::lenet_slab_bytes);
   // device minibatch sampler (rand() % N semantics, cnn.c:455) with the step
   // counter in device memory: graph-capturable (a replay draws fresh indices)
   k.def("sample_indices",

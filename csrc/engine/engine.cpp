@@ -353,6 +353,25 @@ void GpuNet::build() {
                    st.in_ld % 8 == 0 && st.in_ld >= st.Kin && (int64_t)st.Nout * st.Kin >= 8192;
   }
 
+  // ---- LeNet-5 conv block (lenet.hip): conv1 + pool + conv2 + pool as ONE
+  // forward kernel and ONE fused backward kernel (conv2 dW, conv2 dX and the
+  // unpooled conv1 dW per image, dY1 never leaves LDS).  MCC_NO_LENET=1 keeps
+  // the per-layer pipelined kernels (A/B runs).
+  {
+    const char* e = std::getenv("MCC_NO_LENET");
+    lenet_ = false;
+    if (dtype_ == DType::BF16 && stages_.size() >= 3 && !(e && std::atoi(e) != 0)) {
+      const Stage& a = *stages_[0];
+      const Stage& b = *stages_[1];
+      auto pool_relu = [](const Stage& x) {
+        return x.kind == Stage::CONV && x.act == gpu::ACT_RELU && x.pooled && x.pk == 2 && x.ps == 2 && !x.generic &&
+               !x.big && x.stride == 1 && x.KS == 5;
+      };
+      lenet_ = pool_relu(a) && pool_relu(b) && a.inC == 1 && a.inH == 28 && a.inW == 28 && a.C == 6 && a.pad == 2 &&
+               b.inC == 6 && b.C == 16 && b.pad == 0;
+    }
+  }
+
   // ---- data gradient straight into dZ (no grad_xform pass) ----
   // A big stage whose input is a ReLU big conv writes that stage's dZ in its
   // implicit-GEMM data-gradient epilogue: dX * (y > 0) for an unpooled conv
@@ -584,6 +603,7 @@ void GpuNet::build() {
     const int ld = st.last ? r8(spec_.num_classes()) : st.out_ld;
     scratch = std::max(scratch, (size_t)gpu::gemm_fwd_splitk(Bm, st.Nout, st.Kin) * Bm * ld * 4);
   }
+  if (lenet_) scratch = std::max(scratch, gpu::lenet_slab_bytes());
   scratch_bytes_ = scratch;
   for (int pass = 0; pass < 2; ++pass) {
     arena_used_ = 0;
@@ -599,9 +619,13 @@ void GpuNet::build() {
     for (Stage* sp : stages_) {
       Stage& st = *sp;
       const int64_t per = st.kind == Stage::FC ? st.out_ld : st.out_elems;
-      st.act_buf = arena_alloc(es * (size_t)Bm * per);
+      // the LeNet block keeps conv1's pooled output HWC-8 and its argmax planar
+      const bool l0 = lenet_ && sp == stages_[0];
+      st.act_buf = arena_alloc(es * (size_t)Bm * (l0 ? std::max<int64_t>(per, gpu::lenet_y1_elems()) : per));
       st.grad_buf = arena_alloc(es * (size_t)Bm * per);
-      st.arg_buf = st.pooled ? static_cast<uint8_t*>(arena_alloc((size_t)Bm * per)) : nullptr;
+      st.arg_buf = st.pooled ? static_cast<uint8_t*>(arena_alloc(
+                                   (size_t)Bm * (l0 ? std::max<int64_t>(per, gpu::lenet_a1_bytes()) : per)))
+                             : nullptr;
       if (st.kind == Stage::CONV && st.big) {
         const size_t conv_elems = (size_t)Bm * st.OH * st.OW * st.C;
         st.conv_buf = st.pooled && !st.ig_pool ? arena_alloc(es * conv_elems) : nullptr;
@@ -623,6 +647,7 @@ void GpuNet::build() {
 
 std::string GpuNet::plan() const {
   std::ostringstream os;
+  if (lenet_) os << "[lenet block: stages 0+1 fused fwd (lenet_fwd) and bwd (lenet_bwd)]\n";
   os << "GpuNet(" << spec_.name << ", " << dtype_name(dtype_) << ", max_batch=" << max_batch_
      << ", arena=" << (arena_bytes_ >> 20) << " MiB, " << (fused_pack_ ? "fused sgd+pack" : "sgd + pack table")
      << ")\n";
@@ -739,6 +764,16 @@ void GpuNet::forward(const uint8_t* images, const int32_t* idx, int B, hipStream
   const size_t es = dtype_size(dtype_);
   for (size_t si = 0; si < stages_.size(); ++si) {
     Stage& st = *stages_[si];
+    if (lenet_ && si <= 1) {
+      if (si == 1) continue;  // produced with stage 0
+      const Stage& s1 = *stages_[1];
+      gpu::LenetFwdParams f;
+      f.B = B; f.x = images; f.idx = idx;
+      f.w1 = params_ + st.w_off; f.b1 = params_ + st.b_off; f.w2 = params_ + s1.w_off; f.b2 = params_ + s1.b_off;
+      f.y1 = st.act_buf; f.a1 = st.arg_buf; f.y2 = s1.act_buf; f.a2 = s1.arg_buf;
+      gpu::lenet_forward(f, s);
+      continue;
+    }
     if (st.kind == Stage::CONV && st.big && st.ig_fwd) {
       // implicit GEMM with bias+ReLU epilogue -> 2x2 max-pool
       gpu::IgemmParams g;
@@ -876,6 +911,24 @@ void GpuNet::backward(int hi, int lo, hipStream_t s) {
   for (int si = hi; si >= lo; --si) {
     Stage& st = *stages_[si];
     s = s_main;
+    if (lenet_ && si <= 1) {
+      // stage 1 runs the fused block backward (both stages' dW, db); stage 0 is then done
+      if (si == 0) continue;
+      if (forked) {  // the block kernel uses scratch_ on the main stream
+        HIP_OK(hipEventRecord(join_ev_, wstream_));
+        HIP_OK(hipStreamWaitEvent(s_main, join_ev_, 0));
+        forked = false;
+      }
+      const Stage& s0 = *stages_[0];
+      gpu::LenetBwdParams b;
+      b.B = B; b.x = images_; b.idx = idx_;
+      b.w2 = params_ + st.w_off;
+      b.dy2 = st.grad_buf; b.a2 = st.arg_buf; b.y1 = s0.act_buf; b.a1 = s0.arg_buf;
+      b.slab = scratch_;
+      b.gw1 = grads_ + s0.w_off; b.gb1 = grads_ + s0.b_off; b.gw2 = grads_ + st.w_off; b.gb2 = grads_ + st.b_off;
+      gpu::lenet_backward(b, s_main);
+      continue;
+    }
     // Side stream for this stage's weight gradient when the two directions
     // share no scratch: every path except the im2col fallbacks of the
     // large-image conv (col_ is shared by their dW and dX).  All dW work is

@@ -263,6 +263,40 @@ bool conv0_dw_supported(const Conv0DwParams& p);
 size_t conv0_dw_slab_bytes(const Conv0DwParams& p);
 void conv0_dw(const Conv0DwParams& p, float* gw, float* gb, hipStream_t s);
 
+// LeNet-5 conv block (lenet.hip): conv1 1->6 5x5 pad 2 + ReLU + 2x2 pool and
+// conv2 6->16 5x5 + ReLU + 2x2 pool on 28x28 u8 images, bf16.  Layouts:
+// y1 [B][14][14][8] bf16 (channels 6..7 zero), a1 [B][6][14][16] u8,
+// y2 [B][25][16] bf16, a2 [B][25][16] u8 (argmax 0..3 in the window, or 4 =
+// ReLU-inactive window).  Weights are read from the fp32 master (canonical).
+struct LenetFwdParams {
+  int B = 0;
+  const uint8_t* x = nullptr;     // u8 dataset [N][28][28]
+  const int32_t* idx = nullptr;   // [B] sample indices (nullable)
+  const float *w1 = nullptr, *b1 = nullptr, *w2 = nullptr, *b2 = nullptr;
+  void* y1 = nullptr;
+  uint8_t* a1 = nullptr;
+  void* y2 = nullptr;
+  uint8_t* a2 = nullptr;
+};
+struct LenetBwdParams {
+  int B = 0;
+  const uint8_t* x = nullptr;
+  const int32_t* idx = nullptr;
+  const float* w2 = nullptr;      // fp32 master W2 (canonical)
+  const void* dy2 = nullptr;      // [B][25][16] gradient of the pooled conv2 output
+  const uint8_t* a2 = nullptr;
+  const void* y1 = nullptr;
+  const uint8_t* a1 = nullptr;
+  float* slab = nullptr;          // lenet_slab_bytes()
+  float *gw1 = nullptr, *gb1 = nullptr, *gw2 = nullptr, *gb2 = nullptr;  // canonical gradients (written)
+};
+int lenet_bwd_grid();
+size_t lenet_slab_bytes();
+int lenet_y1_elems();   // per image
+int lenet_a1_bytes();   // per image
+void lenet_forward(const LenetFwdParams& p, hipStream_t s);
+void lenet_backward(const LenetBwdParams& p, hipStream_t s);
+
 struct ConvDwRowsParams {
   int N = 0, SH = 0, SW = 0, OH = 0, OW = 0, KS = 1, pad = 0, Cout = 0;
   const uint8_t* x = nullptr;        // u8 images [*][SH][SW]

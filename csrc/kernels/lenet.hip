@@ -1,0 +1,644 @@
+// LeNet-5 conv block on gfx950: conv1 (1->6, 5x5, pad 2) + ReLU + 2x2 pool
+// and conv2 (6->16, 5x5) + ReLU + 2x2 pool on 28x28 u8 images, forward and
+// backward, as two kernels instead of the five generic small-image conv
+// launches (plus their slab reduces) the engine used for these layers.
+//
+// Reference semantics: Layer_feedForw_conv / Layer_feedBack_conv
+// (/root/reference/cnn.c:175-247, with the D1 index bug fixed as in
+// CUDAcnn.cu:167-195); the pool and the LeNet-5 topology are BASELINE.json
+// additions.  Everything here is shaped for one 64-lane wave per image:
+//
+//  * Wave-private LDS, 64-thread workgroups, persistent grids.  A wave stages
+//    one image, computes, and moves on; no workgroup barrier ever waits on
+//    another wave, so LDS and MFMA latency are hidden by the other waves of
+//    the CU instead of by lock-step phases.
+//  * All geometry is compile-time, so every LDS operand read is a base VGPR
+//    plus an immediate offset.
+//  * Forward (lenet_fwd): conv1 as an MFMA GEMM whose columns are (channel,
+//    pixel pair) -- 12 of 16 columns useful, vs 6 -- with the bias in the
+//    accumulator's initial value; the 2x2 max-pool and its argmax take one
+//    integer max tree over keys (bits & ~3 | 3 - pos): positive floats order
+//    as integers, the low two bits break ties toward the first position and
+//    a window whose max is <= 0 is ReLU-inactive anyway.  The pooled conv1
+//    output stays in LDS for conv2 (register-resident weights).
+//  * Backward (lenet_bwd): one pass per image computes
+//      conv2 dW (dZ2^T x im2col(Y1), transposed LDS reads, bias as a ones
+//        column),
+//      conv2 dX (dZ2 padded x flipped W2, rows = output pixels, columns =
+//        (input channel, vertical pixel pair); 10 of each tile's 15 A
+//        fragments are the previous tile's, reused from registers),
+//      and the unpool of dY1 straight into LDS rows of dZ1, then
+//      conv1 dW (rows = (channel, kernel-row half), columns = 15 taps + a
+//        ones column: one MFMA per 32-pixel output row),
+//    accumulating dW2/dW1 in registers across the wave's images; one slab
+//    per wave, reduced in a fixed order (deterministic).
+//
+// Layouts produced by lenet_fwd and consumed by lenet_bwd:
+//   Y1 [B][14][14][8] bf16 (HWC, channels 6..7 zero), A1 [B][6][14][16] u8
+//   (planar, argmax position 0..3 or 4 = ReLU-inactive), Y2 [B][25][16] bf16
+//   (the FC input, NHWC flatten), A2 [B][25][16] u8.
+#include "kernels.h"
+#include "mfma.h"
+
+#include <algorithm>
+
+namespace mcc {
+namespace gpu {
+namespace {
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+// ---- geometry ----
+constexpr int kImgPix = 784;          // 28 x 28 u8
+constexpr int kY1Elems = 14 * 14 * 8; // HWC-8
+constexpr int kA1Bytes = 6 * 14 * 16;
+constexpr int kY2Elems = 25 * 16;
+
+// forward LDS per wave (bytes): two copies of the zero-padded input (shifts
+// 0 and 2 elements, 40-element rows), then the pooled conv1 output (HWC-8)
+constexpr int kFxPitch = 40, kFxRows = 36;
+constexpr int kFxCopy = kFxPitch * kFxRows * 2;  // 2880
+constexpr int kFY1 = 2 * kFxCopy;                // 5760
+constexpr int kFLds = kFY1 + 196 * 16;           // 8896
+
+// backward LDS per wave (bytes)
+constexpr int kBDz2 = 0;                 // dZ2 padded by 4: 18 rows x 20 px x 16 ch bf16 (640 B rows)
+constexpr int kBY1 = 11520;              // Y1 HWC-8: 196 x 16 B
+constexpr int kBOne2 = kBY1 + 3136;      // 16 B of bf16 ones (dW2 bias column)
+constexpr int kBXs = 14720;              // X0 padded by 2, 4 copies shifted by 0..3: 32 rows x 40
+constexpr int kBxCopy = 32 * 80;         // 2560
+constexpr int kBOne1 = kBXs + 4 * kBxCopy;  // 24960: 30 rows x 80 B of ones (dW1 bias column)
+constexpr int kBDz1 = kBOne1 + 30 * 80;  // 27360: dZ1 planar, 6 x 32 rows (zy + 2) x 32 px
+constexpr int kBDz1Plane = 32 * 64;      // 2048
+constexpr int kBLds = kBDz1 + 6 * kBDz1Plane;  // 39648
+
+// per-wave slab of the weight gradients, in MFMA accumulator order
+constexpr int kSlabW2 = 13 * 4 * 64;     // 3328
+constexpr int kSlab = kSlabW2 + 4 * 64;  // 3584
+
+__device__ __forceinline__ uint32_t bf16_bits(float v) {
+  return (uint32_t)__builtin_bit_cast(unsigned short, (bf16)v);
+}
+// four u8 pixels -> two dwords of bf16 holding the exact integers 0..255
+__device__ __forceinline__ void u8x4_ints(uint32_t w, uint32_t& lo, uint32_t& hi) {
+  const uint32_t f0 = __builtin_bit_cast(uint32_t, (float)(w & 0xffu));
+  const uint32_t f1 = __builtin_bit_cast(uint32_t, (float)((w >> 8) & 0xffu));
+  const uint32_t f2 = __builtin_bit_cast(uint32_t, (float)((w >> 16) & 0xffu));
+  const uint32_t f3 = __builtin_bit_cast(uint32_t, (float)(w >> 24));
+  lo = __builtin_amdgcn_perm(f1, f0, 0x07060302u);
+  hi = __builtin_amdgcn_perm(f3, f2, 0x07060302u);
+}
+// DPP: lane i <- lane i-1 / i+1 within each 16-lane row (0 at the row edge)
+__device__ __forceinline__ uint32_t from_left(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, true);
+}
+__device__ __forceinline__ uint32_t from_right(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x101, 0xf, 0xf, true);
+}
+// DPP quad_perm [1,0,3,2]: swap with the neighbouring lane
+__device__ __forceinline__ int swap1(int v) { return __builtin_amdgcn_mov_dpp(v, 0xB1, 0xf, 0xf, false); }
+// (a.hi, b.lo) as a bf16 pair
+__device__ __forceinline__ uint32_t mid16(uint32_t a, uint32_t b) { return __builtin_amdgcn_alignbit(b, a, 16); }
+
+__device__ __forceinline__ int imax(int a, int b) { return a > b ? a : b; }
+// NB: never __builtin_bit_cast an ext_vector element (acc[i]): this clang
+// (ROCm 7.2) lowers it to a bitcast of the whole vector and extracts lane 0,
+// silently reading acc[0] for every i.  __float_as_int on the scalar is fine.
+
+template <int OFF>
+__device__ __forceinline__ bf16x8 lds16(const char* base) {
+  return *reinterpret_cast<const bf16x8*>(base + OFF);
+}
+// 8 elements at 8-byte alignment as two separate ds_read_b64 (2 x 2 LDS
+// cycles, 64-bank service; fused, they would issue as one ds_read2_b64: 8
+// cycles at 32 banks)
+__device__ __forceinline__ bf16x8 lds8(const char* p) {
+  int hb = 8;
+  asm volatile("" : "+v"(hb));
+  const bf16x4 lo = *reinterpret_cast<const bf16x4*>(p);
+  const bf16x4 hi = *reinterpret_cast<const bf16x4*>(p + hb);
+  return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+__device__ __forceinline__ bf16x8 tr8(const char* p0, const char* p1) {
+  const bf16x4 a = tr4(reinterpret_cast<const bf16*>(p0));
+  const bf16x4 b = tr4(reinterpret_cast<const bf16*>(p1));
+  return __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+
+// LDS hand-off between the lanes of the (single-wave) workgroup: a wave's LDS
+// operations execute in order, so the compiler only must not move LDS
+// accesses across this point.  (__syncthreads would also drain vmcnt: the
+// in-flight prefetch loads and epilogue stores.)
+__device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+__device__ __forceinline__ void zero_wave_lds(char* p, int bytes) {
+  const u32x4 z = {0u, 0u, 0u, 0u};
+  for (int i = threadIdx.x * 16; i < bytes; i += 64 * 16) *reinterpret_cast<u32x4*>(p + i) = z;
+}
+
+// ============================================================================
+// Forward
+// ============================================================================
+//
+// conv1 GEMM, per tile of 16 rows x 16 columns, two K chunks of 32:
+//   row m (of the A operand) = the left pixel of a horizontal output pair;
+//     the 16 rows are four 2x4 pixel blocks b = 4T + m/4, block b = (row pair
+//     yp, column quad x4) = divmod(b, 7); row m%4 -> (y + (m&1), x + 2(m>>1)).
+//   column n = 2*co + j (co < 6): output pixel (y, x + j) of channel co.
+//   k = 8*kh + kw' (chunk 0: kh 0..3; chunk 1: kh 4), kw' = 0..7:
+//     A[m][k] = Xpad[y + kh][x + kw'],  B[k][n] = W1[co][kh][kw' - j].
+// The accumulator of lane (n, g) holds rows 4g..4g+3 = (y,x) (y+1,x)
+// (y,x+2) (y+1,x+2) of block 4T+g: window A = cols x..x+1 is split over the
+// lane pair (j = 0, 1), window B = cols x+2..x+3 likewise; one DPP swap
+// finishes both (lane j = 0 keeps A, j = 1 keeps B).
+//
+// conv2 GEMM: rows = output pixels ordered by pool window (R = 4w + pos),
+// columns = 16 output channels, k = 8*tap + ci over the HWC-8 LDS copy of the
+// pooled conv1 output (7 chunks, taps >= 25 carry zero weights).
+__global__ void __launch_bounds__(64) lenet_fwd_kernel(LenetFwdParams p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = threadIdx.x;
+  const int n16 = lane & 15, g = lane >> 4;
+
+  // ---- weights into registers (bf16 of the fp32 master, as the packer) ----
+  bf16x8 w1[2];
+  float bias1;
+  {
+    const int co = n16 >> 1, j = n16 & 1;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const int kh = c == 0 ? g : 4;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int kw = e - j;
+        float v = 0.f;
+        if (n16 < 12 && (c == 0 || g == 0) && kw >= 0 && kw < 5) v = p.w1[co * 25 + kh * 5 + kw];
+        w1[c][e] = (bf16)v;
+      }
+    }
+    bias1 = n16 < 12 ? 255.f * p.b1[co] : 0.f;  // the tile holds raw integer pixels
+  }
+  bf16x8 w2[7];
+  int koff2[7];  // A-fragment byte offset of this lane's tap per chunk (HWC-8 copy)
+#pragma unroll
+  for (int c = 0; c < 7; ++c) {
+    const int t = 4 * c + g, kh = t < 25 ? t / 5 : 0, kw = t < 25 ? t % 5 : 0;
+    koff2[c] = (kh * 14 + kw) * 16;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float v = 0.f;
+      if (t < 25 && e < 6) v = p.w2[(n16 * 6 + e) * 25 + t];
+      w2[c][e] = (bf16)v;
+    }
+  }
+  const float bias2 = p.b2[n16];
+
+  char* xf = smem;
+  char* y1s = smem + kFY1;
+  zero_wave_lds(smem, kFLds);
+
+  // conv1 A-fragment address (chunk 0) of this lane: copy (m>>1)&1 ... see above
+  const int msub = n16 & 3, mblk = n16 >> 2;
+  const int a1base = ((msub >> 1) * kFxCopy) + ((msub & 1) * kFxPitch + g * kFxPitch) * 2;
+  const int a1base_c1 = a1base + (4 - g) * kFxPitch * 2;
+  // conv2 A: rows of a tile
+  const int stride_w = (int)gridDim.x;
+
+  // staging items: 8 lanes per image row (k = lane & 7 -> pixel quad)
+  const int sk = lane & 7, srow = lane >> 3;
+
+  // the u8 image of the next iteration is loaded while this one computes
+  uint32_t xw[4];
+  auto load_img = [&](int img) {
+    const int src = p.idx ? p.idx[img] : img;
+    const uint8_t* xin = p.x + (size_t)src * kImgPix;
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      const int yy = it * 8 + srow;
+      xw[it] = (yy < 28 && sk < 7) ? *reinterpret_cast<const uint32_t*>(xin + yy * 28 + sk * 4) : 0u;
+    }
+  };
+  if ((int)blockIdx.x < p.B) load_img(blockIdx.x);
+  const int co1 = n16 >> 1, j1 = n16 & 1;
+  const int cA = 3 - j1, cB = 1 - j1;  // 3 - position in the window, rows (y) and (y+1)
+
+  for (int img = blockIdx.x; img < p.B; img += stride_w) {
+    wave_lds_sync();  // the previous image's LDS reads are done
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      const int yy = it * 8 + srow;
+      uint32_t lo, hi;
+      u8x4_ints(xw[it], lo, hi);
+      const uint32_t phi = from_left(hi);
+      if (yy < 28) {
+        char* d = xf + ((yy + 2) * kFxPitch + 4 * sk) * 2;
+        *reinterpret_cast<u32x2*>(d) = u32x2{phi, lo};            // Xpad cols 4k .. 4k+3
+        *reinterpret_cast<u32x2*>(d + kFxCopy) = u32x2{lo, hi};   // Xpad cols 4k+2 .. 4k+5
+      }
+    }
+    wave_lds_sync();
+    if (img + stride_w < p.B) load_img(img + stride_w);
+
+    // ---- conv1 + ReLU + pool: the next tile's A fragments are read before this tile's epilogue ----
+    bf16* y1g = static_cast<bf16*>(p.y1) + (size_t)img * kY1Elems;
+    uint8_t* a1g = p.a1 + (size_t)img * kA1Bytes;
+    auto frag_addr = [&](int T) {
+      const int bA = min(4 * T + mblk, 97);
+      const int ypA = (bA * 293) >> 11, x4A = bA - 7 * ypA;
+      return ypA * 4 * kFxPitch + x4A * 8;
+    };
+    bf16x8 fa, fb;
+    {
+      const int off = frag_addr(0);
+      fa = lds8(xf + a1base + off);
+      fb = lds8(xf + a1base_c1 + off);
+    }
+    for (int T = 0; T < 25; ++T) {
+      f32x4 acc = {bias1, bias1, bias1, bias1};
+      acc = mma(acc, fa, w1[0]);
+      acc = mma(acc, fb, w1[1]);
+      if (T + 1 < 25) {
+        const int off = frag_addr(T + 1);
+        fa = lds8(xf + a1base + off);
+        fb = lds8(xf + a1base_c1 + off);
+      }
+      const int b = 4 * T + g;
+      const int k0 = (__float_as_int(acc[0]) & ~3) | cA;
+      const int k1 = (__float_as_int(acc[1]) & ~3) | cB;
+      const int k2 = (__float_as_int(acc[2]) & ~3) | cA;
+      const int k3 = (__float_as_int(acc[3]) & ~3) | cB;
+      const int vA = imax(k0, k1), vB = imax(k2, k3);
+      const int keep = j1 ? vB : vA, send = j1 ? vA : vB;
+      const int best = imax(keep, swap1(send));
+      const float y = __int_as_float(imax(best & ~3, 0)) * (1.f / 255.f);
+      const bf16 yb = (bf16)y;
+      if (b < 98) {
+        const int yp = (b * 293) >> 11, x4 = b - 7 * yp;
+        const int px = 2 * x4 + j1;
+        const int pix = yp * 14 + px;
+        *reinterpret_cast<bf16*>(y1s + pix * 16 + co1 * 2) = yb;
+        y1g[pix * 8 + co1] = yb;
+        if (n16 < 12) a1g[co1 * 224 + yp * 16 + px] = (uint8_t)((float)yb > 0.f ? ((best & 3) ^ 3) : 4);
+      }
+    }
+    wave_lds_sync();  // pooled conv1 output complete in LDS
+
+    // ---- conv2 + ReLU + pool: all seven A fragments in flight before the MFMA chain ----
+    bf16* y2g = static_cast<bf16*>(p.y2) + (size_t)img * kY2Elems;
+    uint8_t* a2g = p.a2 + (size_t)img * kY2Elems;
+#pragma unroll 1
+    for (int T = 0; T < 7; ++T) {
+      const int R = min(16 * T + n16, 99);
+      const int w = R >> 2, pos = R & 3;
+      const int wy = (w * 205) >> 10, wx = w - 5 * wy;
+      const int zy = 2 * wy + (pos >> 1), zx = 2 * wx + (pos & 1);
+      const char* pa = y1s + (zy * 14 + zx) * 16;
+      bf16x8 af[7];
+#pragma unroll
+      for (int c = 0; c < 7; ++c) af[c] = *reinterpret_cast<const bf16x8*>(pa + koff2[c]);
+      __builtin_amdgcn_sched_barrier(0);
+      f32x4 acc = {bias2, bias2, bias2, bias2};
+#pragma unroll
+      for (int c = 0; c < 7; ++c) acc = mma(acc, af[c], w2[c]);
+      const int wo = 4 * T + g;
+      const int k0 = (__float_as_int(acc[0]) & ~3) | 3;
+      const int k1 = (__float_as_int(acc[1]) & ~3) | 2;
+      const int k2 = (__float_as_int(acc[2]) & ~3) | 1;
+      const int k3 = (__float_as_int(acc[3]) & ~3);
+      const int best = imax(imax(k0, k1), imax(k2, k3));
+      const bf16 yb = (bf16)__int_as_float(imax(best & ~3, 0));
+      if (wo < 25) {
+        y2g[wo * 16 + n16] = yb;
+        a2g[wo * 16 + n16] = (uint8_t)((float)yb > 0.f ? ((best & 3) ^ 3) : 4);
+      }
+    }
+  }
+}
+
+// ============================================================================
+// Backward
+// ============================================================================
+//
+// tapoff2(t): byte offset of conv2 tap t in the HWC-8 Y1 copy
+__host__ __device__ constexpr int tapoff2(int t) { return ((t / 5) * 14 + t % 5) * 16; }
+// dX2 chunk c covers taps (u', v) = divmod(2c, 5) and the next one; byte
+// offset of the first in the padded dZ2 copy (20-pixel rows, 32 B pixels)
+__host__ __device__ constexpr int dxoff(int c) { return (((2 * c) / 5) * 20 + (2 * c) % 5) * 32; }
+__host__ __device__ constexpr bool dxwrap(int c) { return (2 * c) % 5 == 4; }
+
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) lenet_bwd_kernel(LenetBwdParams p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = threadIdx.x;
+  const int n16 = lane & 15, g = lane >> 4;
+  const int tq = (lane >> 2) & 3, tp = lane & 3;  // transposed-read roles (row q, column quad p)
+
+  zero_wave_lds(smem, kBLds);
+  wave_lds_sync();
+  {  // bf16 ones: the dW2 bias pixel and the dW1 bias rows (cols 0..31 of 30 rows)
+    const uint32_t one2 = 0x3f803f80u;
+    if (lane < 4) *reinterpret_cast<uint32_t*>(smem + kBOne2 + 4 * lane) = one2;
+    for (int i = lane; i < 30 * 16; i += 64)
+      *reinterpret_cast<uint32_t*>(smem + kBOne1 + (i >> 4) * 80 + (i & 15) * 4) = one2;
+  }
+
+  // ---- conv2 data-gradient weights in registers ----
+  // lane (n, kgroup g): k = 32c + 8g + e -> tap t = 2c + (g>>1) = (u', v),
+  // output channel co = 8(g&1) + e; column n = 2*ci + j (ci < 6):
+  // B = W2[co][ci][4 + j - u'][4 - v] where the row is in range.
+  bf16x8 wdx[15];
+  {
+    const int ci = n16 >> 1, j = n16 & 1;
+#pragma unroll
+    for (int c = 0; c < 15; ++c) {
+      const int t = 2 * c + (g >> 1), u = t / 5, v = t % 5;
+      const int kh = 4 + j - u, kw = 4 - v;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int co = 8 * (g & 1) + e;
+        float w = 0.f;
+        if (n16 < 12 && kh >= 0 && kh < 5) w = p.w2[((co * 6 + ci) * 5 + kh) * 5 + kw];
+        wdx[c][e] = (bf16)w;
+      }
+    }
+  }
+
+  // ---- per-lane LDS bases (image independent) ----
+  // dW2: transposed reads, row z = 32c + 8g + 4hf + tq (z < 100 real)
+  int aw2[4][2], bw2a[4][2], bw2b[4][2], bw2c[4][2];
+#pragma unroll
+  for (int c = 0; c < 4; ++c)
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf) {
+      const int z = 32 * c + 8 * g + 4 * hf + tq;
+      const bool ok = z < 100;
+      const int zy = ok ? z / 10 : 0, zx = ok ? z % 10 : 0;
+      aw2[c][hf] = ok ? kBDz2 + ((zy + 4) * 20 + zx + 4) * 32 + 8 * tp : kBDz2 + 8 * tp;
+      const int yb = kBY1 + (zy * 14 + zx) * 16 + 8 * (tp & 1);
+      bw2a[c][hf] = yb + (tp >> 1) * 16;
+      bw2b[c][hf] = yb + (tp >> 1) * 160;
+      bw2c[c][hf] = (tp >> 1) ? kBOne2 + 8 * (tp & 1) - tapoff2(24) : yb;
+    }
+  // dX2: A rows px = n16, k-group g: chunk tap parity (g>>1), channel half (g&1)
+  const int hxa = kBDz2 + n16 * 32 + 16 * (g & 1) + (g >> 1) * 32;
+  const int hxb = kBDz2 + n16 * 32 + 16 * (g & 1) + (g >> 1) * 512;
+  // dW1: A row m = co + 6s (rows 12..15 idle), B column n = 5*kh' + kw (15 = ones)
+  int a1b;
+  {
+    const int m = n16 < 12 ? n16 : 0, co = m % 6, s = m / 6;
+    a1b = kBDz1 + co * kBDz1Plane + (2 - 2 * s) * 64 + 16 * g;
+  }
+  int b1b;
+  {
+    if (n16 == 15) b1b = kBOne1 + 16 * g;
+    else {
+      const int kh = n16 / 5, kw = n16 % 5, c = kw & 3;
+      b1b = kBXs + c * kBxCopy + (kh * 40 + 8 * g + kw - c) * 2;
+    }
+  }
+
+  f32x4 acc2[13];
+#pragma unroll
+  for (int t = 0; t < 13; ++t) acc2[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  f32x4 acc1 = {0.f, 0.f, 0.f, 0.f};
+
+  const int sk = lane & 7, srow = lane >> 3;  // X0 staging items
+  const int zq = lane >> 1, zh = lane & 1;    // dZ2 staging items (lane < 50)
+  const int zqy = (zq * 205) >> 10, zqx = zq - 5 * zqy;
+  const int zbase = kBDz2 + ((2 * zqy + 4) * 20 + 2 * zqx + 4) * 32 + 16 * zh;
+  const int dxci = n16 < 12 ? n16 >> 1 : 5, dxj = n16 & 1;
+
+  // Per-image global loads, issued one image ahead (one wave per SIMD: nothing
+  // else would hide their latency): dY2 + argmax codes of conv2 (lanes < 50),
+  // Y1 (196 x 16 B), the u8 image (8 lanes per row), conv1 codes per dX tile.
+  u32x4 dy = {0u, 0u, 0u, 0u}, yv[4];
+  u32x2 cw = {0u, 0u};
+  uint32_t xw[4], a1n[7], a1w[7];
+  auto load_img = [&](int img) {
+    if (lane < 50) {
+      dy = *reinterpret_cast<const u32x4*>(static_cast<const bf16*>(p.dy2) + (size_t)img * kY2Elems + zq * 16 + 8 * zh);
+      cw = *reinterpret_cast<const u32x2*>(p.a2 + (size_t)img * kY2Elems + zq * 16 + 8 * zh);
+    }
+    const bf16* y1g = static_cast<const bf16*>(p.y1) + (size_t)img * kY1Elems;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int px = min(lane + 64 * r, 195);
+      yv[r] = *reinterpret_cast<const u32x4*>(y1g + px * 8);
+    }
+    const int src = p.idx ? p.idx[img] : img;
+    const uint8_t* xin = p.x + (size_t)src * kImgPix;
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      const int yy = it * 8 + srow;
+      xw[it] = (yy < 28 && sk < 7) ? *reinterpret_cast<const uint32_t*>(xin + yy * 28 + sk * 4) : 0u;
+    }
+    const uint8_t* a1g = p.a1 + (size_t)img * kA1Bytes + dxci * 224 + 4 * g;
+#pragma unroll
+    for (int t = 0; t < 7; ++t) a1n[t] = *reinterpret_cast<const uint32_t*>(a1g + (2 * t + dxj) * 16);
+  };
+  if ((int)blockIdx.x < p.B) load_img(blockIdx.x);
+
+  for (int img = blockIdx.x; img < p.B; img += (int)gridDim.x) {
+    wave_lds_sync();  // previous image: every LDS read done
+    // ---- stage dZ2 (unpool of dY2 by the argmax codes) ----
+    if (lane < 50) {
+      const u32x4 z = {0u, 0u, 0u, 0u};
+      *reinterpret_cast<u32x4*>(smem + zbase) = z;
+      *reinterpret_cast<u32x4*>(smem + zbase + 32) = z;
+      *reinterpret_cast<u32x4*>(smem + zbase + 640) = z;
+      *reinterpret_cast<u32x4*>(smem + zbase + 672) = z;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const uint32_t code = (cw[i >> 2] >> (8 * (i & 3))) & 0xffu;
+        const uint32_t v = (dy[i >> 1] >> (16 * (i & 1))) & 0xffffu;
+        const int off = ((code & 2u) ? 640 : 0) + ((code & 1u) ? 32 : 0);  // code 4: value 0 at TL
+        *reinterpret_cast<unsigned short*>(smem + zbase + off + 2 * i) = (unsigned short)(code < 4u ? v : 0u);
+      }
+    }
+    // ---- stage Y1 ----
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int px = lane + 64 * r;
+      if (px < 196) *reinterpret_cast<u32x4*>(smem + kBY1 + px * 16) = yv[r];
+    }
+    // ---- stage X0: copy c holds Xpad[r][p + c] at position p ----
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      const int yy = it * 8 + srow;
+      uint32_t lo, hi;
+      u8x4_ints(xw[it], lo, hi);
+      const uint32_t phi = from_left(hi);
+      const uint32_t rlo = from_right(lo);
+      const uint32_t nlo = sk == 7 ? 0u : rlo;
+      if (yy < 28) {
+        char* d = smem + kBXs + ((yy + 2) * 40 + 4 * sk) * 2;
+        *reinterpret_cast<u32x2*>(d) = u32x2{phi, lo};
+        *reinterpret_cast<u32x2*>(d + kBxCopy) = u32x2{mid16(phi, lo), mid16(lo, hi)};
+        *reinterpret_cast<u32x2*>(d + 2 * kBxCopy) = u32x2{lo, hi};
+        *reinterpret_cast<u32x2*>(d + 3 * kBxCopy) = u32x2{mid16(lo, hi), mid16(hi, nlo)};
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < 7; ++t) a1w[t] = a1n[t];
+    wave_lds_sync();
+    // next image's loads fly while this one computes
+    if (img + (int)gridDim.x < p.B) load_img(img + (int)gridDim.x);
+
+    // ---- conv2 weight gradient (operands of chunk c+1 read during chunk c) ----
+    {
+      bf16x8 af[2], bfr[2][13];
+      auto load_chunk = [&](int c, int buf) {
+        af[buf] = tr8(smem + aw2[c][0], smem + aw2[c][1]);
+#pragma unroll
+        for (int t = 0; t < 13; ++t) {
+          const int o = tapoff2(2 * t);
+          const int* base = t == 12 ? bw2c[c] : ((2 * t) % 5 == 4 ? bw2b[c] : bw2a[c]);
+          bfr[buf][t] = tr8(smem + base[0] + o, smem + base[1] + o);
+        }
+      };
+      load_chunk(0, 0);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        if (c + 1 < 4) load_chunk(c + 1, (c + 1) & 1);
+        __builtin_amdgcn_sched_barrier(0);  // keep the reads of chunk c+1 ahead of chunk c's MFMAs
+#pragma unroll
+        for (int t = 0; t < 13; ++t) acc2[t] = mma(acc2[t], af[c & 1], bfr[c & 1][t]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+
+    // ---- conv2 data gradient -> dZ1 rows (unpool by the conv1 argmax) ----
+    {
+      bf16x8 fr[15], nx[5];
+#pragma unroll
+      for (int c = 0; c < 15; ++c)
+        fr[c] = *reinterpret_cast<const bf16x8*>(smem + (dxwrap(c) ? hxb : hxa) + dxoff(c));
+#pragma unroll
+      for (int T = 0; T < 7; ++T) {
+        if (T + 1 < 7) {  // tile T+1 reuses fr[5..14] as its chunks 0..9; read its chunks 10..14 now
+#pragma unroll
+          for (int c = 10; c < 15; ++c)
+            nx[c - 10] = *reinterpret_cast<const bf16x8*>(smem + (dxwrap(c) ? hxb : hxa) + dxoff(c) + (T + 1) * 1280);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int c = 0; c < 15; ++c) acc = mma(acc, fr[c], wdx[c]);
+        __builtin_amdgcn_sched_barrier(0);
+        // lane (n = 2ci + j, g): rows px = 4g + i of dY1 row py = 2T + j
+        uint32_t top[4], bot[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const uint32_t code = (a1w[T] >> (8 * i)) & 0xffu;
+          const uint64_t h = code < 4u ? (uint64_t)bf16_bits(acc[i]) : 0ull;
+          const uint64_t w = h << (16u * (code & 3u));
+          top[i] = (uint32_t)w;
+          bot[i] = (uint32_t)(w >> 32);
+        }
+        if (n16 < 12) {
+          char* d = smem + kBDz1 + dxci * kBDz1Plane + (4 * T + 2 * dxj + 2) * 64 + 16 * g;
+          *reinterpret_cast<u32x4*>(d) = u32x4{top[0], top[1], top[2], top[3]};
+          *reinterpret_cast<u32x4*>(d + 64) = u32x4{bot[0], bot[1], bot[2], bot[3]};
+        }
+#pragma unroll
+        for (int c = 0; c < 10; ++c) fr[c] = fr[c + 5];
+#pragma unroll
+        for (int c = 10; c < 15; ++c) fr[c] = nx[c - 10];
+      }
+    }
+    wave_lds_sync();  // dZ1 complete
+
+    // ---- conv1 weight gradient: one MFMA per output row (32 pixels), 4 rows of reads in flight ----
+    {
+      constexpr int D = 4;
+      bf16x8 a[D], b[D];
+#pragma unroll
+      for (int zy = 0; zy < D; ++zy) {
+        a[zy] = *reinterpret_cast<const bf16x8*>(smem + a1b + zy * 64);
+        b[zy] = lds8(smem + b1b + zy * 80);
+      }
+#pragma unroll
+      for (int zy = 0; zy < 30; ++zy) {
+        const bf16x8 ca = a[zy % D], cb = b[zy % D];
+        if (zy + D < 30) {
+          a[zy % D] = *reinterpret_cast<const bf16x8*>(smem + a1b + (zy + D) * 64);
+          b[zy % D] = lds8(smem + b1b + (zy + D) * 80);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        acc1 = mma(acc1, ca, cb);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  }
+
+  // ---- per-wave slab (accumulator order) ----
+  float* slab = p.slab + (size_t)blockIdx.x * kSlab;
+#pragma unroll
+  for (int t = 0; t < 13; ++t)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) slab[(t * 4 + i) * 64 + lane] = acc2[t][i];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) slab[kSlabW2 + i * 64 + lane] = acc1[i];
+}
+
+// Fixed-order sum of the per-wave slabs, mapped to the canonical gradients.
+// Block = 1024 threads over 64 slab positions: wave w sums slabs w, w+16, ...
+// of position blk*64 + lane (16 loads in flight per lane), then wave 0 adds
+// the sixteen partials in order.
+constexpr int kRedWaves = 16;
+__global__ void __launch_bounds__(64 * kRedWaves) lenet_bwd_reduce_kernel(LenetBwdParams p, int nslabs) {
+  __shared__ float part[kRedWaves][64];
+  const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int pos = blockIdx.x * 64 + l;
+  float s = 0.f;
+#pragma unroll 8
+  for (int k = w; k < nslabs; k += kRedWaves) s += p.slab[(size_t)k * kSlab + pos];
+  part[w][l] = s;
+  __syncthreads();
+  if (w != 0) return;
+  float v = part[0][l];
+#pragma unroll
+  for (int i = 1; i < kRedWaves; ++i) v += part[i][l];
+  if (pos < kSlabW2) {
+    const int t = pos / 256, i = (pos / 64) & 3, ln = pos & 63;
+    const int co = 4 * (ln >> 4) + i, n = 16 * t + (ln & 15);
+    const int tap = n >> 3, ci = n & 7;
+    if (n == 200) p.gb2[co] = v;
+    else if (tap < 25 && ci < 6) p.gw2[(co * 6 + ci) * 25 + tap] = v;
+  } else {
+    const int q = pos - kSlabW2, i = q >> 6, ln = q & 63;
+    const int m = 4 * (ln >> 4) + i, n = ln & 15;
+    if (m >= 12) return;
+    const int co = m % 6, s2 = m / 6;
+    if (n == 15) {
+      if (s2 == 0) p.gb1[co] = v;
+      return;
+    }
+    const int khp = n / 5, kw = n % 5;
+    if (s2 == 1 && khp == 0) return;  // tap row 2 comes from s = 0
+    p.gw1[co * 25 + (khp + 2 * s2) * 5 + kw] = v * (1.f / 255.f);
+  }
+}
+
+}  // namespace
+
+int lenet_bwd_grid() { return 1024; }
+size_t lenet_slab_bytes() { return (size_t)lenet_bwd_grid() * kSlab * 4; }
+int lenet_y1_elems() { return kY1Elems; }
+int lenet_a1_bytes() { return kA1Bytes; }
+
+void lenet_forward(const LenetFwdParams& p, hipStream_t s) {
+  if (p.B <= 0) return;
+  const int grid = std::min(p.B, 256 * 16);
+  hipLaunchKernelGGL(lenet_fwd_kernel, dim3(grid), dim3(64), kFLds, s, p);
+}
+
+void lenet_backward(const LenetBwdParams& p, hipStream_t s) {
+  if (p.B <= 0) return;
+  const int grid = lenet_bwd_grid();
+  hipLaunchKernelGGL(lenet_bwd_kernel, dim3(grid), dim3(64), kBLds, s, p);
+  hipLaunchKernelGGL(lenet_bwd_reduce_kernel, dim3(kSlab / 64), dim3(64 * kRedWaves), 0, s, p, grid);
+}
+
+}  // namespace gpu
+}  // namespace mcc

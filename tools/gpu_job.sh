@@ -1,0 +1,55 @@
+#!/bin/bash
+# One GPU-box job, parametrised by environment (run through gpurun):
+#   OUT=name           results under gpurun_out/<name>/
+#   TESTS="args"       pytest arguments (-m gpu is added); empty: skip
+#   BENCH="a;b;..."    bench.py argument sets, one JSON line each; empty: skip
+#   PROF="args"        bench.py arguments for a rocprofv3 kernel-trace + stats run
+#   PMC="c1 c2;..."    PMC passes (one rocprofv3 run each) over PROF's bench args
+#   PRE="cmd"          a command run first (e.g. a probe binary), time-limited
+# Every GPU step has its own time limit; the first failure ends the job.
+set -o pipefail
+cd "$(dirname "$0")/.."
+R=$PWD
+O=$R/gpurun_out/${OUT:-job}
+mkdir -p $O
+export TMPDIR=/tmp
+if [ -n "$PRE" ]; then
+  timeout -k 10 120 bash -c "$PRE" > $O/pre.txt 2>&1 || { echo "PRE failed rc=$?"; tail -20 $O/pre.txt; exit 1; }
+  cat $O/pre.txt
+fi
+if [ -n "$TESTS" ]; then
+  timeout -k 10 ${TEST_TIMEOUT:-500} python -u -m pytest -m gpu -x -v --timeout 120 --timeout-method thread $TESTS > $O/pytest.log 2>&1
+  rc=$?
+  grep -E "PASSED|FAILED|ERROR" $O/pytest.log | tail -${TEST_LINES:-40}
+  tail -3 $O/pytest.log
+  [ $rc -eq 0 ] || { grep -E "Error|assert|error" $O/pytest.log | head -40; echo "pytest rc=$rc"; exit 1; }
+fi
+if [ -n "$BENCH" ]; then
+  IFS=';' read -ra SETS <<< "$BENCH"
+  i=0
+  for a in "${SETS[@]}"; do
+    i=$((i+1))
+    timeout -k 10 200 python bench.py $a > $O/bench_$i.json 2> $O/bench_$i.err || { echo "bench '$a' failed"; tail -20 $O/bench_$i.err; exit 1; }
+    echo "[$a] $(grep -h '^{' $O/bench_$i.json | python3 -c "import json,sys;d=json.loads(sys.stdin.read());print(d['value'], d['ms_per_step'], d['config'].get('train_loss_last'))")"
+  done
+fi
+if [ -n "$PROF" ]; then
+  (cd /tmp && timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv -- python3 $R/bench.py $PROF > $O/prof.log 2>&1) \
+    || { echo "prof failed"; tail -20 $O/prof.log; exit 1; }
+  python3 $R/tools/prof_summary.py $O/prof/run_kernel_stats.csv > $O/kernel_summary.txt 2>/dev/null || true
+  f=$(ls $O/prof/*kernel_trace.csv 2>/dev/null | head -1)
+  [ -n "$f" ] && python3 $R/tools/step_timeline.py $f > $O/step_timeline.txt 2>/dev/null
+  tail -30 $O/step_timeline.txt 2>/dev/null
+fi
+if [ -n "$PMC" ]; then
+  IFS=';' read -ra PS <<< "$PMC"
+  i=0
+  for c in "${PS[@]}"; do
+    i=$((i+1))
+    (cd /tmp && timeout -s KILL 120 rocprofv3 --kernel-trace --pmc $c -d $O/pmc$i -o run --output-format csv -- python3 $R/bench.py ${PROF:---steps 3 --warmup 1} --no-dist > $O/pmc$i.log 2>&1) \
+      || { echo "pmc $i failed"; tail -5 $O/pmc$i.log; exit 1; }
+    python3 $R/tools/pmc_summary.py $O/pmc$i/run_counter_collection.csv > $O/pmc$i.txt
+  done
+  cat $O/pmc*.txt | grep -A12 -E "${KPAT:-lenet|conv}" | head -${PMC_LINES:-80}
+fi
+exit 0
