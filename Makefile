@@ -59,6 +59,10 @@ $(OBJ)/kernels/%.o: csrc/kernels/%.hip $(HDRS)
 	@mkdir -p $(dir $@)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
+# lenet.hip: MFMA results in VGPRs (no v_accvgpr_read per accumulator in the
+# VALU-bound epilogues; the register file is unified on gfx950)
+$(OBJ)/kernels/lenet.o: HIPFLAGS += -mllvm -amdgpu-mfma-vgpr-form=1
+
 $(OBJ)/engine/%.o: csrc/engine/%.cpp $(HDRS)
 	@mkdir -p $(dir $@)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
@@ -101,12 +105,18 @@ build/bin/cnn_dist: $(OBJ)/apps/cnn_dist.o $(OBJ)/apps/trainer.o $(CORE_OBJ) $(K
 # Host sanitizers: the CPU trainer and the core library
 # under AddressSanitizer + UBSan.  GPU-side sanitizers are not available on
 # the MI355X pool; device code is covered by bounds reasoning + tests.
+# (only cpu_kernels_v3.cpp is compiled with -mavx2 -mfma, as in the main
+# build, so the sanitized binary's baseline kernel table is baseline code)
+ASAN_FLAGS := -O1 -g -std=c++17 $(INC) -fsanitize=address,undefined -fno-omit-frame-pointer -fno-sanitize-recover=undefined
+ASAN_OBJ   := build/obj_asan
+ASAN_SRC   := csrc/apps/cnn.cpp $(filter-out %_v3.cpp,$(CORE_SRC))
 asan: build/bin/cnn_asan
-build/bin/cnn_asan: csrc/apps/cnn.cpp $(CORE_SRC) $(HDRS)
+$(ASAN_OBJ)/cpu_kernels_v3.o: csrc/core/cpu_kernels_v3.cpp csrc/core/cpu_kernels.inc $(HDRS)
 	@mkdir -p $(dir $@)
-	$(CXX) -O1 -g -std=c++17 $(INC) -fsanitize=address,undefined -fno-omit-frame-pointer \
-	  -fno-sanitize-recover=undefined -o $@ csrc/apps/cnn.cpp $(filter-out %_v3.cpp,$(CORE_SRC)) \
-	  csrc/core/cpu_kernels_v3.cpp -mavx2 -mfma -lm
+	$(CXX) $(ASAN_FLAGS) -mavx2 -mfma -c $< -o $@
+build/bin/cnn_asan: $(ASAN_SRC) $(ASAN_OBJ)/cpu_kernels_v3.o $(HDRS)
+	@mkdir -p $(dir $@)
+	$(CXX) $(ASAN_FLAGS) -o $@ $(ASAN_SRC) $(ASAN_OBJ)/cpu_kernels_v3.o -lm
 
 # Device bounds checks (MCC_DCHECK in the pipelined conv kernels): a separate
 # module under build/checked/ (same Python package, checked _C); run e.g.

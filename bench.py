@@ -101,7 +101,8 @@ def main():
     spec = mcc.make_model(args.model)
     C, H, W = spec.input_shape()
     if args.model in SIDE_STREAM:
-        os.environ.setdefault("MCC_SIDE_STREAM", "1")
+        ab = os.environ.get("MCC_AB", "")
+        os.environ["MCC_AB"] = ",".join(x for x in (ab, "side_stream") if x)
     B = args.batch_per_gpu or DEFAULT_BATCH.get(args.model, 1024)
     if not args.dataset:
         args.dataset = max(65536, B) if H * W <= 32 * 32 else max(256, 8 * B)

@@ -20,6 +20,7 @@
 // single-GPU run executes the same broadcast, bucketed all-reduce on the comm
 // stream and graph-captured collectives as an 8-GPU one.  MCC_LOCAL_COMM=1
 // (world 1 only) swaps in the collective-free LocalComm for A/B runs.
+#include "mcc/ab.h"
 #include <arpa/inet.h>
 #include <netdb.h>
 #include <netinet/in.h>
@@ -178,7 +179,11 @@ struct RcclComm : Comm {
   }
   // Collective watchdog: poll the event and the communicator's async error
   // state until the deadline (watchdog.h).
-  void wait(hipEvent_t ev) override {
+  void wait(hipEvent_t ev) override { wait_for(ev, timeout_s_, "MCC_COMM_TIMEOUT"); }
+  void wait_long(hipEvent_t ev) override { wait_for(ev, test_phase_timeout_s(), "MCC_TEST_TIMEOUT"); }
+  // On a timeout or an asynchronous error the communicator is aborted here,
+  // before the exception unwinds the caller's device buffers (collective_fail).
+  void wait_for(hipEvent_t ev, double timeout_s, const char* knob) {
     ncclResult_t async = ncclSuccess;
     hipError_t herr = hipSuccess;
     const WaitStatus st = bounded_wait(
@@ -193,13 +198,15 @@ struct RcclComm : Comm {
             return 2;
           return 0;
         },
-        timeout_s_);
+        timeout_s);
     if (st == WaitStatus::Done && herr == hipSuccess) return;
+    auto abort_now = [this](const char* why) { abort(why); };
     if (st == WaitStatus::Timeout)
-      throw Error("collective watchdog: no progress within " + std::to_string(timeout_s_) +
-                  " s (MCC_COMM_TIMEOUT); a peer rank is gone or hung");
-    if (herr != hipSuccess && herr != hipErrorNotReady) throw Error(std::string("HIP: ") + hipGetErrorString(herr));
-    throw Error(std::string("RCCL async error: ") + ncclGetErrorString(async));
+      collective_fail<Error>(abort_now, "collective watchdog: no progress within " + std::to_string(timeout_s) + " s (" +
+                                            knob + "); a peer rank is gone or hung");
+    if (herr != hipSuccess && herr != hipErrorNotReady)
+      collective_fail<Error>(abort_now, std::string("HIP: ") + hipGetErrorString(herr));
+    collective_fail<Error>(abort_now, std::string("RCCL async error: ") + ncclGetErrorString(async));
   }
   void barrier() override {
     NCCLCHK(ncclAllReduce(dummy_, dummy_, 1, ncclFloat32, ncclSum, comm_, bs_));
@@ -227,8 +234,7 @@ int main(int argc, char** argv) {
       mcc::env_int((const char*[]){"LOCAL_RANK", "OMPI_COMM_WORLD_LOCAL_RANK", "MPI_LOCALRANKID", nullptr}, rank);
   std::unique_ptr<mcc::Comm> comm;
   try {
-    const char* lc = std::getenv("MCC_LOCAL_COMM");
-    if (world == 1 && lc && std::atoi(lc) != 0) comm.reset(new mcc::LocalComm());
+    if (world == 1 && mcc::ab_flag("local_comm")) comm.reset(new mcc::LocalComm());
     else comm.reset(new mcc::RcclComm(rank, world, local));
   } catch (const mcc::Error& e) {
     std::fprintf(stderr, "rank %d: %s\n", rank, e.what());

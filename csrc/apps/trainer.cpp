@@ -137,9 +137,13 @@ int run_gpu_training(const CliArgs& a, Comm& comm, const char* program) {
   HIPCHK(hipMemcpy(d_lab.p, tr_lab.data.data(), (size_t)N, hipMemcpyHostToDevice));
   DevBuf d_idx(4 * (size_t)eval_b), d_step(8);
   DevBuf d_red(64);  // log / timing / exit-code reductions (no allocation in the loop)
+  // pinned host side of those reductions: floats [0, 16), doubles from byte 64.
+  // Every device->host copy lands here and is read only after an event the
+  // watchdog waits on (a pageable hipMemcpyAsync would block, unbounded).
   float* h_red = nullptr;
-  HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&h_red), 64, hipHostMallocDefault));
+  HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&h_red), 128, hipHostMallocDefault));
   std::unique_ptr<float, hipError_t (*)(void*)> h_red_guard(h_red, hipHostFree);
+  double* h_dbl = reinterpret_cast<double*>(h_red + 16);
   HIPCHK(hipMemset(d_step.p, 0, 8));
 
   // Comm stream C from the high-priority pool: HIP spreads streams over
@@ -276,11 +280,13 @@ int run_gpu_training(const CliArgs& a, Comm& comm, const char* program) {
   double train_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   if (coll) {  // the slowest rank's time
     double* d = d_red.as<double>();
-    HIPCHK(hipMemcpyAsync(d, &train_s, 8, hipMemcpyHostToDevice, S));
+    h_dbl[0] = train_s;
+    HIPCHK(hipMemcpyAsync(d, h_dbl, 8, hipMemcpyHostToDevice, S));
     comm.allreduce_max_f64(d, 1, S);
-    HIPCHK(hipMemcpyAsync(&train_s, d, 8, hipMemcpyDeviceToHost, S));
+    HIPCHK(hipMemcpyAsync(h_dbl + 1, d, 8, hipMemcpyDeviceToHost, S));
     HIPCHK(hipEventRecord(ev_sync, S));
     comm.wait(ev_sync);
+    train_s = h_dbl[1];
   }
   for (auto& e : ev_step) (void)hipEventDestroy(e);
   if (gexec) (void)hipGraphExecDestroy(gexec);
@@ -331,14 +337,16 @@ int run_gpu_training(const CliArgs& a, Comm& comm, const char* program) {
   // every rank leaves with rank 0's verdict (a failed test phase must not
   // leave the others in the final barrier; advisor finding, D9)
   if (coll) {
+    // the other ranks wait here while rank 0 evaluates and saves: the longer
+    // test-phase deadline, not the per-collective one
     double* d = d_red.as<double>();
-    double v = rc;
-    HIPCHK(hipMemcpyAsync(d, &v, 8, hipMemcpyHostToDevice, S));
+    h_dbl[0] = rc;
+    HIPCHK(hipMemcpyAsync(d, h_dbl, 8, hipMemcpyHostToDevice, S));
     comm.allreduce_max_f64(d, 1, S);
-    HIPCHK(hipMemcpyAsync(&v, d, 8, hipMemcpyDeviceToHost, S));
+    HIPCHK(hipMemcpyAsync(h_dbl + 1, d, 8, hipMemcpyDeviceToHost, S));
     HIPCHK(hipEventRecord(ev_sync, S));
-    comm.wait(ev_sync);
-    rc = (int)v;
+    comm.wait_long(ev_sync);
+    rc = (int)h_dbl[1];
   }
   if (rank == 0 && !a.log_json.empty()) {
     FILE* f = a.log_json == "-" ? stdout : std::fopen(a.log_json.c_str(), "w");

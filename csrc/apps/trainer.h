@@ -31,6 +31,9 @@ struct Comm {
   virtual void wait(hipEvent_t ev) {
     if (hipEventSynchronize(ev) != hipSuccess) throw Error("hipEventSynchronize failed");
   }
+  // wait() with the longer deadline of the post-training agreement, which
+  // covers rank 0's test phase (MCC_TEST_TIMEOUT)
+  virtual void wait_long(hipEvent_t ev) { wait(ev); }
   virtual void allreduce_sum_f32(float* buf, int64_t n, hipStream_t s) = 0;
   virtual void allreduce_max_f64(double* buf, int64_t n, hipStream_t s) = 0;
   virtual void broadcast_f32(float* buf, int64_t n, int root, hipStream_t s) = 0;

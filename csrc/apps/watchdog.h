@@ -15,6 +15,7 @@
 
 #include <chrono>
 #include <cstdlib>
+#include <string>
 #include <thread>
 
 namespace mcc {
@@ -42,6 +43,27 @@ inline double comm_timeout_s() {
   const char* v = std::getenv("MCC_COMM_TIMEOUT");
   const double t = v && *v ? std::atof(v) : 300.0;
   return t > 0 ? t : 300.0;
+}
+
+// Deadline of the post-training agreement that waits for rank 0's test
+// phase (evaluation + weight save can outlast a collective deadline):
+// MCC_TEST_TIMEOUT seconds, default 3600, never below the collective one.
+inline double test_phase_timeout_s() {
+  const char* v = std::getenv("MCC_TEST_TIMEOUT");
+  const double t = v && *v ? std::atof(v) : 3600.0;
+  const double c = comm_timeout_s();
+  return t > c ? t : c;
+}
+
+// Failure path of a bounded wait: abort the communicator FIRST (so the RCCL
+// kernels spinning on a dead peer are torn down), then throw.  Throwing first
+// would run the destructors of the caller's device buffers while those
+// kernels still spin; hipFree synchronises the device, so the rank would hang
+// instead of exiting 111.  `Err` is the exception type thrown.
+template <class Err, class AbortFn>
+[[noreturn]] void collective_fail(AbortFn&& abort_now, const std::string& msg) {
+  abort_now(msg.c_str());
+  throw Err(msg);
 }
 
 }  // namespace mcc

@@ -2,6 +2,7 @@
 // as raw device pointers + HIP stream handles (torch's data_ptr() and
 // current_stream().cuda_stream), so this translation unit needs no torch
 // headers and the same engine serves the native drivers and Python.
+#include <limits>
 #include <pybind11/numpy.h>
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
@@ -265,12 +266,13 @@ PYBIND11_MODULE(_C, m) {
            })
       .def("get_stats",
            [](const GpuNet& n) {
-             unsigned long long h[3];
+             unsigned long long h[4];
              if (hipDeviceSynchronize() != hipSuccess) throw Error("hipDeviceSynchronize failed");
-             if (hipMemcpy(h, n.stats(), 24, hipMemcpyDeviceToHost) != hipSuccess) throw Error("hipMemcpy failed");
+             if (hipMemcpy(h, n.stats(), 32, hipMemcpyDeviceToHost) != hipSuccess) throw Error("hipMemcpy failed");
              py::dict d;
-             d["loss_sum"] = (double)h[0] / gpu::kStatScale;
-             d["mse_sum"] = (double)h[1] / gpu::kStatScale;
+             const double nan = std::numeric_limits<double>::quiet_NaN();
+             d["loss_sum"] = h[gpu::kStatNaN] ? nan : (double)h[0] / gpu::kStatScale;
+             d["mse_sum"] = h[gpu::kStatNaN] ? nan : (double)h[1] / gpu::kStatScale;
              d["correct"] = (double)h[2];
              return d;
            })

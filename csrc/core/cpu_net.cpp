@@ -1,4 +1,5 @@
 // CPU reference executor.  See mcc/cpu_net.h for the reference mapping.
+#include "mcc/ab.h"
 #include "mcc/cpu_net.h"
 #include "mcc/cpu_kernels.h"
 
@@ -94,8 +95,7 @@ CpuNet<T>::CpuNet(const ModelSpec& spec, bool ref_compat) : spec_(spec), ref_com
 template <typename T>
 const CpuKernels<T>& cpu_kernels() {
   static const CpuKernels<T> k = [] {
-    const char* e = std::getenv("MCC_CPU_BASELINE");
-    const bool base = e && std::atoi(e) != 0;
+    const bool base = ab_flag("cpu_baseline");  // A/B: the portable kernel table
 #if defined(__x86_64__) && defined(__GNUC__)
     __builtin_cpu_init();
     if (!base && __builtin_cpu_supports("avx2") && __builtin_cpu_supports("fma")) return cpu_v3::kernels<T>();

@@ -8,6 +8,7 @@
 #include <sstream>
 
 #include "kernels.h"
+#include "mcc/ab.h"
 
 #include <cstdlib>
 
@@ -55,7 +56,6 @@ struct GpuNet::Stage {
   // not fit the whole-image LDS kernels
   bool big = false;
   bool dz_fused = false;  // big ReLU stage whose dZ the next stage's dX epilogue writes
-  bool fc_fbwd = false;   // small FC: dX + dW in one fused pass (fc_bwd.hip)
   bool generic = false;  // tanh conv / pool after a non-ReLU conv / non-2x2 pool: im2col or igemm path + grad_xform
   int pk = 2, ps = 2;    // pooled: window / stride
   int kgem = 0, kgem_d = 0;      // im2col row strides (fwd/dW, data grad)
@@ -115,18 +115,18 @@ GpuNet::GpuNet(const ModelSpec& spec, DType dtype, int max_batch, int device)
   for (const LayerSpec& l : spec.layers)
     MCC_CHECK((int64_t)max_batch * ((l.C + 15) / 16 * 16) * l.H * l.W < (1ll << 31),
               "GpuNet: max_batch too large for 32-bit activation indexing");
-  if (const char* a = std::getenv("MCC_ABLATE")) ablate_ = std::atoi(a);  // kernel diagnostics only
-  if (const char* a = std::getenv("MCC_NO_PIPE")) no_pipe_ = std::atoi(a) != 0;  // A/B against conv_small
-  if (const char* a = std::getenv("MCC_NO_FC")) no_fc_ = std::atoi(a) != 0;      // A/B against the tiled GEMM
-  if (const char* a = std::getenv("MCC_NO_IGEMM")) no_igemm_ = std::atoi(a) != 0;  // A/B against im2col + GEMM
-  if (const char* a = std::getenv("MCC_IGEMM_SMALL")) igemm_small_ = std::atoi(a) != 0;  // wide small-image convs
-  if (const char* a = std::getenv("MCC_NO_HEAD")) no_head_ = std::atoi(a) != 0;    // A/B against softmax_xent + FC backward
+  // A/B switches (mcc/ab.h, MCC_AB=...)
+  ablate_ = ab_int("ablate", 0);         // kernel diagnostics only
+  no_pipe_ = ab_flag("no_pipe");         // conv_small instead of the pipelined kernels
+  no_fc_ = ab_flag("no_fc");             // tiled GEMM instead of the weights-resident FC kernel
+  no_igemm_ = ab_flag("no_igemm");       // im2col + GEMM instead of the implicit GEMM
+  igemm_small_ = !ab_flag("no_igemm_small");  // LDS kernels for wide small-image convs
+  no_head_ = ab_flag("no_head");         // softmax_xent + FC backward instead of the fused head
   // dW side stream: opt-in (MCC_SIDE_STREAM=1).  Measured on MI355X (one GPU,
   // bench.py): CIFAR-3conv 2.27 -> 2.17 ms/step, but LeNet-5 0.452 -> 0.502 and
   // VGG-11 12.14 -> 12.40: the persistent conv kernels are sized to own every
   // CU, so a concurrent dW kernel steals their slots and stretches both.
-  no_side_ = true;
-  if (const char* a = std::getenv("MCC_SIDE_STREAM")) no_side_ = std::atoi(a) == 0;
+  no_side_ = !ab_flag("side_stream");
   if (device_ >= 0) HIP_OK(hipSetDevice(device_));
   else HIP_OK(hipGetDevice(&device_));
   build();
@@ -309,7 +309,7 @@ void GpuNet::build() {
       // first layer weight gradient straight from the pooled dY / argmax
       if (st.ig_dw0 && st.ig_fwd && st.pooled && st.pk == 2 && st.ps == 2 && st.act == gpu::ACT_RELU && st.KS == 3 &&
           st.stride == 1 && st.pad == 1 &&
-          !std::getenv("MCC_NO_C0DW")) {
+          !ab_flag("no_c0dw")) {
         gpu::Conv0DwParams& c = st.pc0;
         c.B = max_batch_; c.H = st.OH; c.W = st.OW; c.C = st.inC; c.PH = st.outH; c.PW = st.outW; c.Cout = st.C;
         st.c0dw = st.OH == st.inH && st.OW == st.inW && gpu::conv0_dw_supported(c);
@@ -356,11 +356,10 @@ void GpuNet::build() {
   // ---- LeNet-5 conv block (lenet.hip): conv1 + pool + conv2 + pool as ONE
   // forward kernel and ONE fused backward kernel (conv2 dW, conv2 dX and the
   // unpooled conv1 dW per image, dY1 never leaves LDS).  MCC_NO_LENET=1 keeps
-  // the per-layer pipelined kernels (A/B runs).
+  // the per-layer pipelined kernels (MCC_AB=no_lenet).
   {
-    const char* e = std::getenv("MCC_NO_LENET");
     lenet_ = false;
-    if (dtype_ == DType::BF16 && stages_.size() >= 3 && !(e && std::atoi(e) != 0)) {
+    if (dtype_ == DType::BF16 && stages_.size() >= 3 && !ab_flag("no_lenet")) {
       const Stage& a = *stages_[0];
       const Stage& b = *stages_[1];
       auto pool_relu = [](const Stage& x) {
@@ -379,36 +378,18 @@ void GpuNet::build() {
   // pooled one (conv2/4/6); the separate grad_xform pass re-reads dX (and y /
   // argmax) and re-writes dZ.
   {
-    // 0: off, 1: ReLU mask + unpool, 2 (default): ReLU mask only -- the
-    // unpool epilogue's four scattered 8-byte stores per fragment cost more
-    // in the dX kernel than the grad_xform pass they replace (VGG-11 B=512:
-    // off 15.61k, mask-only 15.77k, mask+unpool 15.46k img/s)
-    const char* e = std::getenv("MCC_DZ_FUSE");
-    const int mode = e ? std::atoi(e) : 2;
-    const bool on = mode != 0;
+    // ReLU mask only: an unpool in the same epilogue (four scattered 8-byte
+    // stores per fragment) cost more in the dX kernel than the grad_xform pass
+    // it replaced (VGG-11 B=512: off 15.61k, mask-only 15.77k, mask+unpool
+    // 15.46k img/s) and was removed in round 3.  MCC_AB=no_dz_fuse: off.
+    const bool on = !ab_flag("no_dz_fuse");
     for (size_t s = 1; on && s < stages_.size(); ++s) {
       Stage& cur = *stages_[s];
       Stage& pv = *stages_[s - 1];
-      const bool unpool_ok = pv.pooled && pv.pk == 2 && pv.ps == 2 && pv.OH % 2 == 0 && pv.OW % 2 == 0 &&
-                             pv.outH * 2 == pv.OH && pv.outW * 2 == pv.OW;
       // (not for a conv0_dw first layer: its weight gradient reads the pooled dY itself)
       pv.dz_fused = cur.kind == Stage::CONV && cur.big && cur.ig_dx && pv.kind == Stage::CONV && pv.big && !pv.c0dw &&
-                    (!pv.pooled || (unpool_ok && mode != 2)) && pv.act == gpu::ACT_RELU && dtype_ == DType::BF16 &&
+                    !pv.pooled && pv.act == gpu::ACT_RELU && dtype_ == DType::BF16 &&
                     pv.C == cur.inC;
-    }
-  }
-
-  // ---- small FC layers: data + weight gradient in one pass (MCC_FC_FBWD=1) ----
-  // Off by default: measured 50 us + a 15 us slab reduce for LeNet-5's 120 -> 84
-  // layer at B = 131072, vs 54 us for the split-K dW + reduce + FC dX kernels
-  // (one wave per SIMD, LDS-staged 2-byte epilogue; tools/gpu_r2w.sh).
-  {
-    const char* e = std::getenv("MCC_FC_FBWD");
-    const bool on = (e && std::atoi(e) != 0) && dtype_ == DType::BF16 && !no_fc_;
-    for (size_t s = 1; on && s < stages_.size(); ++s) {
-      Stage& st = *stages_[s];
-      st.fc_fbwd = st.kind == Stage::FC && !st.last && gpu::fc_small_bwd_supported(st.Nout, st.Kin) &&
-                   st.in_ld % 8 == 0 && st.out_ld % 8 == 0 && st.ldp >= st.Kin + 1 && st.permC == 0;
     }
   }
 
@@ -499,7 +480,7 @@ void GpuNet::build() {
   // (n, c, kh, kw) index; verified below against the table, entry by entry.
   pack_.nstages = 0;
   bool maps_ok = (int)stages_.size() <= gpu::kMaxPackStages;
-  if (const char* a = std::getenv("MCC_NO_FUSED_PACK")) maps_ok = maps_ok && std::atoi(a) == 0;  // A/B: table path
+  if (ab_flag("no_fused_pack")) maps_ok = false;  // A/B: the gather-table path
   for (Stage* sp : stages_) {
     if (!maps_ok) break;
     const Stage& st = *sp;
@@ -561,8 +542,6 @@ void GpuNet::build() {
   col_bytes_ = 0;
   for (Stage* sp : stages_) {
     const Stage& st = *sp;
-    if (st.kind == Stage::FC && st.fc_fbwd)
-      scratch = std::max(scratch, (size_t)gpu::fc_small_bwd_grid(Bm) * st.Nout * st.ldp * 4);
     if (st.kind == Stage::CONV && st.big) {
       const int KK = st.KS * st.KS;
       const int64_t rows = (int64_t)Bm * st.OH * st.OW;
@@ -674,7 +653,7 @@ std::string GpuNet::plan() const {
       os << "\n";
     } else {
       os << "  [" << s << "] fc " << st.Kin << " -> " << st.Nout << (st.last ? " (logits)" : "")
-         << (st.permC ? " nhwc-flatten" : "") << (st.fc_fbwd ? " fused-bwd" : "") << "\n";
+         << (st.permC ? " nhwc-flatten" : "") << "\n";
     }
   }
   return os.str();
@@ -935,8 +914,7 @@ void GpuNet::backward(int hi, int lo, hipStream_t s) {
     // serialised on wstream_, so scratch_ (split-K slabs) stays single-user;
     // the dX kernels never touch scratch_.
     const bool side = wstream_ && !(st.kind == Stage::CONV && st.big &&
-                                    !((st.ig_dw || st.ig_dw0 || st.c0dw) && (st.ig_dx || si == 0))) &&
-                      !(st.kind == Stage::FC && st.fc_fbwd);
+                                    !((st.ig_dw || st.ig_dw0 || st.c0dw) && (st.ig_dx || si == 0)));
     hipStream_t ws = s_main;
     if (!side && forked) {  // this stage's dW uses scratch_ on the main stream: drain the side stream first
       HIP_OK(hipEventRecord(join_ev_, wstream_));
@@ -1044,8 +1022,7 @@ void GpuNet::backward(int hi, int lo, hipStream_t s) {
           if (stages_[si - 1]->dz_fused) {  // dZ of the ReLU stage below: masked / unpooled in the epilogue
             const Stage& pv = *stages_[si - 1];
             d.out = pv.dz_buf;
-            if (pv.pooled) d.unpool_arg = pv.arg_buf;
-            else d.relu_mask = pv.act_buf;
+            d.relu_mask = pv.act_buf;
           }
           gpu::igemm_conv(d, s);
         } else if (si > 0) {
@@ -1147,25 +1124,6 @@ void GpuNet::backward(int hi, int lo, hipStream_t s) {
     } else {
       const Stage& pv = *stages_[si - 1];
       if (st.head && head_done_) continue;  // done by loss() (xent_head)
-      if (st.fc_fbwd) {  // dX and dW/db in one pass (main stream: it owns scratch_ here)
-        gpu::FcBwdParams f;
-        f.M = B; f.N = st.Nout; f.K = st.Kin;
-        f.dz = st.grad_buf; f.ldz = st.out_ld;
-        f.x = pv.act_buf; f.ldx = st.in_ld;
-        f.w = params_ + st.w_off;
-        f.act = pv.kind == Stage::FC ? pv.act : gpu::ACT_NONE;  // conv masks are applied by its staging
-        f.dx = pv.grad_buf; f.lddx = st.in_ld;
-        f.slab = scratch_; f.ldp = st.ldp;
-        MCC_CHECK((size_t)gpu::fc_small_bwd_grid(B) * st.Nout * st.ldp * 4 <= scratch_bytes_, "fc fused bwd scratch");
-        gpu::fc_small_bwd(f, s);
-        gpu::DwReduceParams r;
-        r.S = gpu::fc_small_bwd_grid(B); r.Nout = st.Nout; r.kfeat = st.Kin; r.ldp = st.ldp; r.part = scratch_;
-        r.partial_stride = (int64_t)st.Nout * st.ldp;
-        r.gw = grads_ + st.w_off; r.gb = grads_ + st.b_off;
-        r.permC = 0; r.permHW = 0;
-        gpu::dw_reduce(r, s);
-        continue;
-      }
       fork();
       if (st.fc_igdw) {
         gpu::IgemmDwParams w;

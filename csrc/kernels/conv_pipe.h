@@ -2,6 +2,7 @@
 // See conv_pipe_fwd.hip for the design notes.
 #pragma once
 
+#include "mcc/ab.h"
 #include <cstdlib>
 
 #include <algorithm>
@@ -449,16 +450,13 @@ bool plan_src(PipeSrc& s, int layout, int CLdst, int LH, int LWp, int IMGextra) 
   return true;
 }
 
-// Occupancy / group-size knobs of the pipelined conv planners, read once
-// (A/B tuning only; defaults are the measured choices).
-inline int pipe_knob(const char* name, int def) {
-  const char* v = std::getenv(name);
-  return v && *v ? std::atoi(v) : def;
-}
-inline int dw_wgs_cap() { static const int v = pipe_knob("MCC_DW_WGS", 2); return v; }
-inline int fwd_wgs_cap() { static const int v = pipe_knob("MCC_FWD_WGS", 4); return v; }
-inline size_t dw_lds_target() { static const size_t v = (size_t)pipe_knob("MCC_DW_LDS_KB", 64) * 1024; return v; }
-inline size_t fwd_lds_target() { static const size_t v = (size_t)pipe_knob("MCC_FWD_LDS_KB", 64) * 1024; return v; }
+// Occupancy / group-size knobs of the pipelined conv planners (A/B tuning
+// only, MCC_AB=dw_wgs=N etc.; defaults are the measured choices).
+inline int pipe_knob(const char* name, int def) { return ab_int(name, def); }
+inline int dw_wgs_cap() { return pipe_knob("dw_wgs", 2); }
+inline int fwd_wgs_cap() { return pipe_knob("fwd_wgs", 4); }
+inline size_t dw_lds_target() { return (size_t)pipe_knob("dw_lds_kb", 64) * 1024; }
+inline size_t fwd_lds_target() { return (size_t)pipe_knob("fwd_lds_kb", 64) * 1024; }
 
 int wgs_per_cu(size_t lds, int cap) {
   int w = (int)(kLdsPerCU / (lds + 512));

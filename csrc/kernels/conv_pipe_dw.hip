@@ -304,7 +304,7 @@ bool conv_dw_pipe_plan(ConvDwPipeParams& p) {
   // there are enough of them (4 waves x NTW)
   {
     const int mtw = p.cout_pad / 16, nct = p.ncols_pad / 16;
-    p.wsplit = mtw >= 4 && nct >= 2 * dw_ntw(mtw, nct) && !pipe_knob("MCC_NO_DW_WSPLIT", 0) ? 1 : 0;
+    p.wsplit = mtw >= 4 && nct >= 2 * dw_ntw(mtw, nct) && !pipe_knob("no_dw_wsplit", 0) ? 1 : 0;
   }
   const int nix = mode_ni(x.mode) * kT / std::max(1, x.per_img);
   const int nid = mode_ni(d.mode) * kT / std::max(1, d.per_img);

@@ -400,7 +400,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WR > 0 
 // register-resident weights for the LeNet-class shapes (one column tile, 7
 // or 13 K chunks): conv2 forward and conv2 data gradient
 int fwd_wreg(const ConvPipeParams& p) {
-  if (p.layout != XL_C8 || cdiv(p.Cout, 16) != 1 || pipe_knob("MCC_NO_WREG", 0)) return 0;
+  if (p.layout != XL_C8 || cdiv(p.Cout, 16) != 1 || pipe_knob("no_wreg", 0)) return 0;
   if (p.nchunks == 7 && p.in.mode == PM_PLAIN && p.epi == FE_POOL) return 7;
   if (p.nchunks == 13 && p.in.mode == PM_UNPOOL && p.epi == FE_PLAIN) return 13;
   return 0;
@@ -491,7 +491,7 @@ static void fwd_pick_strides(ConvPipeParams& p) {
       }
     }
   }
-  if (pipe_knob("MCC_BANK_LOG", 0))
+  if (pipe_knob("bank_log", 0))
     fprintf(stderr, "conv_pipe fwd Cin=%d Cout=%d OH=%d mode=%d: LWp %d->%d imgs %d->%d CS %d, A-read conflict cycles/read %.2f -> %.2f\n",
             p.Cin, p.Cout, p.OH, s.mode, LW0, bp.in.LWp, imgs0, bp.imgs, bp.in.CS,
             (double)e0.first / std::max(1L, e0.second), best);
@@ -509,7 +509,7 @@ bool conv_pipe_plan(ConvPipeParams& p) {
            (p.epi == FE_POOL || (p.epi == FE_ACT && (p.act == ACT_RELU || p.act == ACT_NONE)));
   // window pairs (the second column half computes the next 2x2 window, taps
   // shifted by two): the pool is in-lane, no DPP exchange
-  if (p.pair && p.epi == FE_POOL && p.KS <= 6 && (p.OW & 3) == 0 && (p.OH & 1) == 0 && !pipe_knob("MCC_NO_PAIR2", 0))
+  if (p.pair && p.epi == FE_POOL && p.KS <= 6 && (p.OW & 3) == 0 && (p.OH & 1) == 0 && !pipe_knob("no_pair2", 0))
     p.pair = 2;
   if (s1) {  // align the source columns to 4 (shift the conv origin accordingly)
     const int ox = s.offx < 4 ? 4 : (s.offx + 3) & ~3;
@@ -542,7 +542,7 @@ bool conv_pipe_plan(ConvPipeParams& p) {
   }
   if (imgs < 1) return false;
   if ((size_t)fwd_layout(p).total > kLdsPerCU) return false;
-  if (!pipe_knob("MCC_NO_SWIZZLE", 0)) fwd_pick_strides(p);
+  if (!pipe_knob("no_swizzle", 0)) fwd_pick_strides(p);
   const FwdLayout L = fwd_layout(p);
   p.lds = (size_t)L.total;
   p.ngroups = cdiv(p.N, p.imgs);

@@ -349,7 +349,7 @@ int rows_b_conflicts(const ConvDwRowsParams& p, int Pw, int CS) {
 }  // namespace
 
 bool conv_dw_rows_plan(ConvDwRowsParams& p) {
-  if (pipe_knob("MCC_NO_ROWS", 0)) return false;
+  if (pipe_knob("no_rows", 0)) return false;
   const int cw = p.Cout / 2;
   if ((p.Cout & 1) || !(cw == 1 || cw == 2 || cw == 3 || cw == 4 || cw == 8) || p.OW > 32 || p.OW < 1 || p.OH < 4)
     return false;

@@ -55,19 +55,8 @@ __host__ __device__ inline size_t fc_lds(int N, int ldw, int K) {
 template <int EPI, int ACT, int NCH, bool P>
 __global__ void __launch_bounds__(kFcThreads) fc_kernel(FcParams p0) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  // column split: this workgroup's W rows / bias / aux / output columns
-  FcParams p = p0;
-  int cols = p.ldc;  // stored columns (up to the leading dim: its padding is written as 0)
-  if (p.nsub > 0) {
-    const int n0 = (int)blockIdx.y * p.nsub;
-    p.N = min(p.nsub, p.N - n0);
-    p.W = static_cast<const bf16*>(p.W) + (size_t)n0 * p.ldw;
-    if (p.bias) p.bias += n0;
-    if (p.aux) p.aux = static_cast<const bf16*>(p.aux) + n0;
-    if (p.C) p.C = static_cast<bf16*>(p.C) + n0;
-    if (p.Cf) p.Cf += n0;
-    cols = blockIdx.y + 1 < gridDim.y ? p.nsub : p.ldc - n0;
-  }
+  const FcParams& p = p0;
+  const int cols = p.ldc;  // stored columns (up to the leading dim: its padding is written as 0)
   const int ldk = p.ldw;
   const int npad = fc_npad(p.N);
   const int wel = fc_welems(p.N, p.ldw, p.K);
@@ -236,32 +225,16 @@ void fc_forward(const FcParams& p, hipStream_t s) {
                 (p.epi == EPI_LOGITS || p.ldc % 8 == 0),
             "fc_forward: leading dims must be multiples of 8 covering K");
   if (p.M <= 0) return;
-  FcParams pl = p;
-  // a W that leaves room for only ONE workgroup per CU (LeNet-5 FC1 forward
-  // and data gradient: 96 KB) is split by columns over blockIdx.y: half of W
-  // per workgroup, several workgroups per CU to hide the A / store latency
-  // (MCC_FC_SPLIT: 0 never, 1 forward and data gradient, 2 data gradient only)
-  const char* split_env = std::getenv("MCC_FC_SPLIT");
-  // default: never.  With 4-wave workgroups the data-gradient split paid
-  // (LeNet-5 FC1 dX 48.8 -> 43.2 us) but the forward did not (37.6 -> 43.7 us);
-  // with 8-wave workgroups one whole-W workgroup per CU already streams A with
-  // 8 waves and the split loses both ways (dX 39.6 -> 45.0 us, forward
-  // 34.9 -> 47.7 us: profiles/fc_split_ab_r2.txt)
-  const int split_mode = split_env ? std::atoi(split_env) : 0;  // 0 off, 1 all, 2 data gradient
-  const bool split_ok = p.epi != EPI_LOGITS && (split_mode == 1 || (split_mode == 2 && p.epi == EPI_DACT));
-  int nsplit = 1;
-  if (split_ok && p.N >= 64 && (160 * 1024) / (fc_lds(p.N, p.ldw, p.K) + 1024) <= 1) {
-    pl.nsub = (cdiv(p.N, 2) + 15) & ~15;
-    nsplit = cdiv(p.N, pl.nsub);
-  }
-  const int nmax = pl.nsub ? pl.nsub : p.N;
-  const size_t lds = fc_lds(nmax, p.ldw, p.K);
+  const FcParams& pl = p;
+  // (a column split of a W that fills a CU over blockIdx.y measured slower
+  // both ways with 8-wave workgroups -- LeNet-5 FC1 dX 39.6 -> 45.0 us, forward
+  // 34.9 -> 47.7 us, profiles/fc_split_ab_r2.txt -- and was removed in round 3)
+  const size_t lds = fc_lds(p.N, p.ldw, p.K);
   // persistent (as many workgroups as the LDS lets every CU hold) when W
   // limits the CU to one or two workgroups
   const int per_cu = std::max(1, std::min(8, (int)((160 * 1024) / (lds + 1024))));
   const bool persist = per_cu <= 2;
-  const dim3 grid((unsigned)(persist ? std::min(cdiv(p.M, kFcRows), 256 * per_cu) : cdiv(p.M, kFcRows)),
-                  (unsigned)nsplit),
+  const dim3 grid((unsigned)(persist ? std::min(cdiv(p.M, kFcRows), 256 * per_cu) : cdiv(p.M, kFcRows))),
       block(kFcThreads);
   MCC_CHECK(lds <= 160 * 1024, "fc_forward: weights do not fit in LDS");
   const int nchb = fc_nchb(p.K);

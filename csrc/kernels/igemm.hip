@@ -33,6 +33,7 @@
 // store.  The weight gradient computes dW[co][k] per tile into fp32 split-K
 // slabs laid out [k][co] (16-byte stores), reduced by a deterministic pass.
 #include "kernels.h"
+#include "mcc/ab.h"
 #include "mfma.h"
 
 #include <algorithm>
@@ -402,21 +403,6 @@ __global__ void __launch_bounds__(kIgT, 2) igemm_conv_kernel(IgemmParams p) {
         v[e] += bv[e];
         if (BIAS_ACT) v[e] = act_apply(p.act, v[e]);
       }
-      if (!BIAS_ACT && p.unpool_arg) {  // dX straight to the unpooled dZ of a 2x2-pooled ReLU layer
-        const int b = mdiv(p.div_ohw, m);
-        const int rem = m - b * p.OH * p.OW;
-        const int py = mdiv(p.div_ow, rem), px = rem - py * p.OW;
-        const uint32_t a4 = *reinterpret_cast<const uint32_t*>(p.unpool_arg + (size_t)m * p.N + ch);
-        bf16* base = out + (((size_t)b * 2 * p.OH + 2 * py) * 2 * p.OW + 2 * px) * p.ldo + ch;
-      #pragma unroll
-        for (int q = 0; q < 4; ++q) {  // argmax 4 (ReLU-inactive window): all four zero
-          bf16x4 oq;
-      #pragma unroll
-          for (int e = 0; e < 4; ++e) oq[e] = ((a4 >> (8 * e)) & 0xffu) == (uint32_t)q ? (bf16)v[e] : (bf16)0.f;
-          *reinterpret_cast<bf16x4*>(base + ((size_t)(q >> 1) * 2 * p.OW + (q & 1)) * p.ldo) = oq;
-        }
-        continue;
-      }
       if (!BIAS_ACT && p.relu_mask) {  // data gradient straight to dZ of a ReLU layer: dX * (y > 0)
         const bf16x4 y = *reinterpret_cast<const bf16x4*>(static_cast<const bf16*>(p.relu_mask) + (size_t)m * p.ldo + ch);
 #pragma unroll
@@ -475,19 +461,14 @@ constexpr int kBigBP = 256;
 // (A1,B0); phase q reads its new register subtile (rd q: 0 = A0+B0, 1 = B1,
 // 2 = A1), stages quarter q of the next K-tile (st q: A0', B0', B1', A1') and
 // runs its MFMAs (mm q).  GA / GB = glds per thread per A / B quarter.
-// PP = false: one barrier per phase, all waves in step (reads, then MFMAs).
-// PP = true (ping-pong): each phase is [reads + stage] barrier [MFMAs]
-// barrier, and wave group 1 (waves 4-7: one wave per SIMD) runs one barrier
-// behind group 0, so on every SIMD one wave's MFMA cluster overlaps the other
-// wave's LDS reads, DMA issue and address math (guide §5, 8-phase template:
-// staggered groups, s_setprio around the MFMA clusters).  The quarter read in
-// phase P is retired by every wave before barrier 2P-1 (group 0: after its
-// MFMAs of P-1; group 1: after its stage of P-1), which both groups' reads of
-// P follow ("read a staged buffer one barrier after the wait").
-template <bool PP, int GA, int GB, class RD, class ST, class MM>
-__device__ __forceinline__ void pipe_loop(int nk, bool grp1, RD&& rd, ST&& st, MM&& mm) {
+// One barrier per phase, all waves in step (reads, then MFMAs).  (A staggered
+// ping-pong variant, wave group 1 one barrier behind with s_setprio around the
+// MFMA clusters, measured slower on VGG-11: 18.41 vs 17.66 ms/step, and was
+// removed in round 3.)
+template <int GA, int GB, class RD, class ST, class MM>
+__device__ __forceinline__ void pipe_loop(int nk, RD&& rd, ST&& st, MM&& mm) {
   st(0, 0); st(0, 1); st(0, 2); st(0, 3);
-  if constexpr (!PP) {
+  {
     for (int kt = 0; kt < nk; ++kt) {
       const bool nx = kt + 1 < nk;
       vm_wait<GA + GB>();  // A0, B0 landed (B1, A1 in flight)
@@ -508,52 +489,10 @@ __device__ __forceinline__ void pipe_loop(int nk, bool grp1, RD&& rd, ST&& st, M
       if (nx) st(kt + 1, 3);
       mm(3);
     }
-  } else {
-    auto mf = [&](int q) {
-      __builtin_amdgcn_s_setprio(1);
-      mm(q);
-      __builtin_amdgcn_s_setprio(0);
-    };
-    vm_wait<GA + GB>();
-    raw_barrier();
-    if (grp1) raw_barrier();  // stagger
-    for (int kt = 0; kt < nk; ++kt) {
-      const bool nx = kt + 1 < nk;
-      // p0: retire B1 for p1 (A1, A0' may stay in flight)
-      rd(kt, 0);
-      if (nx) st(kt + 1, 0);
-      if (grp1) { if (nx) vm_wait<2 * GA>(); else vm_wait<GA>(); }
-      raw_barrier();
-      mf(0);
-      if (!grp1) { if (nx) vm_wait<2 * GA>(); else vm_wait<GA>(); }
-      raw_barrier();
-      // p1: retire A1 for p2 (A0', B0' may stay in flight)
-      rd(kt, 1);
-      if (nx) st(kt + 1, 1);
-      if (grp1) { if (nx) vm_wait<GA + GB>(); else vm_wait<0>(); }
-      raw_barrier();
-      mf(1);
-      if (!grp1) { if (nx) vm_wait<GA + GB>(); else vm_wait<0>(); }
-      raw_barrier();
-      // p2: p3 reads nothing
-      rd(kt, 2);
-      if (nx) st(kt + 1, 2);
-      raw_barrier();
-      mf(2);
-      raw_barrier();
-      // p3: retire A0', B0' for the next p0 (B1', A1' may stay in flight)
-      if (nx) st(kt + 1, 3);
-      if (grp1 && nx) vm_wait<GA + GB>();
-      raw_barrier();
-      mf(3);
-      if (!grp1 && nx) vm_wait<GA + GB>();
-      raw_barrier();
-    }
-    if (!grp1) raw_barrier();  // balance the stagger
   }
 }
 
-template <int BC, bool BIAS_ACT, bool POOL, bool PP>
+template <int BC, bool BIAS_ACT, bool POOL>
 __global__ void __launch_bounds__(kBigT, 1) igemm_big_kernel(IgemmParams p) {
   constexpr int BK = kIgBK;
   constexpr int HA = BC / 2, HB = kBigBP / 2;    // rows per A / B half
@@ -679,8 +618,8 @@ __global__ void __launch_bounds__(kBigT, 1) igemm_big_kernel(IgemmParams p) {
   };
 
   const int nk = p.K / BK;  // host: K % 64 == 0
-  pipe_loop<PP, GA, GB>(
-      nk, wr == 1,
+  pipe_loop<GA, GB>(
+      nk,
       [&](int kt, int q) {
         const bf16* img = smem + (kt & 1) * BUF;
         if (q == 0) { read_a(img, 0); read_b(img, 0, fb0); }
@@ -742,21 +681,6 @@ __global__ void __launch_bounds__(kBigT, 1) igemm_big_kernel(IgemmParams p) {
           for (int e = 0; e < 4; ++e) {
             v[e] += bv[e];
             if (BIAS_ACT) v[e] = act_apply(p.act, v[e]);
-          }
-          if (!BIAS_ACT && p.unpool_arg) {  // dX straight to the unpooled dZ of a 2x2-pooled ReLU layer
-            const int b = mdiv(p.div_ohw, m);
-            const int rem = m - b * p.OH * p.OW;
-            const int py = mdiv(p.div_ow, rem), px = rem - py * p.OW;
-            const uint32_t a4 = *reinterpret_cast<const uint32_t*>(p.unpool_arg + (size_t)m * p.N + ch);
-            bf16* base = out + (((size_t)b * 2 * p.OH + 2 * py) * 2 * p.OW + 2 * px) * p.ldo + ch;
-          #pragma unroll
-            for (int q = 0; q < 4; ++q) {  // argmax 4 (ReLU-inactive window): all four zero
-              bf16x4 oq;
-          #pragma unroll
-              for (int e = 0; e < 4; ++e) oq[e] = ((a4 >> (8 * e)) & 0xffu) == (uint32_t)q ? (bf16)v[e] : (bf16)0.f;
-              *reinterpret_cast<bf16x4*>(base + ((size_t)(q >> 1) * 2 * p.OW + (q & 1)) * p.ldo) = oq;
-            }
-            continue;
           }
           if (!BIAS_ACT && p.relu_mask) {  // data gradient straight to dZ of a ReLU layer
             const bf16x4 y = *reinterpret_cast<const bf16x4*>(static_cast<const bf16*>(p.relu_mask) + (size_t)m * p.ldo + ch);
@@ -1013,7 +937,7 @@ __global__ void __launch_bounds__(256) igemm_dw_reduce_kernel(IgemmDwParams p, f
 // 256-byte rows).
 __device__ __forceinline__ int swz_tr64(int row) { return 2 * (((row >> 1) & 1) | (((row >> 3) & 1) << 1)); }
 
-template <int BA, bool PP>
+template <int BA>
 __global__ void __launch_bounds__(kBigT, 1) igemm_dwbig_kernel(IgemmDwParams p) {
   constexpr int BK = 64;
   constexpr int CA = BA / 2, CB = 128;            // columns per A / B half
@@ -1182,8 +1106,8 @@ __global__ void __launch_bounds__(kBigT, 1) igemm_dwbig_kernel(IgemmDwParams p) 
   };
 
   if (ks0 < ks1)
-    pipe_loop<PP, GA, GB>(
-        ks1 - ks0, wr == 1,
+    pipe_loop<GA, GB>(
+        ks1 - ks0,
         [&](int t, int q) {
           const bf16* img = smem + (t & 1) * BUF;
           if (q == 0) { read_a(img, 0); read_b(img, 0, fb0); }
@@ -1262,16 +1186,6 @@ void launch_conv(const IgemmParams& p, hipStream_t s) {
 }  // namespace
 
 static int igemm_env_mode();
-// MCC_IGEMM_PP=1: the staggered ping-pong schedule instead of lockstep phases
-// (measured slower on VGG-11: 18.41 vs 17.66 ms/step, tools/gpu_r2i.sh)
-static bool igemm_pp_mode() {
-  static const bool m = [] {
-    const char* e = getenv("MCC_IGEMM_PP");
-    return e ? atoi(e) != 0 : false;
-  }();
-  return m;
-}
-
 bool igemm_conv_supported(int C, int N, int KS) {
   // 128x128 kernel: C % 32 (a K-step spans <= 2 taps; K padded to 64 with
   // zero pieces); the 256-tile kernels additionally need C % 64 (igemm_conv)
@@ -1290,8 +1204,7 @@ void igemm_conv(const IgemmParams& p0, hipStream_t s) {
   MCC_CHECK(p.K == p.KS * p.KS * p.C, "igemm_conv: K must be KS*KS*C");
   MCC_CHECK(p.M == p.B * p.OH * p.OW && p.M > 0, "igemm_conv: M must be B*OH*OW");
   MCC_CHECK(p.ldw >= p.K && p.ldw % 8 == 0 && p.ldo >= p.N && p.ldo % 4 == 0, "igemm_conv: bad leading dims");
-  MCC_CHECK((!p.relu_mask && !p.unpool_arg) || (!p.epi_bias_act && !p.pool && !(p.relu_mask && p.unpool_arg)),
-            "igemm_conv: relu_mask / unpool_arg are data-gradient epilogues (one of them)");
+  MCC_CHECK(!p.relu_mask || (!p.epi_bias_act && !p.pool), "igemm_conv: relu_mask is a data-gradient epilogue");
   MCC_CHECK((int64_t)(p.u8 ? 1 : p.B) * p.H * p.W * p.C < (1ll << 31), "igemm_conv: input exceeds 2^31");
   MCC_CHECK(p.OH == (p.H + 2 * p.pad - p.KS) / p.stride + 1 && p.OW == (p.W + 2 * p.pad - p.KS) / p.stride + 1,
             "igemm_conv: output geometry mismatch");
@@ -1307,8 +1220,7 @@ void igemm_conv(const IgemmParams& p0, hipStream_t s) {
   const bool ba = p.epi_bias_act;
   if (p.u8) {
     MCC_CHECK(p.N > 64 || p.N % 8 == 0, "igemm_conv(u8): N");
-    const char* runs_env = getenv("MCC_U8_RUNS");  // =0: single-byte staging (A/B; read per launch)
-    const bool runs_ok = runs_env ? atoi(runs_env) != 0 : true;
+    const bool runs_ok = !ab_flag("u8_bytes");  // A/B: single-byte staging
     p.u8_runs = runs_ok && p.C == 3 && p.KS == 3 && p.pad == 1 && p.stride == 1 && p.W >= 6 && (p.W * 3) % 4 == 0 &&
                 reinterpret_cast<uintptr_t>(p.in) % 4 == 0;
     if (p.pool) {
@@ -1327,13 +1239,8 @@ void igemm_conv(const IgemmParams& p0, hipStream_t s) {
       ((big_mode == 1 && p.N % 256 == 0) || ((big_mode == 128 || big_mode == 256) && p.N % 128 == 0))) {
     const bool c256 = p.N % 256 == 0 && big_mode != 128;
     const int nwg = cdiv(p.M, kBigBP) * (p.N / (c256 ? 256 : 128));
-#define MCC_BIG(BC, BA, PL)                                                                              \
-  do {                                                                                                   \
-    if (igemm_pp_mode())                                                                                 \
-      hipLaunchKernelGGL((igemm_big_kernel<BC, BA, PL, true>), dim3((unsigned)nwg), dim3(kBigT), 0, s, p);  \
-    else                                                                                                 \
-      hipLaunchKernelGGL((igemm_big_kernel<BC, BA, PL, false>), dim3((unsigned)nwg), dim3(kBigT), 0, s, p); \
-  } while (0)
+#define MCC_BIG(BC, BA, PL) \
+  hipLaunchKernelGGL((igemm_big_kernel<BC, BA, PL>), dim3((unsigned)nwg), dim3(kBigT), 0, s, p)
     if (c256) {
       if (p.pool) MCC_BIG(256, true, true); else if (ba) MCC_BIG(256, true, false); else MCC_BIG(256, false, false);
     } else {
@@ -1351,13 +1258,9 @@ void igemm_conv(const IgemmParams& p0, hipStream_t s) {
   }
 }
 
-static int igemm_env_mode() {
-  static const int m = [] {
-    const char* e = getenv("MCC_IGEMM_BIG");
-    return e ? atoi(e) : 1;
-  }();
-  return m;
-}
+// MCC_AB=igemm_tile=N: 1 auto (256x256 tiles where N % 256 == 0), 0 the
+// 128x128 kernels only, 128 / 256 force that tile (read per call)
+static int igemm_env_mode() { return ab_int("igemm_tile", 1); }
 
 // weight-gradient tile: 0 = 128x128 kernel, 128 / 256 = igemm_dwbig_kernel<BA>
 static int dw_big_ba(int Cout, int kf, int tile) {
@@ -1417,11 +1320,8 @@ void igemm_dw(const IgemmDwParams& p0, float* gw, float* gb, float beta, hipStre
     MCC_CHECK(p.KS < 16, "igemm_dw: 256-column kernel packs ky, kx in 4 bits");
     p.direct = p.splitk == 1 && p.KS == 1 && p.perm_c == 0 && beta == 0.f;
     const int nwg = (p.Cout / ba) * cdiv(p.kf, 256) * p.splitk;
-    const bool pp = igemm_pp_mode();
-    if (ba == 256 && pp) hipLaunchKernelGGL((igemm_dwbig_kernel<256, true>), dim3((unsigned)nwg), dim3(kBigT), 0, s, p);
-    else if (ba == 256) hipLaunchKernelGGL((igemm_dwbig_kernel<256, false>), dim3((unsigned)nwg), dim3(kBigT), 0, s, p);
-    else if (pp) hipLaunchKernelGGL((igemm_dwbig_kernel<128, true>), dim3((unsigned)nwg), dim3(kBigT), 0, s, p);
-    else hipLaunchKernelGGL((igemm_dwbig_kernel<128, false>), dim3((unsigned)nwg), dim3(kBigT), 0, s, p);
+    if (ba == 256) hipLaunchKernelGGL((igemm_dwbig_kernel<256>), dim3((unsigned)nwg), dim3(kBigT), 0, s, p);
+    else hipLaunchKernelGGL((igemm_dwbig_kernel<128>), dim3((unsigned)nwg), dim3(kBigT), 0, s, p);
     if (p.direct) return;
   } else {
     const int nwg = cdiv(p.Cout, 128) * cdiv(p.kf + 1, 128) * p.splitk;

@@ -356,32 +356,14 @@ struct FcParams {
   float* Cf = nullptr;
   long long* dbg = nullptr;  // diagnostics: per-wave phase timestamps [grid][4 waves][4]
   int ablate = 0;            // diagnostics: 1 skip the output copy, 2 skip the MFMAs
-  int nsub = 0;              // set at launch: column split (blockIdx.y owns columns [y*nsub, +nsub))
 };
 bool fc_supported(int N, int K);
 void fc_forward(const FcParams& p, hipStream_t s);
 
+
+
 // Reduce split-K partials of a weight gradient into the canonical grad:
 // gw[n*Kc + perm(k)] (k < kfeat), gb[n] (k == kfeat).
-// Fused backward of a small FC layer (fc_bwd.hip): dX = act'(X) * (dZ W) and
-// per-workgroup dW/db slabs [grid][N][ldp] (column K = bias) in one pass.
-struct FcBwdParams {
-  int M = 0, N = 0, K = 0;           // rows, outputs (<= 96), inputs (< 128, % 8)
-  const void* dz = nullptr;          // bf16 [M][ldz] pre-activation gradient of this layer
-  int ldz = 0;
-  const void* x = nullptr;           // bf16 [M][ldx] layer input (the previous layer's output)
-  int ldx = 0;
-  const float* w = nullptr;          // [N][K] fp32 master weights (rounded to bf16 in LDS)
-  int act = 0;                       // activation of the previous layer (act' from X)
-  void* dx = nullptr;                // bf16 [M][lddx]
-  int lddx = 0;
-  float* slab = nullptr;             // [fc_small_bwd_grid(M)][N][ldp]
-  int ldp = 0;
-};
-bool fc_small_bwd_supported(int N, int K);
-int fc_small_bwd_grid(int M);
-void fc_small_bwd(const FcBwdParams& p, hipStream_t s);
-
 struct DwReduceParams {
   int S = 1, Nout = 0, kfeat = 0, ldp = 0;
   const float* part = nullptr;  // [S][Nout][ldp]
@@ -395,6 +377,9 @@ struct DwReduceParams {
 // Training statistics accumulate as fixed point (loss and mse per sample
 // are >= 0): value * kStatScale rounded, added with 64-bit integer atomics.
 constexpr double kStatScale = 4294967296.0;  // 2^32
+// stats[kStatNaN] != 0: a non-finite / overflowing partial was seen since the
+// last zero_stats (loss and MSE then read as NaN)
+constexpr int kStatNaN = 3;
 // stats[0..2] -> out[0..2] as floats (device side, for the drivers' logs)
 void stats_to_f32(const unsigned long long* stats, float* out, hipStream_t s);
 
@@ -475,8 +460,6 @@ struct IgemmParams {
   bool u8_runs = false;              // set at launch: u8 C=3 3x3 pad-1 im2col rows from dword runs
   const void* relu_mask = nullptr;   // bf16; data gradient only: out = dX * (relu_mask > 0), same layout as out
                                      // (writes the next-lower ReLU layer's dZ directly: no grad_xform pass)
-  const uint8_t* unpool_arg = nullptr;  // data gradient only: 2x2/2 argmax bytes [M][N] of the layer below;
-                                     // out = its unpooled dZ [B][2*OH][2*OW][ldo] (argmax 4: inactive window)
   int tile = -1;                     // -1 auto (MCC_IGEMM_BIG, default on), 0: 128x128 kernel,
                                      // 128 / 256: 256-pixel x 128 / 256-channel kernel where legal
   DivMagic div_ohw, div_ow;

@@ -56,22 +56,37 @@ constexpr int kA1Bytes = 6 * 14 * 16;
 constexpr int kY2Elems = 25 * 16;
 
 // forward LDS per wave (bytes): two copies of the zero-padded input (shifts
-// 0 and 2 elements, 40-element rows), then the pooled conv1 output (HWC-8)
-constexpr int kFxPitch = 40, kFxRows = 36;
-constexpr int kFxCopy = kFxPitch * kFxRows * 2;  // 2880
-constexpr int kFY1 = 2 * kFxCopy;                // 5760
-constexpr int kFLds = kFY1 + 196 * 16;           // 8896
+// 0 and 2 elements; 36-element rows: 18 dwords, so the five kernel rows a
+// fragment group reads sit on different banks), the pooled conv1 output
+// (HWC-8) and its argmax codes (planar), both copied out in bulk, and the
+// image-invariant index tables of the tile loops.
+constexpr int kFxPitch = 36, kFxRows = 32;
+constexpr int kFxCopy = kFxPitch * kFxRows * 2;  // 2304
+constexpr int kFY1 = 2 * kFxCopy;                // 4608: Y1 HWC-8, 196 x 16 B
+constexpr int kFJunk = kFY1 + 196 * 16;          // 7744: 32 B sink for the two padding blocks' Y1
+constexpr int kFA1 = kFJunk + 32;                // 7776: A1 [8][14][16] u8 (planes 6, 7: the idle
+                                                 // columns' codes, never copied out)
+constexpr int kFTabA = kFA1 + 8 * 224;           // 9568: u16 [100] conv1 A offset of block b
+constexpr int kFTabE = kFTabA + 200;             // 9768: u16 [100] epilogue: pixel (lo byte), A1 offset (hi)
+constexpr int kFTab2 = kFTabE + 200;             // 9968: u16 [112] conv2 row -> Y1 pixel offset
+constexpr int kFLds = kFTab2 + 224;              // 10192 (16 waves per CU fit the 160 KB)
 
 // backward LDS per wave (bytes)
 constexpr int kBDz2 = 0;                 // dZ2 padded by 4: 18 rows x 20 px x 16 ch bf16 (640 B rows)
 constexpr int kBY1 = 11520;              // Y1 HWC-8: 196 x 16 B
 constexpr int kBOne2 = kBY1 + 3136;      // 16 B of bf16 ones (dW2 bias column)
+// The copy and plane strides are padded off multiples of 256 B (the 64-bank
+// period): with 2560 / 2048 B strides every copy / plane mapped to the same
+// banks and the dW1 operand reads and the dZ1 row writes ran 4-6-way
+// conflicted (measured: 258M conflict cycles of 376M LDS-active cycles per
+// step).  +24 B / +32 B leave the dW1 reads at 8 extra cycles per MFMA pair
+// of fragments and the dZ1 writes conflict-free (LDS bank model).
 constexpr int kBXs = 14720;              // X0 padded by 2, 4 copies shifted by 0..3: 32 rows x 40
-constexpr int kBxCopy = 32 * 80;         // 2560
-constexpr int kBOne1 = kBXs + 4 * kBxCopy;  // 24960: 30 rows x 80 B of ones (dW1 bias column)
-constexpr int kBDz1 = kBOne1 + 30 * 80;  // 27360: dZ1 planar, 6 x 32 rows (zy + 2) x 32 px
-constexpr int kBDz1Plane = 32 * 64;      // 2048
-constexpr int kBLds = kBDz1 + 6 * kBDz1Plane;  // 39648
+constexpr int kBxCopy = 32 * 80 + 24;    // 2584
+constexpr int kBOne1 = kBXs + 4 * kBxCopy;  // 25056: 30 rows x 80 B of ones (dW1 bias column)
+constexpr int kBDz1 = kBOne1 + 30 * 80;  // 27456: dZ1 planar, 6 x 32 rows (zy + 2) x 32 px
+constexpr int kBDz1Plane = 32 * 64 + 32; // 2080
+constexpr int kBLds = kBDz1 + 6 * kBDz1Plane;  // 39936
 
 // per-wave slab of the weight gradients, in MFMA accumulator order
 constexpr int kSlabW2 = 13 * 4 * 64;     // 3328
@@ -120,6 +135,13 @@ __device__ __forceinline__ bf16x8 lds8(const char* p) {
   const bf16x4 hi = *reinterpret_cast<const bf16x4*>(p + hb);
   return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
 }
+// 8 elements at 8-byte alignment; the compiler fuses the pair into one
+// ds_read2_b64 (fewer instructions, 8 LDS cycles): for the VALU-bound forward
+__device__ __forceinline__ bf16x8 lds8x2(const char* p) {
+  const bf16x4 lo = *reinterpret_cast<const bf16x4*>(p);
+  const bf16x4 hi = *reinterpret_cast<const bf16x4*>(p + 8);
+  return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+}
 __device__ __forceinline__ bf16x8 tr8(const char* p0, const char* p1) {
   const bf16x4 a = tr4(reinterpret_cast<const bf16*>(p0));
   const bf16x4 b = tr4(reinterpret_cast<const bf16*>(p1));
@@ -131,6 +153,18 @@ __device__ __forceinline__ bf16x8 tr8(const char* p0, const char* p1) {
 // accesses across this point.  (__syncthreads would also drain vmcnt: the
 // in-flight prefetch loads and epilogue stores.)
 __device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+// Dataset index of the k-th image of this wave (images blockIdx.x + k*stride):
+// the indices of 64 consecutive iterations come in one vector load (lane k),
+// so an image's pixel loads never wait on a dependent scalar index load.
+struct WaveIdx {
+  int v = 0;
+  __device__ __forceinline__ void load(const int32_t* idx, int first, int stride, int B, int k0) {
+    const int i = first + (k0 + (int)threadIdx.x) * stride;
+    v = idx ? idx[min(i, B - 1)] : min(i, B - 1);
+  }
+  __device__ __forceinline__ int get(int k) const { return __builtin_amdgcn_readlane(v, k & 63); }
+};
 
 __device__ __forceinline__ void zero_wave_lds(char* p, int bytes) {
   const u32x4 z = {0u, 0u, 0u, 0u};
@@ -196,13 +230,32 @@ __global__ void __launch_bounds__(64) lenet_fwd_kernel(LenetFwdParams p) {
 
   char* xf = smem;
   char* y1s = smem + kFY1;
+  char* a1s = smem + kFA1;
   zero_wave_lds(smem, kFLds);
+  wave_lds_sync();
+  // index tables (image invariant): block b = (row pair yp, column quad x4)
+  for (int b = lane; b < 100; b += 64) {
+    const int bb = b < 98 ? b : 97;
+    const int yp = bb / 7, x4 = bb % 7;
+    reinterpret_cast<unsigned short*>(smem + kFTabA)[b] = (unsigned short)(yp * 4 * kFxPitch + x4 * 8);
+    // low byte: Y1 pixel of the block's left window (x16 = byte offset); high
+    // byte: A1 offset of that window.  The two padding blocks write Y1 into
+    // the sink (pixel index (kFJunk - kFY1) / 16) and A1 into the unused
+    // columns 14, 15 of row 13.
+    const uint32_t e = b < 98 ? (uint32_t)(yp * 14 + 2 * x4) | ((uint32_t)(yp * 16 + 2 * x4) << 8)
+                              : (uint32_t)((kFJunk - kFY1) / 16) | ((uint32_t)(13 * 16 + 14) << 8);
+    reinterpret_cast<unsigned short*>(smem + kFTabE)[b] = (unsigned short)e;
+  }
+  for (int r = lane; r < 112; r += 64) {
+    const int R = r < 100 ? r : 99, w = R >> 2, pos = R & 3;
+    const int zy = 2 * (w / 5) + (pos >> 1), zx = 2 * (w % 5) + (pos & 1);
+    reinterpret_cast<unsigned short*>(smem + kFTab2)[r] = (unsigned short)((zy * 14 + zx) * 16);
+  }
 
-  // conv1 A-fragment address (chunk 0) of this lane: copy (m>>1)&1 ... see above
+  // conv1 A-fragment address of this lane: copy (m>>1)&1, row (m&1) + kh
   const int msub = n16 & 3, mblk = n16 >> 2;
   const int a1base = ((msub >> 1) * kFxCopy) + ((msub & 1) * kFxPitch + g * kFxPitch) * 2;
   const int a1base_c1 = a1base + (4 - g) * kFxPitch * 2;
-  // conv2 A: rows of a tile
   const int stride_w = (int)gridDim.x;
 
   // staging items: 8 lanes per image row (k = lane & 7 -> pixel quad)
@@ -210,20 +263,27 @@ __global__ void __launch_bounds__(64) lenet_fwd_kernel(LenetFwdParams p) {
 
   // the u8 image of the next iteration is loaded while this one computes
   uint32_t xw[4];
-  auto load_img = [&](int img) {
-    const int src = p.idx ? p.idx[img] : img;
-    const uint8_t* xin = p.x + (size_t)src * kImgPix;
+  WaveIdx widx;
+  widx.load(p.idx, blockIdx.x, stride_w, p.B, 0);
+  auto load_img = [&](int k) {  // k-th image of this wave
+    if ((k & 63) == 0 && k > 0) widx.load(p.idx, blockIdx.x, stride_w, p.B, k);
+    const uint8_t* xin = p.x + (size_t)widx.get(k) * kImgPix;
 #pragma unroll
     for (int it = 0; it < 4; ++it) {
       const int yy = it * 8 + srow;
       xw[it] = (yy < 28 && sk < 7) ? *reinterpret_cast<const uint32_t*>(xin + yy * 28 + sk * 4) : 0u;
     }
   };
-  if ((int)blockIdx.x < p.B) load_img(blockIdx.x);
+  if ((int)blockIdx.x < p.B) load_img(0);
   const int co1 = n16 >> 1, j1 = n16 & 1;
   const int cA = 3 - j1, cB = 1 - j1;  // 3 - position in the window, rows (y) and (y+1)
+  const int ey1 = j1 * 16 + co1 * 2;   // lane part of the epilogue's Y1 / A1 offsets
+  const int ea1 = co1 * 224 + j1;
+  const unsigned short* tabA = reinterpret_cast<const unsigned short*>(smem + kFTabA);
+  const unsigned short* tabE = reinterpret_cast<const unsigned short*>(smem + kFTabE);
+  const unsigned short* tab2 = reinterpret_cast<const unsigned short*>(smem + kFTab2);
 
-  for (int img = blockIdx.x; img < p.B; img += stride_w) {
+  for (int img = blockIdx.x, kimg = 0; img < p.B; img += stride_w, ++kimg) {
     wave_lds_sync();  // the previous image's LDS reads are done
 #pragma unroll
     for (int it = 0; it < 4; ++it) {
@@ -238,32 +298,25 @@ __global__ void __launch_bounds__(64) lenet_fwd_kernel(LenetFwdParams p) {
       }
     }
     wave_lds_sync();
-    if (img + stride_w < p.B) load_img(img + stride_w);
+    if (img + stride_w < p.B) load_img(kimg + 1);
 
     // ---- conv1 + ReLU + pool: the next tile's A fragments are read before this tile's epilogue ----
-    bf16* y1g = static_cast<bf16*>(p.y1) + (size_t)img * kY1Elems;
-    uint8_t* a1g = p.a1 + (size_t)img * kA1Bytes;
-    auto frag_addr = [&](int T) {
-      const int bA = min(4 * T + mblk, 97);
-      const int ypA = (bA * 293) >> 11, x4A = bA - 7 * ypA;
-      return ypA * 4 * kFxPitch + x4A * 8;
-    };
     bf16x8 fa, fb;
     {
-      const int off = frag_addr(0);
-      fa = lds8(xf + a1base + off);
-      fb = lds8(xf + a1base_c1 + off);
+      const int off = tabA[mblk];
+      fa = lds8x2(xf + a1base + off);
+      fb = lds8x2(xf + a1base_c1 + off);
     }
     for (int T = 0; T < 25; ++T) {
       f32x4 acc = {bias1, bias1, bias1, bias1};
       acc = mma(acc, fa, w1[0]);
       acc = mma(acc, fb, w1[1]);
+      const uint32_t e = tabE[4 * T + g];
       if (T + 1 < 25) {
-        const int off = frag_addr(T + 1);
-        fa = lds8(xf + a1base + off);
-        fb = lds8(xf + a1base_c1 + off);
+        const int off = tabA[4 * T + 4 + mblk];
+        fa = lds8x2(xf + a1base + off);
+        fb = lds8x2(xf + a1base_c1 + off);
       }
-      const int b = 4 * T + g;
       const int k0 = (__float_as_int(acc[0]) & ~3) | cA;
       const int k1 = (__float_as_int(acc[1]) & ~3) | cB;
       const int k2 = (__float_as_int(acc[2]) & ~3) | cA;
@@ -271,29 +324,33 @@ __global__ void __launch_bounds__(64) lenet_fwd_kernel(LenetFwdParams p) {
       const int vA = imax(k0, k1), vB = imax(k2, k3);
       const int keep = j1 ? vB : vA, send = j1 ? vA : vB;
       const int best = imax(keep, swap1(send));
-      const float y = __int_as_float(imax(best & ~3, 0)) * (1.f / 255.f);
-      const bf16 yb = (bf16)y;
-      if (b < 98) {
-        const int yp = (b * 293) >> 11, x4 = b - 7 * yp;
-        const int px = 2 * x4 + j1;
-        const int pix = yp * 14 + px;
-        *reinterpret_cast<bf16*>(y1s + pix * 16 + co1 * 2) = yb;
-        y1g[pix * 8 + co1] = yb;
-        if (n16 < 12) a1g[co1 * 224 + yp * 16 + px] = (uint8_t)((float)yb > 0.f ? ((best & 3) ^ 3) : 4);
+      // the two code bits left in the value perturb it by < 2^-21: below the bf16 rounding
+      const bf16 yb = (bf16)(__int_as_float(imax(best, 0)) * (1.f / 255.f));
+      *reinterpret_cast<bf16*>(y1s + (e & 0xffu) * 16 + ey1) = yb;
+      a1s[(e >> 8) + ea1] = (uint8_t)((float)yb > 0.f ? ((best & 3) ^ 3) : 4);
+    }
+    wave_lds_sync();  // pooled conv1 output and codes complete in LDS
+    {  // bulk copies to HBM: Y1 (196 x 16 B), A1 (84 x 16 B)
+      u32x4* y1g = reinterpret_cast<u32x4*>(static_cast<bf16*>(p.y1) + (size_t)img * kY1Elems);
+      u32x4* a1g = reinterpret_cast<u32x4*>(p.a1 + (size_t)img * kA1Bytes);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int i = lane + 64 * r;
+        if (i < 196) y1g[i] = *reinterpret_cast<const u32x4*>(y1s + i * 16);
+      }
+#pragma unroll
+      for (int r = 0; r < 2; ++r) {
+        const int i = lane + 64 * r;
+        if (i < 84) a1g[i] = *reinterpret_cast<const u32x4*>(a1s + i * 16);
       }
     }
-    wave_lds_sync();  // pooled conv1 output complete in LDS
 
     // ---- conv2 + ReLU + pool: all seven A fragments in flight before the MFMA chain ----
     bf16* y2g = static_cast<bf16*>(p.y2) + (size_t)img * kY2Elems;
     uint8_t* a2g = p.a2 + (size_t)img * kY2Elems;
 #pragma unroll 1
     for (int T = 0; T < 7; ++T) {
-      const int R = min(16 * T + n16, 99);
-      const int w = R >> 2, pos = R & 3;
-      const int wy = (w * 205) >> 10, wx = w - 5 * wy;
-      const int zy = 2 * wy + (pos >> 1), zx = 2 * wx + (pos & 1);
-      const char* pa = y1s + (zy * 14 + zx) * 16;
+      const char* pa = y1s + tab2[16 * T + n16];
       bf16x8 af[7];
 #pragma unroll
       for (int c = 0; c < 7; ++c) af[c] = *reinterpret_cast<const bf16x8*>(pa + koff2[c]);
@@ -302,12 +359,12 @@ __global__ void __launch_bounds__(64) lenet_fwd_kernel(LenetFwdParams p) {
 #pragma unroll
       for (int c = 0; c < 7; ++c) acc = mma(acc, af[c], w2[c]);
       const int wo = 4 * T + g;
-      const int k0 = (__float_as_int(acc[0]) & ~3) | 3;
+      const int k0 = __float_as_int(acc[0]) | 3;
       const int k1 = (__float_as_int(acc[1]) & ~3) | 2;
       const int k2 = (__float_as_int(acc[2]) & ~3) | 1;
-      const int k3 = (__float_as_int(acc[3]) & ~3);
+      const int k3 = __float_as_int(acc[3]) & ~3;
       const int best = imax(imax(k0, k1), imax(k2, k3));
-      const bf16 yb = (bf16)__int_as_float(imax(best & ~3, 0));
+      const bf16 yb = (bf16)__int_as_float(imax(best, 0));
       if (wo < 25) {
         y2g[wo * 16 + n16] = yb;
         a2g[wo * 16 + n16] = (uint8_t)((float)yb > 0.f ? ((best & 3) ^ 3) : 4);
@@ -414,7 +471,11 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1)))
   u32x4 dy = {0u, 0u, 0u, 0u}, yv[4];
   u32x2 cw = {0u, 0u};
   uint32_t xw[4], a1n[7], a1w[7];
-  auto load_img = [&](int img) {
+  WaveIdx widx;
+  widx.load(p.idx, blockIdx.x, (int)gridDim.x, p.B, 0);
+  auto load_img = [&](int k) {  // k-th image of this wave
+    const int img = blockIdx.x + k * (int)gridDim.x;
+    if ((k & 63) == 0 && k > 0) widx.load(p.idx, blockIdx.x, (int)gridDim.x, p.B, k);
     if (lane < 50) {
       dy = *reinterpret_cast<const u32x4*>(static_cast<const bf16*>(p.dy2) + (size_t)img * kY2Elems + zq * 16 + 8 * zh);
       cw = *reinterpret_cast<const u32x2*>(p.a2 + (size_t)img * kY2Elems + zq * 16 + 8 * zh);
@@ -425,8 +486,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1)))
       const int px = min(lane + 64 * r, 195);
       yv[r] = *reinterpret_cast<const u32x4*>(y1g + px * 8);
     }
-    const int src = p.idx ? p.idx[img] : img;
-    const uint8_t* xin = p.x + (size_t)src * kImgPix;
+    const uint8_t* xin = p.x + (size_t)widx.get(k) * kImgPix;
 #pragma unroll
     for (int it = 0; it < 4; ++it) {
       const int yy = it * 8 + srow;
@@ -436,9 +496,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1)))
 #pragma unroll
     for (int t = 0; t < 7; ++t) a1n[t] = *reinterpret_cast<const uint32_t*>(a1g + (2 * t + dxj) * 16);
   };
-  if ((int)blockIdx.x < p.B) load_img(blockIdx.x);
+  if ((int)blockIdx.x < p.B) load_img(0);
 
-  for (int img = blockIdx.x; img < p.B; img += (int)gridDim.x) {
+  for (int img = blockIdx.x, kimg = 0; img < p.B; img += (int)gridDim.x, ++kimg) {
     wave_lds_sync();  // previous image: every LDS read done
     // ---- stage dZ2 (unpool of dY2 by the argmax codes) ----
     if (lane < 50) {
@@ -482,7 +542,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1)))
     for (int t = 0; t < 7; ++t) a1w[t] = a1n[t];
     wave_lds_sync();
     // next image's loads fly while this one computes
-    if (img + (int)gridDim.x < p.B) load_img(img + (int)gridDim.x);
+    if (img + (int)gridDim.x < p.B) load_img(kimg + 1);
 
     // ---- conv2 weight gradient (operands of chunk c+1 read during chunk c) ----
     {

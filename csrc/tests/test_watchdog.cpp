@@ -4,6 +4,8 @@
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
+#include <stdexcept>
+#include <string>
 
 #include "watchdog.h"
 
@@ -42,6 +44,33 @@ int main() {
   CHECK(comm_timeout_s() == 300.0);
   unsetenv("MCC_COMM_TIMEOUT");
   CHECK(comm_timeout_s() == 300.0);
+  // MCC_TEST_TIMEOUT: default 3600, never below the collective deadline
+  CHECK(test_phase_timeout_s() == 3600.0);
+  setenv("MCC_COMM_TIMEOUT", "5000", 1);
+  CHECK(test_phase_timeout_s() == 5000.0);
+  unsetenv("MCC_COMM_TIMEOUT");
+  setenv("MCC_TEST_TIMEOUT", "900", 1);
+  CHECK(test_phase_timeout_s() == 900.0);
+  unsetenv("MCC_TEST_TIMEOUT");
+  // failure path: the communicator abort runs BEFORE the caller's device
+  // buffers are released (their destructors run while the exception unwinds)
+  {
+    std::string order;
+    struct DeviceBuffer {  // stands for a DevBuf / arena whose hipFree syncs the device
+      std::string* o;
+      ~DeviceBuffer() { *o += "free;"; }
+    };
+    bool thrown = false;
+    try {
+      DeviceBuffer buf{&order};
+      (void)buf;
+      collective_fail<std::runtime_error>([&](const char*) { order += "abort;"; }, "peer gone");
+    } catch (const std::runtime_error& e) {
+      thrown = std::string(e.what()) == "peer gone";
+    }
+    CHECK(thrown);
+    CHECK(order == "abort;free;");
+  }
   std::printf("watchdog ok\n");
   return 0;
 }

@@ -47,9 +47,9 @@ def test_step_matches_torch(cuda, model, dtype):
 @pytest.mark.parametrize("dtype", ["fp32", "bf16"])
 @pytest.mark.parametrize("model", ["lenet5", "cifar3"])
 def test_step_matches_torch_side_stream(cuda, model, dtype, monkeypatch):
-    """Weight gradients on the engine's side stream (MCC_SIDE_STREAM=1), data
+    """Weight gradients on the engine's side stream (MCC_AB=side_stream), data
     gradients on the caller's: same numbers as the single-stream step."""
-    monkeypatch.setenv("MCC_SIDE_STREAM", "1")
+    monkeypatch.setenv("MCC_AB", "side_stream")
     _check_step(cuda, model, dtype)
 
 
@@ -132,7 +132,7 @@ def _sgd_steps(cuda, spec, dtype, B, steps=2):
                                          ("vgg11", "bf16")])
 def test_fused_sgd_pack_matches_table(cuda, model, dtype, monkeypatch):
     """One-pass SGD + packed-copy refresh (analytic per-stage maps, no index
-    table) vs the gather-table path (MCC_NO_FUSED_PACK=1): bit-identical
+    table) vs the gather-table path (MCC_AB=no_fused_pack): bit-identical
     parameters after SGD with momentum + weight decay, and bit-identical
     logits from the refreshed bf16/fp32 compute copies (every packed layout:
     S1 pair, C8, flipped data-gradient copies, im2col, FC and FC^T)."""
@@ -145,7 +145,7 @@ def test_fused_sgd_pack_matches_table(cuda, model, dtype, monkeypatch):
     B = {"big": 8, "wide": 8, "vgg11": 2}.get(model, 64)
     plan, p_fused, l_fused = _sgd_steps(cuda, spec, dtype, B)
     assert "fused sgd+pack" in plan, plan
-    monkeypatch.setenv("MCC_NO_FUSED_PACK", "1")
+    monkeypatch.setenv("MCC_AB", "no_fused_pack")
     plan2, p_tab, l_tab = _sgd_steps(cuda, spec, dtype, B)
     assert "pack table" in plan2
     np.testing.assert_array_equal(p_fused, p_tab)
@@ -218,9 +218,9 @@ def test_igemm_conv_path_matches_torch(cuda, no_igemm, monkeypatch):
     """Large-image path on implicit-GEMM kernels (bf16, C % 64 == 0 layers:
     forward with the bias+ReLU epilogue, the flipped-weight data gradient and
     the split-K weight gradient) vs the fp64 oracle; the same model with
-    MCC_NO_IGEMM=1 runs the explicit im2col + GEMM path."""
+    MCC_AB=no_igemm runs the explicit im2col + GEMM path."""
     if no_igemm:
-        monkeypatch.setenv("MCC_NO_IGEMM", "1")
+        monkeypatch.setenv("MCC_AB", "no_igemm")
     spec = mcc.parse_model_spec("input 3 80 80; conv 64 k3 s1 p1 relu; pool 2; conv 64 k3 s1 p1 relu; "
                                 "conv 128 k3 s1 p1 relu; pool 2; fc 32 relu; fc 10 softmax", "big80")
     B = 5
@@ -346,14 +346,15 @@ def _lenet_grads(cuda, B, seed=7):
 @pytest.mark.parametrize("B", [96, 4099])
 def test_rows_dw_matches_pipe_dw(cuda, B, monkeypatch):
     """conv1 weight gradient on the row-chunked kernel (conv_rows.hip) vs the
-    pixel-major conv_dw_pipe kernel (MCC_NO_ROWS=1).  Same bf16 dZ; the
+    pixel-major conv_dw_pipe kernel (MCC_AB=no_rows).  Same bf16 dZ; the
     pixels differ only in rounding (conv_rows stages the exact integers
     0..255 and applies 1/255 in fp32 at the end, conv_dw_pipe rounds x/255 to
     bf16: <= 2^-9 relative per pixel), so every output channel agrees to a
     few 1e-3 and the bias (no pixel operand) to ~1e-5."""
+    monkeypatch.setenv("MCC_AB", "no_lenet")  # the per-layer kernels (the LeNet block fuses this layer)
     spec, plan, g_rows = _lenet_grads(cuda, B)
     assert "dw:rows" in plan, plan
-    monkeypatch.setenv("MCC_NO_ROWS", "1")
+    monkeypatch.setenv("MCC_AB", "no_rows,no_lenet")
     _, plan2, g_pipe = _lenet_grads(cuda, B)
     assert "dw:rows" not in plan2
     L = spec.layers()[1]
@@ -521,11 +522,10 @@ def test_generic_activation_convs_match_torch(cuda, name, dtype):
 
 @pytest.mark.gpu
 def test_dz_fused_into_next_dgrad_bit_equal(cuda, monkeypatch):
-    """ReLU big convs get their dZ from the next stage's implicit-GEMM
-    data-gradient epilogue -- dX * (y > 0), or the 2x2 unpool by the stored
-    argmax for a pooled conv -- instead of a grad_xform pass (MCC_DZ_FUSE=0:
-    the pass): bit-identical logits and gradients (masking / routing commute
-    with the bf16 rounding of dX)."""
+    """Unpooled ReLU big convs get their dZ from the next stage's implicit-GEMM
+    data-gradient epilogue -- dX * (y > 0) -- instead of a grad_xform pass
+    (MCC_AB=no_dz_fuse: the pass): bit-identical logits and gradients (the
+    masking commutes with the bf16 rounding of dX)."""
     spec = mcc.parse_model_spec("input 3 72 72; conv 64 k3 s1 p1 relu; conv 64 k3 s1 p1 relu; pool 2; "
                                 "conv 128 k3 s1 p1 relu; conv 128 k3 s1 p1 relu; pool 2; fc 10 softmax", "dzfuse")
     C, H, W = spec.input_shape()
@@ -536,8 +536,8 @@ def test_dz_fused_into_next_dgrad_bit_equal(cuda, monkeypatch):
     d_lab = torch.from_numpy(labels).to(cuda)
     s = torch.cuda.current_stream().cuda_stream
     out = {}
-    for mode in ("1", "2", "0"):
-        monkeypatch.setenv("MCC_DZ_FUSE", mode)
+    for mode in ("2", "0"):
+        monkeypatch.setenv("MCC_AB", "" if mode == "2" else "no_dz_fuse")
         net = mcc.GpuNet(spec, "bf16", B)
         net.set_params(params)
         net.zero_stats(s)
@@ -547,42 +547,8 @@ def test_dz_fused_into_next_dgrad_bit_equal(cuda, monkeypatch):
         torch.cuda.synchronize()
         out[mode] = (net.plan(), net.get_logits(B), net.get_grads())
         del net
-    assert out["1"][0].count("dz<-next-dx") == 3, out["1"][0]  # conv1, conv2 (pooled: unpool), conv3
     assert out["2"][0].count("dz<-next-dx") == 2, out["2"][0]  # conv1, conv3 (ReLU mask only, the default)
     assert "dz<-next-dx" not in out["0"][0]
-    for m in ("1", "2"):
+    for m in ("2",):
         np.testing.assert_array_equal(out[m][1], out["0"][1])
         np.testing.assert_array_equal(out[m][2], out["0"][2])
-
-
-@pytest.mark.gpu
-def test_fc_fused_bwd_matches_unfused(cuda, monkeypatch):
-    """Small FC layers (LeNet-5 120 -> 84) run dX and dW/db in one fused pass
-    (fc_bwd.hip); MCC_FC_FBWD=0 runs the split-K dW GEMM + reduce and the FC
-    data-gradient kernel.  Same step up to fp32 summation order."""
-    spec = mcc.make_model("lenet5")
-    B = 200  # not a multiple of the 64-row block
-    imgs, labels = mcc.synth_dataset(B, 1, 28, 28, 10, seed=6)
-    params = mcc.init_params(spec, seed=5).astype(np.float32)
-    d_img = torch.from_numpy(imgs).to(cuda)
-    d_lab = torch.from_numpy(labels).to(cuda)
-    s = torch.cuda.current_stream().cuda_stream
-    out = {}
-    for mode in ("1", "0"):
-        monkeypatch.setenv("MCC_FC_FBWD", mode)
-        net = mcc.GpuNet(spec, "bf16", B)
-        net.set_params(params)
-        net.zero_stats(s)
-        net.forward(d_img.data_ptr(), 0, B, s)
-        net.loss(d_lab.data_ptr(), 0, 1.0 / B, True, s)
-        net.backward_all(s)
-        torch.cuda.synchronize()
-        out[mode] = (net.plan(), net.get_grads())
-        del net
-    assert "fused-bwd" in out["1"][0] and "fused-bwd" not in out["0"][0], out["1"][0]
-    for L in spec.layers():
-        if L["nweights"] == 0:
-            continue
-        for off, n, what in ((L["w_off"], L["nweights"], "W"), (L["b_off"], L["nbiases"], "b")):
-            err = _relerr(out["1"][1][off : off + n], out["0"][1][off : off + n])
-            assert err < 1e-2, f"{L['kind']} {what} fused vs unfused rel err {err:.3e}"

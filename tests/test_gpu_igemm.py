@@ -221,7 +221,7 @@ def test_u8_first_layer_runs_match_bytes(cuda, monkeypatch, hw):
     s = torch.cuda.current_stream().cuda_stream
     out = {}
     for mode in ("1", "0"):
-        monkeypatch.setenv("MCC_U8_RUNS", mode)
+        monkeypatch.setenv("MCC_AB", "" if mode == "1" else "u8_bytes")
         net = mcc.GpuNet(spec, "bf16", B)
         net.set_params(params)
         net.zero_stats(s)

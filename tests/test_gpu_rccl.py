@@ -7,7 +7,7 @@ trained weights must be BIT-equal to the collective-free path.
   * Python: GpuTrainer under a world-1 "nccl" process group (bench.py's N=1
     path) vs no process group.
   * Native: cnn_dist with its RcclComm (hipGraph replay, eager, --profile)
-    vs MCC_LOCAL_COMM=1.
+    vs MCC_AB=local_comm.
 """
 
 import json
@@ -86,7 +86,7 @@ def idx_files(tmp_path_factory):
 
 def _cnn_dist(idx_files, w, extra, env_extra=None):
     env = dict(os.environ, RANK="0", WORLD_SIZE="1", LOCAL_RANK="0", MCC_COMM_TIMEOUT="120")
-    env.pop("MCC_LOCAL_COMM", None)
+    env.pop("MCC_AB", None)
     env.update(env_extra or {})
     r = subprocess.run([os.path.join(ROOT, "build/bin/cnn_dist")] + idx_files +
                        ["--model", "lenet5", "--batch", "512", "--epochs", "1", "--lr", "0.05", "--momentum", "0.9",
@@ -104,7 +104,7 @@ def test_cnn_dist_rccl_world1_bit_equal(idx_files, tmp_path):
     assert js_e["comm"] == "rccl" and js_e["hipgraph"] is False
     js_p, p_p = _cnn_dist(idx_files, str(tmp_path / "p.w"), ["--profile"])
     assert js_p["comm"] == "rccl" and "phase_ms" in js_p
-    js_l, p_l = _cnn_dist(idx_files, str(tmp_path / "l.w"), [], {"MCC_LOCAL_COMM": "1"})
+    js_l, p_l = _cnn_dist(idx_files, str(tmp_path / "l.w"), [], {"MCC_AB": "local_comm"})
     assert js_l["comm"] == "local" and js_l["hipgraph"] is True
     np.testing.assert_array_equal(p_g, p_l)  # RCCL world-1 == no collectives
     np.testing.assert_array_equal(p_g, p_e)  # graph replay == eager
