@@ -71,6 +71,10 @@ def main():
     ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
                     help="nccl (= RCCL, the measured path) or gloo: a rehearsal of the multi-rank bench logic "
                          "with more ranks than GPUs (ranks share GPUs round-robin; not a performance number)")
+    ap.add_argument("--force-reduce", action="store_true",
+                    help="N=1: make each bucket's collective a real RCCL reduction kernel (AVG; bit-identical "
+                         "result) instead of the in-place SUM RCCL elides at one rank -- measures comm/compute "
+                         "contention (profiles/comm_contention_r3.txt)")
     args = ap.parse_args()
 
     import torch
@@ -119,6 +123,7 @@ def main():
         momentum=args.momentum,
         init="fast",
         bucket_bytes=int(args.bucket_mb * (1 << 20)),
+        force_reduce=args.force_reduce,
     )
     # device minibatch sampler (rand() % N semantics, cnn.c:455): indices and
     # its step counter live on the GPU, so a graph replay draws a fresh batch
@@ -208,6 +213,10 @@ def main():
                 "optimizer": f"sgd lr={args.lr} momentum={args.momentum}",
                 "allreduce": (f"{'rccl' if args.dist_backend == 'nccl' else 'gloo (rehearsal)'}: {coll_per_step:g} all-reduce(s)/step over {len(tr.sync.buckets)} "
                               f"bucket(s) <= {args.bucket_mb} MiB, async on RCCL's stream, joined before SGD"
+                              + ("; at one rank RCCL elides the in-place SUM: no reduction kernel runs"
+                                 " (--force-reduce runs one)" if tr.sync.elided else "")
+                              + ("; forced one-rank reduction kernel (AVG)" if args.force_reduce and world == 1
+                                 else "")
                               if coll_per_step else "none (--no-dist)"),
                 "train_loss_last": round(st["loss_sum"] / (B * args.steps), 4),
                 "launch": graph_note,

@@ -18,7 +18,7 @@
 //
 // The RCCL communicator is created at every world size, 1 included, so a
 // single-GPU run executes the same broadcast, bucketed all-reduce on the comm
-// stream and graph-captured collectives as an 8-GPU one.  MCC_LOCAL_COMM=1
+// stream and graph-captured collectives as an 8-GPU one.  MCC_AB=local_comm
 // (world 1 only) swaps in the collective-free LocalComm for A/B runs.
 #include "mcc/ab.h"
 #include <arpa/inet.h>

@@ -122,7 +122,7 @@ GpuNet::GpuNet(const ModelSpec& spec, DType dtype, int max_batch, int device)
   no_igemm_ = ab_flag("no_igemm");       // im2col + GEMM instead of the implicit GEMM
   igemm_small_ = !ab_flag("no_igemm_small");  // LDS kernels for wide small-image convs
   no_head_ = ab_flag("no_head");         // softmax_xent + FC backward instead of the fused head
-  // dW side stream: opt-in (MCC_SIDE_STREAM=1).  Measured on MI355X (one GPU,
+  // dW side stream: opt-in (MCC_AB=side_stream).  Measured on MI355X (one GPU,
   // bench.py): CIFAR-3conv 2.27 -> 2.17 ms/step, but LeNet-5 0.452 -> 0.502 and
   // VGG-11 12.14 -> 12.40: the persistent conv kernels are sized to own every
   // CU, so a concurrent dW kernel steals their slots and stretches both.
@@ -292,7 +292,7 @@ void GpuNet::build() {
                (int64_t)LHd * LWd * st.CLd * (int64_t)es > lds_cap || (int64_t)dw_img_b > lds_cap || st.generic;
       MCC_CHECK(!st.generic || st.C % 8 == 0, "GPU engine: tanh convs / pools after a non-ReLU conv need Cout % 8 == 0");
       // small images with wide channels (C % 64, Cout % 8, stride 1) go to the
-      // 128x128 / 256-tile MFMA kernels (MCC_IGEMM_SMALL=0: the whole-image LDS
+      // 128x128 / 256-tile MFMA kernels (MCC_AB=no_igemm_small: the whole-image LDS
       // kernels).  CIFAR-3conv conv3 (64 -> 128): 3.91 -> 4.32 M img/s; conv2
       // (32 -> 64) measured slower on igemm (3.83 M), so C % 64 only.
       if (!st.big && igemm_small_ && s > 0 && dtype_ == DType::BF16 && !no_igemm_ && st.stride == 1 &&
@@ -355,7 +355,7 @@ void GpuNet::build() {
 
   // ---- LeNet-5 conv block (lenet.hip): conv1 + pool + conv2 + pool as ONE
   // forward kernel and ONE fused backward kernel (conv2 dW, conv2 dX and the
-  // unpooled conv1 dW per image, dY1 never leaves LDS).  MCC_NO_LENET=1 keeps
+  // unpooled conv1 dW per image, dY1 never leaves LDS).  MCC_AB=no_lenet keeps
   // the per-layer pipelined kernels (MCC_AB=no_lenet).
   {
     lenet_ = false;

@@ -23,7 +23,7 @@ namespace cpu_v3 {
 template <typename T> CpuKernels<T> kernels();
 }
 
-// The table for this CPU (AVX2+FMA when available).  MCC_CPU_BASELINE=1 forces
+// The table for this CPU (AVX2+FMA when available).  MCC_AB=cpu_baseline forces
 // the baseline build.
 template <typename T> const CpuKernels<T>& cpu_kernels();
 

@@ -1230,11 +1230,11 @@ void igemm_conv(const IgemmParams& p0, hipStream_t s) {
     }
     return;
   }
-  // 256-pixel tiles for the wide layers (MCC_IGEMM_BIG=0: 128x128 kernel
+  // 256-pixel tiles for the wide layers (MCC_AB=igemm_tile=0: 128x128 kernel
   // only; =128: 256x128 tiles only)
   const int big_mode = p.tile >= 0 ? p.tile : igemm_env_mode();
   // auto: 256x256 tiles where N % 256 == 0 (the 128-channel variant measured
-  // slower than the 128x128 kernel on VGG conv2 / conv3-dX: tools/gpu_r2i.sh)
+  // slower than the 128x128 kernel on VGG conv2 / conv3-dX: profiles/igemm256_ab_r2.txt)
   if (p.C % 64 == 0 &&
       ((big_mode == 1 && p.N % 256 == 0) || ((big_mode == 128 || big_mode == 256) && p.N % 128 == 0))) {
     const bool c256 = p.N % 256 == 0 && big_mode != 128;

@@ -176,7 +176,7 @@ struct ConvPipeParams {
   int pair = 0;
   size_t lds = 0;
   uint32_t rows_mh = 0, rows_ml = 0;  // division magic for the GEMM rows per image (set at launch)
-  int ablate = 0;  // diagnostics (MCC_ABLATE bits): 1 no staging, 2 no MFMA loop, 4 no epilogue/copy-out
+  int ablate = 0;  // diagnostics (MCC_AB=ablate=bits): 1 no staging, 2 no MFMA loop, 4 no epilogue/copy-out
 };
 // Geometry for a layer (N may be the maximum batch); false when the layer is
 // outside what the pipelined kernels cover (the caller keeps conv_small).
@@ -311,7 +311,7 @@ struct ConvDwRowsParams {
   int A = 0, Pw = 0, LH = 0, CS = 0, ximg = 0, dplane = 0, dzimg = 0, KK = 0, ntiles = 0;
   int m0 = 0, nblk = 0, imgs = 1, ngroups = 0, grid = 0;
   size_t lds = 0;
-  int ablate = 0;  // diagnostics (MCC_ABLATE): 1 no staging, 2 no MFMA loop
+  int ablate = 0;  // diagnostics (MCC_AB=ablate=bits): 1 no staging, 2 no MFMA loop
 };
 bool conv_dw_rows_plan(ConvDwRowsParams& p);
 size_t conv_dw_rows_scratch_bytes(const ConvDwRowsParams& p);
@@ -460,7 +460,7 @@ struct IgemmParams {
   bool u8_runs = false;              // set at launch: u8 C=3 3x3 pad-1 im2col rows from dword runs
   const void* relu_mask = nullptr;   // bf16; data gradient only: out = dX * (relu_mask > 0), same layout as out
                                      // (writes the next-lower ReLU layer's dZ directly: no grad_xform pass)
-  int tile = -1;                     // -1 auto (MCC_IGEMM_BIG, default on), 0: 128x128 kernel,
+  int tile = -1;                     // -1 auto, 0: 128x128 kernel,
                                      // 128 / 256: 256-pixel x 128 / 256-channel kernel where legal
   DivMagic div_ohw, div_ow;
 };
@@ -487,7 +487,7 @@ struct IgemmDwParams {
   float* gb = nullptr;
   DivMagic div_ohw, div_ow;
   int adv_x = 0, adv_y = 0, adv_b = 0;  // set at launch: +BK pixels as (ox, oy, b) increments
-  int tile = -1;                     // -1 auto (MCC_IGEMM_BIG), 0: 128x128 kernel, 128 / 256: BA x 256
+  int tile = -1;                     // -1 auto (MCC_AB=igemm_tile=), 0: 128x128 kernel, 128 / 256: BA x 256
                                      // phase-pipelined kernel (igemm_dw_splitk must see the same value)
 };
 int igemm_dw_splitk(int M, int Cout, int kf, int tile = -1);

@@ -86,13 +86,21 @@ class BucketedAllReduce:
     (any world size, 1 included: with the "nccl" backend that is a real RCCL
     collective on RCCL's stream)."""
 
-    def __init__(self, net, grads: torch.Tensor, group=None, bucket_bytes: int = 4 << 20):
+    def __init__(self, net, grads: torch.Tensor, group=None, bucket_bytes: int = 4 << 20,
+                 force_kernel: bool = False):
         self.net = net
         self.grads = grads
         self.group = group
         self.active = dist.is_initialized()
         self.world = dist.get_world_size(group) if self.active else 1
         self.op = dist.ReduceOp.SUM
+        # force_kernel: make the one-rank collective a real reduction kernel
+        # (AVG = a pre-multiplied sum; x * 1 is exact, so the result is
+        # bit-identical) to measure comm/compute contention on one GPU.  At
+        # world > 1 the SUM already runs RCCL's ring kernels.
+        self.elided = self.active and self.world == 1 and not force_kernel
+        if self.active and self.world == 1 and force_kernel:
+            self.op = dist.ReduceOp.AVG
         self.buckets = [tuple(b) for b in net.buckets(int(bucket_bytes))]
         self.issued = 0  # collectives issued so far (introspection / tests)
         covered = sum(b[3] for b in self.buckets)

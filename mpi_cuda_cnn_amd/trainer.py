@@ -36,6 +36,7 @@ class GpuTrainer:
         params=None,
         group=None,
         bucket_bytes: int = 4 << 20,
+        force_reduce: bool = False,
     ):
         self.spec = _C.make_model(model) if isinstance(model, str) else model
         self.device = torch.cuda.current_device() if device is None else device
@@ -55,7 +56,7 @@ class GpuTrainer:
         if dist.is_initialized():  # identical replicas (fixes D6: srand(rank), no broadcast)
             broadcast_params(self.params, 0, group)
             self.net.pack(self.stream)
-        self.sync = BucketedAllReduce(self.net, self.grads, group, bucket_bytes)
+        self.sync = BucketedAllReduce(self.net, self.grads, group, bucket_bytes, force_reduce)
 
     @property
     def stream(self) -> int:

@@ -25,7 +25,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 STEPS, B, LR, MOM, BUCKET = 4, 256, 0.05, 0.9, 16 << 10
 
 
-def _train(model, dtype):
+def _train(model, dtype, force=False):
     from mpi_cuda_cnn_amd.trainer import GpuTrainer
 
     dev = torch.device("cuda", 0)
@@ -34,7 +34,7 @@ def _train(model, dtype):
     imgs, labels = mcc.synth_dataset(STEPS * B, C, H, W, spec.num_classes(), seed=9)
     d_img, d_lab = torch.from_numpy(imgs).to(dev), torch.from_numpy(labels).to(dev)
     tr = GpuTrainer(spec, dtype=dtype, batch=B, device=0, lr=LR, momentum=MOM,
-                    params=mcc.init_params(spec, seed=3, mode="fast"), bucket_bytes=BUCKET)
+                    params=mcc.init_params(spec, seed=3, mode="fast"), bucket_bytes=BUCKET, force_reduce=force)
     for s in range(STEPS):
         idx = torch.arange(s * B, (s + 1) * B, device=dev, dtype=torch.int32)
         tr.step(d_img, d_lab, idx)
@@ -42,7 +42,7 @@ def _train(model, dtype):
     return tr.state_dict(), len(tr.sync.buckets), tr.sync.issued
 
 
-def _rccl_worker(rank, model, dtype, out):
+def _rccl_worker(rank, model, dtype, out, force=False):
     import torch.distributed as dist
 
     from mpi_cuda_cnn_amd.parallel.ddp import init_process_group
@@ -52,16 +52,18 @@ def _rccl_worker(rank, model, dtype, out):
     torch.cuda.set_device(0)
     init_process_group("nccl", torch.device("cuda", 0))
     assert dist.get_backend() == "nccl" and dist.get_world_size() == 1
-    p, nb, issued = _train(model, dtype)
+    p, nb, issued = _train(model, dtype, force)
     np.save(os.path.join(out, "p.npy"), p)
     np.save(os.path.join(out, "n.npy"), np.array([nb, issued]))
     dist.destroy_process_group()
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("model,dtype", [("lenet5", "bf16"), ("cifar3", "bf16"), ("ref", "fp32")])
-def test_python_rccl_world1_bit_equal(cuda, model, dtype, tmp_path):
-    mp.spawn(_rccl_worker, args=(model, dtype, str(tmp_path)), nprocs=1, join=True)
+@pytest.mark.parametrize("model,dtype,force", [("lenet5", "bf16", False), ("cifar3", "bf16", False),
+                                               ("ref", "fp32", False), ("lenet5", "bf16", True)])
+def test_python_rccl_world1_bit_equal(cuda, model, dtype, force, tmp_path):
+    """force: bench.py --force-reduce (a real one-rank AVG reduction kernel per bucket) is bit-equal too."""
+    mp.spawn(_rccl_worker, args=(model, dtype, str(tmp_path), force), nprocs=1, join=True)
     p_rccl = np.load(tmp_path / "p.npy")
     nb, issued = np.load(tmp_path / "n.npy")
     assert nb > 1, "expected several buckets"
