@@ -33,7 +33,7 @@ ENG_OBJ   := $(patsubst csrc/engine/%.cpp,$(OBJ)/engine/%.o,$(ENG_SRC))
 HDRS      := $(wildcard csrc/include/mcc/*.h csrc/kernels/*.h csrc/apps/*.h) csrc/core/cpu_kernels.inc
 
 MODULE    := mpi_cuda_cnn_amd/_C$(EXT)
-BINS      := build/bin/cnn build/bin/cnn_hip build/bin/cnn_dist build/bin/test_watchdog
+BINS      := build/bin/cnn build/bin/cnn_hip build/bin/cnn_dist build/bin/test_watchdog build/bin/test_comm
 ifneq ($(MPICXX),)
 BINS      += build/bin/cnnmpi
 endif
@@ -82,6 +82,12 @@ build/bin/test_watchdog: csrc/tests/test_watchdog.cpp csrc/apps/watchdog.h
 	@mkdir -p $(dir $@)
 	$(CXX) $(CXXFLAGS) -Icsrc/apps -o $@ csrc/tests/test_watchdog.cpp
 
+# host-only rendezvous + shared-memory collectives (cnn_dist --comm host)
+COMM_SRC := csrc/apps/bootstrap.cpp csrc/apps/shm_group.cpp
+build/bin/test_comm: csrc/tests/test_comm.cpp $(COMM_SRC) $(HDRS)
+	@mkdir -p $(dir $@)
+	$(CXX) $(CXXFLAGS) -Icsrc/apps -o $@ csrc/tests/test_comm.cpp $(COMM_SRC) -lrt
+
 # MPICH's wrapper would put its own (older) libstdc++ first; link with the
 # system compiler against the MPI library instead, libstdc++ static.
 MPI_PREFIX := $(patsubst %/bin/mpicxx,%,$(MPICXX))
@@ -98,7 +104,8 @@ build/bin/cnn_hip: $(OBJ)/apps/cnn_hip.o $(OBJ)/apps/trainer.o $(CORE_OBJ) $(KER
 	@mkdir -p $(dir $@)
 	$(HIPCC) --offload-arch=$(ARCH) -o $@ $^ $(LDHIP) -lrocprofiler-sdk-roctx
 
-build/bin/cnn_dist: $(OBJ)/apps/cnn_dist.o $(OBJ)/apps/trainer.o $(CORE_OBJ) $(KERN_OBJ) $(ENG_OBJ)
+build/bin/cnn_dist: $(OBJ)/apps/cnn_dist.o $(OBJ)/apps/trainer.o $(OBJ)/apps/bootstrap.o $(OBJ)/apps/shm_group.o \
+                   $(OBJ)/apps/host_comm.o $(CORE_OBJ) $(KERN_OBJ) $(ENG_OBJ)
 	@mkdir -p $(dir $@)
 	$(HIPCC) --offload-arch=$(ARCH) -o $@ $^ $(LDHIP) -lrccl -lrocprofiler-sdk-roctx
 

@@ -1,0 +1,120 @@
+// TCP rendezvous (bootstrap.h).  Host-only code: built into cnn_dist and the
+// CPU test binary test_comm (csrc/tests/test_comm.cpp).
+#include "bootstrap.h"
+
+#include <netdb.h>
+#include <netinet/in.h>
+#include <poll.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <cstdlib>
+#include <memory>
+#include <thread>
+
+#include "mcc/common.h"
+
+namespace mcc {
+namespace {
+
+using Clock = std::chrono::steady_clock;
+
+int env_int(const char* name, int dflt) {
+  const char* v = std::getenv(name);
+  return v && *v ? std::atoi(v) : dflt;
+}
+
+int ms_left(Clock::time_point deadline) {
+  const auto ms = std::chrono::duration_cast<std::chrono::milliseconds>(deadline - Clock::now()).count();
+  return ms > 0 ? (int)std::min<long long>(ms, 1 << 30) : 0;
+}
+
+bool send_all(int fd, const char* p, size_t n) {
+  while (n) {
+    const ssize_t k = ::send(fd, p, n, MSG_NOSIGNAL);
+    if (k <= 0) return false;
+    p += k;
+    n -= (size_t)k;
+  }
+  return true;
+}
+
+bool recv_all(int fd, char* p, size_t n, Clock::time_point deadline) {
+  while (n) {
+    pollfd pf{fd, POLLIN, 0};
+    const int left = ms_left(deadline);
+    if (left <= 0 || ::poll(&pf, 1, left) <= 0) return false;
+    const ssize_t k = ::recv(fd, p, n, 0);
+    if (k <= 0) return false;
+    p += k;
+    n -= (size_t)k;
+  }
+  return true;
+}
+
+struct Fd {
+  int fd;
+  explicit Fd(int f) : fd(f) {}
+  ~Fd() {
+    if (fd >= 0) ::close(fd);
+  }
+};
+
+}  // namespace
+
+BootstrapAddr bootstrap_addr_from_env() {
+  BootstrapAddr a;
+  if (const char* h = std::getenv("MASTER_ADDR"); h && *h) a.host = h;
+  a.port = env_int("MCC_BOOTSTRAP_PORT", -1);
+  if (a.port < 0) a.port = env_int("MASTER_PORT", 29500) + 1;
+  a.timeout_s = env_int("MCC_BOOTSTRAP_TIMEOUT", 300);
+  return a;
+}
+
+void serve_blob(const void* blob, size_t n, int clients, const BootstrapAddr& addr) {
+  const auto deadline = Clock::now() + std::chrono::milliseconds((long long)(addr.timeout_s * 1000));
+  Fd srv(::socket(AF_INET, SOCK_STREAM, 0));
+  if (srv.fd < 0) throw Error("bootstrap: socket() failed");
+  int one = 1;
+  ::setsockopt(srv.fd, SOL_SOCKET, SO_REUSEADDR, &one, sizeof(one));
+  sockaddr_in sa{};
+  sa.sin_family = AF_INET;
+  sa.sin_addr.s_addr = htonl(INADDR_ANY);
+  sa.sin_port = htons((uint16_t)addr.port);
+  if (::bind(srv.fd, reinterpret_cast<sockaddr*>(&sa), sizeof(sa)) != 0 || ::listen(srv.fd, clients + 4) != 0)
+    throw Error("bootstrap: cannot listen on port " + std::to_string(addr.port));
+  for (int served = 0; served < clients;) {
+    pollfd pf{srv.fd, POLLIN, 0};
+    const int left = ms_left(deadline);
+    if (left <= 0 || ::poll(&pf, 1, left) <= 0)
+      throw Error("bootstrap: timed out waiting for ranks (" + std::to_string(served) + " of " +
+                  std::to_string(clients) + " served)");
+    Fd c(::accept(srv.fd, nullptr, nullptr));
+    if (c.fd < 0) continue;
+    if (send_all(c.fd, static_cast<const char*>(blob), n)) ++served;
+  }
+}
+
+void fetch_blob(void* blob, size_t n, const BootstrapAddr& addr) {
+  const auto deadline = Clock::now() + std::chrono::milliseconds((long long)(addr.timeout_s * 1000));
+  addrinfo hints{}, *res = nullptr;
+  hints.ai_family = AF_INET;
+  hints.ai_socktype = SOCK_STREAM;
+  if (::getaddrinfo(addr.host.c_str(), std::to_string(addr.port).c_str(), &hints, &res) != 0 || !res)
+    throw Error("bootstrap: cannot resolve MASTER_ADDR " + addr.host);
+  std::unique_ptr<addrinfo, void (*)(addrinfo*)> guard(res, ::freeaddrinfo);
+  while (true) {
+    {
+      Fd fd(::socket(AF_INET, SOCK_STREAM, 0));
+      if (fd.fd >= 0 && ::connect(fd.fd, res->ai_addr, res->ai_addrlen) == 0 &&
+          recv_all(fd.fd, static_cast<char*>(blob), n, deadline))
+        return;
+    }
+    if (Clock::now() >= deadline) throw Error("bootstrap: timed out connecting to rank 0 at " + addr.host + ":" +
+                                              std::to_string(addr.port));
+    std::this_thread::sleep_for(std::chrono::milliseconds(50));
+  }
+}
+
+}  // namespace mcc

@@ -41,6 +41,7 @@ struct CliArgs {
   bool no_graph = false;    // run the step eagerly instead of replaying a hipGraph
   bool quiet = false;
   int64_t synthetic = 0;    // --synthetic N: generated data instead of IDX files
+  std::string comm = "rccl";  // cnn_dist: rccl | host (several ranks on one GPU) | local (world 1)
 };
 
 inline void usage(const char* prog) {
@@ -50,6 +51,8 @@ inline void usage(const char* prog) {
                "  [--momentum X] [--weight-decay X] [--seed S] [--dtype bf16|fp32]\n"
                "  [--ref-compat] [--fp32] [--save W] [--load W] [--max-train N]\n"
                "  [--bucket-mb MB] [--log-every N] [--profile] [--no-graph] [--json PATH|-]\n"
+               "  [--comm rccl|host|local]   (cnn_dist: RCCL; host shared memory for several ranks\n"
+               "                             on one GPU; no collectives at world 1)\n"
                "  [--synthetic N]   (no IDX files: N generated training images, N/5 test images\n"
                "                     of the model's input shape; positional paths optional)\n",
                prog);
@@ -84,6 +87,7 @@ inline int parse_cli(int argc, char** argv, CliArgs& a) {
     else if (s == "--profile") a.profile = true;
     else if (s == "--no-graph") a.no_graph = true;
     else if (s == "--quiet") a.quiet = true;
+    else if (s == "--comm") a.comm = next();
     else if (s == "-h" || s == "--help") { usage(argv[0]); std::exit(0); }
     else if (s.size() > 2 && s[0] == '-' && s[1] == '-') { usage(argv[0]); std::exit(100); }
     else pos.push_back(s);

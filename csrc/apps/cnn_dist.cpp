@@ -18,27 +18,20 @@
 //
 // The RCCL communicator is created at every world size, 1 included, so a
 // single-GPU run executes the same broadcast, bucketed all-reduce on the comm
-// stream and graph-captured collectives as an 8-GPU one.  MCC_AB=local_comm
-// (world 1 only) swaps in the collective-free LocalComm for A/B runs.
-#include "mcc/ab.h"
-#include <arpa/inet.h>
-#include <netdb.h>
-#include <netinet/in.h>
-#include <netinet/tcp.h>
-#include <poll.h>
-#include <sys/socket.h>
-#include <unistd.h>
-
+// stream and graph-captured collectives as an 8-GPU one.  --comm local
+// (world 1 only) swaps in the collective-free LocalComm for A/B runs;
+// --comm host runs several ranks on ONE GPU with host shared-memory
+// collectives (host_comm.h) -- the multi-rank rehearsal of the test box.
 #include <rccl/rccl.h>
 
-#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <string>
-#include <thread>
 
+#include "bootstrap.h"
 #include "cli.h"
+#include "host_comm.h"
 #include "trainer.h"
 #include "watchdog.h"
 
@@ -57,85 +50,9 @@ int env_int(const char* const* names, int dflt) {
   return dflt;
 }
 
-bool send_all(int fd, const void* buf, size_t n) {
-  const char* p = static_cast<const char*>(buf);
-  while (n) {
-    ssize_t k = ::send(fd, p, n, MSG_NOSIGNAL);
-    if (k <= 0) return false;
-    p += k;
-    n -= (size_t)k;
-  }
-  return true;
-}
-
-bool recv_all(int fd, void* buf, size_t n, int timeout_ms) {
-  char* p = static_cast<char*>(buf);
-  while (n) {
-    pollfd pf{fd, POLLIN, 0};
-    if (::poll(&pf, 1, timeout_ms) <= 0) return false;
-    ssize_t k = ::recv(fd, p, n, 0);
-    if (k <= 0) return false;
-    p += k;
-    n -= (size_t)k;
-  }
-  return true;
-}
-
 void bootstrap_id(ncclUniqueId& id, int rank, int world) {
-  const char* addr = std::getenv("MASTER_ADDR");
-  std::string host = addr ? addr : "127.0.0.1";
-  int port = env_int((const char*[]){"MCC_BOOTSTRAP_PORT", nullptr}, -1);
-  if (port < 0) port = env_int((const char*[]){"MASTER_PORT", nullptr}, 29500) + 1;
-  const int timeout_s = env_int((const char*[]){"MCC_BOOTSTRAP_TIMEOUT", nullptr}, 300);
-  const auto deadline = std::chrono::steady_clock::now() + std::chrono::seconds(timeout_s);
-  if (rank == 0) {
-    NCCLCHK(ncclGetUniqueId(&id));
-    if (world == 1) return;  // nobody to serve
-    int srv = ::socket(AF_INET, SOCK_STREAM, 0);
-    int one = 1;
-    ::setsockopt(srv, SOL_SOCKET, SO_REUSEADDR, &one, sizeof(one));
-    sockaddr_in sa{};
-    sa.sin_family = AF_INET;
-    sa.sin_addr.s_addr = htonl(INADDR_ANY);
-    sa.sin_port = htons((uint16_t)port);
-    if (::bind(srv, reinterpret_cast<sockaddr*>(&sa), sizeof(sa)) != 0 || ::listen(srv, world) != 0) {
-      ::close(srv);
-      throw Error("bootstrap: cannot listen on port " + std::to_string(port));
-    }
-    for (int served = 1; served < world;) {
-      pollfd pf{srv, POLLIN, 0};
-      const int left = (int)std::chrono::duration_cast<std::chrono::milliseconds>(deadline - std::chrono::steady_clock::now()).count();
-      if (left <= 0 || ::poll(&pf, 1, left) <= 0) { ::close(srv); throw Error("bootstrap: timed out waiting for ranks"); }
-      int c = ::accept(srv, nullptr, nullptr);
-      if (c < 0) continue;
-      const bool ok = send_all(c, &id, sizeof(id));
-      ::close(c);
-      if (ok) ++served;
-    }
-    ::close(srv);
-    return;
-  }
-  addrinfo hints{}, *res = nullptr;
-  hints.ai_family = AF_INET;
-  hints.ai_socktype = SOCK_STREAM;
-  if (::getaddrinfo(host.c_str(), std::to_string(port).c_str(), &hints, &res) != 0 || !res)
-    throw Error("bootstrap: cannot resolve MASTER_ADDR " + host);
-  while (true) {
-    int fd = ::socket(AF_INET, SOCK_STREAM, 0);
-    if (::connect(fd, res->ai_addr, res->ai_addrlen) == 0) {
-      const bool ok = recv_all(fd, &id, sizeof(id), 60000);
-      ::close(fd);
-      if (ok) break;
-    } else {
-      ::close(fd);
-    }
-    if (std::chrono::steady_clock::now() > deadline) {
-      ::freeaddrinfo(res);
-      throw Error("bootstrap: timed out connecting to rank 0");
-    }
-    std::this_thread::sleep_for(std::chrono::milliseconds(100));
-  }
-  ::freeaddrinfo(res);
+  if (rank == 0) NCCLCHK(ncclGetUniqueId(&id));
+  bootstrap_blob(&id, sizeof(id), rank, world, bootstrap_addr_from_env());
 }
 
 struct RcclComm : Comm {
@@ -234,8 +151,16 @@ int main(int argc, char** argv) {
       mcc::env_int((const char*[]){"LOCAL_RANK", "OMPI_COMM_WORLD_LOCAL_RANK", "MPI_LOCALRANKID", nullptr}, rank);
   std::unique_ptr<mcc::Comm> comm;
   try {
-    if (world == 1 && mcc::ab_flag("local_comm")) comm.reset(new mcc::LocalComm());
-    else comm.reset(new mcc::RcclComm(rank, world, local));
+    if (a.comm == "local") {
+      if (world != 1) throw mcc::Error("--comm local needs world size 1");
+      comm.reset(new mcc::LocalComm());
+    } else if (a.comm == "host") {
+      comm = mcc::make_host_comm(rank, world, local);
+    } else if (a.comm == "rccl") {
+      comm.reset(new mcc::RcclComm(rank, world, local));
+    } else {
+      throw mcc::Error("--comm must be rccl, host or local");
+    }
   } catch (const mcc::Error& e) {
     std::fprintf(stderr, "rank %d: %s\n", rank, e.what());
     return 111;

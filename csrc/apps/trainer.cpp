@@ -10,9 +10,13 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
 #include <memory>
 #include <vector>
 
@@ -39,6 +43,48 @@ struct DevBuf {
   ~DevBuf() { if (p) (void)hipFree(p); }
   template <typename T> T* as() const { return static_cast<T*>(p); }
 };
+
+// Host -> device upload of a dataset through two pinned 32 MiB staging
+// buffers (a pageable hipMemcpy is staged by the runtime one small chunk at a
+// time): memcpy into one buffer while the DMA engine drains the other.
+void upload_pinned(void* dst, const void* src, size_t bytes) {
+  constexpr size_t kChunk = 32u << 20;
+  if (bytes <= (1u << 20)) {
+    HIPCHK(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice));
+    return;
+  }
+  char* pin[2] = {nullptr, nullptr};
+  hipEvent_t done[2] = {nullptr, nullptr};
+  hipStream_t s = nullptr;
+  auto cleanup = [&] {
+    if (s) (void)hipStreamSynchronize(s);
+    for (int i = 0; i < 2; ++i) {
+      if (pin[i]) (void)hipHostFree(pin[i]);
+      if (done[i]) (void)hipEventDestroy(done[i]);
+    }
+    if (s) (void)hipStreamDestroy(s);
+  };
+  try {
+    HIPCHK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    for (int i = 0; i < 2; ++i) {
+      HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&pin[i]), kChunk, hipHostMallocDefault));
+      HIPCHK(hipEventCreateWithFlags(&done[i], hipEventDisableTiming));
+    }
+    for (size_t off = 0, k = 0; off < bytes; off += kChunk, ++k) {
+      const int b = (int)(k & 1);
+      const size_t len = std::min(kChunk, bytes - off);
+      if (k >= 2) HIPCHK(hipEventSynchronize(done[b]));  // buffer b's previous copy has drained
+      std::memcpy(pin[b], static_cast<const char*>(src) + off, len);
+      HIPCHK(hipMemcpyAsync(static_cast<char*>(dst) + off, pin[b], len, hipMemcpyHostToDevice, s));
+      HIPCHK(hipEventRecord(done[b], s));
+    }
+    HIPCHK(hipStreamSynchronize(s));
+  } catch (...) {
+    cleanup();
+    throw;
+  }
+  cleanup();
+}
 
 struct PhaseTimer {
   bool on;
@@ -133,8 +179,8 @@ int run_gpu_training(const CliArgs& a, Comm& comm, const char* program) {
     net.set_params(p32.data());
   }
   DevBuf d_img((size_t)N * in_nodes), d_lab((size_t)N);
-  HIPCHK(hipMemcpy(d_img.p, tr_img.data.data(), (size_t)N * in_nodes, hipMemcpyHostToDevice));
-  HIPCHK(hipMemcpy(d_lab.p, tr_lab.data.data(), (size_t)N, hipMemcpyHostToDevice));
+  upload_pinned(d_img.p, tr_img.data.data(), (size_t)N * in_nodes);
+  upload_pinned(d_lab.p, tr_lab.data.data(), (size_t)N);
   DevBuf d_idx(4 * (size_t)eval_b), d_step(8);
   DevBuf d_red(64);  // log / timing / exit-code reductions (no allocation in the loop)
   // pinned host side of those reductions: floats [0, 16), doubles from byte 64.
@@ -248,7 +294,16 @@ int run_gpu_training(const CliArgs& a, Comm& comm, const char* program) {
   HIPCHK(hipDeviceSynchronize());
   const auto t0 = std::chrono::steady_clock::now();
   int64_t seen = 0, last_log = 0;
+  // fault injection for the rank-death tests (same variables as train.py):
+  // MCC_FAULT_RANK=r MCC_FAULT_STEP=k makes rank r die abruptly before step k
+  const char* fr = std::getenv("MCC_FAULT_RANK");
+  const char* fs = std::getenv("MCC_FAULT_STEP");
+  const int64_t fault_step = fr && fs && std::atoi(fr) == rank ? std::atoll(fs) : -1;
   for (int64_t it = 0; it < steps; ++it) {
+    if (it == fault_step) {
+      std::fprintf(stderr, "rank %d: injected fault before step %lld\n", rank, (long long)it);
+      std::_Exit(9);
+    }
     if (it >= kInFlight) comm.wait(ev_step[it % kInFlight]);
     if (use_graph) HIPCHK(hipGraphLaunch(gexec, S));
     else step(a.profile);
@@ -296,6 +351,22 @@ int run_gpu_training(const CliArgs& a, Comm& comm, const char* program) {
   int rc = 0;
   int64_t ntests = 0, ncorrect = 0;
   double test_s = 0;
+  // --save PATH saves rank 0's weights; a PATH containing "{rank}" makes
+  // every rank save its own replica (the multi-rank tests compare them)
+  const size_t rk = a.save.find("{rank}");
+  if (rank != 0 && rk != std::string::npos) {
+    std::vector<float> p32(net.nparams());
+    net.get_params(p32.data());
+    std::vector<double> pd(p32.begin(), p32.end());
+    std::string path = a.save;
+    path.replace(rk, 6, std::to_string(rank));
+    try {
+      save_weights(path, spec, pd.data());
+    } catch (const Error& e) {
+      std::fprintf(stderr, "%s\n", e.what());
+      rc = 111;
+    }
+  }
   if (rank == 0) {
     try {
       te_img = load_idx(a.test_images, spec);
@@ -305,8 +376,8 @@ int run_gpu_training(const CliArgs& a, Comm& comm, const char* program) {
       std::fprintf(stderr, "testing...\n");
       ntests = te_img.count();
       DevBuf t_img((size_t)ntests * in_nodes), t_lab((size_t)ntests);
-      HIPCHK(hipMemcpy(t_img.p, te_img.data.data(), (size_t)ntests * in_nodes, hipMemcpyHostToDevice));
-      HIPCHK(hipMemcpy(t_lab.p, te_lab.data.data(), (size_t)ntests, hipMemcpyHostToDevice));
+      upload_pinned(t_img.p, te_img.data.data(), (size_t)ntests * in_nodes);
+      upload_pinned(t_lab.p, te_lab.data.data(), (size_t)ntests);
       net.zero_stats(S);
       const auto t1 = std::chrono::steady_clock::now();
       for (int64_t i = 0; i < ntests; i += eval_b) {
@@ -327,7 +398,9 @@ int run_gpu_training(const CliArgs& a, Comm& comm, const char* program) {
         std::vector<float> p32(net.nparams());
         net.get_params(p32.data());
         std::vector<double> pd(p32.begin(), p32.end());
-        save_weights(a.save, spec, pd.data());
+        std::string path = a.save;
+        if (rk != std::string::npos) path.replace(rk, 6, "0");
+        save_weights(path, spec, pd.data());
       }
     } catch (const Error& e) {
       std::fprintf(stderr, "%s\n", e.what());

@@ -14,7 +14,7 @@
 namespace mcc {
 
 // Collective interface of the data-parallel driver.  Implementations:
-// LocalComm (no collectives: cnn_hip, or cnn_dist with MCC_AB=local_comm) and
+// LocalComm (no collectives: cnn_hip, or cnn_dist --comm local), HostComm (host_comm.h: several ranks on one GPU) and
 // RcclComm (cnn_dist.cpp, any world size including 1).  Every collective is
 // enqueued on the given stream; the host blocks only in wait() and barrier(),
 // which RcclComm bounds with the collective watchdog (watchdog.h).

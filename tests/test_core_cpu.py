@@ -251,3 +251,19 @@ def test_watchdog_policy():
         subprocess.run(["make", "-C", root, "build/bin/test_watchdog"], check=True, capture_output=True)
     r = subprocess.run([binp], capture_output=True, text=True, timeout=60)
     assert r.returncode == 0 and "watchdog ok" in r.stdout, r.stderr
+
+
+def test_native_bootstrap_and_host_collectives():
+    """TCP rendezvous of cnn_dist (csrc/apps/bootstrap.cpp) serving 4 forked
+    processes, both of its timeout branches, and the shared-memory
+    collectives of `cnn_dist --comm host` (csrc/apps/shm_group.cpp): bit-equal
+    sums on every rank in fixed rank order, max with NaN, broadcast, a dead
+    peer / a poisoned group / a rank that never attaches -- as a native CPU
+    test binary (csrc/tests/test_comm.cpp)."""
+    import subprocess
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    binp = os.path.join(root, "build", "bin", "test_comm")
+    subprocess.run(["make", "-C", root, "build/bin/test_comm"], check=True, capture_output=True)
+    r = subprocess.run([binp], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and "comm ok" in r.stdout, r.stdout + r.stderr

@@ -7,7 +7,7 @@ trained weights must be BIT-equal to the collective-free path.
   * Python: GpuTrainer under a world-1 "nccl" process group (bench.py's N=1
     path) vs no process group.
   * Native: cnn_dist with its RcclComm (hipGraph replay, eager, --profile)
-    vs MCC_AB=local_comm.
+    vs --comm local.
 """
 
 import json
@@ -106,7 +106,7 @@ def test_cnn_dist_rccl_world1_bit_equal(idx_files, tmp_path):
     assert js_e["comm"] == "rccl" and js_e["hipgraph"] is False
     js_p, p_p = _cnn_dist(idx_files, str(tmp_path / "p.w"), ["--profile"])
     assert js_p["comm"] == "rccl" and "phase_ms" in js_p
-    js_l, p_l = _cnn_dist(idx_files, str(tmp_path / "l.w"), [], {"MCC_AB": "local_comm"})
+    js_l, p_l = _cnn_dist(idx_files, str(tmp_path / "l.w"), ["--comm", "local"])
     assert js_l["comm"] == "local" and js_l["hipgraph"] is True
     np.testing.assert_array_equal(p_g, p_l)  # RCCL world-1 == no collectives
     np.testing.assert_array_equal(p_g, p_e)  # graph replay == eager
