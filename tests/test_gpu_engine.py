@@ -273,14 +273,14 @@ def test_vgg11_step_runs(cuda):
 
 @pytest.mark.gpu
 def test_bench_batch_step_matches_small_batches(cuda):
-    """bench.py's per-GPU batch (65,536, plus a ragged tail): the persistent
+    """bench.py's per-GPU batch (131,072, plus a ragged tail): the persistent
     kernels' many-group loops and 32-bit activation offsets at full size must
     give the same logits and summed gradients as 1,024-image chunks through
     the small-batch path (which test_step_matches_torch pins to PyTorch).
     A PyTorch reference at this size would spend minutes in MIOpen's first
     backward-convolution search on a fresh box."""
     spec = mcc.make_model("lenet5")
-    B, b = 65536 + 37, 1024
+    B, b = 131072 + 37, 2048
     imgs, labels = mcc.synth_dataset(B, 1, 28, 28, 10, seed=21)
     params = mcc.init_params(spec, seed=4).astype(np.float32)
     d_img = torch.from_numpy(imgs).to(cuda)
@@ -317,6 +317,48 @@ def test_bench_batch_step_matches_small_batches(cuda):
         for off, n, what in ((L["w_off"], L["nweights"], "W"), (L["b_off"], L["nbiases"], "b")):
             err = _relerr(grads[off : off + n], ref_grads[off : off + n])
             assert err < 2e-2, f"layer {L['kind']} {what} grad rel err {err:.3e}"
+
+
+@pytest.mark.gpu
+def test_vgg11_bench_batch_matches_small_batches(cuda):
+    """VGG-11 at bench.py's default per-GPU batch (640: 95.7 % of the 32-bit
+    activation-index bound) vs 64-image chunks: logits and every layer's
+    summed weight / bias gradient."""
+    spec = mcc.make_model("vgg11")
+    B, b = 640, 64
+    imgs, labels = mcc.synth_dataset(B, 3, 224, 224, 1000, seed=5)
+    params = mcc.init_params(spec, seed=2, mode="fast").astype(np.float32)
+    d_img = torch.from_numpy(imgs).to(cuda)
+    d_lab = torch.from_numpy(labels).to(cuda)
+    s = torch.cuda.current_stream().cuda_stream
+    big = mcc.GpuNet(spec, "bf16", B)
+    big.set_params(params)
+    big.forward(d_img.data_ptr(), 0, B, s)
+    big.loss(d_lab.data_ptr(), 0, 1.0 / B, True, s)
+    big.backward_all(s)
+    torch.cuda.synchronize()
+    logits, grads = big.get_logits(B), big.get_grads()
+    del big
+    torch.cuda.empty_cache()
+    small = mcc.GpuNet(spec, "bf16", b)
+    small.set_params(params)
+    ref_logits = np.empty_like(logits)
+    ref_grads = np.zeros_like(grads, dtype=np.float64)
+    for i in range(0, B, b):
+        idx = torch.arange(i, i + b, device=cuda, dtype=torch.int32)
+        small.forward(d_img.data_ptr(), idx.data_ptr(), b, s)
+        small.loss(d_lab.data_ptr(), idx.data_ptr(), 1.0 / B, True, s)
+        small.backward_all(s)
+        torch.cuda.synchronize()
+        ref_logits[i : i + b] = small.get_logits(b)
+        ref_grads += small.get_grads()
+    assert _relerr(logits, ref_logits) < 1e-2
+    for L in spec.layers():
+        if L["nweights"] == 0:
+            continue
+        for off, n, what in ((L["w_off"], L["nweights"], "W"), (L["b_off"], L["nbiases"], "b")):
+            err = _relerr(grads[off : off + n], ref_grads[off : off + n])
+            assert err < 2e-2, f"layer {L['kind']} C={L['C']} {what} grad rel err {err:.3e}"
 
 
 @pytest.mark.gpu
@@ -377,6 +419,10 @@ _BIG_SPECS = {
              "conv 32 k3 s1 p1 relu; pool 2; fc 64 relu; fc 10 softmax",
     "big80": "input 3 80 80; conv 64 k3 s1 p1 relu; pool 2; conv 64 k3 s1 p1 relu; "
              "conv 128 k3 s1 p1 relu; pool 2; fc 32 relu; fc 10 softmax",
+    # VGG-shaped at 224^2 with VGG-11's layer widths but fewer layers: the u8
+    # 64-channel first layer, the 128 / 256 / 512-channel large-image kernels
+    "vgg224": "input 3 224 224; conv 64 k3 s1 p1 relu; pool 2; conv 128 k3 s1 p1 relu; pool 2; "
+              "conv 256 k3 s1 p1 relu; pool 2; conv 512 k3 s1 p1 relu; pool 2; fc 64 relu; fc 10 softmax",
 }
 
 
@@ -392,6 +438,15 @@ def _oracle_bf16(spec, params, imgs, labels, round_input):
     logits = ref(x)
     F.cross_entropy(logits, torch.from_numpy(labels.astype(np.int64))).backward()
     return logits.detach().numpy(), ref.flat_grads().numpy()
+
+
+def _per_channel_errs(g, r, C, floor_frac=1e-2):
+    """per-channel relative L2 errors (see _per_channel_err)"""
+    g = g.reshape(C, -1).astype(np.float64)
+    r = r.reshape(C, -1).astype(np.float64)
+    rn = np.linalg.norm(r, axis=1)
+    floor = floor_frac * np.linalg.norm(r) / np.sqrt(C)
+    return np.linalg.norm(g - r, axis=1) / np.maximum(rn, max(floor, 1e-30))
 
 
 def _per_channel_err(g, r, C, floor_frac=1e-2):
@@ -413,6 +468,14 @@ def _per_channel_err(g, r, C, floor_frac=1e-2):
 # 2.3e-2 / 3.6e-2, b 3.2e-2 / 2.0e-2 / 2.3e-2 / 5.1e-2 / 5.3e-2; a wrong
 # channel is O(1) (test_per_channel_check_flags_one_bad_channel).
 PER_CHANNEL_TOL = {"W": 6e-2, "b": 8e-2, "logit": 1e-2}
+# vgg224 (224^2 images, 28^2..224^2-pixel sums per channel): a few channels
+# per layer sit at 0.1-0.25 while the median is 1e-3..1e-2 (measured on
+# MI355X, tools/probes/perchannel_diag.py; the fp32 engine on the same spec is
+# <= 6e-6 per channel except conv1 W 3e-3) -- a handful of pooling / ReLU
+# decisions taken on the other side of a bf16 rounding.  Bounded by the
+# distribution: median and 99th percentile tight, the max loose but below
+# the O(1) error of a wrong channel.
+PER_CHANNEL_DIST_TOL = {"vgg224": dict(median=2.5e-2, p99=1.2e-1, W=0.3, b=0.4)}
 
 
 def test_per_channel_check_flags_one_bad_channel():
@@ -429,7 +492,7 @@ def test_per_channel_check_flags_one_bad_channel():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("model", ["lenet5", "cifar3", "ref", "big96", "big80"])
+@pytest.mark.parametrize("model", ["lenet5", "cifar3", "ref", "big96", "big80", "vgg224"])
 def test_bf16_grads_per_channel_vs_rounded_oracle(cuda, model):
     """bf16 engine step vs an fp64 oracle fed the same bf16-rounded weights,
     activations and inter-layer gradients, checked PER OUTPUT CHANNEL (weight
@@ -437,7 +500,7 @@ def test_bf16_grads_per_channel_vs_rounded_oracle(cuda, model):
     which one wrong channel of 64 could pass."""
     spec = mcc.parse_model_spec(_BIG_SPECS[model], model) if model in _BIG_SPECS else mcc.make_model(model)
     C, H, W = spec.input_shape()
-    B = {"big96": 6, "big80": 5}.get(model, 96)
+    B = {"big96": 6, "big80": 5, "vgg224": 2}.get(model, 96)
     imgs, labels = mcc.synth_dataset(B, C, H, W, spec.num_classes(), seed=3)
     params = mcc.init_params(spec, seed=1).astype(np.float32)
     net = mcc.GpuNet(spec, "bf16", B)
@@ -465,7 +528,16 @@ def test_bf16_grads_per_channel_vs_rounded_oracle(cuda, model):
             e, c = _per_channel_err(grads[off : off + n], ref_grads[off : off + n], L["C"],
                                     floor_frac=0.3 if what == "b" else 1e-2)
             report.append(f"  {L['kind']} C={L['C']} {what}: max per-channel {e:.2e} (channel {c})")
-            if e > PER_CHANNEL_TOL[what]:
+            dist = PER_CHANNEL_DIST_TOL.get(model)
+            if dist is None:
+                if e > PER_CHANNEL_TOL[what]:
+                    bad.append(report[-1])
+                continue
+            es = _per_channel_errs(grads[off : off + n], ref_grads[off : off + n], L["C"],
+                                   floor_frac=0.3 if what == "b" else 1e-2)
+            med, p99 = np.quantile(es, [0.5, 0.99])
+            report[-1] += f", p99 {p99:.2e}, median {med:.2e}"
+            if e > dist[what] or p99 > dist["p99"] or med > dist["median"]:
                 bad.append(report[-1])
     print("\n".join(report + [plan]))
     assert lerr < PER_CHANNEL_TOL["logit"], report[0]

@@ -2,8 +2,10 @@
 # One GPU-box job, parametrised by environment (run through gpurun):
 #   OUT=name           results under gpurun_out/<name>/
 #   TESTS="args"       pytest arguments (-m gpu is added); empty: skip
-#   BENCH="a;b;..."    bench.py argument sets, one JSON line each; empty: skip
+#   BENCH="a;b;..."    bench.py argument sets, one JSON line each (leading NAME=value
+#                      words are that run's environment, e.g. "MCC_AB=no_lenet --steps 20")
 #   PROF="args"        bench.py arguments for a rocprofv3 kernel-trace + stats run
+#   PROF_ENV="A=b"     environment of the PROF run
 #   PMC="c1 c2;..."    PMC passes (one rocprofv3 run each) over PROF's bench args
 #   PRE="cmd"          a command run first (e.g. a probe binary), time-limited
 # Every GPU step has its own time limit; the first failure ends the job.
@@ -29,14 +31,17 @@ if [ -n "$BENCH" ]; then
   i=0
   for a in "${SETS[@]}"; do
     i=$((i+1))
-    timeout -k 10 200 python bench.py $a > $O/bench_$i.json 2> $O/bench_$i.err || { echo "bench '$a' failed"; tail -20 $O/bench_$i.err; exit 1; }
+    # leading NAME=value words of an argument set are environment for that run
+    envs=(); args=()
+    for w in $a; do if [ ${#args[@]} -eq 0 ] && [[ "$w" == *=* ]]; then envs+=("$w"); else args+=("$w"); fi; done
+    (for e in "${envs[@]}"; do export "$e"; done; timeout -k 10 200 python bench.py "${args[@]}") > $O/bench_$i.json 2> $O/bench_$i.err || { echo "bench '$a' failed"; tail -20 $O/bench_$i.err; exit 1; }
     echo "[$a] $(grep -h '^{' $O/bench_$i.json | python3 -c "import json,sys;d=json.loads(sys.stdin.read());print(d['value'], d['ms_per_step'], d['config'].get('train_loss_last'))")"
   done
 fi
 if [ -n "$PROF" ]; then
-  (cd /tmp && timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv -- python3 $R/bench.py $PROF > $O/prof.log 2>&1) \
+  (cd /tmp && { [ -z "$PROF_ENV" ] || export $PROF_ENV; } && timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv -- python3 $R/bench.py $PROF > $O/prof.log 2>&1) \
     || { echo "prof failed"; tail -20 $O/prof.log; exit 1; }
-  python3 $R/tools/prof_summary.py $O/prof/run_kernel_stats.csv > $O/kernel_summary.txt 2>/dev/null || true
+  python3 $R/tools/prof_summary.py $O/prof > $O/kernel_summary.txt 2>/dev/null || true
   f=$(ls $O/prof/*kernel_trace.csv 2>/dev/null | head -1)
   [ -n "$f" ] && python3 $R/tools/step_timeline.py $f > $O/step_timeline.txt 2>/dev/null
   tail -30 $O/step_timeline.txt 2>/dev/null
