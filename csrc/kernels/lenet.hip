@@ -38,7 +38,6 @@
 //   (planar, argmax position 0..3 or 4 = ReLU-inactive), Y2 [B][25][16] bf16
 //   (the FC input, NHWC flatten), A2 [B][25][16] u8.
 #include "kernels.h"
-#include "mcc/ab.h"
 #include "mfma.h"
 
 #include <algorithm>
@@ -673,324 +672,6 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1)))
   for (int i = 0; i < 4; ++i) slab[kSlabW2 + i * 64 + lane] = acc1[i];
 }
 
-// ---------------------------------------------------------------------------
-// Two-wave variant: a 128-thread workgroup shares one image's LDS (the same
-// 39,936-B layout), so 4 workgroups = 8 waves per CU (2 per SIMD) instead of
-// 4 single-wave ones -- the one-wave kernel is latency-bound (its wave is
-// active 45 % of the time, waiting on LDS data and MFMA dependencies with no
-// second wave on the SIMD to switch to).  Work split per image (MFMAs):
-//   wave 0: conv2 dX tiles 0..3 (60) + conv2 dW column tiles 0..4 (20)
-//   wave 1: conv2 dX tiles 4..6 (45) + conv2 dW column tiles 5..12 (32)
-//   both:   conv1 dW output rows 0..14 / 15..29 (15 each, after a barrier:
-//           they read dZ1 rows written by the other wave)
-// Staging: wave 0 unpools dZ2 and copies Y1, wave 1 builds the shifted X0
-// copies.  Three workgroup barriers per image (staged / dZ1 complete / all
-// reads done before the next staging); the per-workgroup slab is combined
-// through LDS at the end, so the reduce kernel is unchanged.
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ void wg_lds_sync() {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-}
-
-__global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2, 2)))
-lenet_bwd2_kernel(LenetBwdParams p) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int wv = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  const int n16 = lane & 15, g = lane >> 4;
-  const int tq = (lane >> 2) & 3, tp = lane & 3;
-
-  {
-    const u32x4 z = {0u, 0u, 0u, 0u};
-    for (int i = threadIdx.x * 16; i < kBLds; i += 128 * 16) *reinterpret_cast<u32x4*>(smem + i) = z;
-  }
-  wg_lds_sync();
-  if (wv == 0) {
-    const uint32_t one2 = 0x3f803f80u;
-    if (lane < 4) *reinterpret_cast<uint32_t*>(smem + kBOne2 + 4 * lane) = one2;
-    for (int i = lane; i < 30 * 16; i += 64)
-      *reinterpret_cast<uint32_t*>(smem + kBOne1 + (i >> 4) * 80 + (i & 15) * 4) = one2;
-  }
-
-  bf16x8 wdx[15];
-  {
-    const int ci = n16 >> 1, j = n16 & 1;
-#pragma unroll
-    for (int c = 0; c < 15; ++c) {
-      const int t = 2 * c + (g >> 1), u = t / 5, v = t % 5;
-      const int kh = 4 + j - u, kw = 4 - v;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const int co = 8 * (g & 1) + e;
-        float w = 0.f;
-        if (n16 < 12 && kh >= 0 && kh < 5) w = p.w2[((co * 6 + ci) * 5 + kh) * 5 + kw];
-        wdx[c][e] = (bf16)w;
-      }
-    }
-  }
-
-  const int hxa = kBDz2 + n16 * 32 + 16 * (g & 1) + (g >> 1) * 32;
-  const int hxb = kBDz2 + n16 * 32 + 16 * (g & 1) + (g >> 1) * 512;
-  int a1b;
-  {
-    const int m = n16 < 12 ? n16 : 0, co = m % 6, s = m / 6;
-    a1b = kBDz1 + co * kBDz1Plane + (2 - 2 * s) * 64 + 16 * g;
-  }
-  int b1b;
-  if (n16 == 15) b1b = kBOne1 + 16 * g;
-  else {
-    const int kh = n16 / 5, kw = n16 % 5, c = kw & 3;
-    b1b = kBXs + c * kBxCopy + (kh * 40 + 8 * g + kw - c) * 2;
-  }
-
-  // conv2 dW column tiles: wave 0 [0, 6), wave 1 [6, 13) -> acc2[t - first]
-  f32x4 acc2[7];
-#pragma unroll
-  for (int t = 0; t < 7; ++t) acc2[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-  f32x4 acc1 = {0.f, 0.f, 0.f, 0.f};
-
-  const int sk = lane & 7, srow = lane >> 3;
-  const int zq = lane >> 1, zh = lane & 1;
-  const int zqy = (zq * 205) >> 10, zqx = zq - 5 * zqy;
-  const int zbase = kBDz2 + ((2 * zqy + 4) * 20 + 2 * zqx + 4) * 32 + 16 * zh;
-  const int dxci = n16 < 12 ? n16 >> 1 : 5, dxj = n16 & 1;
-  const int t0 = wv == 0 ? 0 : 4;  // this wave's first conv2 dX tile
-
-  // Next image's global data, one register set whose meaning depends on the
-  // wave (the compiler cannot see that the waves' branches are exclusive):
-  //   wave 0: pf[0] = dY2 (lanes < 50), pf[1].xy = conv2 codes, pf[2] = u8 X0 words
-  //   wave 1: pf[0..3] = Y1 (196 x 16 B)
-  u32x4 pf[4];
-  uint32_t a1n[4];  // conv1 codes of this wave's dX tiles (loaded one phase ahead)
-  WaveIdx widx;
-  if (wv == 0) widx.load(p.idx, blockIdx.x, (int)gridDim.x, p.B, 0);
-  auto load_img = [&](int k) {
-    const int img = blockIdx.x + k * (int)gridDim.x;
-    if (wv == 0) {
-      if (lane < 50) {
-        pf[0] = *reinterpret_cast<const u32x4*>(static_cast<const bf16*>(p.dy2) + (size_t)img * kY2Elems + zq * 16 + 8 * zh);
-        const u32x2 c2 = *reinterpret_cast<const u32x2*>(p.a2 + (size_t)img * kY2Elems + zq * 16 + 8 * zh);
-        pf[1] = u32x4{c2.x, c2.y, 0u, 0u};
-      }
-      if ((k & 63) == 0 && k > 0) widx.load(p.idx, blockIdx.x, (int)gridDim.x, p.B, k);
-      const uint8_t* xin = p.x + (size_t)widx.get(k) * kImgPix;
-#pragma unroll
-      for (int it = 0; it < 4; ++it) {
-        const int yy = it * 8 + srow;
-        pf[2][it] = (yy < 28 && sk < 7) ? *reinterpret_cast<const uint32_t*>(xin + yy * 28 + sk * 4) : 0u;
-      }
-    } else {
-      const bf16* y1g = static_cast<const bf16*>(p.y1) + (size_t)img * kY1Elems;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int px = min(lane + 64 * r, 195);
-        pf[r] = *reinterpret_cast<const u32x4*>(y1g + px * 8);
-      }
-    }
-  };
-  auto load_codes = [&](int img) {
-    const uint8_t* a1g = p.a1 + (size_t)img * kA1Bytes + dxci * 224 + 4 * g;
-#pragma unroll
-    for (int t = 0; t < 4; ++t) a1n[t] = *reinterpret_cast<const uint32_t*>(a1g + (2 * min(t0 + t, 6) + dxj) * 16);
-  };
-  if ((int)blockIdx.x < p.B) {
-    load_img(0);
-    load_codes(blockIdx.x);
-  }
-
-  // conv2 dX for tiles [T0, T1): a ring of 15 fragments -- tile T uses slots
-  // (5T + c) % 15; the next tile's chunks 10..14 land in the slots of this
-  // tile's chunks 0..4 right after those MFMAs have issued.
-  auto dx_tiles = [&]<int T0, int T1>() {
-    bf16x8 fr[15];
-#pragma unroll
-    for (int c = 0; c < 15; ++c)
-      fr[(5 * T0 + c) % 15] = *reinterpret_cast<const bf16x8*>(smem + (dxwrap(c) ? hxb : hxa) + dxoff(c) + T0 * 1280);
-#pragma unroll
-    for (int T = T0; T < T1; ++T) {
-      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int c = 0; c < 5; ++c) acc = mma(acc, fr[(5 * T + c) % 15], wdx[c]);
-      __builtin_amdgcn_sched_barrier(0);
-      if (T + 1 < T1) {
-#pragma unroll
-        for (int c = 10; c < 15; ++c)
-          fr[(5 * (T + 1) + c) % 15] =
-              *reinterpret_cast<const bf16x8*>(smem + (dxwrap(c) ? hxb : hxa) + dxoff(c) + (T + 1) * 1280);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int c = 5; c < 15; ++c) acc = mma(acc, fr[(5 * T + c) % 15], wdx[c]);
-      __builtin_amdgcn_sched_barrier(0);
-      uint32_t top[4], bot[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const uint32_t code = (a1n[T - T0] >> (8 * i)) & 0xffu;
-        const uint64_t h = code < 4u ? (uint64_t)bf16_bits(acc[i]) : 0ull;
-        const uint64_t w = h << (16u * (code & 3u));
-        top[i] = (uint32_t)w;
-        bot[i] = (uint32_t)(w >> 32);
-      }
-      if (n16 < 12) {
-        char* d = smem + kBDz1 + dxci * kBDz1Plane + (4 * T + 2 * dxj + 2) * 64 + 16 * g;
-        *reinterpret_cast<u32x4*>(d) = u32x4{top[0], top[1], top[2], top[3]};
-        *reinterpret_cast<u32x4*>(d + 64) = u32x4{bot[0], bot[1], bot[2], bot[3]};
-      }
-    }
-  };
-  // conv2 dW for column tiles [N0, N1)
-  auto dw2_tiles = [&]<int N0, int N1>() {
-    constexpr int NT = N1 - N0;
-    bf16x8 af[2], bfr[2][NT];
-    // recomputed per image (opaque lane id): hoisted out of the image loop,
-    // the 4 chunks' operand bases would pin ~30 VGPRs for the whole kernel
-    int ln = lane;
-    asm volatile("" : "+v"(ln));
-    const int lg = ln >> 4, ltq = (ln >> 2) & 3, ltp = ln & 3;
-    auto load_chunk = [&](int c, int buf) {
-      const int tq = ltq, tp = ltp;
-      const int z0 = 32 * c + 8 * lg + tq, z1 = z0 + 4;
-      const bool ok0 = z0 < 100, ok1 = z1 < 100;
-      const int zy0 = ok0 ? z0 / 10 : 0, zx0 = ok0 ? z0 % 10 : 0;
-      const int zy1 = ok1 ? z1 / 10 : 0, zx1 = ok1 ? z1 % 10 : 0;
-      const int a0 = ok0 ? kBDz2 + ((zy0 + 4) * 20 + zx0 + 4) * 32 + 8 * tp : kBDz2 + 8 * tp;
-      const int a1 = ok1 ? kBDz2 + ((zy1 + 4) * 20 + zx1 + 4) * 32 + 8 * tp : kBDz2 + 8 * tp;
-      af[buf] = tr8(smem + a0, smem + a1);
-      const int yb0 = kBY1 + (zy0 * 14 + zx0) * 16 + 8 * (tp & 1);
-      const int yb1 = kBY1 + (zy1 * 14 + zx1) * 16 + 8 * (tp & 1);
-#pragma unroll
-      for (int t = N0; t < N1; ++t) {
-        const int o = tapoff2(2 * t);
-        int p0, p1;
-        if (t == 12) {
-          p0 = (tp >> 1) ? kBOne2 + 8 * (tp & 1) - tapoff2(24) : yb0;
-          p1 = (tp >> 1) ? kBOne2 + 8 * (tp & 1) - tapoff2(24) : yb1;
-        } else if ((2 * t) % 5 == 4) {
-          p0 = yb0 + (tp >> 1) * 160;
-          p1 = yb1 + (tp >> 1) * 160;
-        } else {
-          p0 = yb0 + (tp >> 1) * 16;
-          p1 = yb1 + (tp >> 1) * 16;
-        }
-        bfr[buf][t - N0] = tr8(smem + p0 + o, smem + p1 + o);
-      }
-    };
-    load_chunk(0, 0);
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      if (c + 1 < 4) load_chunk(c + 1, (c + 1) & 1);
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int t = 0; t < NT; ++t) acc2[t] = mma(acc2[t], af[c & 1], bfr[c & 1][t]);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  };
-  // conv1 dW for output rows [Z0, Z1)
-  auto dw1_rows = [&]<int Z0, int Z1>() {
-    constexpr int D = 4;
-    bf16x8 a[D], b[D];
-#pragma unroll
-    for (int k = 0; k < D; ++k) {
-      a[k] = *reinterpret_cast<const bf16x8*>(smem + a1b + (Z0 + k) * 64);
-      b[k] = lds8(smem + b1b + (Z0 + k) * 80);
-    }
-#pragma unroll
-    for (int zy = Z0; zy < Z1; ++zy) {
-      const int k = (zy - Z0) % D;
-      const bf16x8 ca = a[k], cb = b[k];
-      if (zy + D < Z1) {
-        a[k] = *reinterpret_cast<const bf16x8*>(smem + a1b + (zy + D) * 64);
-        b[k] = lds8(smem + b1b + (zy + D) * 80);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-      acc1 = mma(acc1, ca, cb);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  };
-
-  for (int img = blockIdx.x, kimg = 0; img < p.B; img += (int)gridDim.x, ++kimg) {
-    wg_lds_sync();  // previous image: every LDS read of both waves done
-    if (wv == 0) {
-      if (lane < 50) {
-        const u32x4 z = {0u, 0u, 0u, 0u};
-        *reinterpret_cast<u32x4*>(smem + zbase) = z;
-        *reinterpret_cast<u32x4*>(smem + zbase + 32) = z;
-        *reinterpret_cast<u32x4*>(smem + zbase + 640) = z;
-        *reinterpret_cast<u32x4*>(smem + zbase + 672) = z;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const uint32_t code = (pf[1][i >> 2] >> (8 * (i & 3))) & 0xffu;
-          const uint32_t v = (pf[0][i >> 1] >> (16 * (i & 1))) & 0xffffu;
-          const int off = ((code & 2u) ? 640 : 0) + ((code & 1u) ? 32 : 0);
-          *reinterpret_cast<unsigned short*>(smem + zbase + off + 2 * i) = (unsigned short)(code < 4u ? v : 0u);
-        }
-      }
-#pragma unroll
-      for (int it = 0; it < 4; ++it) {
-        const int yy = it * 8 + srow;
-        uint32_t lo, hi;
-        u8x4_ints(pf[2][it], lo, hi);
-        const uint32_t phi = from_left(hi);
-        const uint32_t rlo = from_right(lo);
-        const uint32_t nlo = sk == 7 ? 0u : rlo;
-        if (yy < 28) {
-          char* d = smem + kBXs + ((yy + 2) * 40 + 4 * sk) * 2;
-          *reinterpret_cast<u32x2*>(d) = u32x2{phi, lo};
-          *reinterpret_cast<u32x2*>(d + kBxCopy) = u32x2{mid16(phi, lo), mid16(lo, hi)};
-          *reinterpret_cast<u32x2*>(d + 2 * kBxCopy) = u32x2{lo, hi};
-          *reinterpret_cast<u32x2*>(d + 3 * kBxCopy) = u32x2{mid16(lo, hi), mid16(hi, nlo)};
-        }
-      }
-    } else {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int px = lane + 64 * r;
-        if (px < 196) *reinterpret_cast<u32x4*>(smem + kBY1 + px * 16) = pf[r];
-      }
-    }
-    wg_lds_sync();  // staged
-    const bool more = img + (int)gridDim.x < p.B;
-    if (more) load_img(kimg + 1);
-    if (wv == 0) {
-      dx_tiles.template operator()<0, 4>();
-      if (more) load_codes(img + (int)gridDim.x);
-      dw2_tiles.template operator()<0, 6>();
-    } else {
-      dx_tiles.template operator()<4, 7>();
-      if (more) load_codes(img + (int)gridDim.x);
-      dw2_tiles.template operator()<6, 13>();
-    }
-    wg_lds_sync();  // dZ1 complete
-    if (wv == 0) dw1_rows.template operator()<0, 10>();
-    else dw1_rows.template operator()<10, 30>();
-  }
-
-  // ---- per-workgroup slab: wave 1's conv1 dW partial joins wave 0's via LDS ----
-  wg_lds_sync();
-  float* red = reinterpret_cast<float*>(smem);
-  if (wv == 1) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) red[i * 64 + lane] = acc1[i];
-  }
-  wg_lds_sync();
-  float* slab = p.slab + (size_t)blockIdx.x * kSlab;
-  if (wv == 0) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) slab[kSlabW2 + i * 64 + lane] = acc1[i] + red[i * 64 + lane];
-#pragma unroll
-    for (int t = 0; t < 6; ++t)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) slab[(t * 4 + i) * 64 + lane] = acc2[t][i];
-  } else {
-#pragma unroll
-    for (int t = 0; t < 7; ++t)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) slab[((t + 6) * 4 + i) * 64 + lane] = acc2[t][i];
-  }
-}
-
 // Fixed-order sum of the per-wave slabs, mapped to the canonical gradients.
 // Block = 1024 threads over 64 slab positions: wave w sums slabs w, w+16, ...
 // of position blk*64 + lane (16 loads in flight per lane), then wave 0 adds
@@ -1046,8 +727,7 @@ void lenet_forward(const LenetFwdParams& p, hipStream_t s) {
 void lenet_backward(const LenetBwdParams& p, hipStream_t s) {
   if (p.B <= 0) return;
   const int grid = lenet_bwd_grid();
-  if (ab_flag("lenet_bwd2")) hipLaunchKernelGGL(lenet_bwd2_kernel, dim3(grid), dim3(128), kBLds, s, p);
-  else hipLaunchKernelGGL(lenet_bwd_kernel, dim3(grid), dim3(64), kBLds, s, p);
+  hipLaunchKernelGGL(lenet_bwd_kernel, dim3(grid), dim3(64), kBLds, s, p);
   hipLaunchKernelGGL(lenet_bwd_reduce_kernel, dim3(kSlab / 64), dim3(64 * kRedWaves), 0, s, p, grid);
 }
 

@@ -4,9 +4,10 @@
 #   TESTS="args"       pytest arguments (-m gpu is added); empty: skip
 #   BENCH="a;b;..."    bench.py argument sets, one JSON line each (leading NAME=value
 #                      words are that run's environment, e.g. "MCC_AB=no_lenet --steps 20")
-#   PROF="args"        bench.py arguments for a rocprofv3 kernel-trace + stats run
+#   PROF="a;b;..."     bench.py argument sets, one rocprofv3 kernel-trace + stats run each
 #   PROF_ENV="A=b"     environment of the PROF run
 #   PMC="c1 c2;..."    PMC passes (one rocprofv3 run each) over PROF's bench args
+#   PMC_ENV="A=b"      environment of the PMC runs
 #   PRE="cmd"          a command run first (e.g. a probe binary), time-limited
 # Every GPU step has its own time limit; the first failure ends the job.
 set -o pipefail
@@ -39,19 +40,26 @@ if [ -n "$BENCH" ]; then
   done
 fi
 if [ -n "$PROF" ]; then
-  (cd /tmp && { [ -z "$PROF_ENV" ] || export $PROF_ENV; } && timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv -- python3 $R/bench.py $PROF > $O/prof.log 2>&1) \
-    || { echo "prof failed"; tail -20 $O/prof.log; exit 1; }
-  python3 $R/tools/prof_summary.py $O/prof > $O/kernel_summary.txt 2>/dev/null || true
-  f=$(ls $O/prof/*kernel_trace.csv 2>/dev/null | head -1)
-  [ -n "$f" ] && python3 $R/tools/step_timeline.py $f > $O/step_timeline.txt 2>/dev/null
-  tail -30 $O/step_timeline.txt 2>/dev/null
+  # ";"-separated argument sets: prof (first), prof2, prof3, ...
+  IFS=';' read -ra PSETS <<< "$PROF"
+  j=0
+  for a in "${PSETS[@]}"; do
+    j=$((j+1)); d=prof; [ $j -gt 1 ] && d=prof$j
+    (cd /tmp && { [ -z "$PROF_ENV" ] || export $PROF_ENV; } && timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $O/$d -o run --output-format csv -- python3 $R/bench.py $a > $O/$d.log 2>&1) \
+      || { echo "prof '$a' failed"; tail -20 $O/$d.log; exit 1; }
+    python3 $R/tools/prof_summary.py $O/$d > $O/kernel_summary_$j.txt 2>/dev/null || true
+    f=$(ls $O/$d/*kernel_trace.csv 2>/dev/null | head -1)
+    [ -n "$f" ] && python3 $R/tools/step_timeline.py $f > $O/step_timeline_$j.txt 2>/dev/null
+    echo "== prof [$a]"; tail -${PROF_LINES:-30} $O/step_timeline_$j.txt 2>/dev/null
+  done
+  PROF=${PSETS[0]}
 fi
 if [ -n "$PMC" ]; then
   IFS=';' read -ra PS <<< "$PMC"
   i=0
   for c in "${PS[@]}"; do
     i=$((i+1))
-    (cd /tmp && timeout -s KILL 120 rocprofv3 --kernel-trace --pmc $c -d $O/pmc$i -o run --output-format csv -- python3 $R/bench.py ${PROF:---steps 3 --warmup 1} --no-dist > $O/pmc$i.log 2>&1) \
+    (cd /tmp && { [ -z "$PMC_ENV" ] || export $PMC_ENV; } && timeout -s KILL 120 rocprofv3 --kernel-trace --pmc $c -d $O/pmc$i -o run --output-format csv -- python3 $R/bench.py ${PROF:---steps 3 --warmup 1} --no-dist > $O/pmc$i.log 2>&1) \
       || { echo "pmc $i failed"; tail -5 $O/pmc$i.log; exit 1; }
     python3 $R/tools/pmc_summary.py $O/pmc$i/run_counter_collection.csv > $O/pmc$i.txt
   done
