@@ -407,6 +407,31 @@ PYBIND11_MODULE(_C, m) {
         py::arg("B"), py::arg("x"), py::arg("idx"), py::arg("w2"), py::arg("dy2"), py::arg("a2"), py::arg("y1"),
         py::arg("a1"), py::arg("slab"), py::arg("gw1"), py::arg("gb1"), py::arg("gw2"), py::arg("gb2"),
         py::arg("stream") = 0);
+  // reference-model conv block (refnet.hip): raw launches for the kernel unit tests
+  k.def("ref_forward",
+        [](int B, uintptr_t x, uintptr_t idx, uintptr_t w1, uintptr_t b1, uintptr_t w2, uintptr_t b2, uintptr_t y2,
+           uintptr_t s) {
+          gpu::RefFwdParams p;
+          p.B = B; p.x = reinterpret_cast<const uint8_t*>(x); p.idx = reinterpret_cast<const int32_t*>(idx);
+          p.w1 = reinterpret_cast<const float*>(w1); p.b1 = reinterpret_cast<const float*>(b1);
+          p.w2 = reinterpret_cast<const float*>(w2); p.b2 = reinterpret_cast<const float*>(b2);
+          p.y2 = reinterpret_cast<void*>(y2);
+          gpu::ref_forward(p, stream_of(s));
+        });
+  k.def("ref_backward",
+        [](int B, uintptr_t x, uintptr_t idx, uintptr_t w1, uintptr_t b1, uintptr_t w2, uintptr_t y2, uintptr_t dy2,
+           uintptr_t slab, uintptr_t gw1, uintptr_t gb1, uintptr_t gw2, uintptr_t gb2, uintptr_t s) {
+          gpu::RefBwdParams p;
+          p.B = B; p.x = reinterpret_cast<const uint8_t*>(x); p.idx = reinterpret_cast<const int32_t*>(idx);
+          p.w1 = reinterpret_cast<const float*>(w1); p.b1 = reinterpret_cast<const float*>(b1);
+          p.w2 = reinterpret_cast<const float*>(w2);
+          p.y2 = reinterpret_cast<const void*>(y2); p.dy2 = reinterpret_cast<const void*>(dy2);
+          p.slab = reinterpret_cast<float*>(slab);
+          p.gw1 = reinterpret_cast<float*>(gw1); p.gb1 = reinterpret_cast<float*>(gb1);
+          p.gw2 = reinterpret_cast<float*>(gw2); p.gb2 = reinterpret_cast<float*>(gb2);
+          gpu::ref_backward(p, stream_of(s));
+        });
+  k.def("ref_slab_bytes", &gpu::ref_slab_bytes);
   k.def("lenet_slab_bytes", &gpu::lenet_slab_bytes);
   // device minibatch sampler (rand() % N semantics, cnn.c:455) with the step
   // counter in device memory: graph-capturable (a replay draws fresh indices)

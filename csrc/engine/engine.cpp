@@ -370,6 +370,22 @@ void GpuNet::build() {
                b.inC == 6 && b.C == 16 && b.pad == 0;
     }
   }
+  // ---- reference-model conv block (refnet.hip): conv 1->16 and 16->32, 3x3
+  // stride 2 pad 1 ReLU on 28x28, fused forward and fused backward
+  // (recomputed conv1, sub-pixel conv2 dX).  MCC_AB=no_refblk: per-layer kernels.
+  {
+    refblk_ = false;
+    if (dtype_ == DType::BF16 && stages_.size() >= 3 && !ab_flag("no_refblk")) {
+      const Stage& a = *stages_[0];
+      const Stage& b = *stages_[1];
+      auto s2 = [](const Stage& x) {
+        return x.kind == Stage::CONV && x.act == gpu::ACT_RELU && !x.pooled && !x.generic && !x.big && x.stride == 2 &&
+               x.KS == 3 && x.pad == 1;
+      };
+      refblk_ = s2(a) && s2(b) && a.inC == 1 && a.inH == 28 && a.inW == 28 && a.C == 16 && b.inC == 16 &&
+                b.inH == 14 && b.C == 32 && stages_[2]->kind == Stage::FC;
+    }
+  }
 
   // ---- data gradient straight into dZ (no grad_xform pass) ----
   // A big stage whose input is a ReLU big conv writes that stage's dZ in its
@@ -583,6 +599,7 @@ void GpuNet::build() {
     scratch = std::max(scratch, (size_t)gpu::gemm_fwd_splitk(Bm, st.Nout, st.Kin) * Bm * ld * 4);
   }
   if (lenet_) scratch = std::max(scratch, gpu::lenet_slab_bytes());
+  if (refblk_) scratch = std::max(scratch, gpu::ref_slab_bytes());
   scratch_bytes_ = scratch;
   for (int pass = 0; pass < 2; ++pass) {
     arena_used_ = 0;
@@ -627,6 +644,7 @@ void GpuNet::build() {
 std::string GpuNet::plan() const {
   std::ostringstream os;
   if (lenet_) os << "[lenet block: stages 0+1 fused fwd (lenet_fwd) and bwd (lenet_bwd)]\n";
+  if (refblk_) os << "[ref block: stages 0+1 fused fwd (ref_fwd) and bwd (ref_bwd: recomputed conv1, sub-pixel dX)]\n";
   os << "GpuNet(" << spec_.name << ", " << dtype_name(dtype_) << ", max_batch=" << max_batch_
      << ", arena=" << (arena_bytes_ >> 20) << " MiB, " << (fused_pack_ ? "fused sgd+pack" : "sgd + pack table")
      << ")\n";
@@ -751,6 +769,16 @@ void GpuNet::forward(const uint8_t* images, const int32_t* idx, int B, hipStream
       f.w1 = params_ + st.w_off; f.b1 = params_ + st.b_off; f.w2 = params_ + s1.w_off; f.b2 = params_ + s1.b_off;
       f.y1 = st.act_buf; f.a1 = st.arg_buf; f.y2 = s1.act_buf; f.a2 = s1.arg_buf;
       gpu::lenet_forward(f, s);
+      continue;
+    }
+    if (refblk_ && si <= 1) {
+      if (si == 1) continue;  // produced with stage 0 (stage 0's own output is never stored)
+      const Stage& s1 = *stages_[1];
+      gpu::RefFwdParams f;
+      f.B = B; f.x = images; f.idx = idx;
+      f.w1 = params_ + st.w_off; f.b1 = params_ + st.b_off; f.w2 = params_ + s1.w_off; f.b2 = params_ + s1.b_off;
+      f.y2 = s1.act_buf;
+      gpu::ref_forward(f, s);
       continue;
     }
     if (st.kind == Stage::CONV && st.big && st.ig_fwd) {
@@ -906,6 +934,23 @@ void GpuNet::backward(int hi, int lo, hipStream_t s) {
       b.slab = scratch_;
       b.gw1 = grads_ + s0.w_off; b.gb1 = grads_ + s0.b_off; b.gw2 = grads_ + st.w_off; b.gb2 = grads_ + st.b_off;
       gpu::lenet_backward(b, s_main);
+      continue;
+    }
+    if (refblk_ && si <= 1) {
+      if (si == 0) continue;
+      if (forked) {
+        HIP_OK(hipEventRecord(join_ev_, wstream_));
+        HIP_OK(hipStreamWaitEvent(s_main, join_ev_, 0));
+        forked = false;
+      }
+      const Stage& s0 = *stages_[0];
+      gpu::RefBwdParams b;
+      b.B = B; b.x = images_; b.idx = idx_;
+      b.w1 = params_ + s0.w_off; b.b1 = params_ + s0.b_off; b.w2 = params_ + st.w_off;
+      b.y2 = st.act_buf; b.dy2 = st.grad_buf;
+      b.slab = scratch_;
+      b.gw1 = grads_ + s0.w_off; b.gb1 = grads_ + s0.b_off; b.gw2 = grads_ + st.w_off; b.gb2 = grads_ + st.b_off;
+      gpu::ref_backward(b, s_main);
       continue;
     }
     // Side stream for this stage's weight gradient when the two directions

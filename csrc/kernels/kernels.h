@@ -297,6 +297,31 @@ int lenet_a1_bytes();   // per image
 void lenet_forward(const LenetFwdParams& p, hipStream_t s);
 void lenet_backward(const LenetBwdParams& p, hipStream_t s);
 
+// Reference-model conv block (refnet.hip): conv1 1->16 3x3 s2 p1 + ReLU and
+// conv2 16->32 3x3 s2 p1 + ReLU on 28x28 u8 images (cnn.c:416-428), bf16.
+// Forward writes only Y2 [B][49][32] (NHWC, the FC input); the backward
+// recomputes conv1 per image and produces dW1, db1, dW2, db2.
+struct RefFwdParams {
+  int B = 0;
+  const uint8_t* x = nullptr;
+  const int32_t* idx = nullptr;
+  const float *w1 = nullptr, *b1 = nullptr, *w2 = nullptr, *b2 = nullptr;  // fp32 masters (canonical OIHW)
+  void* y2 = nullptr;  // bf16 [B][49][32]
+};
+struct RefBwdParams {
+  int B = 0;
+  const uint8_t* x = nullptr;
+  const int32_t* idx = nullptr;
+  const float *w1 = nullptr, *b1 = nullptr, *w2 = nullptr;
+  const void* y2 = nullptr;   // bf16 [B][49][32] (ReLU mask of conv2)
+  const void* dy2 = nullptr;  // bf16 [B][49][32] gradient of Y2
+  float* slab = nullptr;      // ref_slab_bytes()
+  float *gw1 = nullptr, *gb1 = nullptr, *gw2 = nullptr, *gb2 = nullptr;  // canonical gradients (written)
+};
+size_t ref_slab_bytes();
+void ref_forward(const RefFwdParams& p, hipStream_t s);
+void ref_backward(const RefBwdParams& p, hipStream_t s);
+
 struct ConvDwRowsParams {
   int N = 0, SH = 0, SW = 0, OH = 0, OW = 0, KS = 1, pad = 0, Cout = 0;
   const uint8_t* x = nullptr;        // u8 images [*][SH][SW]
