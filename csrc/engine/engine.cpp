@@ -82,9 +82,12 @@ struct GpuNet::Stage {
   bool rows_dw = false;
   gpu::ConvDwRowsParams prw;
   // fp32 small pooled convs: direct VALU kernels (conv_direct.hip) for the
-  // forward (direct_fwd) and, single-channel first layer, the weight gradient
-  bool direct_fwd = false, direct1 = false, direct_dx = false;
+  // forward (direct_fwd), the weight gradient (direct1: single-channel first
+  // layer; direct_dw: the 6 -> 16 conv) and the data gradient (direct_dx)
+  bool direct_fwd = false, direct1 = false, direct_dx = false, direct_dw = false;
   gpu::Conv1DirectParams pd1;
+  // u8 RGB first layer (3x3 pad 1, ReLU, 2x2 pool), bf16: row-worker forward (conv_u8.hip)
+  bool u8fwd = false;
 };
 
 static inline int r8(int x) { return (x + 7) & ~7; }
@@ -330,6 +333,20 @@ void GpuNet::build() {
         st.direct_fwd = gpu::conv_direct_fwd_supported(d);
         st.direct1 = s == 0 && gpu::conv1_direct_dw_supported(d);
         st.direct_dx = s > 0 && gpu::conv_direct_dx_supported(d);
+        st.direct_dw = s > 0 && gpu::conv_direct_dw_supported(d);
+        if (s > 0 && !st.direct_dx) st.direct_fwd = false;  // the packed copies are then the generic ones
+      }
+      if (s == 0 && dtype_ == DType::BF16 && st.inC == 3 && st.KS == 3 && st.stride == 1 && st.pad == 1 &&
+          st.pooled && st.pk == 2 && st.ps == 2 && st.act == gpu::ACT_RELU && !ab_flag("no_u8fwd")) {
+        gpu::U8ConvParams u;
+        u.N = max_batch_; u.H = st.inH; u.W = st.inW; u.Cout = st.C;
+        st.u8fwd = st.OH == st.inH && st.OW == st.inW && gpu::u8conv_fwd_supported(u);
+        // small images (CIFAR): the first layer's dW from the pooled dY / argmax too
+        if (st.u8fwd && !st.big && !ab_flag("no_c0dw")) {
+          gpu::Conv0DwParams& c = st.pc0;
+          c.B = max_batch_; c.H = st.OH; c.W = st.OW; c.C = st.inC; c.PH = st.outH; c.PW = st.outW; c.Cout = st.C;
+          st.c0dw = gpu::conv0_dw_supported(c);
+        }
       }
     } else {
       st.out_elems = st.Nout;
@@ -447,6 +464,24 @@ void GpuNet::build() {
             idx[st.pk_fwd + (int64_t)n * st.pf.kpad + kh * 8 + kw] = src;
             if (st.pf.pair) idx[st.pk_fwd + (int64_t)(8 + n) * st.pf.kpad + kh * 8 + kw + st.pf.pair] = src;
           }
+    } else if (st.kind == Stage::CONV && st.direct_fwd) {
+      // fp32 direct kernels: tap-major [inC][KK][C] (forward) and flipped
+      // tap-major [C][KK][inC] (data gradient): channel pairs are adjacent
+      // words, loaded as one scalar pair per packed FMA
+      const int KK = st.KS * st.KS;
+      st.pk_fwd = reserve((int64_t)st.inC * KK * st.C);
+      for (int n = 0; n < st.C; ++n)
+        for (int c = 0; c < st.inC; ++c)
+          for (int kp = 0; kp < KK; ++kp)
+            idx[st.pk_fwd + ((int64_t)c * KK + kp) * st.C + n] = (int32_t)(st.w_off + ((int64_t)n * st.inC + c) * KK + kp);
+      if (st.direct_dx) {
+        st.pk_dx = reserve((int64_t)st.C * KK * st.inC);
+        for (int n = 0; n < st.C; ++n)
+          for (int c = 0; c < st.inC; ++c)
+            for (int kp = 0; kp < KK; ++kp)
+              idx[st.pk_dx + ((int64_t)n * KK + (KK - 1 - kp)) * st.inC + c] =
+                  (int32_t)(st.w_off + ((int64_t)n * st.inC + c) * KK + kp);
+      }
     } else if (st.kind == Stage::CONV) {
       const int KK = st.KS * st.KS;
       // forward: [r16(C)][kpad], k = (kp, cgroup, c8) or (kp, c)
@@ -516,6 +551,10 @@ void GpuNet::build() {
       if (st.big) {
         add(st.pk_fwd, st.kgem, 1, KS * st.inC, st.inC, 0);
         if (st.pk_dx >= 0) add(st.pk_dx, 1, st.kgem_d, KS * st.C, st.C, 1);
+      } else if (st.direct_fwd) {
+        const int KK = KS * KS;
+        add(st.pk_fwd, 1, KK * st.C, KS * st.C, st.C, 0);
+        if (st.pk_dx >= 0) add(st.pk_dx, KK * st.inC, 1, KS * st.inC, st.inC, 1);
       } else if (st.pipe_fwd && st.pf.layout == gpu::XL_S1) {
         add(st.pk_fwd, st.pf.kpad, 0, 8, 1, 0);
         if (st.pf.pair) add(st.pk_fwd + 8 * (int64_t)st.pf.kpad + st.pf.pair, st.pf.kpad, 0, 8, 1, 0);
@@ -580,6 +619,8 @@ void GpuNet::build() {
       scratch = std::max(scratch, (size_t)st.nx_dw * st.cout_pad * st.ncols_pad * 4);
       if (st.rows_dw) scratch = std::max(scratch, gpu::conv_dw_rows_scratch_bytes(st.prw));
       if (st.direct1) scratch = std::max(scratch, gpu::conv1_direct_slab_bytes(st.pd1));
+      if (st.direct_dw) scratch = std::max(scratch, gpu::conv_direct_dw_slab_bytes(st.pd1));
+      if (st.c0dw) scratch = std::max(scratch, gpu::conv0_dw_slab_bytes(st.pc0));
       if (st.pipe_dw) {
         const size_t nv = (size_t)st.pdw.cout_pad * st.pdw.ncols_pad;
         scratch = std::max(scratch, (st.pdw.grid + ceil_div(st.pdw.grid, 16)) * nv * 4);
@@ -666,8 +707,10 @@ std::string GpuNet::plan() const {
         if (st.rows_dw) os << "dw:rows x" << st.prw.imgs << "/g" << st.prw.grid;
         os << "]";
       }
-      if (st.direct_fwd || st.direct1 || st.direct_dx)
-        os << " direct-f32[" << (st.direct_fwd ? "fwd" : "") << (st.direct1 ? " dw" : "") << (st.direct_dx ? " dx" : "") << "]";
+      if (st.direct_fwd || st.direct1 || st.direct_dx || st.direct_dw)
+        os << " direct-f32[" << (st.direct_fwd ? "fwd" : "") << (st.direct1 || st.direct_dw ? " dw" : "")
+           << (st.direct_dx ? " dx" : "") << "]";
+      if (st.u8fwd) os << " u8fwd" << (st.c0dw && !st.big ? " dw:pooled-direct" : "");
       os << "\n";
     } else {
       os << "  [" << s << "] fc " << st.Kin << " -> " << st.Nout << (st.last ? " (logits)" : "")
@@ -781,6 +824,15 @@ void GpuNet::forward(const uint8_t* images, const int32_t* idx, int B, hipStream
       gpu::ref_forward(f, s);
       continue;
     }
+    if (st.u8fwd) {
+      gpu::U8ConvParams u;
+      u.N = B; u.H = st.inH; u.W = st.inW; u.Cout = st.C;
+      u.x = images; u.idx = idx;
+      u.w = params_ + st.w_off; u.bias = params_ + st.b_off;
+      u.out = static_cast<uint16_t*>(st.act_buf); u.out_arg = st.arg_buf;
+      gpu::u8conv_forward(u, s);
+      continue;
+    }
     if (st.kind == Stage::CONV && st.big && st.ig_fwd) {
       // implicit GEMM with bias+ReLU epilogue -> 2x2 max-pool
       gpu::IgemmParams g;
@@ -817,7 +869,7 @@ void GpuNet::forward(const uint8_t* images, const int32_t* idx, int B, hipStream
       p.N = B;
       if (si == 0) { p.x = images; p.idx = idx; }
       else p.xf = static_cast<const float*>(stages_[si - 1]->act_buf);
-      p.w = params_ + st.w_off; p.bias = params_ + st.b_off;
+      p.wt = reinterpret_cast<const float*>(packed_) + st.pk_fwd; p.bias = params_ + st.b_off;
       p.out = static_cast<float*>(st.act_buf); p.out_arg = st.arg_buf;
       gpu::conv_direct_forward(p, s);
     } else if (st.kind == Stage::CONV && st.pipe_fwd) {
@@ -1095,6 +1147,18 @@ void GpuNet::backward(int hi, int lo, hipStream_t s) {
         w.dy = static_cast<const float*>(st.grad_buf); w.arg = st.arg_buf;
         w.slab = scratch_;
         gpu::conv1_direct_dw(w, grads_ + st.w_off, grads_ + st.b_off, ws);
+      } else if (st.c0dw) {  // small-image first layer (CIFAR): as the large-image path
+        gpu::Conv0DwParams c = st.pc0;
+        c.B = B; c.x = images_; c.idx = idx_;
+        c.dy = static_cast<const uint16_t*>(st.grad_buf); c.arg = st.arg_buf;
+        c.slab = scratch_;
+        gpu::conv0_dw(c, grads_ + st.w_off, grads_ + st.b_off, ws);
+      } else if (st.direct_dw) {
+        gpu::Conv1DirectParams w = st.pd1;
+        w.N = B; w.xf = static_cast<const float*>(stages_[si - 1]->act_buf);
+        w.dy = static_cast<const float*>(st.grad_buf); w.arg = st.arg_buf;
+        w.slab = scratch_;
+        gpu::conv_direct_dw(w, grads_ + st.w_off, grads_ + st.b_off, ws);
       } else if (st.rows_dw) {
         gpu::ConvDwRowsParams w = st.prw;
         w.N = B; w.ablate = ablate_;
@@ -1120,7 +1184,7 @@ void GpuNet::backward(int hi, int lo, hipStream_t s) {
         p.out = stages_[si - 1]->grad_buf;
         gpu::conv_pipe_forward(p, s);
       }
-      const bool dw_done = st.pipe_dw || st.rows_dw || st.direct1;
+      const bool dw_done = st.pipe_dw || st.rows_dw || st.direct1 || st.direct_dw || st.c0dw;
       if (dw_done && (st.pipe_dx || si == 0)) continue;
       // weight gradient
       if (!dw_done) {
@@ -1148,7 +1212,7 @@ void GpuNet::backward(int hi, int lo, hipStream_t s) {
       // data gradient into the previous stage's output gradient
       if (si > 0 && st.direct_dx) {
         gpu::Conv1DirectParams p = st.pd1;
-        p.N = B; p.w = params_ + st.w_off;
+        p.N = B; p.wd = reinterpret_cast<const float*>(packed_) + st.pk_dx;
         p.dy = static_cast<const float*>(st.grad_buf); p.arg = st.arg_buf;
         gpu::conv_direct_dx(p, static_cast<float*>(stages_[si - 1]->grad_buf), s);
       } else if (si > 0 && !st.pipe_dx) {

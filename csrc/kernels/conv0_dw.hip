@@ -23,6 +23,7 @@
 //     prefetch), LDS double-buffered, one barrier per step;
 //   * per-workgroup fp32 slabs, reduced over workgroups in a fixed order.
 #include "kernels.h"
+#include "mcc/ab.h"
 #include "mfma.h"
 
 #include <algorithm>
@@ -177,6 +178,196 @@ __global__ void __launch_bounds__(256) conv0_dw_reduce_kernel(Conv0DwParams p, i
   }
 }
 
+// ---------------------------------------------------------------------------
+// Row-staged variant for C = 3, Cout = 32 / 64, W % 32 == 0 (CIFAR-3conv
+// conv1 at 32x32, VGG-11 conv1 at 224x224).  The kernel above gathers the X^T
+// tile byte by byte from global memory (8 scattered loads per thread per
+// K-step plus a pixel decode); here the operands come from LDS-staged rows:
+//   * unit = (image, pooled row, 16-window segment) = 2 x 32 pixels; one wave
+//     owns a unit, staging into its own LDS region (no workgroup barriers) the
+//     4 u8 input rows it touches (26 dwords each, zero outside the image) and
+//     the segment's pooled dY / argmax transposed to [co][window]; the next
+//     unit's dwords are in flight in registers meanwhile;
+//   * K-step = one pixel row of the segment (32 pixels), lane group g owns
+//     pixels 8g..8g+7 = windows 4g..4g+3: the A fragment (dZ^T) is one
+//     ds_read_b64 of dY + one ds_read_b32 of argmax, the value routed to its
+//     argmax pixel with selects;
+//   * the B fragment (X^T, column = tap (ky, kx, c) or the ones column) is 8
+//     bytes at stride 3 of one staged row: two ds_read_b128, six v_alignbyte
+//     by the lane-constant (1 + 3kx + c) & 3 (after which every byte sits at a
+//     fixed position), eight v_cvt_f32_ubyteN; u8 integers are exact in bf16
+//     and 1/255 is applied to the fp32 tap columns at the end;
+//   * waves accumulate privately, reduce through LDS once, and write the same
+//     [wg][64][32] slab as the kernel above (same fixed-order reduce).
+constexpr int kRT = 256;          // 4 waves
+constexpr int kRRow = 112;        // staged row pitch (bytes): 26 dwords + b128 over-read
+constexpr int kRDp = 20;          // dY^T pitch (bf16) / argmax^T pitch (bytes)
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+template <int NT>  // NT = Cout / 16
+__global__ void __launch_bounds__(kRT) conv0_dw_rows_kernel(Conv0DwParams p) {
+  constexpr int COUT = 16 * NT;
+  constexpr int PER_WAVE = 4 * kRRow + COUT * kRDp * 2 + COUT * kRDp;  // bytes
+  constexpr int RDY = COUT / 8, RAR = COUT / 16;                      // dY / argmax dwords per lane
+  __shared__ __attribute__((aligned(16))) uint8_t lds[4 * PER_WAVE];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r = lane & 15, g = lane >> 4;
+  uint8_t* rows = lds + wave * PER_WAVE;
+  uint16_t* Dt = reinterpret_cast<uint16_t*>(rows + 4 * kRRow);
+  uint8_t* At = rows + 4 * kRRow + COUT * kRDp * 2;
+  for (int i = lane; i < kRRow; i += 64) reinterpret_cast<uint32_t*>(rows)[i] = 0u;  // 4 rows
+
+  // B column of this lane per tile j: k = 16j + r: tap (ky, kx, c) = (k/9, k%9/3, k%3), 27 = ones
+  int boff[2], bsh[2], bky[2];
+  bool btap[2], bone[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int k = 16 * j + r;
+    const int kk = k < 27 ? k : 0;
+    const int ky = kk / 9, kx = (kk % 9) / 3, c = kk % 3;
+    const int o0 = 1 + 3 * (8 * g + kx) + c;  // byte of pixel 8g - 1 + kx, channel c, in the staged row
+    boff[j] = o0 & ~3;
+    bsh[j] = o0 & 3;
+    bky[j] = ky;
+    btap[j] = k < 27;
+    bone[j] = k == 27;
+  }
+
+  const int PH = p.PH, nseg = p.PW / 16;
+  const int64_t nunits = (int64_t)p.B * PH * nseg;
+  const int64_t wid = (int64_t)blockIdx.x * 4 + wave, nw = (int64_t)gridDim.x * 4;
+  const int RW = 3 * p.W / 4;  // dwords per image row
+
+  uint32_t prow[2], pdy[RDY], par[RAR];
+  auto fetch = [&](int64_t u) {
+    const int seg = (int)(u % nseg);
+    const int64_t bw = u / nseg;
+    const int b = (int)(bw / PH), wy = (int)(bw - (int64_t)b * PH);
+    const int img = p.idx ? p.idx[b] : b;
+    const uint8_t* src = p.x + (size_t)img * p.H * p.W * 3;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {  // 4 rows x 26 dwords: dword 24*seg - 1 + d of row 2wy - 1 + rr
+      const int i = lane + 64 * q;
+      const int rr = i / 26, d = i - rr * 26;
+      const int y = 2 * wy - 1 + rr, dw = 24 * seg - 1 + d;
+      const bool ok = i < 104 && (unsigned)y < (unsigned)p.H && (unsigned)dw < (unsigned)RW;
+      prow[q] = ok ? reinterpret_cast<const uint32_t*>(src + (size_t)y * p.W * 3)[dw] : 0u;
+    }
+    const size_t w0 = ((size_t)b * PH + wy) * p.PW + 16 * seg;  // first window of the segment
+    const uint32_t* gdy = reinterpret_cast<const uint32_t*>(p.dy + w0 * COUT);
+    const uint32_t* gar = reinterpret_cast<const uint32_t*>(p.arg + w0 * COUT);
+#pragma unroll
+    for (int q = 0; q < RDY; ++q) pdy[q] = gdy[lane + 64 * q];
+#pragma unroll
+    for (int q = 0; q < RAR; ++q) par[q] = gar[lane + 64 * q];
+  };
+  auto stash = [&]() {
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int i = lane + 64 * q;
+      const int rr = i / 26, d = i - rr * 26;
+      if (i < 104) reinterpret_cast<uint32_t*>(rows + rr * kRRow)[d] = prow[q];
+    }
+#pragma unroll
+    for (int q = 0; q < RDY; ++q) {  // dword = channels (co, co+1) of window wx
+      const int e = 2 * (lane + 64 * q);
+      const int wx = e / COUT, co = e % COUT;
+      Dt[co * kRDp + wx] = (uint16_t)(pdy[q] & 0xffffu);
+      Dt[(co + 1) * kRDp + wx] = (uint16_t)(pdy[q] >> 16);
+    }
+#pragma unroll
+    for (int q = 0; q < RAR; ++q) {  // dword = channels co..co+3 of window wx
+      const int e = 4 * (lane + 64 * q);
+      const int wx = e / COUT, co = e % COUT;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) At[(co + t) * kRDp + wx] = (uint8_t)(par[q] >> (8 * t));
+    }
+  };
+
+  f32x4 acc[NT][2];
+#pragma unroll
+  for (int i = 0; i < NT; ++i) acc[i][0] = acc[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+  int64_t u = wid;
+  if (u < nunits) fetch(u);
+  for (; u < nunits; u += nw) {
+    stash();  // wave-private: in-order after this wave's reads of the previous unit
+    if (u + nw < nunits) fetch(u + nw);
+#pragma unroll
+    for (int dy = 0; dy < 2; ++dy) {
+      bf16x8 bf[2];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const uint8_t* rp = rows + (dy + bky[j]) * kRRow + boff[j];
+        const u32x4 d0 = *reinterpret_cast<const u32x4*>(rp);
+        const u32x4 d1 = *reinterpret_cast<const u32x4*>(rp + 16);
+        const int sh = bsh[j];
+        const uint32_t e0 = __builtin_amdgcn_alignbyte(d0.y, d0.x, sh);
+        const uint32_t e1 = __builtin_amdgcn_alignbyte(d0.z, d0.y, sh);
+        const uint32_t e2 = __builtin_amdgcn_alignbyte(d0.w, d0.z, sh);
+        const uint32_t e3 = __builtin_amdgcn_alignbyte(d1.x, d0.w, sh);
+        const uint32_t e4 = __builtin_amdgcn_alignbyte(d1.y, d1.x, sh);
+        const uint32_t e5 = __builtin_amdgcn_alignbyte(d1.z, d1.y, sh);
+        // pixel j' at byte 3j' of e0..e5
+        float f[8] = {(float)(e0 & 0xffu), (float)(e0 >> 24), (float)((e1 >> 16) & 0xffu), (float)((e2 >> 8) & 0xffu),
+                      (float)(e3 & 0xffu), (float)(e3 >> 24), (float)((e4 >> 16) & 0xffu), (float)((e5 >> 8) & 0xffu)};
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const float v = btap[j] ? f[q] : (bone[j] ? 1.f : 0.f);
+          bf[j][q] = (bf16)v;
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < NT; ++i) {
+        const int co = 16 * i + r;
+        const uint2 dv = *reinterpret_cast<const uint2*>(Dt + co * kRDp + 4 * g);
+        const uint32_t av = *reinterpret_cast<const uint32_t*>(At + co * kRDp + 4 * g);
+        uint32_t w[4];
+#pragma unroll
+        for (int ww = 0; ww < 4; ++ww) {
+          const uint32_t v = ((ww < 2 ? dv.x : dv.y) >> (16 * (ww & 1))) & 0xffffu;
+          const uint32_t a = (av >> (8 * ww)) & 0xffu;
+          w[ww] = (a == (uint32_t)(2 * dy) ? v : 0u) | (a == (uint32_t)(2 * dy + 1) ? v << 16 : 0u);
+        }
+        const bf16x8 af = __builtin_bit_cast(bf16x8, u32x4{w[0], w[1], w[2], w[3]});
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = mma(acc[i][j], af, bf[j]);
+      }
+    }
+  }
+  // waves in order through LDS, then the slab [64][kC0K] (tap columns scaled by 1/255)
+  __syncthreads();
+  float* red = reinterpret_cast<float*>(lds);  // COUT x 32 floats (<= 8 KB < 4 * PER_WAVE)
+  for (int w = 0; w < 4; ++w) {
+    if (wave == w) {
+#pragma unroll
+      for (int i = 0; i < NT; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            float& d = red[(16 * i + 4 * g + q) * kC0K + 16 * j + r];
+            d = w == 0 ? acc[i][j][q] : d + acc[i][j][q];
+          }
+    }
+    __syncthreads();
+  }
+  float* slab = p.slab + (size_t)blockIdx.x * 64 * kC0K;
+  for (int i = threadIdx.x; i < 64 * kC0K; i += kRT) {
+    const int co = i / kC0K, k = i - co * kC0K;
+    slab[i] = co < COUT ? red[i] * (k < 27 ? 1.0f / 255.0f : 1.0f) : 0.f;
+  }
+}
+
+bool conv0_dw_rows_ok(const Conv0DwParams& p) {
+  return p.C == 3 && (p.Cout == 32 || p.Cout == 64) && p.W % 32 == 0 && p.H % 2 == 0 && p.PH == p.H / 2 &&
+         p.PW == p.W / 2 && (int64_t)p.B * p.PH * (p.PW / 16) < (1ll << 40);
+}
+int conv0_dw_rows_grid(const Conv0DwParams& p) {
+  const int64_t nunits = (int64_t)p.B * p.PH * (p.PW / 16);
+  return (int)std::max<int64_t>(1, std::min<int64_t>((nunits + 3) / 4, 256 * 4));
+}
+
 int conv0_dw_grid(const Conv0DwParams& p) {
   const int64_t nsteps = ((int64_t)p.B * p.PH * p.PW + kC0W - 1) / kC0W;
   return (int)std::max<int64_t>(1, std::min<int64_t>(nsteps, 256 * 8));
@@ -190,12 +381,21 @@ bool conv0_dw_supported(const Conv0DwParams& p) {
          (int64_t)p.B * p.PH * p.PW < (1 << 24);
 }
 
-size_t conv0_dw_slab_bytes(const Conv0DwParams& p) { return (size_t)conv0_dw_grid(p) * 64 * kC0K * 4; }
+size_t conv0_dw_slab_bytes(const Conv0DwParams& p) {
+  return (size_t)std::max(conv0_dw_grid(p), conv0_dw_rows_ok(p) ? conv0_dw_rows_grid(p) : 0) * 64 * kC0K * 4;
+}
 
 void conv0_dw(const Conv0DwParams& p, float* gw, float* gb, hipStream_t s) {
   MCC_CHECK(conv0_dw_supported(p) && p.x && p.dy && p.arg && p.slab, "conv0_dw: bad params");
-  const int grid = conv0_dw_grid(p);
-  hipLaunchKernelGGL(conv0_dw_kernel, dim3((unsigned)grid), dim3(kC0T), 0, s, p);
+  int grid;
+  if (conv0_dw_rows_ok(p) && !ab_flag("no_c0dw_rows")) {
+    grid = conv0_dw_rows_grid(p);
+    if (p.Cout == 32) hipLaunchKernelGGL((conv0_dw_rows_kernel<2>), dim3((unsigned)grid), dim3(kRT), 0, s, p);
+    else hipLaunchKernelGGL((conv0_dw_rows_kernel<4>), dim3((unsigned)grid), dim3(kRT), 0, s, p);
+  } else {
+    grid = conv0_dw_grid(p);
+    hipLaunchKernelGGL(conv0_dw_kernel, dim3((unsigned)grid), dim3(kC0T), 0, s, p);
+  }
   hipLaunchKernelGGL(conv0_dw_reduce_kernel, dim3((unsigned)(p.Cout * kC0K)), dim3(256), 0, s, p, grid, gw, gb);
 }
 

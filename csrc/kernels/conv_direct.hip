@@ -59,8 +59,11 @@ __host__ __device__ inline Tile d_tile(const Conv1DirectParams& p) {
 //    two 8-byte LDS stores at the padded position), the image's dataset index
 //    from a per-group LDS table.
 constexpr int kDU8Items = 8;  // u8 items per thread: kDImgs * H * W / 4 <= 8 * kDT
+// (each item packed in one register -- source offset (10 bits), LDS offset
+// (14 bits), image + 1 (4 bits, 0: no item) -- to keep the per-thread table
+// at 8 registers in the register-hungry accumulator kernels)
 struct Stager {
-  int src[kDU8Items], dst[kDU8Items], img[kDU8Items];
+  uint32_t it[kDU8Items];
   __device__ __forceinline__ void init(const Conv1DirectParams& p, const Tile& t) {
     const int wq = p.W >> 2, per = p.H * wq;
 #pragma unroll
@@ -68,9 +71,8 @@ struct Stager {
       const int e = threadIdx.x + i * kDT;
       const int m = e / per, r = e - m * per;
       const int y = r / wq, xq = r - y * wq;
-      img[i] = m < kDImgs ? m : -1;
-      src[i] = y * p.W + 4 * xq;
-      dst[i] = m * t.IMG + (y + p.pad) * t.TW + 4 * xq + p.pad;
+      const uint32_t src = y * p.W + 4 * xq, dst = m * t.IMG + (y + p.pad) * t.TW + 4 * xq + p.pad;
+      it[i] = m < kDImgs ? src | dst << 10 | (uint32_t)(m + 1) << 24 : 0u;
     }
   }
   __device__ __forceinline__ void stage(const Conv1DirectParams& p, const Tile& t, float* xs, const int* sidx,
@@ -82,84 +84,116 @@ struct Stager {
       return;
     }
     const float sc = 1.0f / 255.0f;
+    uint32_t v[kDU8Items];  // all loads in flight first (invalid items read image 0's first word)
 #pragma unroll
     for (int i = 0; i < kDU8Items; ++i) {
-      if (img[i] < 0 || img[i] >= nimg) continue;
-      const uint32_t v = *reinterpret_cast<const uint32_t*>(p.x + (size_t)sidx[img[i]] * p.H * p.W + src[i]);
-      float* d = xs + dst[i];  // 8-byte aligned (pad even)
-      *reinterpret_cast<float2*>(d) = make_float2((float)(v & 0xffu) * sc, (float)((v >> 8) & 0xffu) * sc);
-      *reinterpret_cast<float2*>(d + 2) = make_float2((float)((v >> 16) & 0xffu) * sc, (float)(v >> 24) * sc);
+      const int m = (int)(it[i] >> 24) - 1;
+      const bool ok = m >= 0 && m < nimg;
+      v[i] = *reinterpret_cast<const uint32_t*>(p.x + (ok ? (size_t)sidx[m] * p.H * p.W + (it[i] & 1023u) : 0));
+    }
+#pragma unroll
+    for (int i = 0; i < kDU8Items; ++i) {
+      const int m = (int)(it[i] >> 24) - 1;
+      if (m < 0 || m >= nimg) continue;
+      float* d = xs + ((it[i] >> 10) & 16383u);  // 8-byte aligned (pad even)
+      *reinterpret_cast<float2*>(d) = make_float2((float)(v[i] & 0xffu) * sc, (float)((v[i] >> 8) & 0xffu) * sc);
+      *reinterpret_cast<float2*>(d + 2) = make_float2((float)((v[i] >> 16) & 0xffu) * sc, (float)(v[i] >> 24) * sc);
     }
   }
 };
+// the packed fields' ranges (host check)
+__host__ __device__ inline bool stager_fits(const Conv1DirectParams& p, const Tile& t) {
+  return p.H * p.W <= 1024 && kDImgs * t.IMG <= 16384 && p.W % 4 == 0 && p.pad % 2 == 0 &&
+         kDImgs * p.H * (p.W / 4) <= kDU8Items * kDT;
+}
 
 // dataset indices of the group's images (read by Stager::stage after the barrier)
 __device__ __forceinline__ void d_index(const Conv1DirectParams& p, int* sidx, int img0, int nimg) {
   if ((int)threadIdx.x < nimg) sidx[threadIdx.x] = p.idx ? p.idx[img0 + threadIdx.x] : img0 + threadIdx.x;
 }
 
-// (KS+1)^2 patch of input channel ci at the 2x2 window (py, px)
+// fp32 pairs: one v_pk_fma_f32 does two FMAs (the VALU's full fp32 rate).
+// Accumulators pair adjacent channels; the other operand is one input value
+// splatted to both halves.  Input values are kept as register PAIRS (f2) and
+// splatted with a shuffle that folds into the instruction's op_sel: a lone
+// float used as a splat source would occupy a whole aligned register pair.
+typedef float f2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f2 splat(f2 v, int hi) {  // hi: a constant once the loops are unrolled
+  return hi ? __builtin_shufflevector(v, v, 1, 1) : __builtin_shufflevector(v, v, 0, 0);
+}
+#define MCC_PS(row, j) splat((row)[(j) >> 1], (j) & 1)
+__device__ __forceinline__ f2 pfma(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
+
+// (KS+1)^2 patch of input channel ci at the 2x2 window (py, px), rows as
+// (KS+1)/2 register pairs (KS odd)
 template <int KS, int CIN>
-__device__ __forceinline__ void d_patch(const float* img, int TW, int py, int px, int ci, float (&P)[KS + 1][KS + 1]) {
+__device__ __forceinline__ void d_patch(const float* img, int TW, int py, int px, int ci,
+                                        f2 (&P)[KS + 1][(KS + 1) / 2]) {
+  static_assert(KS & 1, "odd kernel: even patch rows");
   const float* b = img + ((2 * py) * TW + 2 * px) * CIN + ci;
 #pragma unroll
   for (int i = 0; i <= KS; ++i) {
-    if constexpr (CIN == 1) {  // 8-byte aligned rows (TW, pad even)
 #pragma unroll
-      for (int j = 0; j + 1 <= KS; j += 2) {
-        const float2 v = *reinterpret_cast<const float2*>(b + i * TW + j);
-        P[i][j] = v.x;
-        P[i][j + 1] = v.y;
-      }
-      if ((KS + 1) & 1) P[i][KS] = b[i * TW + KS];
-    } else {
-#pragma unroll
-      for (int j = 0; j <= KS; ++j) P[i][j] = b[(i * TW + j) * CIN];
+    for (int j = 0; j < (KS + 1) / 2; ++j) {
+      if constexpr (CIN == 1)  // 8-byte aligned rows (TW, pad even)
+        P[i][j] = *reinterpret_cast<const f2*>(b + i * TW + 2 * j);
+      else
+        P[i][j] = f2{b[(i * TW + 2 * j) * CIN], b[(i * TW + 2 * j + 1) * CIN]};
     }
   }
 }
 
 // (weights and outputs are separate __restrict__ arguments: the weight loads
-// are then provably unclobbered by the output stores and become scalar loads)
+// are then provably unclobbered by the output stores and become scalar loads;
+// waves_per_eu(4): four waves per SIMD)
+// wt: tap-major weights [Cin][KS*KS][COUT] (the engine's packed copy)
 template <int KS, int CIN, int COUT>
-__global__ void __launch_bounds__(kDT) conv_direct_fwd_kernel(Conv1DirectParams p, const float* __restrict__ wgt,
+__global__ void __launch_bounds__(kDT) __attribute__((amdgpu_waves_per_eu(4))) conv_direct_fwd_kernel(Conv1DirectParams p, const float* __restrict__ wt,
                                                             const float* __restrict__ bias, float* __restrict__ out,
                                                             uint8_t* __restrict__ out_arg) {
+  static_assert(COUT % 2 == 0, "channel pairs");
+  constexpr int CP = COUT / 2;
   extern __shared__ __attribute__((aligned(16))) float xs[];
   __shared__ int sidx[kDImgs];
   const Tile t = d_tile(p);
   for (int i = threadIdx.x; i < kDImgs * t.IMG; i += kDT) xs[i] = 0.f;
   Stager sg;
-  sg.init(p, t);
+  if constexpr (CIN == 1) sg.init(p, t);
   const int PHW = p.PH * p.PW;
   const int ngroups = (p.N + kDImgs - 1) / kDImgs;
   for (int grp = blockIdx.x; grp < ngroups; grp += gridDim.x) {
     const int img0 = grp * kDImgs, nimg = min(kDImgs, p.N - img0);
     d_index(p, sidx, img0, nimg);
     __syncthreads();  // previous group's reads done (and the zero fill, first time)
-    sg.stage(p, t, xs, sidx, img0, nimg);
+    if constexpr (CIN == 1) {
+      sg.stage(p, t, xs, sidx, img0, nimg);
+    } else {  // fp32 NHWC input without padding: the tile is the global layout
+      const int n4 = nimg * t.IMG / 4;
+      const float4* g = reinterpret_cast<const float4*>(p.xf + (size_t)img0 * t.IMG);
+      for (int i = threadIdx.x; i < n4; i += kDT) reinterpret_cast<float4*>(xs)[i] = g[i];
+    }
     __syncthreads();
     for (int it = threadIdx.x; it < nimg * PHW; it += kDT) {
       const int m = it / PHW, w = it - m * PHW;
       const int py = w / p.PW, px = w - py * p.PW;
-      float acc[COUT][4];  // TL, TR, BL, BR
+      f2 acc[CP][4];  // TL, TR, BL, BR
 #pragma unroll
-      for (int c = 0; c < COUT; ++c) acc[c][0] = acc[c][1] = acc[c][2] = acc[c][3] = 0.f;
+      for (int c = 0; c < CP; ++c) acc[c][0] = acc[c][1] = acc[c][2] = acc[c][3] = f2{0.f, 0.f};
       for (int ci = 0; ci < CIN; ++ci) {
-        float P[KS + 1][KS + 1];
+        f2 P[KS + 1][(KS + 1) / 2];
         d_patch<KS, CIN>(xs + m * t.IMG, t.TW, py, px, ci, P);
+        const float* wc = wt + ci * KS * KS * COUT;  // wave-uniform: scalar loads
 #pragma unroll
-        for (int c = 0; c < COUT; ++c) {
-          const float* wc = wgt + (c * CIN + ci) * KS * KS;  // wave-uniform: scalar loads
+        for (int kh = 0; kh < KS; ++kh) {
 #pragma unroll
-          for (int kh = 0; kh < KS; ++kh) {
+          for (int kw = 0; kw < KS; ++kw) {
 #pragma unroll
-            for (int kw = 0; kw < KS; ++kw) {
-              const float wv = wc[kh * KS + kw];
-              acc[c][0] = fmaf(wv, P[kh][kw], acc[c][0]);
-              acc[c][1] = fmaf(wv, P[kh][kw + 1], acc[c][1]);
-              acc[c][2] = fmaf(wv, P[kh + 1][kw], acc[c][2]);
-              acc[c][3] = fmaf(wv, P[kh + 1][kw + 1], acc[c][3]);
+            for (int c = 0; c < CP; ++c) {
+              const f2 wv = *reinterpret_cast<const f2*>(wc + (kh * KS + kw) * COUT + 2 * c);
+              acc[c][0] = pfma(wv, MCC_PS(P[kh], kw), acc[c][0]);
+              acc[c][1] = pfma(wv, MCC_PS(P[kh], kw + 1), acc[c][1]);
+              acc[c][2] = pfma(wv, MCC_PS(P[kh + 1], kw), acc[c][2]);
+              acc[c][3] = pfma(wv, MCC_PS(P[kh + 1], kw + 1), acc[c][3]);
             }
           }
         }
@@ -170,11 +204,14 @@ __global__ void __launch_bounds__(kDT) conv_direct_fwd_kernel(Conv1DirectParams 
       for (int q = 0; q < (COUT + 3) / 4; ++q) arg[q] = 0;
 #pragma unroll
       for (int c = 0; c < COUT; ++c) {
-        float best = acc[c][0];
+        float v[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = (c & 1) ? acc[c >> 1][q].y : acc[c >> 1][q].x;
+        float best = v[0];
         int a = 0;
-        if (acc[c][1] > best) { best = acc[c][1]; a = 1; }
-        if (acc[c][2] > best) { best = acc[c][2]; a = 2; }
-        if (acc[c][3] > best) { best = acc[c][3]; a = 3; }
+        if (v[1] > best) { best = v[1]; a = 1; }
+        if (v[2] > best) { best = v[2]; a = 2; }
+        if (v[3] > best) { best = v[3]; a = 3; }
         y[c] = fmaxf(best + bias[c], 0.f);
         arg[c >> 2] |= (uint32_t)(y[c] > 0.f ? a : 4) << (8 * (c & 3));
       }
@@ -186,7 +223,6 @@ __global__ void __launch_bounds__(kDT) conv_direct_fwd_kernel(Conv1DirectParams 
 #pragma unroll
         for (int q = 0; q < COUT / 4; ++q) *reinterpret_cast<uint32_t*>(out_arg + o + 4 * q) = arg[q];
       } else {
-        static_assert(COUT % 2 == 0, "even channel count");
 #pragma unroll
         for (int c = 0; c < COUT; c += 2) *reinterpret_cast<float2*>(out + o + c) = make_float2(y[c], y[c + 1]);
 #pragma unroll
@@ -198,9 +234,10 @@ __global__ void __launch_bounds__(kDT) conv_direct_fwd_kernel(Conv1DirectParams 
   }
 }
 
-template <int KS, int CM>  // CM: channel bound of the accumulator array (registers)
-__global__ void __launch_bounds__(kDT) conv1_direct_dw_kernel(Conv1DirectParams p) {
-  constexpr int KK = KS * KS;
+template <int KS, int CM, bool EXACT>  // CM: channel bound of the accumulator array (registers), even; EXACT: p.C == CM
+__global__ void __launch_bounds__(kDT) __attribute__((amdgpu_waves_per_eu(2))) conv1_direct_dw_kernel(Conv1DirectParams p) {
+  static_assert(CM % 2 == 0, "channel pairs");
+  constexpr int KK = KS * KS, CP = CM / 2;
   extern __shared__ __attribute__((aligned(16))) float xs[];
   __shared__ float red[kDT / 64][CM * (KK + 1)];
   __shared__ int sidx[kDImgs];
@@ -213,11 +250,11 @@ __global__ void __launch_bounds__(kDT) conv1_direct_dw_kernel(Conv1DirectParams 
   Stager sg;
   sg.init(p, t);
   const int ngroups = (p.N + kDImgs - 1) / kDImgs;
-  float acc[CM][KK + 1];
+  f2 acc[CP][KK + 1];  // channel pairs (2c, 2c+1); [KK]: bias
 #pragma unroll
-  for (int c = 0; c < CM; ++c)
+  for (int c = 0; c < CP; ++c)
 #pragma unroll
-    for (int k = 0; k <= KK; ++k) acc[c][k] = 0.f;
+    for (int k = 0; k <= KK; ++k) acc[c][k] = f2{0.f, 0.f};
   for (int grp = blockIdx.x; grp < ngroups; grp += gridDim.x) {
     const int img0 = grp * kDImgs, nimg = min(kDImgs, p.N - img0);
     d_index(p, sidx, img0, nimg);
@@ -236,29 +273,31 @@ __global__ void __launch_bounds__(kDT) conv1_direct_dw_kernel(Conv1DirectParams 
     for (int it = threadIdx.x; it < nimg * PHW; it += kDT) {
       const int m = it / PHW, w = it - m * PHW;
       const int py = w / p.PW, px = w - py * p.PW;
-      float P[KS + 1][KS + 1];
+      f2 P[KS + 1][(KS + 1) / 2];
       d_patch<KS, 1>(xs + m * t.IMG, t.TW, py, px, 0, P);
       const int o = it * p.C;
 #pragma unroll
-      for (int c = 0; c < CM; ++c) {
-        if (c >= p.C) break;
-        const float gy = dys[o + c];
-        const int a = args[o + c];  // 4: ReLU-inactive window, nothing routed
-        const float g0 = a == 0 ? gy : 0.f, g1 = a == 1 ? gy : 0.f;
-        const float g2 = a == 2 ? gy : 0.f, g3 = a == 3 ? gy : 0.f;
+      for (int c = 0; c < CP; ++c) {
+        if (!EXACT && 2 * c >= p.C) break;  // (p.C even: host check)
+        const float2 gy = *reinterpret_cast<const float2*>(dys + o + 2 * c);
+        const int a0 = args[o + 2 * c], a1 = args[o + 2 * c + 1];  // 4: ReLU-inactive window
+        const f2 g0 = {a0 == 0 ? gy.x : 0.f, a1 == 0 ? gy.y : 0.f};
+        const f2 g1 = {a0 == 1 ? gy.x : 0.f, a1 == 1 ? gy.y : 0.f};
+        const f2 g2 = {a0 == 2 ? gy.x : 0.f, a1 == 2 ? gy.y : 0.f};
+        const f2 g3 = {a0 == 3 ? gy.x : 0.f, a1 == 3 ? gy.y : 0.f};
 #pragma unroll
         for (int kh = 0; kh < KS; ++kh) {
 #pragma unroll
           for (int kw = 0; kw < KS; ++kw) {
-            float v = acc[c][kh * KS + kw];
-            v = fmaf(g0, P[kh][kw], v);
-            v = fmaf(g1, P[kh][kw + 1], v);
-            v = fmaf(g2, P[kh + 1][kw], v);
-            v = fmaf(g3, P[kh + 1][kw + 1], v);
+            f2 v = acc[c][kh * KS + kw];
+            v = pfma(g0, MCC_PS(P[kh], kw), v);
+            v = pfma(g1, MCC_PS(P[kh], kw + 1), v);
+            v = pfma(g2, MCC_PS(P[kh + 1], kw), v);
+            v = pfma(g3, MCC_PS(P[kh + 1], kw + 1), v);
             acc[c][kh * KS + kw] = v;
           }
         }
-        acc[c][KK] += (a < 4) ? gy : 0.f;
+        acc[c][KK] += f2{a0 < 4 ? gy.x : 0.f, a1 < 4 ? gy.y : 0.f};
       }
     }
   }
@@ -266,10 +305,10 @@ __global__ void __launch_bounds__(kDT) conv1_direct_dw_kernel(Conv1DirectParams 
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
   for (int c = 0; c < CM; ++c) {
-    if (c >= p.C) break;
+    if (!EXACT && c >= p.C) break;
 #pragma unroll
     for (int k = 0; k <= KK; ++k) {
-      float v = acc[c][k];
+      float v = (c & 1) ? acc[c >> 1][k].y : acc[c >> 1][k].x;
 #pragma unroll
       for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
       if (lane == 0) red[wave][c * (KK + 1) + k] = v;
@@ -291,13 +330,16 @@ __global__ void __launch_bounds__(kDT) conv1_direct_dw_kernel(Conv1DirectParams 
 // windows (the block is 2-aligned and the halo KS-1 = 4 is even), so the
 // patch is decoded from the group's pooled dY / argmax in LDS (value at the
 // argmax position, zeros elsewhere; argmax 4 routes nothing) instead of
-// staging the 4x larger unpooled tensor.  Then 4*KS*KS FMAs per (input,
-// output channel) pair with scalar-loaded flipped weights, as the forward.
+// staging the 4x larger unpooled tensor.  Then 4*KS*KS packed FMAs per
+// (dZ channel, dX channel pair) with scalar-loaded weight pairs from the
+// flipped tap-major copy wd [CI][KS*KS][CO] (wd[i][t][c] = w[i][c][KK-1-t]).
 constexpr int kDxImgs = 16;
 template <int KS, int CI, int CO>  // CI: dZ channels (forward Cout), CO: dX channels (forward Cin)
-__global__ void __launch_bounds__(kDT) conv_direct_dx_kernel(Conv1DirectParams p, const float* __restrict__ wgt,
+__global__ void __launch_bounds__(kDT) __attribute__((amdgpu_waves_per_eu(4))) conv_direct_dx_kernel(Conv1DirectParams p, const float* __restrict__ wd,
                                                            float* __restrict__ out) {
   static_assert(KS == 5, "the 3x3-window patch decode assumes KS - 1 == 4");
+  static_assert(CO % 2 == 0, "channel pairs");
+  constexpr int CP = CO / 2;
   extern __shared__ __attribute__((aligned(16))) float dys[];
   const int PHW = p.PH * p.PW;  // pooled grid of dY
   const int BH = p.H / 2, BW = p.W / 2, nb = BH * BW;  // 2x2 blocks of the dX grid (H x W)
@@ -319,13 +361,13 @@ __global__ void __launch_bounds__(kDT) conv_direct_dx_kernel(Conv1DirectParams p
     for (int it = threadIdx.x; it < nimg * nb; it += kDT) {
       const int m = it / nb, b = it - m * nb;
       const int by = b / BW, bx = b - by * BW;
-      float acc[CO][4];
+      f2 acc[CP][4];
 #pragma unroll
-      for (int c = 0; c < CO; ++c) acc[c][0] = acc[c][1] = acc[c][2] = acc[c][3] = 0.f;
+      for (int c = 0; c < CP; ++c) acc[c][0] = acc[c][1] = acc[c][2] = acc[c][3] = f2{0.f, 0.f};
       const float* dimg = dys + m * PHW * CI;
       const uint8_t* aimg = args + m * PHW * CI;
       for (int i = 0; i < CI; ++i) {
-        float P[KS + 1][KS + 1];
+        f2 P[KS + 1][(KS + 1) / 2];  // row pairs: window wc's two columns are one pair
 #pragma unroll
         for (int wr = 0; wr < 3; ++wr) {
 #pragma unroll
@@ -335,25 +377,22 @@ __global__ void __launch_bounds__(kDT) conv_direct_dx_kernel(Conv1DirectParams p
             const int o = ok ? (wy * p.PW + wx) * CI + i : 0;
             const float g = ok ? dimg[o] : 0.f;
             const int a = ok ? aimg[o] : 4;
-            P[2 * wr][2 * wc] = a == 0 ? g : 0.f;
-            P[2 * wr][2 * wc + 1] = a == 1 ? g : 0.f;
-            P[2 * wr + 1][2 * wc] = a == 2 ? g : 0.f;
-            P[2 * wr + 1][2 * wc + 1] = a == 3 ? g : 0.f;
+            P[2 * wr][wc] = f2{a == 0 ? g : 0.f, a == 1 ? g : 0.f};
+            P[2 * wr + 1][wc] = f2{a == 2 ? g : 0.f, a == 3 ? g : 0.f};
           }
         }
+        const float* wi = wd + i * KS * KS * CO;  // wave-uniform: scalar loads
 #pragma unroll
-        for (int c = 0; c < CO; ++c) {
-          // flipped weight of (dX channel c, dZ channel i, tap kh, kw) = w[i][c][KS-1-kh][KS-1-kw]
-          const float* wc = wgt + (i * CO + c) * KS * KS;
+        for (int kh = 0; kh < KS; ++kh) {
 #pragma unroll
-          for (int kh = 0; kh < KS; ++kh) {
+          for (int kw = 0; kw < KS; ++kw) {
 #pragma unroll
-            for (int kw = 0; kw < KS; ++kw) {
-              const float wv = wc[(KS - 1 - kh) * KS + (KS - 1 - kw)];
-              acc[c][0] = fmaf(wv, P[kh][kw], acc[c][0]);
-              acc[c][1] = fmaf(wv, P[kh][kw + 1], acc[c][1]);
-              acc[c][2] = fmaf(wv, P[kh + 1][kw], acc[c][2]);
-              acc[c][3] = fmaf(wv, P[kh + 1][kw + 1], acc[c][3]);
+            for (int c = 0; c < CP; ++c) {
+              const f2 wv = *reinterpret_cast<const f2*>(wi + (kh * KS + kw) * CO + 2 * c);
+              acc[c][0] = pfma(wv, MCC_PS(P[kh], kw), acc[c][0]);
+              acc[c][1] = pfma(wv, MCC_PS(P[kh], kw + 1), acc[c][1]);
+              acc[c][2] = pfma(wv, MCC_PS(P[kh + 1], kw), acc[c][2]);
+              acc[c][3] = pfma(wv, MCC_PS(P[kh + 1], kw + 1), acc[c][3]);
             }
           }
         }
@@ -363,21 +402,147 @@ __global__ void __launch_bounds__(kDT) conv_direct_dx_kernel(Conv1DirectParams p
       for (int r = 0; r < 2; ++r) {
         float* d = out + (((size_t)(img0 + m) * p.H + 2 * by + r) * p.W + 2 * bx) * CO;
 #pragma unroll
-        for (int c = 0; c < CO; c += 2) {
-          *reinterpret_cast<float2*>(d + c) = make_float2(acc[c][2 * r], acc[c + 1][2 * r]);
-          *reinterpret_cast<float2*>(d + CO + c) = make_float2(acc[c][2 * r + 1], acc[c + 1][2 * r + 1]);
+        for (int c = 0; c < CP; ++c) {
+          *reinterpret_cast<float2*>(d + 2 * c) = make_float2(acc[c][2 * r].x, acc[c][2 * r].y);
+          *reinterpret_cast<float2*>(d + CO + 2 * c) = make_float2(acc[c][2 * r + 1].x, acc[c][2 * r + 1].y);
         }
       }
     }
   }
 }
 
+// Weight gradient of the pooled 6 -> 16 5x5 conv (fp32, stride 1, no
+// padding): dW[c][ci][t] = sum over images and pooling windows of
+// dY[c] * X[ci][argmax pixel + t].  Item = (image, pooling window); a thread
+// owns one (4-channel group, input channel) combination for the whole launch
+// -- 2 channel pairs x 25 taps of packed accumulators -- and walks the
+// group's items with the other threads of its combination (kWSlots of them).
+// Per item it decodes the four window positions' gradients from the pooled
+// dY / argmax (zeros except at the argmax), streams the 6x6 input patch of
+// its channel row by row from LDS and does 2 x 25 x 4 packed FMAs.  Partial
+// sums: slots in a fixed order through LDS, then one slab per workgroup,
+// reduced by conv1_direct_dw_reduce_kernel (deterministic).
+constexpr int kWCG = 4;                    // channels per combination (two pairs)
+constexpr int kWImgs = 8;                  // images per group
+template <int CIN, int COUT>
+struct DwGeom {
+  static constexpr int combos = (COUT / kWCG) * CIN;
+  static constexpr int slots = 16;
+  static constexpr int threads = combos * slots;
+  static constexpr int ncol = COUT * (CIN * 25 + 1);
+};
+template <int KS, int CIN, int COUT>
+__global__ void __launch_bounds__((DwGeom<CIN, COUT>::threads)) __attribute__((amdgpu_waves_per_eu(3)))
+conv_direct_dw_kernel(Conv1DirectParams p) {
+  using G = DwGeom<CIN, COUT>;
+  static_assert(KS == 5 && COUT % kWCG == 0, "shape");
+  constexpr int KK = KS * KS;
+  extern __shared__ __attribute__((aligned(16))) float xs[];
+  const int TW = p.W, IMG = p.H * p.W * CIN;  // NHWC input, no padding
+  const int PHW = p.PH * p.PW;
+  float* dys = xs + kWImgs * IMG;
+  uint8_t* args = reinterpret_cast<uint8_t*>(dys + kWImgs * PHW * COUT);
+  const int combo = threadIdx.x % G::combos, slot = threadIdx.x / G::combos;
+  const int cg = combo / CIN, ci = combo - cg * CIN;
+  f2 acc[2][KK];
+  f2 accb[2] = {f2{0.f, 0.f}, f2{0.f, 0.f}};
+#pragma unroll
+  for (int q = 0; q < 2; ++q)
+#pragma unroll
+    for (int k = 0; k < KK; ++k) acc[q][k] = f2{0.f, 0.f};
+  const int ngroups = (p.N + kWImgs - 1) / kWImgs;
+  for (int grp = blockIdx.x; grp < ngroups; grp += gridDim.x) {
+    const int img0 = grp * kWImgs, nimg = min(kWImgs, p.N - img0);
+    __syncthreads();
+    {  // contiguous runs: images (IMG % 4 == 0), pooled dY and argmax (PHW * COUT % 4 == 0)
+      const int nx = nimg * IMG / 4;
+      const float4* gx = reinterpret_cast<const float4*>(p.xf + (size_t)img0 * IMG);
+      for (int i = threadIdx.x; i < nx; i += G::threads) reinterpret_cast<float4*>(xs)[i] = gx[i];
+      const int n4 = nimg * PHW * COUT / 4;
+      const float4* gdy = reinterpret_cast<const float4*>(p.dy + (size_t)img0 * PHW * COUT);
+      const uint32_t* garg = reinterpret_cast<const uint32_t*>(p.arg + (size_t)img0 * PHW * COUT);
+      for (int i = threadIdx.x; i < n4; i += G::threads) {
+        reinterpret_cast<float4*>(dys)[i] = gdy[i];
+        reinterpret_cast<uint32_t*>(args)[i] = garg[i];
+      }
+    }
+    __syncthreads();
+    for (int it = slot; it < nimg * PHW; it += G::slots) {
+      const int m = it / PHW, w = it - m * PHW;
+      const int py = w / p.PW, px = w - py * p.PW;
+      const int o = it * COUT + cg * kWCG;
+      const float4 gy = *reinterpret_cast<const float4*>(dys + o);
+      const uint32_t a4 = *reinterpret_cast<const uint32_t*>(args + o);
+      const int a0 = a4 & 0xff, a1 = (a4 >> 8) & 0xff, a2 = (a4 >> 16) & 0xff, a3 = a4 >> 24;
+      f2 g[2][4];  // [pair][window position]
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        g[0][q] = f2{a0 == q ? gy.x : 0.f, a1 == q ? gy.y : 0.f};
+        g[1][q] = f2{a2 == q ? gy.z : 0.f, a3 == q ? gy.w : 0.f};
+      }
+      if (ci == 0) {
+        accb[0] += f2{a0 < 4 ? gy.x : 0.f, a1 < 4 ? gy.y : 0.f};
+        accb[1] += f2{a2 < 4 ? gy.z : 0.f, a3 < 4 ? gy.w : 0.f};
+      }
+      const float* x = xs + m * IMG + ((2 * py) * TW + 2 * px) * CIN + ci;
+#pragma unroll
+      for (int r = 0; r <= KS; ++r) {  // patch row r feeds tap rows r (top positions) and r - 1 (bottom)
+        f2 R[(KS + 1) / 2];
+#pragma unroll
+        for (int j = 0; j < (KS + 1) / 2; ++j) R[j] = f2{x[(r * TW + 2 * j) * CIN], x[(r * TW + 2 * j + 1) * CIN]};
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+#pragma unroll
+          for (int kw = 0; kw < KS; ++kw) {
+            if (r < KS) {
+              acc[q][r * KS + kw] = pfma(g[q][0], MCC_PS(R, kw), acc[q][r * KS + kw]);
+              acc[q][r * KS + kw] = pfma(g[q][1], MCC_PS(R, kw + 1), acc[q][r * KS + kw]);
+            }
+            if (r > 0) {
+              acc[q][(r - 1) * KS + kw] = pfma(g[q][2], MCC_PS(R, kw), acc[q][(r - 1) * KS + kw]);
+              acc[q][(r - 1) * KS + kw] = pfma(g[q][3], MCC_PS(R, kw + 1), acc[q][(r - 1) * KS + kw]);
+            }
+          }
+        }
+      }
+    }
+  }
+  // slots in order into LDS [combo][4 channels][KK + 1], then the slab
+  __syncthreads();
+  constexpr int per = kWCG * (KK + 1);
+  float* red = xs;
+  for (int s = 0; s < G::slots; ++s) {
+    if (slot == s) {
+#pragma unroll
+      for (int c = 0; c < kWCG; ++c) {
+#pragma unroll
+        for (int k = 0; k < KK; ++k) {
+          const float v = (c & 1) ? acc[c >> 1][k].y : acc[c >> 1][k].x;
+          float& d = red[combo * per + c * (KK + 1) + k];
+          d = s == 0 ? v : d + v;
+        }
+        const float vb = (c & 1) ? accb[c >> 1].y : accb[c >> 1].x;
+        float& d = red[combo * per + c * (KK + 1) + KK];
+        d = s == 0 ? vb : d + vb;
+      }
+    }
+    __syncthreads();
+  }
+  // slab column (c, k): k < CIN*KK weight (ci, tap), k == CIN*KK bias (from the ci == 0 combos)
+  for (int i = threadIdx.x; i < G::ncol; i += G::threads) {
+    const int c = i / (CIN * KK + 1), k = i - c * (CIN * KK + 1);
+    const int g4 = c / kWCG, cc = c - g4 * kWCG;
+    const int kci = k < CIN * KK ? k / KK : 0, t = k < CIN * KK ? k - kci * KK : KK;
+    p.slab[(size_t)blockIdx.x * G::ncol + i] = red[(g4 * CIN + kci) * per + cc * (KK + 1) + t];
+  }
+}
+
 // One workgroup per column (c, k): 256 strided partial sums over the slabs,
-// then a fixed LDS tree.  k < KK: weight, k == KK: bias.
+// then a fixed LDS tree.  k < Cin*KS*KS: weight, k == Cin*KS*KS: bias.
 __global__ void __launch_bounds__(256) conv1_direct_dw_reduce_kernel(Conv1DirectParams p, int nslab, float* gw,
                                                                      float* gb) {
   __shared__ float part[256];
-  const int KK = p.KS * p.KS, ncol = p.C * (KK + 1);
+  const int KK = p.Cin * p.KS * p.KS, ncol = p.C * (KK + 1);  // KK: weights per output channel
   const int i = blockIdx.x;
   float v = 0.f;
   for (int s = threadIdx.x; s < nslab; s += 256) v += p.slab[(size_t)s * ncol + i];
@@ -404,8 +569,7 @@ size_t dw_lds(const Conv1DirectParams& p) {
 bool conv_direct_fwd_supported(const Conv1DirectParams& p) {
   const bool shape = p.KS == 5 && ((p.Cin == 1 && p.C == 6) || (p.Cin == 6 && p.C == 16));
   const Tile t = d_tile(p);
-  const bool stage_ok = p.Cin == 1 ? (p.W % 4 == 0 && p.pad % 2 == 0 && kDImgs * p.H * (p.W / 4) <= kDU8Items * kDT)
-                                   : (p.pad == 0 && t.TW == p.W && t.IMG % 4 == 0);
+  const bool stage_ok = p.Cin == 1 ? stager_fits(p, t) : (p.pad == 0 && t.TW == p.W && t.IMG % 4 == 0);
   return shape && stage_ok && p.OH % 2 == 0 && p.OW % 2 == 0 && p.OH == p.H + 2 * p.pad - p.KS + 1 &&
          p.OW == p.W + 2 * p.pad - p.KS + 1 && p.PH == p.OH / 2 && p.PW == p.OW / 2 && fwd_lds(p) <= 64 * 1024;
 }
@@ -418,17 +582,16 @@ bool conv_direct_dx_supported(const Conv1DirectParams& p) {
 }
 
 void conv_direct_dx(const Conv1DirectParams& p, float* dx, hipStream_t s) {
-  MCC_CHECK(conv_direct_dx_supported(p) && p.w && p.dy && p.arg && dx, "conv_direct_dx: bad params");
+  MCC_CHECK(conv_direct_dx_supported(p) && p.wd && p.dy && p.arg && dx, "conv_direct_dx: bad params");
   const int ngroups = (p.N + kDxImgs - 1) / kDxImgs;
   const dim3 grid((unsigned)std::max(1, std::min(ngroups, 256 * 4))), block(kDT);
   const size_t lds = (size_t)kDxImgs * p.PH * p.PW * p.C * 5;
-  hipLaunchKernelGGL((conv_direct_dx_kernel<5, 16, 6>), grid, block, lds, s, p, p.w, dx);
+  hipLaunchKernelGGL((conv_direct_dx_kernel<5, 16, 6>), grid, block, lds, s, p, p.wd, dx);
 }
 
 bool conv1_direct_dw_supported(const Conv1DirectParams& p) {
-  return p.Cin == 1 && p.C >= 1 && p.C <= kDMaxC && (p.KS == 3 || p.KS == 5) && p.OH % 2 == 0 && p.OW % 2 == 0 &&
-         p.W % 4 == 0 && p.pad % 2 == 0 && kDImgs * p.H * (p.W / 4) <= kDU8Items * kDT &&
-         (p.PH * p.PW * p.C) % 4 == 0 &&
+  return p.Cin == 1 && p.C >= 2 && p.C <= kDMaxC && p.C % 2 == 0 && (p.KS == 3 || p.KS == 5) && p.OH % 2 == 0 &&
+         p.OW % 2 == 0 && stager_fits(p, d_tile(p)) && (p.PH * p.PW * p.C) % 4 == 0 &&
          p.OH == p.H + 2 * p.pad - p.KS + 1 && p.OW == p.W + 2 * p.pad - p.KS + 1 && p.PH == p.OH / 2 &&
          p.PW == p.OW / 2 && dw_lds(p) <= 96 * 1024;
 }
@@ -443,25 +606,53 @@ size_t conv1_direct_slab_bytes(const Conv1DirectParams& p) {
 }
 
 void conv_direct_forward(const Conv1DirectParams& p, hipStream_t s) {
-  MCC_CHECK(conv_direct_fwd_supported(p) && (p.x || p.xf) && p.w && p.bias && p.out && p.out_arg,
+  MCC_CHECK(conv_direct_fwd_supported(p) && (p.x || p.xf) && p.wt && p.bias && p.out && p.out_arg,
             "conv_direct_forward: bad params");
   const dim3 grid((unsigned)direct_grid(p)), block(kDT);
   if (p.Cin == 1)
-    hipLaunchKernelGGL((conv_direct_fwd_kernel<5, 1, 6>), grid, block, fwd_lds(p), s, p, p.w, p.bias, p.out, p.out_arg);
-  else
-    hipLaunchKernelGGL((conv_direct_fwd_kernel<5, 6, 16>), grid, block, fwd_lds(p), s, p, p.w, p.bias, p.out,
+    hipLaunchKernelGGL((conv_direct_fwd_kernel<5, 1, 6>), grid, block, fwd_lds(p), s, p, p.wt, p.bias, p.out,
                        p.out_arg);
+  else
+    hipLaunchKernelGGL((conv_direct_fwd_kernel<5, 6, 16>), grid, block, fwd_lds(p), s, p, p.wt, p.bias, p.out,
+                       p.out_arg);
+}
+
+static void dw_reduce(const Conv1DirectParams& p, int grid, float* gw, float* gb, hipStream_t s) {
+  const int ncol = p.C * (p.Cin * p.KS * p.KS + 1);
+  hipLaunchKernelGGL(conv1_direct_dw_reduce_kernel, dim3((unsigned)ncol), dim3(256), 0, s, p, grid, gw, gb);
 }
 
 void conv1_direct_dw(const Conv1DirectParams& p, float* gw, float* gb, hipStream_t s) {
   MCC_CHECK(conv1_direct_dw_supported(p) && p.x && p.dy && p.arg && p.slab, "conv1_direct_dw: bad params");
   const int grid = direct_grid(p);
   const dim3 g((unsigned)grid), b(kDT);
-  if (p.KS == 5 && p.C <= 6) hipLaunchKernelGGL((conv1_direct_dw_kernel<5, 6>), g, b, dw_lds(p), s, p);
-  else if (p.KS == 5) hipLaunchKernelGGL((conv1_direct_dw_kernel<5, kDMaxC>), g, b, dw_lds(p), s, p);
-  else hipLaunchKernelGGL((conv1_direct_dw_kernel<3, kDMaxC>), g, b, dw_lds(p), s, p);
-  const int ncol = p.C * (p.KS * p.KS + 1);
-  hipLaunchKernelGGL(conv1_direct_dw_reduce_kernel, dim3((unsigned)ncol), dim3(256), 0, s, p, grid, gw, gb);
+  if (p.KS == 5 && p.C == 6) hipLaunchKernelGGL((conv1_direct_dw_kernel<5, 6, true>), g, b, dw_lds(p), s, p);
+  else if (p.KS == 5) hipLaunchKernelGGL((conv1_direct_dw_kernel<5, kDMaxC, false>), g, b, dw_lds(p), s, p);
+  else hipLaunchKernelGGL((conv1_direct_dw_kernel<3, kDMaxC, false>), g, b, dw_lds(p), s, p);
+  dw_reduce(p, grid, gw, gb, s);
+}
+
+// conv2-shaped (6 -> 16, 5x5, unpadded, pooled) weight gradient
+static size_t dw2_lds(const Conv1DirectParams& p) {
+  return (size_t)kWImgs * (p.H * p.W * p.Cin * 4 + p.PH * p.PW * p.C * 5);
+}
+static int dw2_grid(const Conv1DirectParams& p) {
+  return std::max(1, std::min((p.N + kWImgs - 1) / kWImgs, 256 * 2));
+}
+bool conv_direct_dw_supported(const Conv1DirectParams& p) {
+  return p.KS == 5 && p.pad == 0 && p.Cin == 6 && p.C == 16 && p.OH == p.H - 4 && p.OW == p.W - 4 &&
+         p.OH % 2 == 0 && p.OW % 2 == 0 && p.PH == p.OH / 2 && p.PW == p.OW / 2 && (p.H * p.W * p.Cin) % 4 == 0 &&
+         (p.PH * p.PW * p.C) % 4 == 0 && dw2_lds(p) <= 64 * 1024;
+}
+size_t conv_direct_dw_slab_bytes(const Conv1DirectParams& p) {
+  return (size_t)dw2_grid(p) * p.C * (p.Cin * p.KS * p.KS + 1) * 4;
+}
+void conv_direct_dw(const Conv1DirectParams& p, float* gw, float* gb, hipStream_t s) {
+  MCC_CHECK(conv_direct_dw_supported(p) && p.xf && p.dy && p.arg && p.slab, "conv_direct_dw: bad params");
+  const int grid = dw2_grid(p);
+  hipLaunchKernelGGL((conv_direct_dw_kernel<5, 6, 16>), dim3((unsigned)grid), dim3(DwGeom<6, 16>::threads),
+                     dw2_lds(p), s, p);
+  dw_reduce(p, grid, gw, gb, s);
 }
 
 }  // namespace gpu

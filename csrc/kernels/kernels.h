@@ -230,13 +230,14 @@ struct Conv1DirectParams {
   const uint8_t* x = nullptr;     // u8 images [.][H][W][Cin] (when xf is null)
   const int32_t* idx = nullptr;   // optional per-image dataset index
   const float* xf = nullptr;      // fp32 NHWC input [N][H][W][Cin] (a previous layer)
-  const float* w = nullptr;       // forward: canonical weights, bias
+  const float* wt = nullptr;      // forward: tap-major weights [Cin][KS*KS][C] (packed copy)
+  const float* wd = nullptr;      // data gradient: flipped tap-major [C][KS*KS][Cin], wd[i][t][c] = w[i][c][KK-1-t]
   const float* bias = nullptr;
   float* out = nullptr;           // forward: pooled [N][PH][PW][C]
   uint8_t* out_arg = nullptr;     //          argmax (4: ReLU-inactive window)
   const float* dy = nullptr;      // weight gradient: pooled output gradient [N][PH][PW][C]
   const uint8_t* arg = nullptr;   //                  its argmax bytes
-  float* slab = nullptr;          //                  [grid][C][KS*KS + 1] partial sums
+  float* slab = nullptr;          //                  [grid][C][Cin*KS*KS + 1] partial sums
 };
 bool conv_direct_fwd_supported(const Conv1DirectParams& p);
 bool conv1_direct_dw_supported(const Conv1DirectParams& p);
@@ -247,6 +248,26 @@ void conv_direct_forward(const Conv1DirectParams& p, hipStream_t s);
 bool conv_direct_dx_supported(const Conv1DirectParams& p);
 void conv_direct_dx(const Conv1DirectParams& p, float* dx, hipStream_t s);
 void conv1_direct_dw(const Conv1DirectParams& p, float* gw, float* gb, hipStream_t s);
+// weight gradient of the 6 -> 16 5x5 pooled conv from its fp32 NHWC input
+// (p.xf) and the pooled dY / argmax
+bool conv_direct_dw_supported(const Conv1DirectParams& p);
+size_t conv_direct_dw_slab_bytes(const Conv1DirectParams& p);
+void conv_direct_dw(const Conv1DirectParams& p, float* gw, float* gb, hipStream_t s);
+
+// Forward of the u8 RGB first conv (C = 3, 3x3, stride 1, pad 1, bias + ReLU
+// + 2x2/2 max-pool fused), bf16 MFMA, output pooled NHWC [N][H/2][W/2][Cout]
+// + argmax bytes (4: ReLU-inactive window) (conv_u8.hip)
+struct U8ConvParams {
+  int N = 0, H = 0, W = 0, Cout = 0;
+  const uint8_t* x = nullptr;     // u8 images [.][H][W][3]
+  const int32_t* idx = nullptr;   // optional per-image dataset index
+  const float* w = nullptr;       // canonical fp32 weights [Cout][3][3][3] (rounded to bf16 in-kernel)
+  const float* bias = nullptr;
+  uint16_t* out = nullptr;       // bf16 bits
+  uint8_t* out_arg = nullptr;
+};
+bool u8conv_fwd_supported(const U8ConvParams& p);
+void u8conv_forward(const U8ConvParams& p, hipStream_t s);
 
 // Weight gradient of a large-image first conv (u8 input, C <= 3, 3x3, stride
 // 1, pad 1, fused ReLU + 2x2/2 max-pool, Cout <= 64), bf16 (conv0_dw.hip):
