@@ -2,6 +2,7 @@
 // as raw device pointers + HIP stream handles (torch's data_ptr() and
 // current_stream().cuda_stream), so this translation unit needs no torch
 // headers and the same engine serves the native drivers and Python.
+#include <cstring>
 #include <limits>
 #include <pybind11/numpy.h>
 #include <pybind11/pybind11.h>
@@ -263,6 +264,31 @@ PYBIND11_MODULE(_C, m) {
              for (int b = 0; b < B; ++b)
                for (int j = 0; j < nc; ++j) a.mutable_at(b, j) = tmp[(size_t)b * ld + j];
              return a;
+           })
+      .def("stage_output",
+           [](const GpuNet& n, int stage, int B) {
+             // (float32 copy of the stored activation, argmax bytes or None)
+             MCC_CHECK(B > 0 && B <= n.max_batch(), "stage_output: bad batch");
+             int64_t per = 0;
+             const uint8_t* arg = nullptr;
+             const void* y = n.stage_output(stage, per, &arg);
+             const size_t cnt = (size_t)B * per, es = n.dtype() == DType::BF16 ? 2 : 4;
+             std::vector<uint8_t> raw(cnt * es);
+             if (hipDeviceSynchronize() != hipSuccess) throw Error("hipDeviceSynchronize failed");
+             if (hipMemcpy(raw.data(), y, raw.size(), hipMemcpyDeviceToHost) != hipSuccess) throw Error("hipMemcpy failed");
+             py::array_t<float> a((py::ssize_t)cnt);
+             float* d = a.mutable_data();
+             for (size_t i = 0; i < cnt; ++i) {
+               if (es == 4) std::memcpy(d + i, raw.data() + 4 * i, 4);
+               else {
+                 const uint32_t bits = (uint32_t)(raw[2 * i] | (raw[2 * i + 1] << 8)) << 16;
+                 std::memcpy(d + i, &bits, 4);
+               }
+             }
+             if (!arg) return py::tuple(py::make_tuple(a, py::none()));
+             py::array_t<uint8_t> g((py::ssize_t)cnt);
+             if (hipMemcpy(g.mutable_data(), arg, cnt, hipMemcpyDeviceToHost) != hipSuccess) throw Error("hipMemcpy failed");
+             return py::tuple(py::make_tuple(a, g));
            })
       .def("get_stats",
            [](const GpuNet& n) {

@@ -1322,6 +1322,13 @@ void GpuNet::stage_param_range(int stage, int64_t& off, int64_t& count) const {
   count = st.nw + st.nb;
 }
 
+const void* GpuNet::stage_output(int stage, int64_t& per_sample, const uint8_t** argmax) const {
+  const Stage& st = *stages_.at(stage);
+  per_sample = st.out_elems;
+  if (argmax) *argmax = st.pooled ? st.arg_buf : nullptr;
+  return st.act_buf;
+}
+
 std::vector<GpuBucket> GpuNet::buckets(int64_t bucket_bytes) const {
   std::vector<GpuBucket> out;
   for (const Bucket& b : plan_buckets(spec_, bucket_bytes)) {

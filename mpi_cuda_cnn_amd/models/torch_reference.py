@@ -46,10 +46,19 @@ class TorchReference(nn.Module):
     it rounded to bf16, fp64 everywhere else (accumulation, logits,
     loss).  Fed the same rounded operands, the engine's per-channel errors
     are then only its fp32 accumulation order, so tests can bound them
-    tightly per output channel."""
+    tightly per output channel.
 
-    def __init__(self, spec, dtype=torch.float32, mimic_bf16=False):
+    ``u8_fp32_first``: the first layer's VALUE as the exact-integer u8 kernels
+    compute it -- the integer sum (exact), x (1/255) and + bias in fp32 --
+    while its gradient stays the fp64 one of conv(x/255).  Without it the
+    fp64 oracle and the fp32 scale land on different sides of a bf16
+    rounding boundary a few times per 10^5 activations, and in a batch of a
+    few images one flipped pool / ReLU decision moves a sparse channel's
+    gradient by O(0.1)."""
+
+    def __init__(self, spec, dtype=torch.float32, mimic_bf16=False, u8_fp32_first=False):
         super().__init__()
+        self.u8_fp32_first = u8_fp32_first
         self.spec = spec
         self.mimic_bf16 = mimic_bf16
         self.layer_info = spec.layers()
@@ -103,7 +112,14 @@ class TorchReference(nn.Module):
                 x = x.reshape(x.shape[0], -1)
             if self.mimic_bf16 and L["kind"] in ("conv", "fc"):
                 w, b = _RoundBF16Weight.apply(m.weight), m.bias
+                xin = x
                 x = (F.conv2d(x, w, b, m.stride, m.padding) if L["kind"] == "conv" else F.linear(x, w, b))
+                if i == 0 and self.u8_fp32_first and L["kind"] == "conv":
+                    with torch.no_grad():  # integer sum, then fp32 scale and bias (value only)
+                        s_int = F.conv2d(torch.round(xin * 255.0), w, None, m.stride, m.padding)
+                        v = (s_int.float() * torch.tensor(1.0 / 255.0, dtype=torch.float32)
+                             + b.detach().float().view(1, -1, 1, 1))
+                    x = x + (v.to(x.dtype) - x).detach()
             else:
                 x = m(x)
             if i == n - 1:

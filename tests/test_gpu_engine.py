@@ -426,11 +426,12 @@ _BIG_SPECS = {
 }
 
 
-def _oracle_bf16(spec, params, imgs, labels, round_input):
+def _oracle_bf16(spec, params, imgs, labels, round_input, u8_fp32_first=False):
     """fp64 oracle fed the engine's bf16 rounding points (TorchReference
     mimic_bf16); round_input: the first layer reads bf16(x/255) (the exact-
-    integer u8 paths read x/255 unrounded)."""
-    ref = TorchReference(spec, dtype=torch.float64, mimic_bf16=True)
+    integer u8 paths read x/255 unrounded); u8_fp32_first: the first layer's
+    value as the u8 RGB kernel forms it (integer sum, fp32 scale + bias)."""
+    ref = TorchReference(spec, dtype=torch.float64, mimic_bf16=True, u8_fp32_first=u8_fp32_first)
     ref.load_flat(torch.from_numpy(params.astype(np.float64)))
     x = images_to_nchw(imgs, torch.float64)
     if round_input:
@@ -515,8 +516,9 @@ def test_bf16_grads_per_channel_vs_rounded_oracle(cuda, model):
     net.backward_all(s)
     torch.cuda.synchronize()
     # exact-integer first layer: the single-channel pipelined conv (plan "fwd:s1")
-    round_input = "fwd:s1" not in plan
-    ref_logits, ref_grads = _oracle_bf16(spec, params, imgs, labels, round_input)
+    # or the u8 RGB row-worker forward (plan "u8fwd", with the row-staged dW)
+    round_input = "fwd:s1" not in plan and "u8fwd" not in plan
+    ref_logits, ref_grads = _oracle_bf16(spec, params, imgs, labels, round_input, u8_fp32_first="u8fwd" in plan)
     grads = net.get_grads()
     lerr = _relerr(net.get_logits(B), ref_logits)
     report = [f"{model}: logits {lerr:.2e} (round_input={round_input})"]
@@ -542,6 +544,81 @@ def test_bf16_grads_per_channel_vs_rounded_oracle(cuda, model):
     print("\n".join(report + [plan]))
     assert lerr < PER_CHANNEL_TOL["logit"], report[0]
     assert not bad, "\n".join(bad)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("hw,cout,B", [(32, 32, 24), (64, 64, 8), (80, 64, 6), (224, 64, 2)])
+def test_u8_first_layer_vs_oracle(cuda, hw, cout, B):
+    """u8 RGB first layer (conv_u8.hip forward, conv0_dw row-staged dW when
+    W % 32 == 0) in a one-conv net: conv 3x3 + ReLU + 2x2 pool -> fc.  The fc
+    weight gradient is the pooled activation x dY, so a wrong forward value,
+    pool decision or argmax shows per output channel there; the conv gradient
+    checks the dW kernel.  Oracle: fp64 with the engine's bf16 rounding points
+    and the exact-integer input (x/255 unrounded, as these kernels)."""
+    spec = mcc.parse_model_spec(f"input 3 {hw} {hw}; conv {cout} k3 s1 p1 relu; pool 2; fc 10 softmax", "u8one")
+    imgs, labels = mcc.synth_dataset(B, 3, hw, hw, 10, seed=5)
+    params = mcc.init_params(spec, seed=2).astype(np.float32)
+    net = mcc.GpuNet(spec, "bf16", B)
+    plan = net.plan()
+    assert "u8fwd" in plan, plan
+    net.set_params(params)
+    d_img = torch.from_numpy(imgs).to(cuda)
+    d_lab = torch.from_numpy(labels).to(cuda)
+    s = torch.cuda.current_stream().cuda_stream
+    net.zero_stats(s)
+    net.forward(d_img.data_ptr(), 0, B, s)
+    net.loss(d_lab.data_ptr(), 0, 1.0 / B, True, s)
+    net.backward_all(s)
+    torch.cuda.synchronize()
+    ref_logits, ref_grads = _oracle_bf16(spec, params, imgs, labels, round_input=False, u8_fp32_first=True)
+    grads = net.get_grads()
+    lerr = _relerr(net.get_logits(B), ref_logits)
+    report = [f"{hw}x{hw} C={cout}: logits {lerr:.2e}"]
+    for L in spec.layers():
+        if L["nweights"] == 0:
+            continue
+        for off, n, what in ((L["w_off"], L["nweights"], "W"), (L["b_off"], L["nbiases"], "b")):
+            e, c = _per_channel_err(grads[off : off + n], ref_grads[off : off + n], L["C"],
+                                    floor_frac=0.3 if what == "b" else 1e-2)
+            report.append(f"  {L['kind']} C={L['C']} {what}: {e:.2e} (channel {c})")
+            assert e < PER_CHANNEL_TOL[what], "\n".join(report + [plan])
+    print("\n".join(report))
+    assert lerr < PER_CHANNEL_TOL["logit"], report[0]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("hw,cout,B", [(32, 32, 9), (80, 64, 3), (224, 64, 2)])
+def test_u8_first_layer_output_matches_generic(cuda, hw, cout, B, monkeypatch):
+    """The u8 RGB first-layer forward (conv_u8.hip) vs the generic path of the
+    same net (MCC_AB=no_u8fwd: conv_small / the implicit GEMM), ELEMENTWISE on
+    the stored pooled activation and argmax.  The generic path rounds x/255 to
+    bf16 before the MFMA, the u8 kernel uses exact integers and scales the
+    fp32 sum, so values agree to bf16 rounding and the argmax everywhere but
+    (near-)ties."""
+    spec = mcc.parse_model_spec(f"input 3 {hw} {hw}; conv {cout} k3 s1 p1 relu; pool 2; fc 10 softmax", "u8one")
+    imgs, _ = mcc.synth_dataset(B, 3, hw, hw, 10, seed=7)
+    params = mcc.init_params(spec, seed=3).astype(np.float32)
+    d_img = torch.from_numpy(imgs).to(cuda)
+    s = torch.cuda.current_stream().cuda_stream
+    outs = []
+    for ab in ("", "no_u8fwd"):
+        monkeypatch.setenv("MCC_AB", ab)
+        net = mcc.GpuNet(spec, "bf16", B)
+        assert ("u8fwd" in net.plan()) == (ab == ""), net.plan()
+        net.set_params(params)
+        net.forward(d_img.data_ptr(), 0, B, s)
+        torch.cuda.synchronize()
+        outs.append(net.stage_output(0, B))
+        del net
+    (y, a), (y0, a0) = outs
+    d = np.abs(y - y0)
+    tol = 2 ** -7 * np.maximum(np.abs(y0), 1e-2)
+    bad = np.flatnonzero(d > tol)
+    assert bad.size == 0, (bad[:10], y[bad[:10]], y0[bad[:10]])
+    arg_diff = np.flatnonzero(a != a0)
+    # an argmax may differ only where the two pooled candidates nearly tie (or ReLU at ~0)
+    assert arg_diff.size <= max(2, a.size // 1000), (arg_diff.size, a.size, arg_diff[:10])
+    print(f"{hw}x{hw} C={cout}: max |dy| {d.max():.3e}, argmax differs at {arg_diff.size} of {a.size}")
 
 
 GENERIC_SPECS = {

@@ -1,6 +1,9 @@
 """Print the engine's per-stage kernel plan for a few model/dtype pairs (GPU box)."""
+import os
 import sys
-import mpi_cuda_cnn_amd as m
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", ".."))
+import mpi_cuda_cnn_amd as m  # noqa: E402
 
 pairs = [a.split(":") for a in sys.argv[1:]] or [("lenet5", "bf16"), ("lenet5", "fp32"), ("cifar3", "bf16"),
                                                  ("vgg11", "bf16")]
