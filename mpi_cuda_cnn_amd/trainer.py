@@ -8,6 +8,8 @@ inside the first conv kernel, so there is no host data path in the step.
 
 from __future__ import annotations
 
+import time
+
 import numpy as np
 import torch
 import torch.distributed as dist
@@ -102,6 +104,16 @@ def capture_step(fn):
     captured pointers: callers keep their buffers (batch indices, sampler
     counter) alive and fixed.  Run ``fn`` eagerly at least once before (code
     objects loaded, RCCL communicator set up)."""
+    torch.cuda.synchronize()
+    if dist.is_available() and dist.is_initialized() and dist.get_backend() == "nccl":
+        # The process-group watchdog polls the end events of the eager
+        # collectives (every ~100 ms) until it has seen them complete, and HIP
+        # fails that query once their RCCL stream is capturing
+        # (hipErrorCapturedEvent: the watchdog then aborts the process -- seen
+        # once on the LeNet-5 bench in round 3 with the event cache already
+        # off).  The eager step has finished (synchronize above), so one poll
+        # retires them: give the watchdog a few of its periods first.
+        time.sleep(1.0)
     g = torch.cuda.CUDAGraph()
     try:
         with torch.cuda.graph(g):
