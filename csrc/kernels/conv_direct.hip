@@ -27,6 +27,7 @@
 // reduced over the wave (shuffles), the workgroup (LDS) and the workgroups
 // (a parallel fixed-order slab sum): deterministic.
 #include "kernels.h"
+#include "mcc/ab.h"
 #include "mfma.h"
 
 #include <algorithm>
@@ -179,10 +180,18 @@ __global__ void __launch_bounds__(kDT) __attribute__((amdgpu_waves_per_eu(4))) c
       f2 acc[CP][4];  // TL, TR, BL, BR
 #pragma unroll
       for (int c = 0; c < CP; ++c) acc[c][0] = acc[c][1] = acc[c][2] = acc[c][3] = f2{0.f, 0.f};
+      // The weights are loop-invariant, and left alone the compiler hoists all
+      // of conv1's (150 floats) out of the item loop -- more than the SGPR
+      // file -- and spills them to VGPR lanes: 712 v_readlane per 300 packed
+      // FMAs (924 us at B = 131072).  An opaque copy of the pointer per item
+      // keeps them as scalar loads next to their use (549 us).  conv2's
+      // weights live inside the channel loop and are not hoisted.
+      const float* wtv = wt;
+      if constexpr (CIN == 1) asm volatile("" : "+s"(wtv));  // (conv2: measured 793 -> 1511 us with it)
       for (int ci = 0; ci < CIN; ++ci) {
         f2 P[KS + 1][(KS + 1) / 2];
         d_patch<KS, CIN>(xs + m * t.IMG, t.TW, py, px, ci, P);
-        const float* wc = wt + ci * KS * KS * COUT;  // wave-uniform: scalar loads
+        const float* wc = wtv + ci * KS * KS * COUT;  // wave-uniform: scalar loads
 #pragma unroll
         for (int kh = 0; kh < KS; ++kh) {
 #pragma unroll
@@ -321,6 +330,95 @@ __global__ void __launch_bounds__(kDT) __attribute__((amdgpu_waves_per_eu(2))) c
 #pragma unroll
     for (int w = 0; w < kDT / 64; ++w) v += red[w][i];
     p.slab[(size_t)blockIdx.x * ncol + i] = v;
+  }
+}
+
+// Single-channel first-layer weight gradient, C = 6, channel pairs split over
+// the waves: 384 threads, waves 2q and 2q+1 own channel pair q (26 packed
+// accumulators each instead of 78: 4 waves per SIMD instead of 2 and no
+// spills) and walk the group's items in halves.  The patch is re-read per
+// pair (18 ds_read_b64 per 100 packed FMAs, still VALU-bound).
+constexpr int kDSplitT = 384;
+template <int KS>
+__global__ void __launch_bounds__(kDSplitT) __attribute__((amdgpu_waves_per_eu(3))) conv1_direct_dw_split_kernel(Conv1DirectParams p) {
+  constexpr int KK = KS * KS, C = 6;
+  extern __shared__ __attribute__((aligned(16))) float xs[];
+  __shared__ float red[kDSplitT / 64][2 * (KK + 1)];
+  __shared__ int sidx[kDImgs];
+  const Tile t = d_tile(p);
+  const int PHW = p.PH * p.PW;
+  const int gsz = kDImgs * PHW * C;
+  float* dys = xs + kDImgs * t.IMG;
+  uint8_t* args = reinterpret_cast<uint8_t*>(dys + gsz);
+  for (int i = threadIdx.x; i < kDImgs * t.IMG; i += kDSplitT) xs[i] = 0.f;
+  const bool stager = threadIdx.x < kDT;
+  Stager sg;
+  if (stager) sg.init(p, t);
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int cp = wave >> 1, slot = (wave & 1) * 64 + lane;  // pair, item slot 0..127
+  const int ngroups = (p.N + kDImgs - 1) / kDImgs;
+  f2 acc[KK + 1];
+#pragma unroll
+  for (int k = 0; k <= KK; ++k) acc[k] = f2{0.f, 0.f};
+  for (int grp = blockIdx.x; grp < ngroups; grp += gridDim.x) {
+    const int img0 = grp * kDImgs, nimg = min(kDImgs, p.N - img0);
+    d_index(p, sidx, img0, nimg);
+    __syncthreads();
+    if (stager) sg.stage(p, t, xs, sidx, img0, nimg);
+    {
+      const int n4 = nimg * PHW * C / 4;
+      const float4* gdy = reinterpret_cast<const float4*>(p.dy + (size_t)img0 * PHW * C);
+      const uint32_t* garg = reinterpret_cast<const uint32_t*>(p.arg + (size_t)img0 * PHW * C);
+      for (int i = threadIdx.x; i < n4; i += kDSplitT) {
+        reinterpret_cast<float4*>(dys)[i] = gdy[i];
+        reinterpret_cast<uint32_t*>(args)[i] = garg[i];
+      }
+    }
+    __syncthreads();
+    for (int it = slot; it < nimg * PHW; it += 128) {
+      const int m = it / PHW, w = it - m * PHW;
+      const int py = w / p.PW, px = w - py * p.PW;
+      f2 P[KS + 1][(KS + 1) / 2];
+      d_patch<KS, 1>(xs + m * t.IMG, t.TW, py, px, 0, P);
+      const int o = it * C + 2 * cp;
+      const float2 gy = *reinterpret_cast<const float2*>(dys + o);
+      const int a0 = args[o], a1 = args[o + 1];
+      const f2 g0 = {a0 == 0 ? gy.x : 0.f, a1 == 0 ? gy.y : 0.f};
+      const f2 g1 = {a0 == 1 ? gy.x : 0.f, a1 == 1 ? gy.y : 0.f};
+      const f2 g2 = {a0 == 2 ? gy.x : 0.f, a1 == 2 ? gy.y : 0.f};
+      const f2 g3 = {a0 == 3 ? gy.x : 0.f, a1 == 3 ? gy.y : 0.f};
+#pragma unroll
+      for (int kh = 0; kh < KS; ++kh) {
+#pragma unroll
+        for (int kw = 0; kw < KS; ++kw) {
+          f2 v = acc[kh * KS + kw];
+          v = pfma(g0, MCC_PS(P[kh], kw), v);
+          v = pfma(g1, MCC_PS(P[kh], kw + 1), v);
+          v = pfma(g2, MCC_PS(P[kh + 1], kw), v);
+          v = pfma(g3, MCC_PS(P[kh + 1], kw + 1), v);
+          acc[kh * KS + kw] = v;
+        }
+      }
+      acc[KK] += f2{a0 < 4 ? gy.x : 0.f, a1 < 4 ? gy.y : 0.f};
+    }
+  }
+  // wave sums (fixed butterfly), the wave pair of a channel pair in order, then the slab
+#pragma unroll
+  for (int k = 0; k <= KK; ++k) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      float v = h ? acc[k].y : acc[k].x;
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+      if (lane == 0) red[wave][h * (KK + 1) + k] = v;
+    }
+  }
+  __syncthreads();
+  const int ncol = C * (KK + 1);
+  for (int i = threadIdx.x; i < ncol; i += kDSplitT) {
+    const int c = i / (KK + 1), k = i - c * (KK + 1);
+    const int q = c >> 1, h = c & 1;
+    p.slab[(size_t)blockIdx.x * ncol + i] = red[2 * q][h * (KK + 1) + k] + red[2 * q + 1][h * (KK + 1) + k];
   }
 }
 
@@ -626,7 +724,9 @@ void conv1_direct_dw(const Conv1DirectParams& p, float* gw, float* gb, hipStream
   MCC_CHECK(conv1_direct_dw_supported(p) && p.x && p.dy && p.arg && p.slab, "conv1_direct_dw: bad params");
   const int grid = direct_grid(p);
   const dim3 g((unsigned)grid), b(kDT);
-  if (p.KS == 5 && p.C == 6) hipLaunchKernelGGL((conv1_direct_dw_kernel<5, 6, true>), g, b, dw_lds(p), s, p);
+  if (p.KS == 5 && p.C == 6 && !ab_flag("no_dw1_split"))
+    hipLaunchKernelGGL((conv1_direct_dw_split_kernel<5>), g, dim3(kDSplitT), dw_lds(p), s, p);
+  else if (p.KS == 5 && p.C == 6) hipLaunchKernelGGL((conv1_direct_dw_kernel<5, 6, true>), g, b, dw_lds(p), s, p);
   else if (p.KS == 5) hipLaunchKernelGGL((conv1_direct_dw_kernel<5, kDMaxC, false>), g, b, dw_lds(p), s, p);
   else hipLaunchKernelGGL((conv1_direct_dw_kernel<3, kDMaxC, false>), g, b, dw_lds(p), s, p);
   dw_reduce(p, grid, gw, gb, s);
