@@ -520,20 +520,21 @@ __global__ void __launch_bounds__(kDT) __attribute__((amdgpu_waves_per_eu(4))) c
 // its channel row by row from LDS and does 2 x 25 x 4 packed FMAs.  Partial
 // sums: slots in a fixed order through LDS, then one slab per workgroup,
 // reduced by conv1_direct_dw_reduce_kernel (deterministic).
-constexpr int kWCG = 4;                    // channels per combination (two pairs)
 constexpr int kWImgs = 8;                  // images per group
-template <int CIN, int COUT>
+template <int CIN, int COUT, int NP>       // NP channel pairs per combination
 struct DwGeom {
-  static constexpr int combos = (COUT / kWCG) * CIN;
-  static constexpr int slots = 16;
+  static constexpr int cg = 2 * NP;        // channels per combination
+  static constexpr int combos = (COUT / cg) * CIN;
+  static constexpr int slots = 384 / combos;
   static constexpr int threads = combos * slots;
   static constexpr int ncol = COUT * (CIN * 25 + 1);
 };
-template <int KS, int CIN, int COUT>
-__global__ void __launch_bounds__((DwGeom<CIN, COUT>::threads)) __attribute__((amdgpu_waves_per_eu(3)))
+template <int KS, int CIN, int COUT, int NP>
+__global__ void __launch_bounds__((DwGeom<CIN, COUT, NP>::threads)) __attribute__((amdgpu_waves_per_eu(NP == 1 ? 4 : 3)))
 conv_direct_dw_kernel(Conv1DirectParams p) {
-  using G = DwGeom<CIN, COUT>;
-  static_assert(KS == 5 && COUT % kWCG == 0, "shape");
+  using G = DwGeom<CIN, COUT, NP>;
+  constexpr int kWCG = G::cg;
+  static_assert(KS == 5 && COUT % kWCG == 0 && (NP == 1 || NP == 2), "shape");
   constexpr int KK = KS * KS;
   extern __shared__ __attribute__((aligned(16))) float xs[];
   const int TW = p.W, IMG = p.H * p.W * CIN;  // NHWC input, no padding
@@ -542,10 +543,12 @@ conv_direct_dw_kernel(Conv1DirectParams p) {
   uint8_t* args = reinterpret_cast<uint8_t*>(dys + kWImgs * PHW * COUT);
   const int combo = threadIdx.x % G::combos, slot = threadIdx.x / G::combos;
   const int cg = combo / CIN, ci = combo - cg * CIN;
-  f2 acc[2][KK];
-  f2 accb[2] = {f2{0.f, 0.f}, f2{0.f, 0.f}};
+  f2 acc[NP][KK];
+  f2 accb[NP];
 #pragma unroll
-  for (int q = 0; q < 2; ++q)
+  for (int q = 0; q < NP; ++q) accb[q] = f2{0.f, 0.f};
+#pragma unroll
+  for (int q = 0; q < NP; ++q)
 #pragma unroll
     for (int k = 0; k < KK; ++k) acc[q][k] = f2{0.f, 0.f};
   const int ngroups = (p.N + kWImgs - 1) / kWImgs;
@@ -569,18 +572,14 @@ conv_direct_dw_kernel(Conv1DirectParams p) {
       const int m = it / PHW, w = it - m * PHW;
       const int py = w / p.PW, px = w - py * p.PW;
       const int o = it * COUT + cg * kWCG;
-      const float4 gy = *reinterpret_cast<const float4*>(dys + o);
-      const uint32_t a4 = *reinterpret_cast<const uint32_t*>(args + o);
-      const int a0 = a4 & 0xff, a1 = (a4 >> 8) & 0xff, a2 = (a4 >> 16) & 0xff, a3 = a4 >> 24;
-      f2 g[2][4];  // [pair][window position]
+      f2 g[NP][4];  // [pair][window position]
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        g[0][q] = f2{a0 == q ? gy.x : 0.f, a1 == q ? gy.y : 0.f};
-        g[1][q] = f2{a2 == q ? gy.z : 0.f, a3 == q ? gy.w : 0.f};
-      }
-      if (ci == 0) {
-        accb[0] += f2{a0 < 4 ? gy.x : 0.f, a1 < 4 ? gy.y : 0.f};
-        accb[1] += f2{a2 < 4 ? gy.z : 0.f, a3 < 4 ? gy.w : 0.f};
+      for (int q = 0; q < NP; ++q) {
+        const float2 gy = *reinterpret_cast<const float2*>(dys + o + 2 * q);
+        const int a0 = args[o + 2 * q], a1 = args[o + 2 * q + 1];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) g[q][e] = f2{a0 == e ? gy.x : 0.f, a1 == e ? gy.y : 0.f};
+        if (ci == 0) accb[q] += f2{a0 < 4 ? gy.x : 0.f, a1 < 4 ? gy.y : 0.f};
       }
       const float* x = xs + m * IMG + ((2 * py) * TW + 2 * px) * CIN + ci;
 #pragma unroll
@@ -589,7 +588,7 @@ conv_direct_dw_kernel(Conv1DirectParams p) {
 #pragma unroll
         for (int j = 0; j < (KS + 1) / 2; ++j) R[j] = f2{x[(r * TW + 2 * j) * CIN], x[(r * TW + 2 * j + 1) * CIN]};
 #pragma unroll
-        for (int q = 0; q < 2; ++q) {
+        for (int q = 0; q < NP; ++q) {
 #pragma unroll
           for (int kw = 0; kw < KS; ++kw) {
             if (r < KS) {
@@ -750,8 +749,12 @@ size_t conv_direct_dw_slab_bytes(const Conv1DirectParams& p) {
 void conv_direct_dw(const Conv1DirectParams& p, float* gw, float* gb, hipStream_t s) {
   MCC_CHECK(conv_direct_dw_supported(p) && p.xf && p.dy && p.arg && p.slab, "conv_direct_dw: bad params");
   const int grid = dw2_grid(p);
-  hipLaunchKernelGGL((conv_direct_dw_kernel<5, 6, 16>), dim3((unsigned)grid), dim3(DwGeom<6, 16>::threads),
-                     dw2_lds(p), s, p);
+  if (ab_flag("dw2_pairs2"))
+    hipLaunchKernelGGL((conv_direct_dw_kernel<5, 6, 16, 2>), dim3((unsigned)grid), dim3(DwGeom<6, 16, 2>::threads),
+                       dw2_lds(p), s, p);
+  else
+    hipLaunchKernelGGL((conv_direct_dw_kernel<5, 6, 16, 1>), dim3((unsigned)grid), dim3(DwGeom<6, 16, 1>::threads),
+                       dw2_lds(p), s, p);
   dw_reduce(p, grid, gw, gb, s);
 }
 
