@@ -71,6 +71,10 @@ struct GpuNet::Stage {
   // forward copy K-major) and the weight gradient on the implicit-GEMM dW
   // kernel as a 1x1 "conv" over the batch
   bool fc_big = false, fc_igdw = false;
+  // wide FC at a large batch (CIFAR-3conv FC1 2048 -> 256): forward / data
+  // gradient as a 1x1 implicit-GEMM "conv" over the batch (igemm.hip's
+  // 256-tile kernels) instead of the generic tiled GEMM
+  bool fc_ig = false, fc_igdx = false;
   void* conv_buf = nullptr;      // pre-pool conv output (big + pooled)
   void* dz_buf = nullptr;        // pre-activation gradient at conv-output size (big)
   // persistent pipelined kernels (bf16 small-image layers; geometry planned
@@ -361,6 +365,16 @@ void GpuNet::build() {
       if (st.kind == Stage::FC) st.in_ld = pv.kind == Stage::FC ? pv.out_ld : (int)pv.out_elems;
     }
     if (st.kind == Stage::FC) MCC_CHECK(st.in_ld % 8 == 0, "fc input leading dim must be a multiple of 8");
+    if (st.kind == Stage::FC && dtype_ == DType::BF16 && !st.last && !st.fc_big && !no_igemm_ &&
+        !ab_flag("no_fc_ig") && max_batch_ >= 8192 && st.Kin % 64 == 0 && st.Nout % 64 == 0 &&
+        st.in_ld == st.Kin && st.out_ld == st.Nout && !gpu::fc_supported(st.Nout, st.Kin)) {
+      st.fc_ig = gpu::igemm_conv_supported(st.Kin, st.Nout, 1);
+      // data gradient: pv's act' is a ReLU mask (FC) or nothing (conv: its staging applies it)
+      const Stage* pv = s > 0 ? stages_[s - 1] : nullptr;
+      st.fc_igdx = st.fc_ig && pv &&
+                   (pv->kind == Stage::CONV || pv->act == gpu::ACT_RELU || pv->act == gpu::ACT_NONE) &&
+                   gpu::igemm_conv_supported(st.Nout, st.Kin, 1);
+    }
     st.head = st.kind == Stage::FC && st.last && s > 0 && dtype_ == DType::BF16 && !no_head_ &&
               gpu::xent_head_supported(st.Nout, st.Kin, st.in_ld);
     // FC weight gradient on the implicit-GEMM dW kernel (a 1x1 "conv" over the
@@ -714,7 +728,8 @@ std::string GpuNet::plan() const {
       os << "\n";
     } else {
       os << "  [" << s << "] fc " << st.Kin << " -> " << st.Nout << (st.last ? " (logits)" : "")
-         << (st.permC ? " nhwc-flatten" : "") << "\n";
+         << (st.permC ? " nhwc-flatten" : "") << (st.fc_ig ? (st.fc_igdx ? " igemm[fwd dx]" : " igemm[fwd]") : "")
+         << "\n";
     }
   }
   return os.str();
@@ -897,6 +912,17 @@ void GpuNet::forward(const uint8_t* images, const int32_t* idx, int B, hipStream
       p.out = st.act_buf; p.out_arg = st.arg_buf;
       p.ablate = ablate_;
       gpu::conv_forward(dtype_, p, s);
+    } else if (st.fc_ig) {
+      const Stage& pv = *stages_[si - 1];
+      gpu::IgemmParams g;
+      g.B = B; g.H = 1; g.W = 1; g.C = st.Kin;
+      g.OH = 1; g.OW = 1; g.KS = 1; g.stride = 1; g.pad = 0;
+      g.M = B; g.N = st.Nout; g.K = st.Kin;
+      g.in = pv.act_buf;
+      g.w = static_cast<const char*>(packed_) + es * st.pk_fwd; g.ldw = r8(st.Kin);
+      g.bias = params_ + st.b_off; g.epi_bias_act = true; g.act = st.act;
+      g.out = st.act_buf; g.ldo = st.out_ld;
+      gpu::igemm_conv(g, s);
     } else if (dtype_ == DType::BF16 && !no_fc_ && gpu::fc_supported(st.Nout, st.Kin)) {
       const Stage& pv = *stages_[si - 1];
       gpu::FcParams p;
@@ -1263,7 +1289,18 @@ void GpuNet::backward(int hi, int lo, hipStream_t s) {
       gpu::dw_reduce(r, ws);
       }
       // data gradient
-      if (si > 0 && dtype_ == DType::BF16 && !no_fc_ && gpu::fc_supported(st.Kin, st.Nout)) {
+      if (si > 0 && st.fc_igdx) {
+        gpu::IgemmParams g;
+        g.B = B; g.H = 1; g.W = 1; g.C = st.Nout;
+        g.OH = 1; g.OW = 1; g.KS = 1; g.stride = 1; g.pad = 0;
+        g.M = B; g.N = st.Kin; g.K = st.Nout;
+        g.in = st.grad_buf;
+        g.w = static_cast<const char*>(packed_) + es * st.pk_dx; g.ldw = st.out_ld;  // W^T [Kin][out_ld]
+        g.epi_bias_act = false;
+        g.relu_mask = pv.kind == Stage::FC && pv.act == gpu::ACT_RELU ? pv.act_buf : nullptr;
+        g.out = pv.grad_buf; g.ldo = st.in_ld;
+        gpu::igemm_conv(g, s);
+      } else if (si > 0 && dtype_ == DType::BF16 && !no_fc_ && gpu::fc_supported(st.Kin, st.Nout)) {
         gpu::FcParams d;
         d.M = B; d.N = st.Kin; d.K = st.Nout;
         d.A = st.grad_buf; d.lda = st.out_ld;

@@ -320,6 +320,53 @@ def test_bench_batch_step_matches_small_batches(cuda):
 
 
 @pytest.mark.gpu
+def test_cifar3_bench_batch_matches_small_batches(cuda):
+    """CIFAR-3conv at bench.py's per-GPU batch (32,768 + a ragged tail): the
+    wide FC1 (2048 -> 256) runs its forward and data gradient on the 1x1
+    implicit-GEMM path there (plan "igemm[fwd dx]", batch >= 8192) and on the
+    tiled GEMM in 1,024-image chunks; logits and every layer's summed gradient
+    must agree (the chunked path is pinned to PyTorch by the other tests)."""
+    spec = mcc.make_model("cifar3")
+    B, b = 32768 + 37, 1024
+    imgs, labels = mcc.synth_dataset(B, 3, 32, 32, 10, seed=23)
+    params = mcc.init_params(spec, seed=6).astype(np.float32)
+    d_img = torch.from_numpy(imgs).to(cuda)
+    d_lab = torch.from_numpy(labels).to(cuda)
+    s = torch.cuda.current_stream().cuda_stream
+    big = mcc.GpuNet(spec, "bf16", B)
+    assert "igemm[fwd dx]" in big.plan(), big.plan()
+    big.set_params(params)
+    big.zero_stats(s)
+    big.forward(d_img.data_ptr(), 0, B, s)
+    big.loss(d_lab.data_ptr(), 0, 1.0 / B, True, s)
+    big.backward_all(s)
+    torch.cuda.synchronize()
+    logits, grads = big.get_logits(B), big.get_grads()
+    del big
+    small = mcc.GpuNet(spec, "bf16", b)
+    assert "igemm[fwd" not in small.plan()
+    small.set_params(params)
+    ref_logits = np.empty_like(logits)
+    ref_grads = np.zeros_like(grads, dtype=np.float64)
+    for i in range(0, B, b):
+        nb = min(b, B - i)
+        idx = torch.arange(i, i + nb, device=cuda, dtype=torch.int32)
+        small.forward(d_img.data_ptr(), idx.data_ptr(), nb, s)
+        small.loss(d_lab.data_ptr(), idx.data_ptr(), 1.0 / B, True, s)
+        small.backward_all(s)
+        torch.cuda.synchronize()
+        ref_logits[i : i + nb] = small.get_logits(nb)
+        ref_grads += small.get_grads()
+    assert _relerr(logits, ref_logits) < 1e-2
+    for L in spec.layers():
+        if L["nweights"] == 0:
+            continue
+        for off, n, what in ((L["w_off"], L["nweights"], "W"), (L["b_off"], L["nbiases"], "b")):
+            err = _relerr(grads[off : off + n], ref_grads[off : off + n])
+            assert err < 2e-2, f"layer {L['kind']} C={L['C']} {what} grad rel err {err:.3e}"
+
+
+@pytest.mark.gpu
 def test_vgg11_bench_batch_matches_small_batches(cuda):
     """VGG-11 at bench.py's default per-GPU batch (640: 95.7 % of the 32-bit
     activation-index bound) vs 64-image chunks: logits and every layer's
