@@ -28,14 +28,16 @@ METRIC = "images/sec (whole node), LeNet-5 MNIST-shaped, at 1/2/4/8 MI355X"
 # batch as the persistent conv kernels' per-step prologue/tail and the launch
 # chain amortise (round 1: 36.7 M img/s at 16,384 -> 45.3 M at 65,536 -> 47.3 M
 # at 131,072, profiles/lenet5_batch_sweep_r1g.txt; round 2 kernels: 59.1 M at
-# 65,536 -> 64.9 M at 131,072, profiles/batch_sweep_r2.txt).  131,072 is the
-# largest power of two under the engine's 32-bit activation-index bound
-# (B * 16 padded channels * 28 * 28 < 2^31).
+# 65,536 -> 64.9 M at 131,072, profiles/batch_sweep_r2.txt; round 3 fused
+# conv-block kernels: 109.3 M at 131,072, 111.2 M at 155,648, 112.6-113.2 M at
+# 163,840, 111.9-112.1 M at 167,936 / 170,496, profiles/batch_sweep_r3.txt).
+# The engine's 32-bit activation-index bound is B * 16 padded channels * 28 *
+# 28 < 2^31 (B < 171,196).
 # CIFAR-3conv: 1.88 M img/s at 4,096 -> 2.58 M at 16,384 (profiles/bench_models_r1g.jsonl);
 # round 2: 3.64 M at 16,384 -> 3.91 M at 32,768 (65,536 exceeds the 32-bit bound).
 # VGG-11: 15.0 k img/s at 256 -> 15.7 k at 512 -> 16.26 k at 640 (640 x 64 x 224^2 is 95.7 % of the
 # 32-bit activation bound; the 224^2 x 64 pre-pool conv1 tensor is never materialised).
-DEFAULT_BATCH = {"lenet5": 131072, "ref": 65536, "cifar3": 32768, "vgg11": 640}
+DEFAULT_BATCH = {"lenet5": 163840, "ref": 65536, "cifar3": 32768, "vgg11": 640}
 # models whose step is faster with the dW side stream (engine.cpp, measured A/B): none with the
 # round-2 kernels (CIFAR-3conv at 32768: 4.38 M img/s without, 4.27 M with; LeNet-5 / VGG-11 / ref
 # also faster without, profiles/side_stream_ab_r2.txt)
@@ -54,7 +56,7 @@ def main():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--model", default="lenet5")
-    ap.add_argument("--batch-per-gpu", type=int, default=0, help="default: per-model (131072 for LeNet-5)")
+    ap.add_argument("--batch-per-gpu", type=int, default=0, help="default: per-model (163840 for LeNet-5)")
     ap.add_argument("--dtype", default="bf16")
     ap.add_argument("--dataset", type=int, default=0,
                     help="synthetic samples resident per GPU (default 65536; 8 batches for large images)")

@@ -273,14 +273,14 @@ def test_vgg11_step_runs(cuda):
 
 @pytest.mark.gpu
 def test_bench_batch_step_matches_small_batches(cuda):
-    """bench.py's per-GPU batch (131,072, plus a ragged tail): the persistent
+    """bench.py's per-GPU batch (163,840, plus a ragged tail): the persistent
     kernels' many-group loops and 32-bit activation offsets at full size must
     give the same logits and summed gradients as 1,024-image chunks through
     the small-batch path (which test_step_matches_torch pins to PyTorch).
     A PyTorch reference at this size would spend minutes in MIOpen's first
     backward-convolution search on a fresh box."""
     spec = mcc.make_model("lenet5")
-    B, b = 131072 + 37, 2048
+    B, b = 163840 + 37, 2048
     imgs, labels = mcc.synth_dataset(B, 1, 28, 28, 10, seed=21)
     params = mcc.init_params(spec, seed=4).astype(np.float32)
     d_img = torch.from_numpy(imgs).to(cuda)
