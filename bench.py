@@ -34,10 +34,14 @@ METRIC = "images/sec (whole node), LeNet-5 MNIST-shaped, at 1/2/4/8 MI355X"
 # The engine's 32-bit activation-index bound is B * 16 padded channels * 28 *
 # 28 < 2^31 (B < 171,196).
 # CIFAR-3conv: 1.88 M img/s at 4,096 -> 2.58 M at 16,384 (profiles/bench_models_r1g.jsonl);
-# round 2: 3.64 M at 16,384 -> 3.91 M at 32,768 (65,536 exceeds the 32-bit bound).
+# round 2: 3.64 M at 16,384 -> 3.91 M at 32,768 (65,536 exceeds the 32-bit bound);
+# round 3: 5.47 M at 32,768, 5.57-5.59 M at 49,152, 5.59 M at 57,344, 5.61 M at
+# 61,440, 5.64 M at 65,000 -> 65,024 (just under the B * 32 * 32 * 32 < 2^31 bound).
+# reference CNN, round 3 fused block: 50.6 M at 65,536, 55.7 M at 131,072, 56.3 M at
+# 163,840 (profiles/batch_sweep_r3.txt).
 # VGG-11: 15.0 k img/s at 256 -> 15.7 k at 512 -> 16.26 k at 640 (640 x 64 x 224^2 is 95.7 % of the
 # 32-bit activation bound; the 224^2 x 64 pre-pool conv1 tensor is never materialised).
-DEFAULT_BATCH = {"lenet5": 163840, "ref": 65536, "cifar3": 32768, "vgg11": 640}
+DEFAULT_BATCH = {"lenet5": 163840, "ref": 163840, "cifar3": 65024, "vgg11": 640}
 # models whose step is faster with the dW side stream (engine.cpp, measured A/B): none with the
 # round-2 kernels (CIFAR-3conv at 32768: 4.38 M img/s without, 4.27 M with; LeNet-5 / VGG-11 / ref
 # also faster without, profiles/side_stream_ab_r2.txt)

@@ -321,13 +321,13 @@ def test_bench_batch_step_matches_small_batches(cuda):
 
 @pytest.mark.gpu
 def test_cifar3_bench_batch_matches_small_batches(cuda):
-    """CIFAR-3conv at bench.py's per-GPU batch (32,768 + a ragged tail): the
+    """CIFAR-3conv at bench.py's per-GPU batch (65,024 + a ragged tail): the
     wide FC1 (2048 -> 256) runs its forward and data gradient on the 1x1
     implicit-GEMM path there (plan "igemm[fwd dx]", batch >= 8192) and on the
     tiled GEMM in 1,024-image chunks; logits and every layer's summed gradient
     must agree (the chunked path is pinned to PyTorch by the other tests)."""
     spec = mcc.make_model("cifar3")
-    B, b = 32768 + 37, 1024
+    B, b = 65024 + 37, 1024
     imgs, labels = mcc.synth_dataset(B, 3, 32, 32, 10, seed=23)
     params = mcc.init_params(spec, seed=6).astype(np.float32)
     d_img = torch.from_numpy(imgs).to(cuda)
