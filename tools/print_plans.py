@@ -2,7 +2,7 @@
 import os
 import sys
 
-sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", ".."))
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
 import mpi_cuda_cnn_amd as m  # noqa: E402
 
 pairs = [a.split(":") for a in sys.argv[1:]] or [("lenet5", "bf16"), ("lenet5", "fp32"), ("cifar3", "bf16"),
