@@ -63,17 +63,18 @@ constexpr int kDU8Items = 8;  // u8 items per thread: kDImgs * H * W / 4 <= 8 * 
 // (each item packed in one register -- source offset (10 bits), LDS offset
 // (14 bits), image + 1 (4 bits, 0: no item) -- to keep the per-thread table
 // at 8 registers in the register-hungry accumulator kernels)
-struct Stager {
+template <int NT, int NIMG>  // threads, images per group
+struct StagerT {
   uint32_t it[kDU8Items];
   __device__ __forceinline__ void init(const Conv1DirectParams& p, const Tile& t) {
     const int wq = p.W >> 2, per = p.H * wq;
 #pragma unroll
     for (int i = 0; i < kDU8Items; ++i) {
-      const int e = threadIdx.x + i * kDT;
+      const int e = threadIdx.x + i * NT;
       const int m = e / per, r = e - m * per;
       const int y = r / wq, xq = r - y * wq;
       const uint32_t src = y * p.W + 4 * xq, dst = m * t.IMG + (y + p.pad) * t.TW + 4 * xq + p.pad;
-      it[i] = m < kDImgs ? src | dst << 10 | (uint32_t)(m + 1) << 24 : 0u;
+      it[i] = m < NIMG ? src | dst << 10 | (uint32_t)(m + 1) << 24 : 0u;
     }
   }
   __device__ __forceinline__ void stage(const Conv1DirectParams& p, const Tile& t, float* xs, const int* sidx,
@@ -81,7 +82,7 @@ struct Stager {
     if (p.xf) {
       const int n4 = nimg * t.IMG / 4;
       const float4* g = reinterpret_cast<const float4*>(p.xf + (size_t)img0 * t.IMG);
-      for (int i = threadIdx.x; i < n4; i += kDT) reinterpret_cast<float4*>(xs)[i] = g[i];
+      for (int i = threadIdx.x; i < n4; i += NT) reinterpret_cast<float4*>(xs)[i] = g[i];
       return;
     }
     const float sc = 1.0f / 255.0f;
@@ -102,6 +103,7 @@ struct Stager {
     }
   }
 };
+using Stager = StagerT<kDT, kDImgs>;
 // the packed fields' ranges (host check)
 __host__ __device__ inline bool stager_fits(const Conv1DirectParams& p, const Tile& t) {
   return p.H * p.W <= 1024 && kDImgs * t.IMG <= 16384 && p.W % 4 == 0 && p.pad % 2 == 0 &&
@@ -333,49 +335,49 @@ __global__ void __launch_bounds__(kDT) __attribute__((amdgpu_waves_per_eu(2))) c
   }
 }
 
-// Single-channel first-layer weight gradient, C = 6, channel pairs split over
-// the waves: 384 threads, waves 2q and 2q+1 own channel pair q (26 packed
-// accumulators each instead of 78: 4 waves per SIMD instead of 2 and no
-// spills) and walk the group's items in halves.  The patch is re-read per
-// pair (18 ds_read_b64 per 100 packed FMAs, still VALU-bound).
-constexpr int kDSplitT = 384;
+// Single-channel first-layer weight gradient, C = 6, one WAVE per channel
+// pair (192 threads; 26 packed accumulators per thread instead of 78: no
+// spills, 3 waves per SIMD) and 4 images per group: 39.5 KB of LDS, so 4
+// workgroups share a CU and one workgroup's staging barriers are covered by
+// the other three.  Measured at B = 163840: 944 us; the all-pairs kernel
+// below 1,237 us at 131072; a 384-thread pair split with 8-image groups (79
+// KB, 2 workgroups per CU) 1,145 us.  The patch is re-read per pair (18
+// ds_read_b64 per 100 packed FMAs, still VALU-bound).
+constexpr int kDW3T = 192, kDW3Imgs = 4;
 template <int KS>
-__global__ void __launch_bounds__(kDSplitT) __attribute__((amdgpu_waves_per_eu(3))) conv1_direct_dw_split_kernel(Conv1DirectParams p) {
+__global__ void __launch_bounds__(kDW3T) __attribute__((amdgpu_waves_per_eu(3))) conv1_direct_dw_w3_kernel(Conv1DirectParams p) {
   constexpr int KK = KS * KS, C = 6;
   extern __shared__ __attribute__((aligned(16))) float xs[];
-  __shared__ float red[kDSplitT / 64][2 * (KK + 1)];
-  __shared__ int sidx[kDImgs];
+  __shared__ float red[3][2 * (KK + 1)];
+  __shared__ int sidx[kDW3Imgs];
   const Tile t = d_tile(p);
   const int PHW = p.PH * p.PW;
-  const int gsz = kDImgs * PHW * C;
-  float* dys = xs + kDImgs * t.IMG;
-  uint8_t* args = reinterpret_cast<uint8_t*>(dys + gsz);
-  for (int i = threadIdx.x; i < kDImgs * t.IMG; i += kDSplitT) xs[i] = 0.f;
-  const bool stager = threadIdx.x < kDT;
-  Stager sg;
-  if (stager) sg.init(p, t);
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int cp = wave >> 1, slot = (wave & 1) * 64 + lane;  // pair, item slot 0..127
-  const int ngroups = (p.N + kDImgs - 1) / kDImgs;
+  float* dys = xs + kDW3Imgs * t.IMG;
+  uint8_t* args = reinterpret_cast<uint8_t*>(dys + kDW3Imgs * PHW * C);
+  for (int i = threadIdx.x; i < kDW3Imgs * t.IMG; i += kDW3T) xs[i] = 0.f;
+  StagerT<kDW3T, kDW3Imgs> sg;
+  sg.init(p, t);
+  const int cp = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int ngroups = (p.N + kDW3Imgs - 1) / kDW3Imgs;
   f2 acc[KK + 1];
 #pragma unroll
   for (int k = 0; k <= KK; ++k) acc[k] = f2{0.f, 0.f};
   for (int grp = blockIdx.x; grp < ngroups; grp += gridDim.x) {
-    const int img0 = grp * kDImgs, nimg = min(kDImgs, p.N - img0);
-    d_index(p, sidx, img0, nimg);
+    const int img0 = grp * kDW3Imgs, nimg = min(kDW3Imgs, p.N - img0);
+    if ((int)threadIdx.x < nimg) sidx[threadIdx.x] = p.idx ? p.idx[img0 + threadIdx.x] : img0 + threadIdx.x;
     __syncthreads();
-    if (stager) sg.stage(p, t, xs, sidx, img0, nimg);
+    sg.stage(p, t, xs, sidx, img0, nimg);
     {
       const int n4 = nimg * PHW * C / 4;
       const float4* gdy = reinterpret_cast<const float4*>(p.dy + (size_t)img0 * PHW * C);
       const uint32_t* garg = reinterpret_cast<const uint32_t*>(p.arg + (size_t)img0 * PHW * C);
-      for (int i = threadIdx.x; i < n4; i += kDSplitT) {
+      for (int i = threadIdx.x; i < n4; i += kDW3T) {
         reinterpret_cast<float4*>(dys)[i] = gdy[i];
         reinterpret_cast<uint32_t*>(args)[i] = garg[i];
       }
     }
     __syncthreads();
-    for (int it = slot; it < nimg * PHW; it += 128) {
+    for (int it = lane; it < nimg * PHW; it += 64) {
       const int m = it / PHW, w = it - m * PHW;
       const int py = w / p.PW, px = w - py * p.PW;
       f2 P[KS + 1][(KS + 1) / 2];
@@ -402,7 +404,6 @@ __global__ void __launch_bounds__(kDSplitT) __attribute__((amdgpu_waves_per_eu(3
       acc[KK] += f2{a0 < 4 ? gy.x : 0.f, a1 < 4 ? gy.y : 0.f};
     }
   }
-  // wave sums (fixed butterfly), the wave pair of a channel pair in order, then the slab
 #pragma unroll
   for (int k = 0; k <= KK; ++k) {
 #pragma unroll
@@ -410,15 +411,14 @@ __global__ void __launch_bounds__(kDSplitT) __attribute__((amdgpu_waves_per_eu(3
       float v = h ? acc[k].y : acc[k].x;
 #pragma unroll
       for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
-      if (lane == 0) red[wave][h * (KK + 1) + k] = v;
+      if (lane == 0) red[cp][h * (KK + 1) + k] = v;
     }
   }
   __syncthreads();
   const int ncol = C * (KK + 1);
-  for (int i = threadIdx.x; i < ncol; i += kDSplitT) {
+  for (int i = threadIdx.x; i < ncol; i += kDW3T) {
     const int c = i / (KK + 1), k = i - c * (KK + 1);
-    const int q = c >> 1, h = c & 1;
-    p.slab[(size_t)blockIdx.x * ncol + i] = red[2 * q][h * (KK + 1) + k] + red[2 * q + 1][h * (KK + 1) + k];
+    p.slab[(size_t)blockIdx.x * ncol + i] = red[c >> 1][(c & 1) * (KK + 1) + k];
   }
 }
 
@@ -698,8 +698,11 @@ static int direct_grid(const Conv1DirectParams& p) {
   return std::max(1, std::min(ngroups, 256 * 4));
 }
 
+static int dw3_grid(const Conv1DirectParams& p) {
+  return std::max(1, std::min((p.N + kDW3Imgs - 1) / kDW3Imgs, 256 * 4));
+}
 size_t conv1_direct_slab_bytes(const Conv1DirectParams& p) {
-  return (size_t)direct_grid(p) * p.C * (p.KS * p.KS + 1) * 4;
+  return (size_t)std::max(direct_grid(p), dw3_grid(p)) * p.C * (p.KS * p.KS + 1) * 4;
 }
 
 void conv_direct_forward(const Conv1DirectParams& p, hipStream_t s) {
@@ -723,8 +726,13 @@ void conv1_direct_dw(const Conv1DirectParams& p, float* gw, float* gb, hipStream
   MCC_CHECK(conv1_direct_dw_supported(p) && p.x && p.dy && p.arg && p.slab, "conv1_direct_dw: bad params");
   const int grid = direct_grid(p);
   const dim3 g((unsigned)grid), b(kDT);
-  if (p.KS == 5 && p.C == 6 && !ab_flag("no_dw1_split"))
-    hipLaunchKernelGGL((conv1_direct_dw_split_kernel<5>), g, dim3(kDSplitT), dw_lds(p), s, p);
+  if (p.KS == 5 && p.C == 6 && !ab_flag("no_dw1_split")) {
+    const int g3 = dw3_grid(p);
+    const size_t lds = (size_t)kDW3Imgs * d_tile(p).IMG * 4 + (size_t)kDW3Imgs * p.PH * p.PW * p.C * 5;
+    hipLaunchKernelGGL((conv1_direct_dw_w3_kernel<5>), dim3((unsigned)g3), dim3(kDW3T), lds, s, p);
+    dw_reduce(p, g3, gw, gb, s);
+    return;
+  }
   else if (p.KS == 5 && p.C == 6) hipLaunchKernelGGL((conv1_direct_dw_kernel<5, 6, true>), g, b, dw_lds(p), s, p);
   else if (p.KS == 5) hipLaunchKernelGGL((conv1_direct_dw_kernel<5, kDMaxC, false>), g, b, dw_lds(p), s, p);
   else hipLaunchKernelGGL((conv1_direct_dw_kernel<3, kDMaxC, false>), g, b, dw_lds(p), s, p);
