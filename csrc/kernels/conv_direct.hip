@@ -520,12 +520,16 @@ __global__ void __launch_bounds__(kDT) __attribute__((amdgpu_waves_per_eu(4))) c
 // its channel row by row from LDS and does 2 x 25 x 4 packed FMAs.  Partial
 // sums: slots in a fixed order through LDS, then one slab per workgroup,
 // reduced by conv1_direct_dw_reduce_kernel (deterministic).
-constexpr int kWImgs = 8;                  // images per group
+// (4-image groups in 192-thread workgroups: 27 KB of LDS, 5 workgroups per
+// CU cover each other's staging barriers: 1,427 us at B = 163840 vs 1,562
+// with 8-image groups in 384-thread workgroups)
+constexpr int kWImgs = 4;                  // images per group
+constexpr int kWThreads = 192;
 template <int CIN, int COUT, int NP>       // NP channel pairs per combination
 struct DwGeom {
   static constexpr int cg = 2 * NP;        // channels per combination
   static constexpr int combos = (COUT / cg) * CIN;
-  static constexpr int slots = 384 / combos;
+  static constexpr int slots = kWThreads / combos;
   static constexpr int threads = combos * slots;
   static constexpr int ncol = COUT * (CIN * 25 + 1);
 };
@@ -744,7 +748,7 @@ static size_t dw2_lds(const Conv1DirectParams& p) {
   return (size_t)kWImgs * (p.H * p.W * p.Cin * 4 + p.PH * p.PW * p.C * 5);
 }
 static int dw2_grid(const Conv1DirectParams& p) {
-  return std::max(1, std::min((p.N + kWImgs - 1) / kWImgs, 256 * 2));
+  return std::max(1, std::min((p.N + kWImgs - 1) / kWImgs, 256 * 5));
 }
 bool conv_direct_dw_supported(const Conv1DirectParams& p) {
   return p.KS == 5 && p.pad == 0 && p.Cin == 6 && p.C == 16 && p.OH == p.H - 4 && p.OW == p.W - 4 &&
