@@ -320,21 +320,22 @@ def test_bench_batch_step_matches_small_batches(cuda):
 
 
 @pytest.mark.gpu
-def test_cifar3_bench_batch_matches_small_batches(cuda):
-    """CIFAR-3conv at bench.py's per-GPU batch (65,024 + a ragged tail): the
-    wide FC1 (2048 -> 256) runs its forward and data gradient on the 1x1
-    implicit-GEMM path there (plan "igemm[fwd dx]", batch >= 8192) and on the
-    tiled GEMM in 1,024-image chunks; logits and every layer's summed gradient
-    must agree (the chunked path is pinned to PyTorch by the other tests)."""
-    spec = mcc.make_model("cifar3")
-    B, b = 65024 + 37, 1024
-    imgs, labels = mcc.synth_dataset(B, 3, 32, 32, 10, seed=23)
+@pytest.mark.parametrize("model,B,b,fc_plan", [("cifar3", 65024 + 37, 1024, "igemm[fwd dx]")])
+def test_fc_igemm_bench_batch_matches_small_batches(cuda, model, B, b, fc_plan):
+    """CIFAR-3conv at bench.py's per-GPU batch (+ a ragged tail): the wide FC1
+    (2048 -> 256) runs on the 1x1 implicit-GEMM path there (batch >= 8192)
+    and on the tiled GEMM in small chunks; logits and every layer's summed
+    gradient must agree (the chunked path is pinned to PyTorch by the other
+    tests)."""
+    spec = mcc.make_model(model)
+    C, H, W = spec.input_shape()
+    imgs, labels = mcc.synth_dataset(B, C, H, W, 10, seed=23)
     params = mcc.init_params(spec, seed=6).astype(np.float32)
     d_img = torch.from_numpy(imgs).to(cuda)
     d_lab = torch.from_numpy(labels).to(cuda)
     s = torch.cuda.current_stream().cuda_stream
     big = mcc.GpuNet(spec, "bf16", B)
-    assert "igemm[fwd dx]" in big.plan(), big.plan()
+    assert fc_plan in big.plan(), big.plan()
     big.set_params(params)
     big.zero_stats(s)
     big.forward(d_img.data_ptr(), 0, B, s)
