@@ -54,6 +54,22 @@ def metric_for(model):
     return METRIC if model == "lenet5" else f"images/sec (whole node), {model}, at 1/2/4/8 MI355X"
 
 
+def _self_launch(n: int) -> int:
+    """Run this script under torch.distributed.run with n ranks on this node
+    (rendezvous on 127.0.0.1, a free port) as a child process; rank 0's JSON
+    line reaches our stdout directly.  Returns the launcher's exit code."""
+    import socket
+    import subprocess
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    print(f"bench: launching {n} ranks: {' '.join(cmd)}", file=sys.stderr, flush=True)
+    return subprocess.run(cmd, env=dict(os.environ, MASTER_ADDR="127.0.0.1")).returncode
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -83,14 +99,21 @@ def main():
                          "contention (profiles/comm_contention_r3.txt)")
     args = ap.parse_args()
 
-    import torch
-    import torch.distributed as dist
-
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # `python bench.py --gpus N` without a launcher: start one rank per GPU
+        # as CHILD processes (before this process touches the GPU) and relay
+        # their result -- never silently measure one rank for an N-GPU request
+        return _self_launch(args.gpus)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and rank == 0:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    if world != args.gpus:
+        raise SystemExit(f"bench: --gpus {args.gpus} but WORLD_SIZE={world}: the JSON line would not describe "
+                         "the requested run")
+
+    import torch
+    import torch.distributed as dist
+
     ndev = torch.cuda.device_count()  # (counting does not initialise the GPU)
     if args.dist_backend == "nccl" and world > ndev:
         raise SystemExit(f"bench: {world} ranks but {ndev} GPU(s): RCCL needs one GPU per rank (--dist-backend gloo "
@@ -234,4 +257,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

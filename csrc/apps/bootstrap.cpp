@@ -11,6 +11,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <memory>
+#include <set>
 #include <thread>
 
 #include "mcc/common.h"
@@ -19,6 +20,7 @@ namespace mcc {
 namespace {
 
 using Clock = std::chrono::steady_clock;
+constexpr int32_t kHelloMagic = 0x4243434d;  // "MCCB"
 
 int env_int(const char* name, int dflt) {
   const char* v = std::getenv(name);
@@ -84,19 +86,29 @@ void serve_blob(const void* blob, size_t n, int clients, const BootstrapAddr& ad
   sa.sin_port = htons((uint16_t)addr.port);
   if (::bind(srv.fd, reinterpret_cast<sockaddr*>(&sa), sizeof(sa)) != 0 || ::listen(srv.fd, clients + 4) != 0)
     throw Error("bootstrap: cannot listen on port " + std::to_string(addr.port));
-  for (int served = 0; served < clients;) {
+  // A client first sends {kHelloMagic, rank}; only a well-formed hello from
+  // a rank in [1, clients] that has not been served yet counts.  A stray
+  // connection (no or a malformed hello) is dropped without the blob, and a
+  // rank that reconnects (e.g. after its own receive timed out) gets the blob
+  // again without taking another rank's slot.
+  std::set<int32_t> served;
+  while ((int)served.size() < clients) {
     pollfd pf{srv.fd, POLLIN, 0};
     const int left = ms_left(deadline);
     if (left <= 0 || ::poll(&pf, 1, left) <= 0)
-      throw Error("bootstrap: timed out waiting for ranks (" + std::to_string(served) + " of " +
+      throw Error("bootstrap: timed out waiting for ranks (" + std::to_string(served.size()) + " of " +
                   std::to_string(clients) + " served)");
     Fd c(::accept(srv.fd, nullptr, nullptr));
     if (c.fd < 0) continue;
-    if (send_all(c.fd, static_cast<const char*>(blob), n)) ++served;
+    int32_t hello[2] = {0, -1};
+    const auto hello_deadline = std::min(deadline, Clock::now() + std::chrono::seconds(5));
+    if (!recv_all(c.fd, reinterpret_cast<char*>(hello), sizeof(hello), hello_deadline)) continue;
+    if (hello[0] != kHelloMagic || hello[1] < 1 || hello[1] > clients) continue;
+    if (send_all(c.fd, static_cast<const char*>(blob), n)) served.insert(hello[1]);
   }
 }
 
-void fetch_blob(void* blob, size_t n, const BootstrapAddr& addr) {
+void fetch_blob(void* blob, size_t n, int rank, const BootstrapAddr& addr) {
   const auto deadline = Clock::now() + std::chrono::milliseconds((long long)(addr.timeout_s * 1000));
   addrinfo hints{}, *res = nullptr;
   hints.ai_family = AF_INET;
@@ -107,7 +119,9 @@ void fetch_blob(void* blob, size_t n, const BootstrapAddr& addr) {
   while (true) {
     {
       Fd fd(::socket(AF_INET, SOCK_STREAM, 0));
+      const int32_t hello[2] = {kHelloMagic, (int32_t)rank};
       if (fd.fd >= 0 && ::connect(fd.fd, res->ai_addr, res->ai_addrlen) == 0 &&
+          send_all(fd.fd, reinterpret_cast<const char*>(hello), sizeof(hello)) &&
           recv_all(fd.fd, static_cast<char*>(blob), n, deadline))
         return;
     }

@@ -22,19 +22,21 @@ struct BootstrapAddr {
 // MCC_BOOTSTRAP_TIMEOUT (seconds, default 300).
 BootstrapAddr bootstrap_addr_from_env();
 
-// Rank 0: accept `clients` connections on addr.port and send each the n-byte
-// blob.  Throws mcc::Error if they have not all been served by the deadline.
+// Rank 0: serve the n-byte blob to ranks 1..clients on addr.port.  Each
+// client identifies itself with its rank first; stray or duplicate
+// connections do not count.  Throws mcc::Error if not every rank has been
+// served by the deadline.
 void serve_blob(const void* blob, size_t n, int clients, const BootstrapAddr& addr);
 
-// Other ranks: connect to addr (retrying until the deadline) and receive the
-// n-byte blob.  Throws mcc::Error on timeout.
-void fetch_blob(void* blob, size_t n, const BootstrapAddr& addr);
+// Other ranks: connect to addr (retrying until the deadline), send this
+// rank's id and receive the n-byte blob.  Throws mcc::Error on timeout.
+void fetch_blob(void* blob, size_t n, int rank, const BootstrapAddr& addr);
 
 // Collective form: rank 0 serves `blob` (already filled), others receive it.
 inline void bootstrap_blob(void* blob, size_t n, int rank, int world, const BootstrapAddr& addr) {
   if (world <= 1) return;
   if (rank == 0) serve_blob(blob, n, world - 1, addr);
-  else fetch_blob(blob, n, addr);
+  else fetch_blob(blob, n, rank, addr);
 }
 
 }  // namespace mcc

@@ -42,6 +42,10 @@ struct CliArgs {
   bool quiet = false;
   int64_t synthetic = 0;    // --synthetic N: generated data instead of IDX files
   std::string comm = "rccl";  // cnn_dist: rccl | host (several ranks on one GPU) | local (world 1)
+  // GPU drivers: "random" = rand() % N semantics within the rank's shard
+  // (cnn.c:455, cnnmpi.c:457-458); "seq" = sequential global batches split
+  // over the ranks, so a world-N run sees exactly the batches of one process
+  std::string sampler = "random";
 };
 
 inline void usage(const char* prog) {
@@ -52,6 +56,7 @@ inline void usage(const char* prog) {
                "  [--ref-compat] [--fp32] [--save W] [--load W] [--max-train N]\n"
                "  [--bucket-mb MB] [--log-every N] [--profile] [--no-graph] [--json PATH|-]\n"
                "  [--comm rccl|host|local]   (cnn_dist: RCCL; host shared memory for several ranks\n"
+               "  [--sampler random|seq]     (GPU: rand() %% N per rank shard, or sequential global batches)\n"
                "                             on one GPU; no collectives at world 1)\n"
                "  [--synthetic N]   (no IDX files: N generated training images, N/5 test images\n"
                "                     of the model's input shape; positional paths optional)\n",
@@ -88,6 +93,7 @@ inline int parse_cli(int argc, char** argv, CliArgs& a) {
     else if (s == "--no-graph") a.no_graph = true;
     else if (s == "--quiet") a.quiet = true;
     else if (s == "--comm") a.comm = next();
+    else if (s == "--sampler") a.sampler = next();
     else if (s == "-h" || s == "--help") { usage(argv[0]); std::exit(0); }
     else if (s.size() > 2 && s[0] == '-' && s[1] == '-') { usage(argv[0]); std::exit(100); }
     else pos.push_back(s);
@@ -102,6 +108,7 @@ inline int parse_cli(int argc, char** argv, CliArgs& a) {
   a.train_images = pos[0]; a.train_labels = pos[1]; a.test_images = pos[2]; a.test_labels = pos[3];
   if (a.batch < 1) a.batch = 1;
   if (a.log_every < 1) a.log_every = 1000;
+  if (a.sampler != "random" && a.sampler != "seq") { usage(argv[0]); std::exit(100); }
   return 0;
 }
 

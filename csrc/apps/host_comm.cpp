@@ -39,13 +39,20 @@ struct HostComm : Comm {
     Kind kind;
     size_t bytes;
     int root;
+    std::atomic<bool> done{false};  // eager ops: the host function has run (slot reusable)
+    Op(HostComm* c_, Kind k, size_t b, int r) : c(c_), kind(k), bytes(b), root(r) {}
   };
 
   int rank_, world_, local_;
   std::unique_ptr<ShmGroup> g_;
   char* in_ = nullptr;   // pinned staging: device -> host
   char* out_ = nullptr;  // pinned staging: host -> device
-  std::deque<Op> ops_;   // stable addresses: a replayed graph calls the same host nodes again
+  // Host-node arguments need stable addresses.  Ops recorded into a graph
+  // are kept for the communicator's lifetime (every replay calls the same
+  // host nodes again); eager ops are released once their host function has
+  // run, so an eager run (--no-graph, --profile) does not grow this per step.
+  std::deque<Op> graph_ops_;
+  std::deque<Op> eager_ops_;
   std::atomic<bool> failed_{false};
   double timeout_s_ = comm_timeout_s();
 
@@ -94,16 +101,23 @@ struct HostComm : Comm {
         break;
     }
     if (!ok) c.failed_.store(true);
+    o.done.store(true, std::memory_order_release);
   }
 
   void issue(void* dev, size_t bytes, size_t elem, Kind kind, int root, hipStream_t s) {
     const size_t chunk = kSlotBytes / elem * elem;
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    HCHK(hipStreamIsCapturing(s, &cap));
+    std::deque<Op>& ops = cap == hipStreamCaptureStatusNone ? eager_ops_ : graph_ops_;
+    // host functions run in issue order (one stream order per collective
+    // sequence), so the finished eager ops are a prefix of the deque
+    while (!eager_ops_.empty() && eager_ops_.front().done.load(std::memory_order_acquire)) eager_ops_.pop_front();
     for (size_t off = 0; off < bytes; off += chunk) {
       const size_t len = std::min(chunk, bytes - off);
       char* d = static_cast<char*>(dev) + off;
       HCHK(hipMemcpyAsync(in_, d, len, hipMemcpyDeviceToHost, s));
-      ops_.push_back(Op{this, kind, len, root});
-      HCHK(hipLaunchHostFunc(s, &HostComm::run_op, &ops_.back()));
+      ops.emplace_back(this, kind, len, root);
+      HCHK(hipLaunchHostFunc(s, &HostComm::run_op, &ops.back()));
       HCHK(hipMemcpyAsync(d, out_, len, hipMemcpyHostToDevice, s));
     }
   }

@@ -223,9 +223,13 @@ int run_gpu_training(const CliArgs& a, Comm& comm, const char* program) {
   // through a "oneRankReduce" kernel, while an in-place one-rank SUM is elided.)
   const float grad_scale = 1.0f / ((float)b * (float)world);
   PhaseTimer timer(a.profile);
+  const bool seq_sampler = a.sampler == "seq";
 
   auto step = [&](bool timed) {
-    gpu::sample_indices(d_idx.as<int32_t>(), b, shard_lo, shard_hi, a.seed * 7919ull + rank, d_step.as<uint64_t>(), S);
+    if (seq_sampler)
+      gpu::seq_sample_indices(d_idx.as<int32_t>(), b, (int64_t)rank * b, B_eff, N, d_step.as<uint64_t>(), S);
+    else
+      gpu::sample_indices(d_idx.as<int32_t>(), b, shard_lo, shard_hi, a.seed * 7919ull + rank, d_step.as<uint64_t>(), S);
     if (timed) timer.mark(0, S);
     net.forward(d_img.as<uint8_t>(), d_idx.as<int32_t>(), b, S);
     net.loss(d_lab.as<uint8_t>(), d_idx.as<int32_t>(), grad_scale, true, S);

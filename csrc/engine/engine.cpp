@@ -1361,6 +1361,11 @@ void GpuNet::stage_param_range(int stage, int64_t& off, int64_t& count) const {
 
 const void* GpuNet::stage_output(int stage, int64_t& per_sample, const uint8_t** argmax) const {
   const Stage& st = *stages_.at(stage);
+  // Stage 0 of a fused conv block keeps a kernel-private layout (LeNet: Y1
+  // HWC-8 + planar argmax codes) or is never written (ref block: conv1 is
+  // recomputed in the backward); its buffer is not the standard NCHW output.
+  MCC_CHECK(!((lenet_ || refblk_) && stage == 0),
+            "stage_output: stage 0 is internal to the fused conv block (no standard-layout output)");
   per_sample = st.out_elems;
   if (argmax) *argmax = st.pooled ? st.arg_buf : nullptr;
   return st.act_buf;
@@ -1371,6 +1376,17 @@ std::vector<GpuBucket> GpuNet::buckets(int64_t bucket_bytes) const {
   for (const Bucket& b : plan_buckets(spec_, bucket_bytes)) {
     GpuBucket g;
     g.stage_hi = b.stage_hi; g.stage_lo = b.stage_lo; g.off = b.off; g.count = b.count;
+    // A fused conv block (lenet_bwd / ref_bwd) finishes stage 0's gradient in
+    // the same kernel as stage 1's: a separate stage-0 bucket would only add a
+    // second latency-bound collective at the end of the step.  Merge it into
+    // the bucket that holds stage 1 (parameters are contiguous, stage 0 first).
+    if ((lenet_ || refblk_) && b.stage_hi == 0 && !out.empty() && out.back().stage_lo == 1 &&
+        b.off + b.count == out.back().off) {
+      out.back().stage_lo = 0;
+      out.back().off = b.off;
+      out.back().count += b.count;
+      continue;
+    }
     out.push_back(g);
   }
   return out;

@@ -602,6 +602,9 @@ void fill_f32(float* dst, float v, int64_t n, hipStream_t s);
 // advance_counter once per step (after the last consumer of idx).
 void sample_indices(int32_t* idx, int B, int64_t lo, int64_t hi, uint64_t seed, const uint64_t* step,
                     hipStream_t s);
+// idx[b] = ((*step) * stride + offset + b) mod n: rank slices of sequential global batches
+void seq_sample_indices(int32_t* idx, int B, int64_t offset, int64_t stride, int64_t n, const uint64_t* step,
+                        hipStream_t s);
 void advance_counter(uint64_t* step, hipStream_t s);
 // idx[b] = start + b (sequential evaluation windows)
 void iota_i32(int32_t* idx, int B, int64_t start, hipStream_t s);

@@ -584,6 +584,16 @@ __global__ void sample_kernel(int32_t* idx, int B, int64_t lo, int64_t span, uin
 
 __global__ void advance_kernel(uint64_t* step) { *step += 1; }
 
+// Sequential global windows: at step t the global batch is dataset positions
+// t*stride .. t*stride + stride - 1 (mod n), and this rank takes the slice
+// starting at `offset` -- world ranks together draw exactly the batch one
+// process of the whole global batch would (cnn_dist --sampler seq).
+__global__ void seq_sample_kernel(int32_t* idx, int B, int64_t offset, int64_t stride, int64_t n, const uint64_t* step) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  idx[b] = (int32_t)(((int64_t)(*step % (uint64_t)n) * stride + offset + b) % n);
+}
+
 __global__ void iota_kernel(int32_t* idx, int B, int64_t start) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b < B) idx[b] = (int32_t)(start + b);
@@ -695,6 +705,12 @@ void sample_indices(int32_t* idx, int B, int64_t lo, int64_t hi, uint64_t seed, 
                     hipStream_t s) {
   MCC_CHECK(B > 0 && hi > lo, "sample_indices: empty range");
   hipLaunchKernelGGL(sample_kernel, dim3((unsigned)cdiv(B, 256)), dim3(256), 0, s, idx, B, lo, hi - lo, seed, step);
+}
+
+void seq_sample_indices(int32_t* idx, int B, int64_t offset, int64_t stride, int64_t n, const uint64_t* step,
+                        hipStream_t s) {
+  MCC_CHECK(B > 0 && n > 0 && stride > 0 && offset >= 0, "seq_sample_indices: bad range");
+  hipLaunchKernelGGL(seq_sample_kernel, dim3((unsigned)cdiv(B, 256)), dim3(256), 0, s, idx, B, offset, stride, n, step);
 }
 
 void advance_counter(uint64_t* step, hipStream_t s) {

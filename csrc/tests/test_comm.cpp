@@ -126,7 +126,7 @@ static void test_bootstrap_timeouts() {
       }
       return 3;  // must not succeed
     }
-    fetch_blob(b, sizeof(b), a);
+    fetch_blob(b, sizeof(b), 1, a);
     return 0;
   });
   CHECK(rcs[0] == 0 && rcs[1] == 0);
@@ -138,13 +138,57 @@ static void test_bootstrap_timeouts() {
   bool threw = false;
   try {
     char b[16];
-    fetch_blob(b, sizeof(b), c);
+    fetch_blob(b, sizeof(b), 1, c);
   } catch (const Error& e) {
     threw = std::strstr(e.what(), "timed out connecting") != nullptr;
   }
   const double s = std::chrono::duration<double>(Clock::now() - t0).count();
   CHECK(threw && s < 5.0);
   std::printf("bootstrap timeouts ok\n");
+}
+
+// Stray connectors (connect + close, a garbage hello, an out-of-range rank)
+// do not take the slots of real ranks: world 3 still serves ranks 1 and 2.
+static void test_bootstrap_stray_connections() {
+  BootstrapAddr a;
+  a.port = free_port();
+  a.timeout_s = 20;
+  auto rcs = run_procs(4, [&](int r) {
+    char b[16] = {};
+    if (r == 0) {
+      std::strcpy(b, "token");
+      serve_blob(b, sizeof(b), 2, a);
+      return 0;
+    }
+    if (r == 3) {  // the stray
+      for (int k = 0; k < 3; ++k) {
+        for (int t = 0; t < 400; ++t) {
+          int fd = ::socket(AF_INET, SOCK_STREAM, 0);
+          sockaddr_in sa{};
+          sa.sin_family = AF_INET;
+          sa.sin_port = htons((uint16_t)a.port);
+          sa.sin_addr.s_addr = htonl(0x7f000001);
+          if (::connect(fd, reinterpret_cast<sockaddr*>(&sa), sizeof(sa)) == 0) {
+            const int32_t bad[2] = {k == 1 ? 0x4243434d : 1234, k == 1 ? 99 : 1};
+            if (k > 0) (void)!::write(fd, bad, sizeof(bad));
+            char junk[16];
+            const ssize_t got = ::read(fd, junk, sizeof(junk));  // the server must not send the blob
+            ::close(fd);
+            if (got > 0) return 6;
+            break;
+          }
+          ::close(fd);
+          ::usleep(5000);
+        }
+      }
+      return 0;
+    }
+    ::usleep(300000);  // the real ranks arrive after the strays
+    fetch_blob(b, sizeof(b), r, a);
+    return std::strcmp(b, "token") == 0 ? 0 : 4;
+  });
+  for (int rc : rcs) CHECK(rc == 0);
+  std::printf("bootstrap stray connections ok\n");
 }
 
 static uint64_t token() {
@@ -257,6 +301,7 @@ static void test_shm_dead_peer_and_poison() {
 int main() {
   test_bootstrap_world4();
   test_bootstrap_timeouts();
+  test_bootstrap_stray_connections();
   test_shm_collectives();
   test_shm_dead_peer_and_poison();
   std::printf("comm ok\n");

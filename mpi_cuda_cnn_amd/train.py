@@ -107,7 +107,23 @@ def main(argv=None) -> int:
         return _train(a, world, rank, local_rank, use_gpu)
     except (RuntimeError, dist.DistBackendError) as e:  # a failed collective (peer gone, deadline passed)
         print(f"rank {rank}: {e}", file=sys.stderr, flush=True)
-        return 111
+        if not dist.is_initialized():
+            return 111
+        _exit_now(111)
+
+
+def _exit_now(rc: int):
+    """Leave the process with ``rc`` without interpreter teardown.
+
+    After a failed collective the process group cannot be destroyed cleanly
+    (its peer is gone), and returning through ``sys.exit`` lets the backend's
+    background threads run into the teardown: gloo's pair thread calls
+    ``std::terminate`` on the read error (rc -6 instead of 111, roughly every
+    other run).  Reference contract: a failing rank exits 111 and its peers
+    must not hang (defect D9, cnnmpi.c:443-453) -- so flush and ``_exit``."""
+    sys.stdout.flush()
+    sys.stderr.flush()
+    os._exit(rc)
 
 
 def _fault(rank, it):

@@ -8,8 +8,6 @@ inside the first conv kernel, so there is no host data path in the step.
 
 from __future__ import annotations
 
-import time
-
 import numpy as np
 import torch
 import torch.distributed as dist
@@ -94,6 +92,24 @@ class GpuTrainer:
         return self.net.get_params()
 
 
+def drain_collective_watchdog(group=None) -> bool:
+    """Block until the RCCL process group's watchdog holds no eager work.
+
+    The watchdog thread polls the end event of every eager collective until it
+    sees it complete, and HIP fails that query once the event's RCCL stream is
+    capturing (hipErrorCapturedEvent: the watchdog then aborts the whole
+    process -- seen once on the LeNet-5 bench in round 3).  Collectives issued
+    during a capture are never handed to the watchdog, so the condition for a
+    safe capture is exactly "its work list is empty", which
+    ``ProcessGroup._wait_for_pending_works`` waits for (it takes the
+    watchdog's own locks).  Returns False when there is no RCCL group."""
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_backend(group) != "nccl":
+        return False
+    pg = group if group is not None else dist.group.WORLD
+    pg._wait_for_pending_works()
+    return True
+
+
 def capture_step(fn):
     """Capture ``fn()`` -- a training step that launches everything on the
     current stream (engine kernels, the device sampler, the bucketed RCCL
@@ -105,15 +121,7 @@ def capture_step(fn):
     counter) alive and fixed.  Run ``fn`` eagerly at least once before (code
     objects loaded, RCCL communicator set up)."""
     torch.cuda.synchronize()
-    if dist.is_available() and dist.is_initialized() and dist.get_backend() == "nccl":
-        # The process-group watchdog polls the end events of the eager
-        # collectives (every ~100 ms) until it has seen them complete, and HIP
-        # fails that query once their RCCL stream is capturing
-        # (hipErrorCapturedEvent: the watchdog then aborts the process -- seen
-        # once on the LeNet-5 bench in round 3 with the event cache already
-        # off).  The eager step has finished (synchronize above), so one poll
-        # retires them: give the watchdog a few of its periods first.
-        time.sleep(1.0)
+    drain_collective_watchdog()
     g = torch.cuda.CUDAGraph()
     try:
         with torch.cuda.graph(g):

@@ -11,6 +11,7 @@ import os
 import re
 import shutil
 import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -171,3 +172,12 @@ def test_out_of_range_label_rejected(cnn_bin, data, tmp_path):
     r = subprocess.run([sys.executable, "-m", "mpi_cuda_cnn_amd.train", data[0], badl, data[2], data[3],
                         "--epochs", "1", "--device", "cpu"], capture_output=True, text=True, cwd=ROOT)
     assert r.returncode == 111 and "label 10" in r.stderr, r.stderr
+
+
+def test_bench_refuses_world_mismatch():
+    """bench.py under a launcher whose WORLD_SIZE differs from --gpus exits
+    non-zero before touching a GPU (its JSON line would mislabel the run)."""
+    env = dict(os.environ, WORLD_SIZE="3", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "1"],
+                       capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode != 0 and "WORLD_SIZE=3" in r.stderr, r.stderr

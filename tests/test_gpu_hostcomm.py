@@ -71,6 +71,41 @@ def test_cnn_dist_host_comm_replicas_bit_equal(idx_files, tmp_path, world):
     assert js["ncorrect"] >= 0.9 * js["ntests"], js
 
 
+def _world1(idx_files, w, extra):
+    env = dict(os.environ, RANK="0", WORLD_SIZE="1", LOCAL_RANK="0", MCC_COMM_TIMEOUT="60")
+    env.pop("MCC_AB", None)
+    r = subprocess.run([CNN_DIST] + idx_files + [
+        "--comm", "local", "--model", "lenet5", "--batch", "512", "--epochs", "1", "--lr", "0.05",
+        "--momentum", "0.9", "--json", "-", "--save", w] + list(extra),
+        capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    return mcc.load_weights(w)[1]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,dtype", [(2, "fp32"), (4, "fp32"), (2, "bf16")])
+def test_cnn_dist_world_n_equals_one_process(idx_files, tmp_path, world, dtype):
+    """World N at global batch 512 (b = 512/N per rank, bucketed sums over the
+    host collectives) ends where ONE process stepping the same global batches
+    ends, to fp32 rounding of the different summation order (reference DP
+    semantics to beat: cnnmpi.c:487-499 all-reduced the wrong buffer).  Both
+    runs use --sampler seq, so step t's global batch is the same 512 images."""
+    extra = ["--sampler", "seq", "--dtype", dtype]
+    r, _ = _launch(world, idx_files, str(tmp_path / "n{rank}.bin"), extra)
+    assert r.returncode == 0, r.stderr[-3000:]
+    pn = mcc.load_weights(str(tmp_path / "n0.bin"))[1]
+    p1 = _world1(idx_files, str(tmp_path / "one.bin"), extra)
+    spec = mcc.make_model("lenet5")
+    p0 = np.asarray(mcc.init_params(spec, seed=0), dtype=np.float64)
+    moved = np.linalg.norm(p1 - p0)
+    assert moved > 1e-2, moved
+    # fp32: only the summation order differs; bf16: additionally a weight's
+    # bf16 compute copy can round the other way after a step
+    tol = 2e-3 if dtype == "fp32" else 3e-2
+    err = np.linalg.norm(pn - p1)
+    assert err < tol * moved, (err, moved)
+
+
 @pytest.mark.gpu
 def test_cnn_dist_host_comm_graph_equals_eager(idx_files, tmp_path):
     r1, _ = _launch(2, idx_files, str(tmp_path / "g{rank}.bin"))

@@ -124,3 +124,20 @@ def test_bench_two_ranks_gloo_rehearsal():
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["steps"] == 3 and d["config"]["global_batch"] == 8192, d
     assert d["config"]["parallelism"] == "dp2" and d["value"] > 0, d
+
+
+@pytest.mark.gpu
+def test_bench_self_launch_without_launcher():
+    """`python bench.py --gpus 2` with no WORLD_SIZE starts torch.distributed.run
+    itself (child process, before any GPU call) instead of measuring one rank."""
+    import json
+
+    r = _run([sys.executable, "bench.py", "--gpus", "2", "--steps", "2", "--warmup", "1",
+              "--batch-per-gpu", "2048", "--dist-backend", "gloo"], cwd=ROOT,
+             env={k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")})
+    assert r.returncode == 0, r.stderr
+    assert "launching 2 ranks" in r.stderr
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "dp2", d

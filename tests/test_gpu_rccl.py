@@ -175,3 +175,44 @@ def test_python_graph_replay_bit_equal(cuda, tmp_path):
     assert ie == (STEPS + 1) * nb and ig == 2 * nb, (ie, ig, nb)  # eager: every step; graph: eager + capture
     assert not np.array_equal(pe, mcc.init_params(mcc.make_model("lenet5"), seed=3, mode="fast"))
     np.testing.assert_array_equal(pe, pg)
+
+
+def _capture_cycles_worker(rank, out):
+    """Eager step (its collectives go to the process-group watchdog) and a
+    graph capture right after it, several times over, with no pause between:
+    capture_step must wait for the watchdog to retire the eager work
+    (drain_collective_watchdog) instead of racing it."""
+    import torch.distributed as dist
+
+    from mpi_cuda_cnn_amd.parallel.ddp import init_process_group
+    from mpi_cuda_cnn_amd.trainer import GpuTrainer, capture_step, drain_collective_watchdog
+
+    os.environ.pop("MASTER_PORT", None)
+    os.environ.update(RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    init_process_group("nccl", dev)
+    spec = mcc.make_model("lenet5")
+    imgs, labels = mcc.synth_dataset(2048, 1, 28, 28, 10, seed=5)
+    d_img, d_lab = torch.from_numpy(imgs).to(dev), torch.from_numpy(labels).to(dev)
+    tr = GpuTrainer(spec, dtype="bf16", batch=B, device=0, lr=LR, momentum=MOM,
+                    params=mcc.init_params(spec, seed=3, mode="fast"), bucket_bytes=BUCKET)
+    idx = torch.arange(B, dtype=torch.int32, device=dev)
+    ok = 0
+    for _ in range(6):
+        tr.step(d_img, d_lab, idx)  # eager: RCCL works queued on the watchdog
+        g, why = capture_step(lambda: tr.step(d_img, d_lab, idx))
+        assert g is not None, why
+        g.replay()
+        torch.cuda.synchronize()
+        ok += 1
+    assert drain_collective_watchdog() is True
+    np.save(os.path.join(out, "ok.npy"), np.array([ok, tr.sync.issued]))
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_capture_right_after_eager_collectives(cuda, tmp_path):
+    mp.spawn(_capture_cycles_worker, args=(str(tmp_path),), nprocs=1, join=True)
+    ok, issued = np.load(tmp_path / "ok.npy")
+    assert ok == 6 and issued > 0
