@@ -255,6 +255,7 @@ PYBIND11_MODULE(_C, m) {
       .def("get_logits",
            [](const GpuNet& n, int B) {
              MCC_CHECK(B > 0 && B <= n.max_batch(), "get_logits: bad batch");
+             n.flush_forward(nullptr);
              const int nc = n.spec().num_classes(), ld = n.logits_ld();
              std::vector<float> tmp((size_t)B * ld);
              if (hipDeviceSynchronize() != hipSuccess) throw Error("hipDeviceSynchronize failed");

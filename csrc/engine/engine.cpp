@@ -417,6 +417,21 @@ void GpuNet::build() {
                 b.inH == 14 && b.C == 32 && stages_[2]->kind == Stage::FC;
     }
   }
+  // ---- LeNet-5 classifier chain (lenet_fc.hip): FC 400 -> 120 -> 84 -> 10
+  // forward, softmax-CE and backward in one kernel launched by loss();
+  // MCC_AB=no_fcchain keeps the per-layer FC kernels + the fused head.
+  {
+    fcchain_ = false;
+    if (lenet_ && stages_.size() == 5 && !ab_flag("no_fcchain")) {
+      const Stage& f1 = *stages_[2];
+      const Stage& f2 = *stages_[3];
+      const Stage& f3 = *stages_[4];
+      fcchain_ = f1.kind == Stage::FC && f2.kind == Stage::FC && f3.kind == Stage::FC && f3.last &&
+                 f1.act == gpu::ACT_RELU && f2.act == gpu::ACT_RELU &&
+                 gpu::lenet_fc_supported(f1.Kin, f1.Nout, f2.Nout, f3.Nout) && f1.in_ld == f1.Kin &&
+                 f2.Kin == f1.Nout && f3.Kin == f2.Nout;
+    }
+  }
 
   // ---- data gradient straight into dZ (no grad_xform pass) ----
   // A big stage whose input is a ReLU big conv writes that stage's dZ in its
@@ -654,6 +669,7 @@ void GpuNet::build() {
     scratch = std::max(scratch, (size_t)gpu::gemm_fwd_splitk(Bm, st.Nout, st.Kin) * Bm * ld * 4);
   }
   if (lenet_) scratch = std::max(scratch, gpu::lenet_slab_bytes());
+  if (fcchain_) scratch = std::max(scratch, gpu::lenet_fc_slab_bytes(Bm));
   if (refblk_) scratch = std::max(scratch, gpu::ref_slab_bytes());
   scratch_bytes_ = scratch;
   for (int pass = 0; pass < 2; ++pass) {
@@ -699,6 +715,7 @@ void GpuNet::build() {
 std::string GpuNet::plan() const {
   std::ostringstream os;
   if (lenet_) os << "[lenet block: stages 0+1 fused fwd (lenet_fwd) and bwd (lenet_bwd)]\n";
+  if (fcchain_) os << "[lenet fc chain: stages 2-4 fwd + softmax-CE + bwd in one kernel (lenet_fc)]\n";
   if (refblk_) os << "[ref block: stages 0+1 fused fwd (ref_fwd) and bwd (ref_bwd: recomputed conv1, sub-pixel dX)]\n";
   os << "GpuNet(" << spec_.name << ", " << dtype_name(dtype_) << ", max_batch=" << max_batch_
      << ", arena=" << (arena_bytes_ >> 20) << " MiB, " << (fused_pack_ ? "fused sgd+pack" : "sgd + pack table")
@@ -816,9 +833,33 @@ void GpuNet::forward(const uint8_t* images, const int32_t* idx, int B, hipStream
   images_ = images;
   idx_ = idx;
   head_done_ = false;
+  fc_pending_ = false;
+  fc_bwd_done_ = false;
+  forward_stages(0, true, s);
+}
+
+// The LeNet-5 classifier chain (lenet_fc.hip) runs its forward inside the
+// fused forward+loss+backward kernel that loss(backward = true) launches, so
+// forward() stops after the conv block and leaves the FC forward pending.
+// Anything that needs the FC outputs without that kernel (loss(backward =
+// false), get_logits) runs the per-layer FC forward first.
+void GpuNet::flush_forward(hipStream_t s) const {
+  if (!fc_pending_) return;
+  fc_pending_ = false;
+  const_cast<GpuNet*>(this)->forward_stages(2, false, s);
+}
+
+void GpuNet::forward_stages(size_t first, bool defer_fc, hipStream_t s) {
+  const int B = B_;
+  const uint8_t* images = images_;
+  const int32_t* idx = idx_;
   const size_t es = dtype_size(dtype_);
-  for (size_t si = 0; si < stages_.size(); ++si) {
+  for (size_t si = first; si < stages_.size(); ++si) {
     Stage& st = *stages_[si];
+    if (fcchain_ && defer_fc && si >= 2) {
+      fc_pending_ = true;
+      return;
+    }
     if (lenet_ && si <= 1) {
       if (si == 1) continue;  // produced with stage 0
       const Stage& s1 = *stages_[1];
@@ -953,6 +994,34 @@ void GpuNet::loss(const uint8_t* labels, const int32_t* idx, float grad_scale, b
                   int32_t* pred) {
   MCC_CHECK(B_ > 0, "loss: call forward first");
   const Stage& last = *stages_.back();
+  if (fc_pending_ && backward) {
+    // forward + softmax-CE + backward of the three FC layers in one kernel;
+    // the weight gradients land in grads_ through a fixed-order slab reduce
+    const Stage& s1 = *stages_[1];
+    const Stage& f1 = *stages_[2];
+    const Stage& f2 = *stages_[3];
+    const Stage& f3 = *stages_[4];
+    const size_t es = dtype_size(dtype_);
+    gpu::LenetFcParams f;
+    f.B = B_;
+    f.y = s1.act_buf; f.ldy = f1.in_ld;
+    f.w1 = static_cast<const char*>(packed_) + es * f1.pk_fwd; f.ldw1 = r8(f1.Kin);
+    f.w2 = static_cast<const char*>(packed_) + es * f2.pk_fwd; f.ldw2 = r8(f2.Kin);
+    f.w3 = static_cast<const char*>(packed_) + es * f3.pk_fwd; f.ldw3 = r8(f3.Kin);
+    f.b1 = params_ + f1.b_off; f.b2 = params_ + f2.b_off; f.b3 = params_ + f3.b_off;
+    f.labels = labels; f.idx = idx;
+    f.scale = grad_scale;
+    f.logits = logits_; f.ldl = logits_ld_;
+    f.pred = pred;
+    f.stats = stats_;
+    f.dy = s1.grad_buf; f.ldd = f1.in_ld;
+    f.slab = scratch_;
+    gpu::lenet_fc(f, grads_ + f1.w_off, s);
+    fc_pending_ = false;
+    fc_bwd_done_ = true;
+    return;
+  }
+  flush_forward(s);
   gpu::XentParams p;
   p.M = B_; p.N = spec_.num_classes();
   p.logits = logits_; p.ldl = logits_ld_;
@@ -996,6 +1065,7 @@ void GpuNet::backward(int hi, int lo, hipStream_t s) {
   for (int si = hi; si >= lo; --si) {
     Stage& st = *stages_[si];
     s = s_main;
+    if (fc_bwd_done_ && si >= 2) continue;  // done by loss() (lenet_fc)
     if (lenet_ && si <= 1) {
       // stage 1 runs the fused block backward (both stages' dW, db); stage 0 is then done
       if (si == 0) continue;

@@ -311,6 +311,33 @@ struct LenetBwdParams {
   float* slab = nullptr;          // lenet_slab_bytes()
   float *gw1 = nullptr, *gb1 = nullptr, *gw2 = nullptr, *gb2 = nullptr;  // canonical gradients (written)
 };
+// LeNet-5 classifier chain (lenet_fc.hip): FC 400 -> 120 ReLU -> 84 ReLU -> 10
+// + softmax-CE forward AND backward in one persistent kernel, bf16 weights
+// (the packed [out][ld] compute copies), fp32 accumulation.  Writes the fp32
+// logits / predictions (optional), the loss statistics, the bf16 gradient of
+// the FC input and -- through per-workgroup slabs and a fixed-order reduce --
+// the canonical gradients of the three layers (W1 b1 W2 b2 W3 b3, contiguous,
+// 59,134 floats starting at `grads`).
+struct LenetFcParams {
+  int B = 0;
+  const void* y = nullptr; int ldy = 0;          // FC input [B][ldy] bf16 (features in device order)
+  const void *w1 = nullptr, *w2 = nullptr, *w3 = nullptr;  // packed bf16 [out][ldw]
+  int ldw1 = 0, ldw2 = 0, ldw3 = 0;
+  const float *b1 = nullptr, *b2 = nullptr, *b3 = nullptr;  // fp32 master biases
+  const uint8_t* labels = nullptr;
+  const int32_t* idx = nullptr;                  // label of row b = labels[idx[b]] (nullable)
+  float scale = 1.f;                             // dlogits scale (1 / global batch)
+  float* logits = nullptr; int ldl = 0;          // optional fp32 logits
+  int32_t* pred = nullptr;                       // optional argmax
+  unsigned long long* stats = nullptr;           // loss / mse / correct (fixed point)
+  void* dy = nullptr; int ldd = 0;               // gradient of the FC input [B][ldd] bf16
+  float* slab = nullptr;                         // lenet_fc_slab_bytes(max batch)
+};
+bool lenet_fc_supported(int kin, int n1, int n2, int n3);
+size_t lenet_fc_slab_bytes(int max_batch);
+int lenet_fc_grad_count();
+void lenet_fc(const LenetFcParams& p, float* grads, hipStream_t s);
+
 int lenet_bwd_grid();
 size_t lenet_slab_bytes();
 int lenet_y1_elems();   // per image
