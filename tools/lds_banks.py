@@ -146,3 +146,152 @@ def fcchain_search():
 if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "fcchain":
         fcchain_search()
+
+
+# ---------------------------------------------------------------- lenet_bwd
+def lenet_bwd_accesses(RZ=20, RY=14, XP=40, XC=2584, R1=64, P1=2080, y1swz=None, dz1swz=None, dz1x=None,
+                       cb=None, onesb=None, zperm=None, dz2full=False):
+    """Every LDS instruction of one image of lenet.hip's lenet_bwd_kernel
+    (per-lane byte addresses), for the layout parameters: dZ2 row pitch RZ
+    (32-B pixels), Y1 row pitch RY (16-B pixels), X row pitch XP (bf16) and
+    copy stride XC (bytes), dZ1 row pitch R1 and plane stride P1 (bytes);
+    y1swz(pixel) / dz1swz(row) optional extra byte offsets (swizzles).
+    Returns (accesses, LDS bytes)."""
+    y1swz = y1swz or (lambda px: 0)
+    dz1swz = dz1swz or (lambda row: 0)
+    dz1x = dz1x or (lambda row: 0)         # dZ1 16-B chunk g of row r stored at chunk g ^ dz1x(r)
+    zperm = zperm or list(range(128))      # K position -> dZ2 pixel z (>= 100: padding)
+    kBDz2 = 0
+    kBY1 = 18 * RZ * 32
+    kBOne2 = kBY1 + 14 * RY * 16 + 64
+    kBXs = (kBOne2 + 16 + 15) // 16 * 16
+    kBOne1 = kBXs + 4 * XC
+    cb = cb or [c * XC for c in range(4)]  # byte base of X copy c (relative to kBXs)
+    onesb = kBOne1 if onesb is None else kBXs + onesb
+    kBDz1 = (kBOne1 + 30 * XP * 2 + 15) // 16 * 16
+    total = kBDz1 + 6 * P1
+    L = range(64)
+    acc = []
+
+    def y1(px):  # byte offset of Y1 pixel px (HWC-8)
+        return kBY1 + ((px // 14) * RY + px % 14) * 16 + y1swz(px)
+
+    def dz1(row):
+        return row * R1 + dz1swz(row)
+
+    zb = []
+    for l in L:
+        if l >= 50:
+            zb.append(None)
+            continue
+        zq, zh = l >> 1, l & 1
+        zqy, zqx = zq // 5, zq % 5
+        zb.append(kBDz2 + ((2 * zqy + 4) * RZ + 2 * zqx + 4) * 32 + 16 * zh)
+    for o in (0, 32, RZ * 32, RZ * 32 + 32):
+        acc.append(("dz2 zero", "write_b128", [None if a is None else a + o for a in zb], 1))
+    if not dz2full:
+        import random
+        rnd = random.Random(1)
+        for i in range(8):
+            for rep in range(4):
+                acc.append(("dz2 val", "write_b16",
+                            [None if a is None else a + rnd.choice((0, 32, RZ * 32, RZ * 32 + 32)) + 2 * i for a in zb],
+                            0.25))
+    for rr in range(4):
+        acc.append(("y1 stage", "write_b128", [y1(l + 64 * rr) if l + 64 * rr < 196 else None for l in L], 1))
+    for it in range(4):
+        for cpy in range(4):
+            addrs = []
+            for l in L:
+                sk, srow = l & 7, l >> 3
+                yy = it * 8 + srow
+                addrs.append(kBXs + ((yy + 2) * XP + 4 * sk) * 2 + cb[cpy] if yy < 28 else None)
+            acc.append(("x stage", "write_b64", addrs, 1))
+    # dW2: A = dZ2 transposed (rows = dZ2 pixels z), B = im2col(Y1) transposed:
+    # column n = 8 * tap + ci, lane quad tp: (tp & 1) channel half, (tp >> 1) second tap
+    for c in range(4):
+        for hf in range(2):
+            aw, bt = [], [[] for _ in range(13)]
+            for l in L:
+                g = l >> 4
+                tq, tp = (l >> 2) & 3, l & 3
+                z = zperm[32 * c + 8 * g + 4 * hf + tq]
+                ok = z < 100
+                zy, zx = (z // 10, z % 10) if ok else (0, 0)
+                aw.append(kBDz2 + ((zy + 4) * RZ + zx + 4) * 32 + 8 * tp if ok else kBDz2 + 8 * tp)
+                for t in range(13):
+                    tap = 2 * t + (tp >> 1)
+                    if tap >= 25:  # the ones column (bias)
+                        bt[t].append(kBOne2 + 8 * (tp & 1))
+                    else:
+                        kh, kw = tap // 5, tap % 5
+                        bt[t].append(y1((zy + kh) * 14 + zx + kw) + 8 * (tp & 1))
+            acc.append(("dw2 A", "tr_b16", aw, 1))
+            for t in range(13):
+                acc.append(("dw2 B", "tr_b16", bt[t], 1))
+
+    def dxoff(c):
+        return (((2 * c) // 5) * RZ + (2 * c) % 5) * 32
+
+    def dxwrap(c):
+        return (2 * c) % 5 == 4
+    hxa = [kBDz2 + (l & 15) * 32 + 16 * ((l >> 4) & 1) + ((l >> 4) >> 1) * 32 for l in L]
+    hxb = [kBDz2 + (l & 15) * 32 + 16 * ((l >> 4) & 1) + ((l >> 4) >> 1) * (RZ - 4) * 32 for l in L]
+    for c in range(15):
+        for T in range(7):
+            if T > 0 and c < 10:
+                continue
+            acc.append(("dx2 A", "read_b128", [(hxb if dxwrap(c) else hxa)[l] + dxoff(c) + T * 2 * RZ * 32 for l in L], 1))
+    for T in range(7):
+        for o in (0, 1):
+            addrs = []
+            for l in L:
+                n16, g = l & 15, l >> 4
+                if n16 >= 12:
+                    addrs.append(None)
+                    continue
+                dxci, dxj = n16 >> 1, n16 & 1
+                row = 4 * T + 2 * dxj + 2 + o
+                addrs.append(kBDz1 + dxci * P1 + dz1(row) + 16 * (g ^ dz1x(row)))
+            acc.append(("dz1 write", "write_b128", addrs, 1))
+    for zy in range(30):
+        a, b = [], []
+        for l in L:
+            n16, g = l & 15, l >> 4
+            m = n16 if n16 < 12 else 0
+            co, s = m % 6, m // 6
+            row = zy + 2 - 2 * s
+            a.append(kBDz1 + co * P1 + dz1(row) + 16 * (g ^ dz1x(row)))
+            if n16 == 15:
+                b.append(onesb + 16 * g + zy * XP * 2)
+            else:
+                kh, kw = n16 // 5, n16 % 5
+                cc = kw & 3
+                b.append(kBXs + cb[cc] + ((kh + zy) * XP + 8 * g + kw - cc) * 2)
+        acc.append(("dw1 A", "read_b128", a, 1))
+        acc.append(("dw1 B", "read_b64", b, 1))
+        acc.append(("dw1 B", "read_b64", [x + 8 for x in b], 1))
+    return acc, total
+
+
+def lenet_bwd_report(**kw):
+    acc, total = lenet_bwd_accesses(**kw)
+    rows = {}
+    tot = ex = 0
+    for name, kind, addrs, n in acc:
+        c = cycles(kind, addrs)
+        e = c - ideal(kind)
+        r = rows.setdefault(name, [0, 0, 0])
+        r[0] += n
+        r[1] += n * c
+        r[2] += n * e
+        tot += n * c
+        ex += n * e
+    print(f"LDS bytes {total}; per image: {tot:.0f} LDS-array cycles, {ex:.0f} conflict cycles")
+    for k, (n, c, e) in rows.items():
+        print(f"  {k:10s} {n:5.0f} instr {c:6.0f} cycles {e:5.0f} extra")
+    return tot, ex, total
+
+
+if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "lenet_bwd":
+    lenet_bwd_report()
