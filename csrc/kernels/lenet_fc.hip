@@ -45,6 +45,8 @@ namespace {
 
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) void gvoid;
+typedef __attribute__((address_space(3))) void lvoid;
 
 constexpr int TM = 32;  // images per tile (the weight-gradient MFMA K)
 constexpr int K0 = 400, N1 = 120, N2 = 84, N3 = 10;
@@ -156,31 +158,39 @@ __global__ void __launch_bounds__(kThreads, 1) lenet_fc_kernel(LenetFcParams P) 
   // image-row reads (b128 / b64): rows r and 16 + r
   const int rm0 = pa(r), rm1 = pa(16 + r);
 
-  // ---- the FC input tile of the next iteration, prefetched in registers ----
-  u32x4 ypre[4];
-  int labpre = 0;
+  // ---- the FC input tile moves HBM -> LDS by DMA (global_load_lds, 16 B per
+  // lane, no registers): the LDS image of the tile is contiguous (row pa(m)
+  // at pa(m) * 800), so 16-byte piece k of it comes from image row pa(k / 50)
+  // (pa is an involution), chunk k % 50.  Issued while the previous tile's
+  // data gradient runs (P6b); the label of the tile's row tid rides along in
+  // a register. ----
   const char* ybase = static_cast<const char*>(P.y);
-  // thread -> (tile row srow, 16-byte chunks sj, sj + 16, sj + 32, sj + 48 < 50)
-  const int srow = tid >> 4, sj = tid & 15;
+  int labpre = 0;
   auto load_tile = [&](int t) {
     const int row0 = t * TM;
-    const char* src = ybase + (size_t)min(row0 + srow, B - 1) * P.ldy * 2 + 16 * sj;
-#pragma unroll
-    for (int i = 0; i < 3; ++i) ypre[i] = *reinterpret_cast<const u32x4*>(src + 256 * i);
-    if (sj < 2) ypre[3] = *reinterpret_cast<const u32x4*>(src + 768);
+    for (int k = tid; k < TM * 50; k += kThreads) {
+      const int prow = k / 50, j = k - 50 * (k / 50);
+      const char* src = ybase + (size_t)min(row0 + pa(prow), B - 1) * P.ldy * 2 + 16 * j;
+      // wave-uniform LDS base of this 64-lane piece; lane l lands at + 16 l
+      __builtin_amdgcn_global_load_lds((gvoid*)src, (lvoid*)(smem + OY + 16 * (k - lane)), 16, 0, 0);
+    }
     if (tid < TM) {
       const int gr = min(row0 + tid, B - 1);
       labpre = P.labels[P.idx ? P.idx[gr] : gr];
     }
   };
 
-  f32x4 dw1[25], dw2[6], dw3, db1, db2, db3;
+  // weight-gradient accumulators, held across all tiles.  The bias gradients
+  // of FC2 and FC3 come out of these tiles too: H1 column 120 and H2 column 84
+  // are ones (padding columns; zero weights in the forward, masked in the data
+  // gradients), so dW2 column 120 = db2 and dW3 column 84 = db3.
+  f32x4 dw1[25], dw2[6], dw3, db1;
   const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int b = 0; b < 25; ++b) dw1[b] = z4;
 #pragma unroll
   for (int a = 0; a < 6; ++a) dw2[a] = z4;
-  dw3 = db1 = db2 = db3 = z4;
+  dw3 = db1 = z4;
   float st_loss = 0.f, st_mse = 0.f, st_cor = 0.f;
 
   int t = blockIdx.x;
@@ -188,17 +198,11 @@ __global__ void __launch_bounds__(kThreads, 1) lenet_fc_kernel(LenetFcParams P) 
   for (; t < ntiles; t += gridDim.x) {
     const int row0 = t * TM;
     const int nvalid = min(TM, B - row0);
-    __syncthreads();  // the previous tile's reads of the input tile are done
-    // ---- P0: input tile + labels into LDS ----
-    {
-      char* dst = smem + OY + pa(srow) * SY + 16 * sj;
-#pragma unroll
-      for (int i = 0; i < 3; ++i) *reinterpret_cast<u32x4*>(dst + 256 * i) = ypre[i];
-      if (sj < 2) *reinterpret_cast<u32x4*>(dst + 768) = ypre[3];
-    }
+    // this wave's input-tile DMAs (and last tile's gradient stores) are done;
+    // the barrier makes every wave's pieces visible
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (tid < TM) reinterpret_cast<int*>(smem + OLAB)[tid] = labpre;
     __syncthreads();
-    if (t + (int)gridDim.x < ntiles) load_tile(t + gridDim.x);
 
     // ---- P1: H1^T = relu(W1 Y^T + b1), wave w: features 16w .. 16w+15 ----
     uint32_t mask1 = 0, mask2 = 0;
@@ -240,8 +244,9 @@ __global__ void __launch_bounds__(kThreads, 1) lenet_fc_kernel(LenetFcParams P) 
         float h[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const float v = 16 * w + 4 * g + i < N1 ? fmaxf(acc[i], 0.f) : 0.f;
-          h[i] = v;
+          const int n1 = 16 * w + 4 * g + i;
+          const float v = n1 < N1 ? fmaxf(acc[i], 0.f) : 0.f;
+          h[i] = n1 == N1 ? 1.f : v;  // the ones column of dW2 (-> db2)
           mask1 |= (bf16_bits(v) & 0x7fffu) ? 1u << (4 * mt + i) : 0u;
         }
         *reinterpret_cast<u32x2*>(smem + OH1 + (mt ? rm1 : rm0) * SH1 + (16 * w + 4 * g) * 2) =
@@ -254,13 +259,14 @@ __global__ void __launch_bounds__(kThreads, 1) lenet_fc_kernel(LenetFcParams P) 
     if (w < 6) {
       f32x4 acc0 = bias[32 + 4 * w + g], acc1 = acc0;
       // rows >= 84 read row 83 (outputs discarded); k 120..127 of the last
-      // chunk reads past the row into finite LDS times H1's zero columns
+      // chunk (past the row; H1 column 120 is the ones column) is zeroed
       const char* aw = smem + OW2 + min(16 * w + r, N2 - 1) * SW2 + 16 * g;
       const char* h0 = smem + OH1 + rm0 * SH1 + 16 * g;
       const char* h1 = smem + OH1 + rm1 * SH1 + 16 * g;
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
-        const bf16x8 a = ld128(aw + 64 * c);
+        bf16x8 a = ld128(aw + 64 * c);
+        if (c == 3 && g == 3) a = bf16x8{};
         acc0 = mma(acc0, a, ld128(h0 + 64 * c));
         acc1 = mma(acc1, a, ld128(h1 + 64 * c));
       }
@@ -270,8 +276,9 @@ __global__ void __launch_bounds__(kThreads, 1) lenet_fc_kernel(LenetFcParams P) 
         float h[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const float v = 16 * w + 4 * g + i < N2 ? fmaxf(acc[i], 0.f) : 0.f;
-          h[i] = v;
+          const int n2 = 16 * w + 4 * g + i;
+          const float v = n2 < N2 ? fmaxf(acc[i], 0.f) : 0.f;
+          h[i] = n2 == N2 ? 1.f : v;  // the ones column of dW3 (-> db3)
           mask2 |= (bf16_bits(v) & 0x7fffu) ? 1u << (4 * mt + i) : 0u;
         }
         *reinterpret_cast<u32x2*>(smem + OH2 + (mt ? rm1 : rm0) * SH2 + (16 * w + 4 * g) * 2) =
@@ -362,9 +369,6 @@ __global__ void __launch_bounds__(kThreads, 1) lenet_fc_kernel(LenetFcParams P) 
       const bf16x8 ae = tr8(smem + OE + tra0 * SE + 8 * p, smem + OE + tra1 * SE + 8 * p);
       const bf16x8 bh = tr8(smem + OH2 + tra0 * SH2 + (16 * w + 4 * p) * 2, smem + OH2 + tra1 * SH2 + (16 * w + 4 * p) * 2);
       dw3 = mma(dw3, ae, bh);
-    } else if (w == 6) {
-      const bf16x8 ae = tr8(smem + OE + tra0 * SE + 8 * p, smem + OE + tra1 * SE + 8 * p);
-      db3 = mma(db3, ae, ones);
     }
     __syncthreads();  // H2 reads done
     if (w < 6) {
@@ -382,7 +386,6 @@ __global__ void __launch_bounds__(kThreads, 1) lenet_fc_kernel(LenetFcParams P) 
         const bf16x8 ad =
             tr8(smem + OH2 + tra0 * SH2 + (16 * a + 4 * p) * 2, smem + OH2 + tra1 * SH2 + (16 * a + 4 * p) * 2);
         dw2[a] = mma(dw2[a], ad, bh);
-        if (a == w) db2 = mma(db2, ad, ones);
       }
       f32x4 x0 = z4, x1 = z4;
 #pragma unroll
@@ -424,7 +427,12 @@ __global__ void __launch_bounds__(kThreads, 1) lenet_fc_kernel(LenetFcParams P) 
         dw1[b] = mma(dw1[b], ad, fy[b & 3]);
         __builtin_amdgcn_sched_barrier(0);
       }
-      // data gradient: unit (k-tile b, image tile mt); wave w takes b = w,
+    }
+    // every wave is done with the input tile: the next one streams into LDS
+    // while the data gradient below runs
+    __syncthreads();
+    if (t + (int)gridDim.x < ntiles) load_tile(t + gridDim.x);
+    {      // data gradient: unit (k-tile b, image tile mt); wave w takes b = w,
       // w + 8, w + 16 of both image tiles and b = 24 of image tile w (w < 2)
       int wrow[8];  // W1 LDS rows of this lane's transposed reads, chunk c, half h
 #pragma unroll
@@ -442,16 +450,21 @@ __global__ void __launch_bounds__(kThreads, 1) lenet_fc_kernel(LenetFcParams P) 
         for (int k = 0; k < 4; ++k) {
           if (k == 3 && w != mt) break;
           const int b = k < 3 ? w + 8 * k : 24;
-          bf16x8 fw[4], fh[4];
-#pragma unroll
-          for (int c = 0; c < 4; ++c) {
-            fw[c] = tr8(smem + wrow[2 * c] + (16 * b + 4 * p) * 2, smem + wrow[2 * c + 1] + (16 * b + 4 * p) * 2);
-            fh[c] = ld128(smem + OH1 + (mt ? rm1 : rm0) * SH1 + 64 * c + 16 * g);
-          }
-          __builtin_amdgcn_sched_barrier(0);
+          const char* hrow = smem + OH1 + (mt ? rm1 : rm0) * SH1 + 16 * g;
+          bf16x8 fw[2], fh[2];
+          fw[0] = tr8(smem + wrow[0] + (16 * b + 4 * p) * 2, smem + wrow[1] + (16 * b + 4 * p) * 2);
+          fh[0] = ld128(hrow);
           f32x4 acc = z4;
 #pragma unroll
-          for (int c = 0; c < 4; ++c) acc = mma(acc, fw[c], fh[c]);
+          for (int c = 0; c < 4; ++c) {
+            if (c + 1 < 4) {
+              fw[(c + 1) & 1] = tr8(smem + wrow[2 * c + 2] + (16 * b + 4 * p) * 2, smem + wrow[2 * c + 3] + (16 * b + 4 * p) * 2);
+              fh[(c + 1) & 1] = ld128(hrow + 64 * (c + 1));
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            acc = mma(acc, fw[c & 1], fh[c & 1]);
+            __builtin_amdgcn_sched_barrier(0);
+          }
           if (store) *reinterpret_cast<u32x2*>(drow + 32 * b) = pack4(acc[0], acc[1], acc[2], acc[3]);
         }
       }
@@ -473,11 +486,16 @@ __global__ void __launch_bounds__(kThreads, 1) lenet_fc_kernel(LenetFcParams P) 
       const int n2 = 16 * a + 4 * g + i, c1 = 16 * w + r;
       if (n2 < N2 && c1 < N1) slab[kSlabW2 + n2 * N1 + c1] = dw2[a][i];
     }
-    const int n2 = 16 * w + 4 * g + i;
-    if (w < 6 && r == 0 && n2 < N2) slab[kSlabB2 + n2] = db2[i];
+    if (w == 7 && r == 8) {  // column 120 of dW2: the bias gradient
+#pragma unroll
+      for (int a = 0; a < 6; ++a) {
+        const int n2 = 16 * a + 4 * g + i;
+        if (n2 < N2) slab[kSlabB2 + n2] = dw2[a][i];
+      }
+    }
     const int n3 = 4 * g + i, c2 = 16 * w + r;
     if (w < 6 && n3 < N3 && c2 < N2) slab[kSlabW3 + n3 * N2 + c2] = dw3[i];
-    if (w == 6 && r == 0 && n3 < N3) slab[kSlabB3 + n3] = db3[i];
+    if (w == 5 && r == 4 && n3 < N3) slab[kSlabB3 + n3] = dw3[i];  // column 84 of dW3
   }
 
   // ---- statistics: lanes, then the 8 waves in a fixed order ----
