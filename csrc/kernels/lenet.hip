@@ -66,17 +66,25 @@ constexpr int kY2Elems = 25 * 16;
 // ds_read2_b64 (8 cycles, 32 banks), with the second copy offset by 8 B so the
 // two copies' lanes do not share banks (extra cycles per image 400 -> 80);
 // A1 planes are 240 B apart (224 B put channels c and c+4 on one bank).
+// Round 4 (tools/lds_banks.py lenet_fwd, conflict cycles per image 308 -> 95):
+// the conv1 tiles take their four 2x4 pixel blocks in the order kC1Blk (not
+// four consecutive blocks) and the second copy sits 80 B past its 2304-byte
+// image, so the 24 distinct 8-byte A-fragment addresses of each half-wave
+// (4 blocks x 2 copies x 3 kernel rows) land in 24 different bank pairs.
 constexpr int kFxPitch = 36, kFxRows = 32;
-constexpr int kFxCopy = kFxPitch * kFxRows * 2 + 8;  // 2312
-constexpr int kFY1 = 2 * kFxCopy;                // 4624: Y1 HWC-8, 196 x 16 B
-constexpr int kFJunk = kFY1 + 196 * 16;          // 7760: 32 B sink for the two padding blocks' Y1
-constexpr int kFA1 = kFJunk + 32;                // 7792: A1 [7][14][16] u8, planes 240 B apart (plane 6:
+constexpr int kFxCopy = kFxPitch * kFxRows * 2 + 80;  // 2384
+constexpr int kFY1 = 2 * kFxCopy;                // 4768: Y1 HWC-8, 196 x 16 B
+constexpr int kFJunk = kFY1 + 196 * 16;          // 7904: 32 B sink for the two padding blocks' Y1
+constexpr int kFA1 = kFJunk + 32;                // 7936: A1 [7][14][16] u8, planes 240 B apart (plane 6:
                                                  // sink of the idle columns 6, 7's codes, never copied out)
 constexpr int kFA1Plane = 240;
-constexpr int kFTabA = kFA1 + 7 * kFA1Plane;     // 9472: u16 [100] conv1 A offset of block b
-constexpr int kFTabE = kFTabA + 200;             // 9672: u16 [100] epilogue: pixel (lo byte), A1 offset (hi)
-constexpr int kFTab2 = kFTabE + 200;             // 9872: u16 [112] conv2 row -> Y1 byte offset
-constexpr int kFLds = kFTab2 + 224;              // 10096 (16 waves per CU fit the 160 KB)
+constexpr int kFTabA = kFA1 + 7 * kFA1Plane;     // 9616: u16 [100] conv1 A offset of tile slot b
+constexpr int kFTabE = kFTabA + 200;             // 9816: u16 [100] epilogue: pixel (lo byte), A1 offset (hi)
+constexpr int kFTab2 = kFTabE + 200;             // 10016: u16 [112] conv2 row -> Y1 byte offset
+constexpr int kFLds = kFTab2 + 224;              // 10240 (16 waves per CU: exactly the 160 KB)
+static_assert(16 * kFLds <= 163840, "lenet_fwd: 16 waves per CU");
+// conv1 tile slot -> 2x4 pixel block (98, 99: padding)
+__device__ constexpr unsigned char kC1Blk[100] = {55, 85, 91, 90, 5, 41, 3, 60, 45, 43, 81, 28, 25, 71, 44, 19, 93, 88, 12, 68, 63, 14, 89, 29, 35, 61, 13, 8, 97, 31, 33, 48, 83, 6, 73, 58, 15, 10, 46, 30, 27, 82, 79, 22, 87, 42, 78, 84, 18, 37, 24, 94, 86, 9, 40, 34, 26, 21, 92, 56, 7, 23, 49, 54, 76, 50, 59, 95, 62, 2, 36, 17, 65, 53, 38, 80, 0, 47, 32, 16, 11, 1, 57, 77, 51, 70, 75, 66, 4, 20, 39, 96, 72, 74, 98, 99, 64, 69, 52, 67};
 
 // conv2 tile order (bank-model search: b128 conflict cycles per image 202 ->
 // 34): tile T's four pool windows are kC2Win[4T..4T+3] (-1: padding row
@@ -102,6 +110,21 @@ constexpr int kBOne1 = kBXs + 4 * kBxCopy;  // 25056: 30 rows x 80 B of ones (dW
 constexpr int kBDz1 = kBOne1 + 30 * 80;  // 27456: dZ1 planar, 6 x 32 rows (zy + 2) x 32 px
 constexpr int kBDz1Plane = 32 * 64 + 32; // 2080
 constexpr int kBLds = kBDz1 + 6 * kBDz1Plane;  // 39936
+// dZ1 rows are stored with their four 16-byte pixel chunks XOR-swizzled by
+// row bit 1 (chunk c of row r at c ^ ((r >> 1) & 1)), and the conv1
+// weight-gradient MFMA rows m hold (channel, kernel-row half) pairs in the
+// order below (rows 12..15 repeat rows 0..3: broadcast reads).  With the
+// 2080-byte plane stride this makes both the dZ1 row writes of the conv2
+// data gradient and the dW1 operand reads conflict-free (bank model,
+// tools/lds_banks.py: 112 + 120 -> 0 extra LDS cycles per image).
+__device__ constexpr int kDw1Co[12] = {0, 1, 4, 5, 2, 3, 4, 5, 0, 1, 2, 3};
+// conv2 weight gradient: MFMA K position (32c + 8g + 4hf + q) -> dZ2 pixel z
+// (< 100), or padding (>= 128: the A operand reads a zero row, the B operand
+// repeats pixel v - 128 of the same half-wave, a broadcast).  Annealed in the
+// bank model so each half-wave's 8 pixels x 2 taps hit 16 different Y1 bank
+// slots: transposed-read conflict cycles per image 150 -> 15.
+__device__ constexpr unsigned char kZPos[128] = {90, 91, 32, 31, 97, 225, 225, 45, 84, 83, 92, 75, 0, 225, 2, 9, 190, 62, 81, 88, 185, 57, 26, 185, 66, 190, 190, 39, 48, 55, 4, 63, 43, 33, 50, 37, 87, 215, 54, 86, 34, 38, 41, 35, 11, 93, 94, 10, 3, 5, 1, 131, 96, 74, 70, 65, 8, 131, 30, 6, 80, 67, 69, 64, 68, 196, 71, 17, 53, 18, 19, 47, 46, 196, 49, 42, 16, 181, 181, 181, 36, 20, 164, 72, 79, 22, 78, 15, 164, 51, 77, 73, 98, 14, 23, 99, 13, 58, 89, 7, 59, 187, 187, 60, 44, 12, 85, 95, 52, 187, 187, 56, 149, 21, 28, 24, 189, 61, 189, 189, 29, 149, 76, 82, 25, 27, 40, 189};
+__device__ constexpr int kDw1S[12] = {0, 0, 1, 1, 0, 0, 0, 0, 1, 1, 1, 1};
 
 // per-wave slab of the weight gradients, in MFMA accumulator order
 constexpr int kSlabW2 = 13 * 4 * 64;     // 3328
@@ -257,14 +280,15 @@ __global__ void __launch_bounds__(64) lenet_fwd_kernel(LenetFwdParams p) {
   wave_lds_sync();
   // index tables (image invariant): block b = (row pair yp, column quad x4)
   for (int b = lane; b < 100; b += 64) {
-    const int bb = b < 98 ? b : 97;
+    const int blk = kC1Blk[b];
+    const int bb = blk < 98 ? blk : 97;
     const int yp = bb / 7, x4 = bb % 7;
     reinterpret_cast<unsigned short*>(smem + kFTabA)[b] = (unsigned short)(yp * 4 * kFxPitch + x4 * 8);
     // low byte: Y1 pixel of the block's left window (x16 = byte offset); high
     // byte: A1 offset of that window.  The two padding blocks write Y1 into
     // the sink (pixel index (kFJunk - kFY1) / 16) and A1 into the unused
     // columns 14, 15 of row 13.
-    const uint32_t e = b < 98 ? (uint32_t)(yp * 14 + 2 * x4) | ((uint32_t)(yp * 16 + 2 * x4) << 8)
+    const uint32_t e = blk < 98 ? (uint32_t)(yp * 14 + 2 * x4) | ((uint32_t)(yp * 16 + 2 * x4) << 8)
                               : (uint32_t)((kFJunk - kFY1) / 16) | ((uint32_t)(13 * 16 + 14) << 8);
     reinterpret_cast<unsigned short*>(smem + kFTabE)[b] = (unsigned short)e;
   }
@@ -452,15 +476,16 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1)))
   }
 
   // ---- per-lane LDS bases (image independent) ----
-  // dW2: transposed reads, row z = 32c + 8g + 4hf + tq (z < 100 real)
+  // dW2: transposed reads, K position 32c + 8g + 4hf + tq holds pixel kZPos[.]
   int aw2[4][2], bw2a[4][2], bw2b[4][2], bw2c[4][2];
 #pragma unroll
   for (int c = 0; c < 4; ++c)
 #pragma unroll
     for (int hf = 0; hf < 2; ++hf) {
-      const int z = 32 * c + 8 * g + 4 * hf + tq;
-      const bool ok = z < 100;
-      const int zy = ok ? z / 10 : 0, zx = ok ? z % 10 : 0;
+      const int v = kZPos[32 * c + 8 * g + 4 * hf + tq];
+      const bool ok = v < 100;
+      const int z = ok ? v : v - 128;
+      const int zy = z / 10, zx = z % 10;
       aw2[c][hf] = ok ? kBDz2 + ((zy + 4) * 20 + zx + 4) * 32 + 8 * tp : kBDz2 + 8 * tp;
       const int yb = kBY1 + (zy * 14 + zx) * 16 + 8 * (tp & 1);
       bw2a[c][hf] = yb + (tp >> 1) * 16;
@@ -470,11 +495,15 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1)))
   // dX2: A rows px = n16, k-group g: chunk tap parity (g>>1), channel half (g&1)
   const int hxa = kBDz2 + n16 * 32 + 16 * (g & 1) + (g >> 1) * 32;
   const int hxb = kBDz2 + n16 * 32 + 16 * (g & 1) + (g >> 1) * 512;
-  // dW1: A row m = co + 6s (rows 12..15 idle), B column n = 5*kh' + kw (15 = ones)
-  int a1b;
+  // dW1: A row m = (kDw1Co[m], kDw1S[m]) (rows 12..15 repeat 0..3), B column
+  // n = 5*kh' + kw (15 = ones).  Row zy + 2 - 2s of the swizzled dZ1 plane:
+  // its chunk bit is (zy >> 1) ^ 1 ^ s, so two bases by the parity of zy >> 1.
+  int a1b[2];
   {
-    const int m = n16 < 12 ? n16 : 0, co = m % 6, s = m / 6;
-    a1b = kBDz1 + co * kBDz1Plane + (2 - 2 * s) * 64 + 16 * g;
+    const int m = n16 < 12 ? n16 : n16 - 12, co = kDw1Co[m], s = kDw1S[m];
+    const int base = kBDz1 + co * kBDz1Plane + (2 - 2 * s) * 64;
+    a1b[0] = base + 16 * (g ^ 1 ^ s);
+    a1b[1] = base + 16 * (g ^ s);
   }
   int b1b;
   {
@@ -627,7 +656,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1)))
           bot[i] = (uint32_t)(w >> 32);
         }
         if (n16 < 12) {
-          char* d = smem + kBDz1 + dxci * kBDz1Plane + (4 * T + 2 * dxj + 2) * 64 + 16 * g;
+          // rows 4T + 2dxj + 2 and + 3: swizzle bit (2T + dxj + 1) & 1 = 1 - dxj
+          char* d = smem + kBDz1 + dxci * kBDz1Plane + (4 * T + 2 * dxj + 2) * 64 + 16 * (g ^ (1 - dxj));
           *reinterpret_cast<u32x4*>(d) = u32x4{top[0], top[1], top[2], top[3]};
           *reinterpret_cast<u32x4*>(d + 64) = u32x4{bot[0], bot[1], bot[2], bot[3]};
         }
@@ -645,14 +675,14 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1)))
       bf16x8 a[D], b[D];
 #pragma unroll
       for (int zy = 0; zy < D; ++zy) {
-        a[zy] = *reinterpret_cast<const bf16x8*>(smem + a1b + zy * 64);
+        a[zy] = *reinterpret_cast<const bf16x8*>(smem + a1b[(zy >> 1) & 1] + zy * 64);
         b[zy] = lds8(smem + b1b + zy * 80);
       }
 #pragma unroll
       for (int zy = 0; zy < 30; ++zy) {
         const bf16x8 ca = a[zy % D], cb = b[zy % D];
         if (zy + D < 30) {
-          a[zy % D] = *reinterpret_cast<const bf16x8*>(smem + a1b + (zy + D) * 64);
+          a[zy % D] = *reinterpret_cast<const bf16x8*>(smem + a1b[((zy + D) >> 1) & 1] + (zy + D) * 64);
           b[zy % D] = lds8(smem + b1b + (zy + D) * 80);
         }
         __builtin_amdgcn_sched_barrier(0);
@@ -700,7 +730,7 @@ __global__ void __launch_bounds__(64 * kRedWaves) lenet_bwd_reduce_kernel(LenetB
     const int q = pos - kSlabW2, i = q >> 6, ln = q & 63;
     const int m = 4 * (ln >> 4) + i, n = ln & 15;
     if (m >= 12) return;
-    const int co = m % 6, s2 = m / 6;
+    const int co = kDw1Co[m], s2 = kDw1S[m];
     if (n == 15) {
       if (s2 == 0) p.gb1[co] = v;
       return;

@@ -150,7 +150,7 @@ if __name__ == "__main__":
 
 # ---------------------------------------------------------------- lenet_bwd
 def lenet_bwd_accesses(RZ=20, RY=14, XP=40, XC=2584, R1=64, P1=2080, y1swz=None, dz1swz=None, dz1x=None,
-                       cb=None, onesb=None, zperm=None, dz2full=False):
+                       cb=None, onesb=None, zperm=None, dz2full=False, dw1rows=None):
     """Every LDS instruction of one image of lenet.hip's lenet_bwd_kernel
     (per-lane byte addresses), for the layout parameters: dZ2 row pitch RZ
     (32-B pixels), Y1 row pitch RY (16-B pixels), X row pitch XP (bf16) and
@@ -160,7 +160,7 @@ def lenet_bwd_accesses(RZ=20, RY=14, XP=40, XC=2584, R1=64, P1=2080, y1swz=None,
     y1swz = y1swz or (lambda px: 0)
     dz1swz = dz1swz or (lambda row: 0)
     dz1x = dz1x or (lambda row: 0)         # dZ1 16-B chunk g of row r stored at chunk g ^ dz1x(r)
-    zperm = zperm or list(range(128))      # K position -> dZ2 pixel z (>= 100: padding)
+    zperm = zperm or list(range(128))      # K position -> dZ2 pixel z (>= 100: padding, see below)
     kBDz2 = 0
     kBY1 = 18 * RZ * 32
     kBOne2 = kBY1 + 14 * RY * 16 + 64
@@ -215,9 +215,10 @@ def lenet_bwd_accesses(RZ=20, RY=14, XP=40, XC=2584, R1=64, P1=2080, y1swz=None,
             for l in L:
                 g = l >> 4
                 tq, tp = (l >> 2) & 3, l & 3
-                z = zperm[32 * c + 8 * g + 4 * hf + tq]
-                ok = z < 100
-                zy, zx = (z // 10, z % 10) if ok else (0, 0)
+                v = zperm[32 * c + 8 * g + 4 * hf + tq]  # < 100: pixel; >= 128: padding (B as pixel v - 128)
+                ok = v < 100
+                z = v if ok else (v - 128 if v >= 128 else 0)
+                zy, zx = z // 10, z % 10
                 aw.append(kBDz2 + ((zy + 4) * RZ + zx + 4) * 32 + 8 * tp if ok else kBDz2 + 8 * tp)
                 for t in range(13):
                     tap = 2 * t + (tp >> 1)
@@ -258,8 +259,11 @@ def lenet_bwd_accesses(RZ=20, RY=14, XP=40, XC=2584, R1=64, P1=2080, y1swz=None,
         a, b = [], []
         for l in L:
             n16, g = l & 15, l >> 4
-            m = n16 if n16 < 12 else 0
-            co, s = m % 6, m // 6
+            if dw1rows:  # MFMA row m -> (channel, kernel-row half); rows 12..15 repeat 0..3
+                co, s = dw1rows[n16 if n16 < 12 else n16 - 12]
+            else:
+                m = n16 if n16 < 12 else 0
+                co, s = m % 6, m // 6
             row = zy + 2 - 2 * s
             a.append(kBDz1 + co * P1 + dz1(row) + 16 * (g ^ dz1x(row)))
             if n16 == 15:
@@ -295,3 +299,104 @@ def lenet_bwd_report(**kw):
 
 if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "lenet_bwd":
     lenet_bwd_report()
+
+
+# ---------------------------------------------------------------- lenet_fwd
+C2WIN = [13, 18, 8, 3, 20, 5, 15, 10, 1, -1, -1, 23, 7, 2, 12, 17, 11, 6, 16, 21, 9, 4, 0, 19, -1, 14, 22, 24]
+C2TAP = [12, 19, 7, 0, 17, 10, 8, 1, 2, 9, 26, 14, 20, 5, 13, 6, 21, 16, 15, 22, 27, 25, 18, 11, 3, 23, 24, 4]
+
+
+def lenet_fwd_accesses(FXP=36, FXC=None, A1P=240, Y1PIX=16, y1swz=None, bperm=None):
+    """LDS instructions of one image of lenet.hip's lenet_fwd_kernel."""
+    FXC = FXC if FXC is not None else FXP * 32 * 2 + 8
+    bperm = bperm or list(range(100))
+    y1swz = y1swz or (lambda px: 0)
+    kFY1 = 2 * FXC
+    kFA1 = kFY1 + 196 * Y1PIX + 32
+    L = range(64)
+    acc = []
+    for it in range(4):
+        for cp in range(2):
+            addrs = []
+            for l in L:
+                sk, srow = l & 7, l >> 3
+                yy = it * 8 + srow
+                addrs.append(((yy + 2) * FXP + 4 * sk) * 2 + cp * FXC if yy < 28 else None)
+            acc.append(("x stage", "write_b64", addrs, 1))
+    def y1(px):
+        return kFY1 + px * Y1PIX + y1swz(px)
+    for T in range(25):
+        for part in range(4):  # fa lo, fa hi, fb lo, fb hi
+            addrs = []
+            for l in L:
+                n16, g = l & 15, l >> 4
+                msub, mblk = n16 & 3, n16 >> 2
+                b = bperm[4 * T + mblk]
+                bb = b if b < 98 else 97
+                yp, x4 = bb // 7, bb % 7
+                off = yp * 4 * FXP + x4 * 8
+                a1base = (msub >> 1) * FXC + ((msub & 1) * FXP + g * FXP) * 2
+                a1c1 = a1base + (4 - g) * FXP * 2
+                base = a1base if part < 2 else a1c1
+                addrs.append(base + off + (8 if part & 1 else 0))
+            acc.append(("conv1 A", "read_b64", addrs, 1))
+        # epilogue writes
+        ya, aa = [], []
+        for l in L:
+            n16, g = l & 15, l >> 4
+            co1, j1 = n16 >> 1, n16 & 1
+            b = bperm[4 * T + g]
+            if b < 98:
+                yp, x4 = b // 7, b % 7
+                px = yp * 14 + 2 * x4
+                a1off = yp * 16 + 2 * x4
+            else:
+                px, a1off = None, 13 * 16 + 14
+            ya.append((y1(px + j1) + co1 * 2) if px is not None else kFY1 + 196 * Y1PIX + j1 * 16 + co1 * 2)
+            aa.append(kFA1 + a1off + min(co1, 6) * A1P + j1)
+        acc.append(("y1 write", "write_b16", ya, 1))
+        acc.append(("a1 write", "write_b16", aa, 1))  # b8: same banking as b16 here
+    for rr in range(4):
+        acc.append(("y1 bulk", "read_b128", [y1(l + 64 * rr) if l + 64 * rr < 196 else None for l in L], 1))
+    for rr in range(2):
+        acc.append(("a1 bulk", "read_b128",
+                    [kFA1 + ((l + 64 * rr) // 14) * A1P + ((l + 64 * rr) % 14) * 16 if l + 64 * rr < 84 else None
+                     for l in L], 1))
+    for T in range(7):
+        for c in range(7):
+            addrs = []
+            for l in L:
+                n16, g = l & 15, l >> 4
+                r = 16 * T + n16
+                wr = C2WIN[4 * (r >> 4) + ((r & 15) >> 2)]
+                w = 24 if wr < 0 else wr
+                pos = r & 3
+                px = (2 * (w // 5) + (pos >> 1)) * 14 + 2 * (w % 5) + (pos & 1)
+                t = C2TAP[4 * c + g]
+                kh, kw = (t // 5, t % 5) if t < 25 else (0, 0)
+                addrs.append(y1(px + kh * 14 + kw))
+            acc.append(("conv2 A", "read_b128", addrs, 1))
+    return acc
+
+
+def lenet_fwd_report(**kw):
+    acc = lenet_fwd_accesses(**kw)
+    rows = {}
+    tot = ex = 0
+    for name, kind, addrs, n in acc:
+        c = cycles(kind, addrs)
+        e = c - ideal(kind)
+        r = rows.setdefault(name, [0, 0, 0])
+        r[0] += n
+        r[1] += n * c
+        r[2] += n * e
+        tot += n * c
+        ex += n * e
+    print(f"per image: {tot:.0f} LDS-array cycles, {ex:.0f} conflict cycles")
+    for k, (n, c, e) in rows.items():
+        print(f"  {k:10s} {n:5.0f} instr {c:6.0f} cycles {e:5.0f} extra")
+    return tot, ex
+
+
+if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "lenet_fwd":
+    lenet_fwd_report()
