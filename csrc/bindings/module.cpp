@@ -358,20 +358,18 @@ PYBIND11_MODULE(_C, m) {
         py::arg("stream") = 0);
   k.def("fc",
         [](int M, int N, int K, uintptr_t A, int lda, uintptr_t W, int ldw, int epi, int act, uintptr_t bias,
-           uintptr_t aux, int ldaux, uintptr_t C, int ldc, uintptr_t Cf, uintptr_t dbg, int ablate, uintptr_t s) {
+           uintptr_t aux, int ldaux, uintptr_t C, int ldc, uintptr_t Cf, uintptr_t dbg, uintptr_t s) {
           gpu::FcParams p;
           p.M = M; p.N = N; p.K = K;
           p.A = ptr<void>(A); p.lda = lda; p.W = ptr<void>(W); p.ldw = ldw;
           p.epi = epi; p.act = act; p.bias = ptr<float>(bias); p.aux = ptr<void>(aux); p.ldaux = ldaux;
           p.C = ptr<void>(C); p.ldc = ldc; p.Cf = ptr<float>(Cf);
           p.dbg = ptr<long long>(dbg);
-          p.ablate = ablate;
           gpu::fc_forward(p, stream_of(s));
         },
         py::arg("M"), py::arg("N"), py::arg("K"), py::arg("A"), py::arg("lda"), py::arg("W"), py::arg("ldw"),
         py::arg("epi") = 0, py::arg("act") = 0, py::arg("bias") = 0, py::arg("aux") = 0, py::arg("ldaux") = 0,
-        py::arg("C") = 0, py::arg("ldc") = 0, py::arg("Cf") = 0, py::arg("dbg") = 0, py::arg("ablate") = 0,
-        py::arg("stream") = 0);
+        py::arg("C") = 0, py::arg("ldc") = 0, py::arg("Cf") = 0, py::arg("dbg") = 0, py::arg("stream") = 0);
   k.def("fc_supported", &gpu::fc_supported);
   k.def("igemm_conv_supported", &gpu::igemm_conv_supported);
   k.def("igemm_conv",

@@ -1,5 +1,4 @@
 // CPU reference executor.  See mcc/cpu_net.h for the reference mapping.
-#include "mcc/ab.h"
 #include "mcc/cpu_net.h"
 #include "mcc/cpu_kernels.h"
 
@@ -95,10 +94,9 @@ CpuNet<T>::CpuNet(const ModelSpec& spec, bool ref_compat) : spec_(spec), ref_com
 template <typename T>
 const CpuKernels<T>& cpu_kernels() {
   static const CpuKernels<T> k = [] {
-    const bool base = ab_flag("cpu_baseline");  // A/B: the portable kernel table
 #if defined(__x86_64__) && defined(__GNUC__)
     __builtin_cpu_init();
-    if (!base && __builtin_cpu_supports("avx2") && __builtin_cpu_supports("fma")) return cpu_v3::kernels<T>();
+    if (__builtin_cpu_supports("avx2") && __builtin_cpu_supports("fma")) return cpu_v3::kernels<T>();
 #endif
     return cpu_base::kernels<T>();
   }();

@@ -123,12 +123,7 @@ GpuNet::GpuNet(const ModelSpec& spec, DType dtype, int max_batch, int device)
     MCC_CHECK((int64_t)max_batch * ((l.C + 15) / 16 * 16) * l.H * l.W < (1ll << 31),
               "GpuNet: max_batch too large for 32-bit activation indexing");
   // A/B switches (mcc/ab.h, MCC_AB=...)
-  ablate_ = ab_int("ablate", 0);         // kernel diagnostics only
-  no_pipe_ = ab_flag("no_pipe");         // conv_small instead of the pipelined kernels
-  no_fc_ = ab_flag("no_fc");             // tiled GEMM instead of the weights-resident FC kernel
   no_igemm_ = ab_flag("no_igemm");       // im2col + GEMM instead of the implicit GEMM
-  igemm_small_ = !ab_flag("no_igemm_small");  // LDS kernels for wide small-image convs
-  no_head_ = ab_flag("no_head");         // softmax_xent + FC backward instead of the fused head
   // dW side stream: opt-in (MCC_AB=side_stream).  Measured on MI355X (one GPU,
   // bench.py): CIFAR-3conv 2.27 -> 2.17 ms/step, but LeNet-5 0.452 -> 0.502 and
   // VGG-11 12.14 -> 12.40: the persistent conv kernels are sized to own every
@@ -299,10 +294,10 @@ void GpuNet::build() {
                (int64_t)LHd * LWd * st.CLd * (int64_t)es > lds_cap || (int64_t)dw_img_b > lds_cap || st.generic;
       MCC_CHECK(!st.generic || st.C % 8 == 0, "GPU engine: tanh convs / pools after a non-ReLU conv need Cout % 8 == 0");
       // small images with wide channels (C % 64, Cout % 8, stride 1) go to the
-      // 128x128 / 256-tile MFMA kernels (MCC_AB=no_igemm_small: the whole-image LDS
-      // kernels).  CIFAR-3conv conv3 (64 -> 128): 3.91 -> 4.32 M img/s; conv2
+      // 128x128 / 256-tile MFMA kernels (the whole-image LDS kernels
+      // measured slower there).  CIFAR-3conv conv3 (64 -> 128): 3.91 -> 4.32 M img/s; conv2
       // (32 -> 64) measured slower on igemm (3.83 M), so C % 64 only.
-      if (!st.big && igemm_small_ && s > 0 && dtype_ == DType::BF16 && !no_igemm_ && st.stride == 1 &&
+      if (!st.big && s > 0 && dtype_ == DType::BF16 && !no_igemm_ && st.stride == 1 &&
           st.inC % 64 == 0 && st.C % 64 == 0 &&
           gpu::igemm_conv_supported(st.inC, st.C, st.KS) && gpu::igemm_conv_supported(st.C, st.inC, st.KS))
         st.big = true;
@@ -315,8 +310,7 @@ void GpuNet::build() {
       if (st.ig_dw0 && st.KS * st.KS * st.inC <= 64) st.ig_fwd = true;
       // first layer weight gradient straight from the pooled dY / argmax
       if (st.ig_dw0 && st.ig_fwd && st.pooled && st.pk == 2 && st.ps == 2 && st.act == gpu::ACT_RELU && st.KS == 3 &&
-          st.stride == 1 && st.pad == 1 &&
-          !ab_flag("no_c0dw")) {
+          st.stride == 1 && st.pad == 1) {
         gpu::Conv0DwParams& c = st.pc0;
         c.B = max_batch_; c.H = st.OH; c.W = st.OW; c.C = st.inC; c.PH = st.outH; c.PW = st.outW; c.Cout = st.C;
         st.c0dw = st.OH == st.inH && st.OW == st.inW && gpu::conv0_dw_supported(c);
@@ -328,8 +322,8 @@ void GpuNet::build() {
         st.ig_dx = st.stride == 1 && gpu::igemm_conv_supported(st.C, st.inC, st.KS);
       }
       st.ig_pool = st.ig_fwd && st.pooled && st.pk == 2 && st.ps == 2 && st.OH % 2 == 0 && st.OW % 2 == 0;
-      if (!st.big && dtype_ == DType::BF16 && !no_pipe_) plan_pipe(st, s == 0);
-      if (!st.big && dtype_ == DType::F32 && st.pooled && st.stride == 1 && !no_pipe_ &&
+      if (!st.big && dtype_ == DType::BF16) plan_pipe(st, s == 0);
+      if (!st.big && dtype_ == DType::F32 && st.pooled && st.stride == 1 &&
           (s == 0 || st.inC > 1)) {
         gpu::Conv1DirectParams& d = st.pd1;
         d.N = max_batch_; d.H = st.inH; d.W = st.inW; d.Cin = st.inC; d.KS = st.KS; d.pad = st.pad; d.C = st.C;
@@ -346,7 +340,7 @@ void GpuNet::build() {
         u.N = max_batch_; u.H = st.inH; u.W = st.inW; u.Cout = st.C;
         st.u8fwd = st.OH == st.inH && st.OW == st.inW && gpu::u8conv_fwd_supported(u);
         // small images (CIFAR): the first layer's dW from the pooled dY / argmax too
-        if (st.u8fwd && !st.big && !ab_flag("no_c0dw")) {
+        if (st.u8fwd && !st.big) {
           gpu::Conv0DwParams& c = st.pc0;
           c.B = max_batch_; c.H = st.OH; c.W = st.OW; c.C = st.inC; c.PH = st.outH; c.PW = st.outW; c.Cout = st.C;
           st.c0dw = gpu::conv0_dw_supported(c);
@@ -357,7 +351,7 @@ void GpuNet::build() {
       st.out_ld = r8(st.Nout);
       st.ldp = r8(st.Kin + 1);
       st.fc_big = (int64_t)st.Nout * st.Kin >= (1 << 20) &&
-                  !(dtype_ == DType::BF16 && !no_fc_ && gpu::fc_supported(st.Kin, st.Nout));
+                  !(dtype_ == DType::BF16 && gpu::fc_supported(st.Kin, st.Nout));
     }
     if (s > 0) {
       const Stage& pv = *stages_[s - 1];
@@ -366,7 +360,7 @@ void GpuNet::build() {
     }
     if (st.kind == Stage::FC) MCC_CHECK(st.in_ld % 8 == 0, "fc input leading dim must be a multiple of 8");
     if (st.kind == Stage::FC && dtype_ == DType::BF16 && !st.last && !st.fc_big && !no_igemm_ &&
-        !ab_flag("no_fc_ig") && max_batch_ >= 8192 && st.Kin % 64 == 0 && st.Nout % 64 == 0 &&
+        max_batch_ >= 8192 && st.Kin % 64 == 0 && st.Nout % 64 == 0 &&
         st.in_ld == st.Kin && st.out_ld == st.Nout && !gpu::fc_supported(st.Nout, st.Kin)) {
       st.fc_ig = gpu::igemm_conv_supported(st.Kin, st.Nout, 1);
       // data gradient: pv's act' is a ReLU mask (FC) or nothing (conv: its staging applies it)
@@ -375,7 +369,7 @@ void GpuNet::build() {
                    (pv->kind == Stage::CONV || pv->act == gpu::ACT_RELU || pv->act == gpu::ACT_NONE) &&
                    gpu::igemm_conv_supported(st.Nout, st.Kin, 1);
     }
-    st.head = st.kind == Stage::FC && st.last && s > 0 && dtype_ == DType::BF16 && !no_head_ &&
+    st.head = st.kind == Stage::FC && st.last && s > 0 && dtype_ == DType::BF16 &&
               gpu::xent_head_supported(st.Nout, st.Kin, st.in_ld);
     // FC weight gradient on the implicit-GEMM dW kernel (a 1x1 "conv" over the
     // batch, C = in_ld with the pad columns dropped by the reduce)
@@ -403,10 +397,10 @@ void GpuNet::build() {
   }
   // ---- reference-model conv block (refnet.hip): conv 1->16 and 16->32, 3x3
   // stride 2 pad 1 ReLU on 28x28, fused forward and fused backward
-  // (recomputed conv1, sub-pixel conv2 dX).  MCC_AB=no_refblk: per-layer kernels.
+  // (recomputed conv1, sub-pixel conv2 dX).
   {
     refblk_ = false;
-    if (dtype_ == DType::BF16 && stages_.size() >= 3 && !ab_flag("no_refblk")) {
+    if (dtype_ == DType::BF16 && stages_.size() >= 3) {
       const Stage& a = *stages_[0];
       const Stage& b = *stages_[1];
       auto s2 = [](const Stage& x) {
@@ -930,7 +924,7 @@ void GpuNet::forward_stages(size_t first, bool defer_fc, hipStream_t s) {
       gpu::conv_direct_forward(p, s);
     } else if (st.kind == Stage::CONV && st.pipe_fwd) {
       gpu::ConvPipeParams p = st.pf;
-      p.N = B; p.ablate = ablate_;
+      p.N = B;
       if (si == 0) { p.in.src = images; p.in.idx = idx; }
       else p.in.src = stages_[si - 1]->act_buf;
       p.wpk = static_cast<const char*>(packed_) + es * st.pk_fwd;
@@ -951,7 +945,7 @@ void GpuNet::forward_stages(size_t first, bool defer_fc, hipStream_t s) {
       p.wpk = static_cast<const char*>(packed_) + es * st.pk_fwd;
       p.bias = params_ + st.b_off;
       p.out = st.act_buf; p.out_arg = st.arg_buf;
-      p.ablate = ablate_;
+     
       gpu::conv_forward(dtype_, p, s);
     } else if (st.fc_ig) {
       const Stage& pv = *stages_[si - 1];
@@ -964,7 +958,7 @@ void GpuNet::forward_stages(size_t first, bool defer_fc, hipStream_t s) {
       g.bias = params_ + st.b_off; g.epi_bias_act = true; g.act = st.act;
       g.out = st.act_buf; g.ldo = st.out_ld;
       gpu::igemm_conv(g, s);
-    } else if (dtype_ == DType::BF16 && !no_fc_ && gpu::fc_supported(st.Nout, st.Kin)) {
+    } else if (dtype_ == DType::BF16 && gpu::fc_supported(st.Nout, st.Kin)) {
       const Stage& pv = *stages_[si - 1];
       gpu::FcParams p;
       p.M = B; p.N = st.Nout; p.K = st.Kin;
@@ -1257,14 +1251,14 @@ void GpuNet::backward(int hi, int lo, hipStream_t s) {
         gpu::conv_direct_dw(w, grads_ + st.w_off, grads_ + st.b_off, ws);
       } else if (st.rows_dw) {
         gpu::ConvDwRowsParams w = st.prw;
-        w.N = B; w.ablate = ablate_;
+        w.N = B;
         w.x = images_; w.idx = idx_;
         w.dy = st.grad_buf; w.aux_y = st.act_buf; w.aux_arg = st.arg_buf;
         w.slab = scratch_;
         gpu::conv_dw_rows(w, grads_ + st.w_off, grads_ + st.b_off, ws);
       } else if (st.pipe_dw) {
         gpu::ConvDwPipeParams w = st.pdw;
-        w.N = B; w.ablate = ablate_;
+        w.N = B;
         if (si == 0) { w.x.src = images_; w.x.idx = idx_; }
         else w.x.src = stages_[si - 1]->act_buf;
         w.dy.src = st.grad_buf; w.dy.aux_y = st.act_buf; w.dy.aux_arg = st.arg_buf;
@@ -1274,7 +1268,7 @@ void GpuNet::backward(int hi, int lo, hipStream_t s) {
       }
       if (st.pipe_dx && si > 0) {
         gpu::ConvPipeParams p = st.pdx;
-        p.N = B; p.ablate = ablate_;
+        p.N = B;
         p.in.src = st.grad_buf; p.in.aux_y = st.act_buf; p.in.aux_arg = st.arg_buf;
         p.wpk = static_cast<const char*>(packed_) + es * st.pk_dx;
         p.out = stages_[si - 1]->grad_buf;
@@ -1297,7 +1291,7 @@ void GpuNet::backward(int hi, int lo, hipStream_t s) {
       w.dy = dy;
       w.slab = scratch_;
       MCC_CHECK((size_t)w.nx * w.cout_pad * w.ncols_pad * 4 <= scratch_bytes_, "conv dW scratch too small");
-      w.ablate = ablate_;
+     
       gpu::conv_dw(dtype_, w, ws);
       gpu::ConvDwReduceParams r;
       r.nx = w.nx; r.Cout = st.C; r.Cin = st.inC; r.KS = st.KS; r.CG = st.CLdw; r.cvec = st.cvec;
@@ -1323,7 +1317,7 @@ void GpuNet::backward(int hi, int lo, hipStream_t s) {
         p.in.off = st.KS - 1 - st.pad; p.in.up = st.stride;
         p.wpk = static_cast<const char*>(packed_) + es * st.pk_dx;
         p.out = stages_[si - 1]->grad_buf;
-        p.ablate = ablate_;
+       
         gpu::conv_forward(dtype_, p, s);
       }
     } else {
@@ -1370,7 +1364,7 @@ void GpuNet::backward(int hi, int lo, hipStream_t s) {
         g.relu_mask = pv.kind == Stage::FC && pv.act == gpu::ACT_RELU ? pv.act_buf : nullptr;
         g.out = pv.grad_buf; g.ldo = st.in_ld;
         gpu::igemm_conv(g, s);
-      } else if (si > 0 && dtype_ == DType::BF16 && !no_fc_ && gpu::fc_supported(st.Kin, st.Nout)) {
+      } else if (si > 0 && dtype_ == DType::BF16 && gpu::fc_supported(st.Kin, st.Nout)) {
         gpu::FcParams d;
         d.M = B; d.N = st.Kin; d.K = st.Nout;
         d.A = st.grad_buf; d.lda = st.out_ld;

@@ -428,7 +428,7 @@ __global__ void __launch_bounds__(256) conv_fwd_kernel(ConvParams p) {
   }
   pixel_table(ptab, rows_per_img, pool, p.OW, PW, p.cs, p.LW, p.CL);
   __syncthreads();
-  if (p.ablate != 1) stage_scatter<T, false>(p.in, ScatterPlan(p.in), xs, img0, nimg, p.LH, p.LW, p.CL);
+  stage_scatter<T, false>(p.in, ScatterPlan(p.in), xs, img0, nimg, p.LH, p.LW, p.CL);
   __syncthreads();
 
   const int lane = tid & 63, wave = tid >> 6, nwaves = blockDim.x >> 6;
@@ -439,7 +439,7 @@ __global__ void __launch_bounds__(256) conv_fwd_kernel(ConvParams p) {
   T* out = static_cast<T*>(p.out);
   const size_t obase = pool ? (size_t)img0 * PH * PW : (size_t)img0 * p.OH * p.OW;
 
-  for (int item = wave; item < (p.ablate == 2 ? 0 : ntiles * mgroups); item += nwaves) {
+  for (int item = wave; item < ntiles * mgroups; item += nwaves) {
     const int nt = item / mgroups, mg = item - nt * mgroups;
     int base[MT];
 #pragma unroll
@@ -586,13 +586,11 @@ __global__ void __launch_bounds__(256) conv_dw_tr_kernel(ConvDwParams p) {
     const int npix = nimg * opix;
     __syncthreads();  // previous stage fully consumed (and the zero fill done)
     if (nimg < p.imgs) lds_zero(dys + npix * drow, (p.ppad - npix) * drow);  // stale rows of a tail stage
-    if (p.ablate != 1) {
-      stage_scatter<T, false>(p.x, plx, xs, img0, nimg, p.LH, p.LW, CL);
-      stage_scatter<T, false, true>(p.dy, pldy, dys, img0, nimg, p.OH, p.OW, drow);
-    }
+    stage_scatter<T, false>(p.x, plx, xs, img0, nimg, p.LH, p.LW, CL);
+    stage_scatter<T, false, true>(p.dy, pldy, dys, img0, nimg, p.OH, p.OW, drow);
     __syncthreads();
     const int nq = cdiv(npix, 32);
-    for (int qc = wave; qc < (p.ablate == 2 ? 0 : nq); qc += nwaves) {
+    for (int qc = wave; qc < nq; qc += nwaves) {
       // fragment k -> pixel: lane group g reads rows 4g..4g+3 (and +16), so
       // the four groups of a read cover 16 consecutive 32-byte rows
       const int pix1 = qc * 32 + 4 * g + q, pix2 = pix1 + 16;
@@ -720,17 +718,15 @@ __global__ void __launch_bounds__(256) conv_dw_kernel(ConvDwParams p) {
     lds_zero(xs, xs_elems);
     lds_zero(dys, p.cout_pad * drow);
     __syncthreads();
-    if (p.ablate != 1) {
-      stage_scatter<T, false>(p.x, plx, xs, img0, nimg, p.LH, p.LW, p.CL);
-      stage_scatter<T, true>(p.dy, pldy, dys, img0, nimg, p.OH, p.OW, drow);
-    }
+    stage_scatter<T, false>(p.x, plx, xs, img0, nimg, p.LH, p.LW, p.CL);
+    stage_scatter<T, true>(p.dy, pldy, dys, img0, nimg, p.OH, p.OW, drow);
     for (int pix = tid; pix < p.ppad; pix += blockDim.x) {
       const int img = dopix.div(pix);
       pixbase[pix] = pix < npix ? img * img_elems + ptab[pix - img * opix] : 0;  // dY is 0 there
     }
     __syncthreads();
     const int nq = cdiv(npix, 32);
-    for (int q = wave; q < (p.ablate == 2 ? 0 : nq); q += nwaves) {
+    for (int q = wave; q < nq; q += nwaves) {
       int pb[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) pb[j] = pixbase[q * 32 + 8 * g + j];

@@ -389,7 +389,7 @@ size_t conv0_dw_slab_bytes(const Conv0DwParams& p) {
 void conv0_dw(const Conv0DwParams& p, float* gw, float* gb, hipStream_t s) {
   MCC_CHECK(conv0_dw_supported(p) && p.x && p.dy && p.arg && p.slab, "conv0_dw: bad params");
   int grid;
-  if (conv0_dw_rows_ok(p) && !ab_flag("no_c0dw_rows")) {
+  if (conv0_dw_rows_ok(p)) {
     grid = conv0_dw_rows_grid(p);
     if (p.Cout == 32) hipLaunchKernelGGL((conv0_dw_rows_kernel<2>), dim3((unsigned)grid), dim3(kRT), 0, s, p);
     else hipLaunchKernelGGL((conv0_dw_rows_kernel<4>), dim3((unsigned)grid), dim3(kRT), 0, s, p);

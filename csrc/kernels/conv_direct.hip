@@ -730,14 +730,13 @@ void conv1_direct_dw(const Conv1DirectParams& p, float* gw, float* gb, hipStream
   MCC_CHECK(conv1_direct_dw_supported(p) && p.x && p.dy && p.arg && p.slab, "conv1_direct_dw: bad params");
   const int grid = direct_grid(p);
   const dim3 g((unsigned)grid), b(kDT);
-  if (p.KS == 5 && p.C == 6 && !ab_flag("no_dw1_split")) {
+  if (p.KS == 5 && p.C == 6) {
     const int g3 = dw3_grid(p);
     const size_t lds = (size_t)kDW3Imgs * d_tile(p).IMG * 4 + (size_t)kDW3Imgs * p.PH * p.PW * p.C * 5;
     hipLaunchKernelGGL((conv1_direct_dw_w3_kernel<5>), dim3((unsigned)g3), dim3(kDW3T), lds, s, p);
     dw_reduce(p, g3, gw, gb, s);
     return;
   }
-  else if (p.KS == 5 && p.C == 6) hipLaunchKernelGGL((conv1_direct_dw_kernel<5, 6, true>), g, b, dw_lds(p), s, p);
   else if (p.KS == 5) hipLaunchKernelGGL((conv1_direct_dw_kernel<5, kDMaxC, false>), g, b, dw_lds(p), s, p);
   else hipLaunchKernelGGL((conv1_direct_dw_kernel<3, kDMaxC, false>), g, b, dw_lds(p), s, p);
   dw_reduce(p, grid, gw, gb, s);

@@ -310,7 +310,7 @@ __host__ __device__ inline int row_offset(int r, bool pool, int OW, int cs, int 
   }
 }
 // Entries rows..rows_pad-1 (tile padding) repeat row 0.
-__device__ void row_table(int* tab, int rows, bool pool, int OW, int cs, int ty0, int tx0, int LWp, int CL,
+[[maybe_unused]] __device__ void row_table(int* tab, int rows, bool pool, int OW, int cs, int ty0, int tx0, int LWp, int CL,
                           int pair = 0, int rows_pad = 0) {
   for (int rr = threadIdx.x; rr < max(rows, rows_pad); rr += blockDim.x)
     tab[rr] = row_offset(rr < rows ? rr : 0, pool, OW, cs, ty0, tx0, LWp, CL, pair);
@@ -431,7 +431,7 @@ constexpr int kCUs = 256;
 constexpr size_t kLdsPerCU = 160 * 1024;
 
 // Destination geometry of a staged source; returns false if unsupported.
-bool plan_src(PipeSrc& s, int layout, int CLdst, int LH, int LWp, int IMGextra) {
+[[maybe_unused]] bool plan_src(PipeSrc& s, int layout, int CLdst, int LH, int LWp, int IMGextra) {
   (void)LH; (void)IMGextra;
   if (s.mode == PM_U8S1) {
     if (s.SC != 1 || (s.SW & 3) != 0 || s.up != 1 || (s.offx & 3) != 0 || s.offx < 4) return false;
@@ -450,13 +450,12 @@ bool plan_src(PipeSrc& s, int layout, int CLdst, int LH, int LWp, int IMGextra) 
   return true;
 }
 
-// Occupancy / group-size knobs of the pipelined conv planners (A/B tuning
-// only, MCC_AB=dw_wgs=N etc.; defaults are the measured choices).
-inline int pipe_knob(const char* name, int def) { return ab_int(name, def); }
-inline int dw_wgs_cap() { return pipe_knob("dw_wgs", 2); }
-inline int fwd_wgs_cap() { return pipe_knob("fwd_wgs", 4); }
-inline size_t dw_lds_target() { return (size_t)pipe_knob("dw_lds_kb", 64) * 1024; }
-inline size_t fwd_lds_target() { return (size_t)pipe_knob("fwd_lds_kb", 64) * 1024; }
+// Occupancy / group-size choices of the pipelined conv planners (measured:
+// workgroups per CU and the LDS footprint a group of images may grow to).
+constexpr int dw_wgs_cap() { return 2; }
+constexpr int fwd_wgs_cap() { return 4; }
+constexpr size_t dw_lds_target() { return (size_t)64 * 1024; }
+constexpr size_t fwd_lds_target() { return (size_t)64 * 1024; }
 
 int wgs_per_cu(size_t lds, int cap) {
   int w = (int)(kLdsPerCU / (lds + 512));

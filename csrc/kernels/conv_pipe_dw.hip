@@ -112,17 +112,15 @@ __global__ void __launch_bounds__(kT) conv_dw_pipe_kernel(ConvDwPipeParams p) {
     const int nimg = min(p.imgs, p.N - img0);
     const int npix = nimg * opix;
     __syncthreads();  // previous group consumed
-    if (!(p.ablate & 1)) {
-      lx.store(sx, xs, nimg);
-      ld.store(sd, dys, nimg);
-    }
+    lx.store(sx, xs, nimg);
+    ld.store(sd, dys, nimg);
     if (nimg < p.imgs) zero_lds(dys + npix * drow, (p.ppad - npix) * drow);  // stale rows of a tail group
     __syncthreads();
-    if (!(p.ablate & 1) && grp + (int)gridDim.x < p.ngroups) {
+    if (grp + (int)gridDim.x < p.ngroups) {
       lx.load(sx, (grp + gridDim.x) * p.imgs, p.N);
       ld.load(sd, (grp + gridDim.x) * p.imgs, p.N);
     }
-    const int nq = (p.ablate & 2) ? 0 : cdiv(npix, 32);
+    const int nq = cdiv(npix, 32);
     // fragment k -> pixel: lane group g reads rows 4g..4g+3 (and +16).
     // Pipelined one pixel chunk deep (pixbase is padded by one chunk).
     constexpr int QS = WS ? 1 : kT / 64;  // chunk step: WS waves walk every chunk
@@ -304,7 +302,7 @@ bool conv_dw_pipe_plan(ConvDwPipeParams& p) {
   // there are enough of them (4 waves x NTW)
   {
     const int mtw = p.cout_pad / 16, nct = p.ncols_pad / 16;
-    p.wsplit = mtw >= 4 && nct >= 2 * dw_ntw(mtw, nct) && !pipe_knob("no_dw_wsplit", 0) ? 1 : 0;
+    p.wsplit = mtw >= 4 && nct >= 2 * dw_ntw(mtw, nct) ? 1 : 0;
   }
   const int nix = mode_ni(x.mode) * kT / std::max(1, x.per_img);
   const int nid = mode_ni(d.mode) * kT / std::max(1, d.per_img);

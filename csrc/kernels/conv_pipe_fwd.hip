@@ -144,10 +144,10 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WR > 0 
     const int nimg = min(p.imgs, p.N - img0);
     if (k > 0) {
       __syncthreads();  // tiles free: previous compute and copy-out done (and setup, first time)
-      if (!(p.ablate & 1)) ld.store(s, xs, nimg);
+      ld.store(s, xs, nimg);
       __syncthreads();
     }
-    if (!(p.ablate & 1) && lgrp < p.ngroups) ld.load(s, lgrp * p.imgs, p.N, (lgrp + (int)gridDim.x) * p.imgs);
+    if (lgrp < p.ngroups) ld.load(s, lgrp * p.imgs, p.N, (lgrp + (int)gridDim.x) * p.imgs);
     if (k == 0) continue;
 
     if constexpr (PAIR == 2) {
@@ -156,7 +156,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WR > 0 
       // index and every bound are wave-uniform scalars; the lane's row offset
       // is one table read.  Weights are register-resident (<= 2 K chunks).
       const int tpi = rows_pad >> 4, ntl = nimg * tpi, nbw = rows_img >> 2;
-      for (int item = wave; item < ((p.ablate & 2) ? 0 : cdiv(ntl, MT)); item += NT / 64) {
+      for (int item = wave; item < cdiv(ntl, MT); item += NT / 64) {
         int img[MT], ti[MT], base[MT];
 #pragma unroll
         for (int t = 0; t < MT; ++t) {
@@ -182,10 +182,6 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WR > 0 
         } else {
 #pragma unroll
           for (int t = 0; t < MT; ++t) acc[t] = mma(acc[t], a0[t], wreg[0]);
-        }
-        if (p.ablate & 4) {  // keep the accumulators live, skip the epilogue
-          if (acc[0][0] == 1234.5f && acc[MT - 1][3] == -1.f) outs[0] = (bf16)0.f;
-          continue;
         }
         // rows 4g..4g+3 = positions (TL, TR, BL, BR) of window pair bw;
         // column r16 = channel (r16 & 7) of its left (r16 < 8) or right
@@ -214,7 +210,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WR > 0 
     const int M = nimg * rows_img;
     const int mtiles = cdiv(M, 16), mgroups = cdiv(mtiles, MT);
     const int ko_s0 = ktab[g], ko_s1 = ktab[4 + g];  // XL_S1: at most two chunks, item-invariant
-    for (int item = wave; item < ((p.ablate & 2) ? 0 : ntiles * mgroups); item += NT / 64) {
+    for (int item = wave; item < ntiles * mgroups; item += NT / 64) {
       const int nt = ntiles == 1 ? 0 : item / mgroups, mg = item - nt * mgroups;
       // rows past M (last tile of a partial group) re-read row M-1: finite, discarded
       int base[MT], ti[MT];
@@ -301,10 +297,6 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WR > 0 
         }
       }
       // epilogue into the LDS output tile: lane holds rows 4g..4g+3, column n
-      if (p.ablate & 4) {  // keep the accumulators live, skip the epilogue
-        if (acc[0][0] == 1234.5f && acc[MT - 1][3] == -1.f) outs[0] = (bf16)0.f;
-        continue;
-      }
       if constexpr (PAIR == 1) {
         // column r16 = channel (r16 & 7) of the left (r16 < 8) or right pixel
         const int c = r16 & 7;
@@ -387,7 +379,6 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WR > 0 
     }
     }  // PAIR != 2
     __syncthreads();
-    if (p.ablate & 4) continue;
     char* gout = static_cast<char*>(p.out) + (size_t)img0 * out_img * 2;
     copy_out(gout, reinterpret_cast<const char*>(outs), nimg * out_img * 2, pow2_align(out_img * 2));
     if (pool) {
@@ -400,7 +391,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WR > 0 
 // register-resident weights for the LeNet-class shapes (one column tile, 7
 // or 13 K chunks): conv2 forward and conv2 data gradient
 int fwd_wreg(const ConvPipeParams& p) {
-  if (p.layout != XL_C8 || cdiv(p.Cout, 16) != 1 || pipe_knob("no_wreg", 0)) return 0;
+  if (p.layout != XL_C8 || cdiv(p.Cout, 16) != 1) return 0;
   if (p.nchunks == 7 && p.in.mode == PM_PLAIN && p.epi == FE_POOL) return 7;
   if (p.nchunks == 13 && p.in.mode == PM_UNPOOL && p.epi == FE_PLAIN) return 13;
   return 0;
@@ -491,10 +482,6 @@ static void fwd_pick_strides(ConvPipeParams& p) {
       }
     }
   }
-  if (pipe_knob("bank_log", 0))
-    fprintf(stderr, "conv_pipe fwd Cin=%d Cout=%d OH=%d mode=%d: LWp %d->%d imgs %d->%d CS %d, A-read conflict cycles/read %.2f -> %.2f\n",
-            p.Cin, p.Cout, p.OH, s.mode, LW0, bp.in.LWp, imgs0, bp.imgs, bp.in.CS,
-            (double)e0.first / std::max(1L, e0.second), best);
   p = bp;
 }
 
@@ -509,7 +496,7 @@ bool conv_pipe_plan(ConvPipeParams& p) {
            (p.epi == FE_POOL || (p.epi == FE_ACT && (p.act == ACT_RELU || p.act == ACT_NONE)));
   // window pairs (the second column half computes the next 2x2 window, taps
   // shifted by two): the pool is in-lane, no DPP exchange
-  if (p.pair && p.epi == FE_POOL && p.KS <= 6 && (p.OW & 3) == 0 && (p.OH & 1) == 0 && !pipe_knob("no_pair2", 0))
+  if (p.pair && p.epi == FE_POOL && p.KS <= 6 && (p.OW & 3) == 0 && (p.OH & 1) == 0)
     p.pair = 2;
   if (s1) {  // align the source columns to 4 (shift the conv origin accordingly)
     const int ox = s.offx < 4 ? 4 : (s.offx + 3) & ~3;
@@ -542,7 +529,7 @@ bool conv_pipe_plan(ConvPipeParams& p) {
   }
   if (imgs < 1) return false;
   if ((size_t)fwd_layout(p).total > kLdsPerCU) return false;
-  if (!pipe_knob("no_swizzle", 0)) fwd_pick_strides(p);
+  fwd_pick_strides(p);
   const FwdLayout L = fwd_layout(p);
   p.lds = (size_t)L.total;
   p.ngroups = cdiv(p.N, p.imgs);

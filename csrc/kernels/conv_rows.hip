@@ -240,21 +240,21 @@ __global__ void __launch_bounds__(kT) conv_dw_rows_kernel(ConvDwRowsParams p) {
   // one before it.  ONE load site: the prefetched values stay in the load
   // destination registers until the store after the next barrier (two sites
   // would merge through register moves, each of which waits on its load).
-  if (!(p.ablate & 1) && (int)blockIdx.x < p.ngroups) load_idx(blockIdx.x * p.imgs);
+  if ((int)blockIdx.x < p.ngroups) load_idx(blockIdx.x * p.imgs);
   for (int k = 0;; ++k) {
     const int lgrp = blockIdx.x + k * gridDim.x, grp = lgrp - gridDim.x;
     if (grp >= p.ngroups) break;
     if (k > 0) {
       __syncthreads();  // previous group consumed (and the zero fill, first time)
-      if (!(p.ablate & 1)) store_group(min(p.imgs, p.N - grp * p.imgs));
+      store_group(min(p.imgs, p.N - grp * p.imgs));
       __syncthreads();
     }
-    if (!(p.ablate & 1) && lgrp < p.ngroups) load_group(lgrp * p.imgs, (lgrp + gridDim.x) * p.imgs);
+    if (lgrp < p.ngroups) load_group(lgrp * p.imgs, (lgrp + gridDim.x) * p.imgs);
     if (k == 0) continue;
     const int nimg = min(p.imgs, p.N - grp * p.imgs);
 
     // chunks q = (image, output row), wave-strided; offsets are wave-uniform
-    const int nq = (p.ablate & 2) ? 0 : nimg * p.OH;
+    const int nq = nimg * p.OH;
     const char* lds = smem;
     auto frag = [&](int im, int y, bf16x8& a, bf16x8 (&b)[NT]) {
       a = *reinterpret_cast<const bf16x8*>(lds + a_lane + 2 * (im * p.dzimg + y * 32));
@@ -349,7 +349,7 @@ int rows_b_conflicts(const ConvDwRowsParams& p, int Pw, int CS) {
 }  // namespace
 
 bool conv_dw_rows_plan(ConvDwRowsParams& p) {
-  if (pipe_knob("no_rows", 0)) return false;
+  if (ab_flag("no_rows")) return false;  // A/B: the pixel-major conv_dw_pipe kernel (tested)
   const int cw = p.Cout / 2;
   if ((p.Cout & 1) || !(cw == 1 || cw == 2 || cw == 3 || cw == 4 || cw == 8) || p.OW > 32 || p.OW < 1 || p.OH < 4)
     return false;

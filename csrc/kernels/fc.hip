@@ -176,19 +176,15 @@ __global__ void __launch_bounds__(kFcThreads) fc_kernel(FcParams p0) {
         bb[q] = load8(wb + q * 32);
       }
       __builtin_amdgcn_sched_barrier(0);
-      if (!(p.ablate & 2)) {
 #pragma unroll
-        for (int q = 0; q < NCH; ++q) {
-          c0 = mma(c0, a[q], ba[q]);
-          c1 = mma(c1, a[q], bb[q]);
-        }
-      } else {
-        c0[0] = (float)ba[0][0] + (float)bb[NCH - 1][7];
+      for (int q = 0; q < NCH; ++q) {
+        c0 = mma(c0, a[q], ba[q]);
+        c1 = mma(c1, a[q], bb[q]);
       }
       epilogue(c0, t0 + tt, tt);
       if (two) epilogue(c1, t0 + tt + 1, tt + 1);
     }
-    if (EPI == EPI_LOGITS || (p.ablate & 1)) continue;
+    if (EPI == EPI_LOGITS) continue;
     // wave-private tile -> 16 rows x (tn*16) columns, 16-byte stores (ldc % 8 == 0)
     __builtin_amdgcn_wave_barrier();
     const int c0 = t0 * 16;

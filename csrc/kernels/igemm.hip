@@ -1185,7 +1185,6 @@ void launch_conv(const IgemmParams& p, hipStream_t s) {
 
 }  // namespace
 
-static int igemm_env_mode();
 bool igemm_conv_supported(int C, int N, int KS) {
   // 128x128 kernel: C % 32 (a K-step spans <= 2 taps; K padded to 64 with
   // zero pieces); the 256-tile kernels additionally need C % 64 (igemm_conv)
@@ -1230,9 +1229,9 @@ void igemm_conv(const IgemmParams& p0, hipStream_t s) {
     }
     return;
   }
-  // 256-pixel tiles for the wide layers (MCC_AB=igemm_tile=0: 128x128 kernel
-  // only; =128: 256x128 tiles only)
-  const int big_mode = p.tile >= 0 ? p.tile : igemm_env_mode();
+  // 256-pixel tiles for the wide layers (p.tile = 0: 128x128 kernel only;
+  // 128: 256x128 tiles only; -1 = auto, as 1)
+  const int big_mode = p.tile >= 0 ? p.tile : 1;
   // auto: 256x256 tiles where N % 256 == 0 (the 128-channel variant measured
   // slower than the 128x128 kernel on VGG conv2 / conv3-dX: profiles/igemm256_ab_r2.txt)
   if (p.C % 64 == 0 &&
@@ -1258,13 +1257,9 @@ void igemm_conv(const IgemmParams& p0, hipStream_t s) {
   }
 }
 
-// MCC_AB=igemm_tile=N: 1 auto (256x256 tiles where N % 256 == 0), 0 the
-// 128x128 kernels only, 128 / 256 force that tile (read per call)
-static int igemm_env_mode() { return ab_int("igemm_tile", 1); }
-
 // weight-gradient tile: 0 = 128x128 kernel, 128 / 256 = igemm_dwbig_kernel<BA>
 static int dw_big_ba(int Cout, int kf, int tile) {
-  const int mode = tile >= 0 ? tile : igemm_env_mode();
+  const int mode = tile >= 0 ? tile : 1;  // 1: auto
   if (mode == 0 || Cout % 128 != 0 || kf < 256 || kf >= (1 << 23)) return 0;  // kernel packs c << 8
   if (mode == 1) return Cout % 256 == 0 ? 256 : 0;  // auto: the 128-channel variant lost to 128x128 (conv2)
   return (Cout % 256 == 0 && mode != 128) ? 256 : 128;

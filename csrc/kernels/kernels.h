@@ -66,7 +66,6 @@ struct ConvParams {
   int act = ACT_RELU;
   bool bias_act = true;  // false: plain store (data-gradient form)
   StageSrc in;
-  int ablate = 0;               // diagnostics: 1 = skip staging scatter, 2 = skip MFMA loop
   const void* wpk = nullptr;    // packed weights [round_up(Cout,16)][kpad], T
   const float* bias = nullptr;  // fp32 canonical bias [Cout]
   void* out = nullptr;          // T NHWC [N][OH'][OW'][Cout]
@@ -90,7 +89,6 @@ struct ConvDwParams {
   StageSrc x;          // forward input of the layer
   StageSrc dy;         // gradient w.r.t. the conv output (via RELU/UNPOOL)
   float* slab = nullptr;  // [nx][cout_pad][ncols_pad]
-  int ablate = 0;         // diagnostics: 1 = skip staging scatter, 2 = skip MFMA loop
 };
 
 // Row stride (elements) of the pixel-major dY tile of the bf16 transpose-read
@@ -176,7 +174,6 @@ struct ConvPipeParams {
   int pair = 0;
   size_t lds = 0;
   uint32_t rows_mh = 0, rows_ml = 0;  // division magic for the GEMM rows per image (set at launch)
-  int ablate = 0;  // diagnostics (MCC_AB=ablate=bits): 1 no staging, 2 no MFMA loop, 4 no epilogue/copy-out
 };
 // Geometry for a layer (N may be the maximum batch); false when the layer is
 // outside what the pipelined kernels cover (the caller keeps conv_small).
@@ -201,7 +198,6 @@ struct ConvDwPipeParams {
   // columns; otherwise the waves split the pixel chunks of the same tiles)
   int wsplit = 0;
   size_t lds = 0;
-  int ablate = 0;  // diagnostics: 1 no staging, 2 no MFMA loop
 };
 bool conv_dw_pipe_plan(ConvDwPipeParams& p);
 void conv_dw_pipe(const ConvDwPipeParams& p, hipStream_t s);
@@ -384,7 +380,6 @@ struct ConvDwRowsParams {
   int A = 0, Pw = 0, LH = 0, CS = 0, ximg = 0, dplane = 0, dzimg = 0, KK = 0, ntiles = 0;
   int m0 = 0, nblk = 0, imgs = 1, ngroups = 0, grid = 0;
   size_t lds = 0;
-  int ablate = 0;  // diagnostics (MCC_AB=ablate=bits): 1 no staging, 2 no MFMA loop
 };
 bool conv_dw_rows_plan(ConvDwRowsParams& p);
 size_t conv_dw_rows_scratch_bytes(const ConvDwRowsParams& p);
@@ -428,7 +423,6 @@ struct FcParams {
   void* C = nullptr; int ldc = 0;
   float* Cf = nullptr;
   long long* dbg = nullptr;  // diagnostics: per-wave phase timestamps [grid][4 waves][4]
-  int ablate = 0;            // diagnostics: 1 skip the output copy, 2 skip the MFMAs
 };
 bool fc_supported(int N, int K);
 void fc_forward(const FcParams& p, hipStream_t s);

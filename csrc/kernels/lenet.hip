@@ -182,11 +182,6 @@ __device__ __forceinline__ bf16x8 lds8p(const char* p, const char* p2) {
   const bf16x4 hi = *reinterpret_cast<const bf16x4*>(p2);
   return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
 }
-__device__ __forceinline__ bf16x8 lds8x2(const char* p) {
-  const bf16x4 lo = *reinterpret_cast<const bf16x4*>(p);
-  const bf16x4 hi = *reinterpret_cast<const bf16x4*>(p + 8);
-  return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
-}
 __device__ __forceinline__ bf16x8 tr8(const char* p0, const char* p1) {
   const bf16x4 a = tr4(reinterpret_cast<const bf16*>(p0));
   const bf16x4 b = tr4(reinterpret_cast<const bf16*>(p1));

@@ -333,7 +333,6 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1)))
   }
 
   // ---- staged per image: X words, dY2 and Y2 (16 B pieces) ----
-  const int sk = lane & 7;
   uint32_t xw[4];
   u32x4 dyv[4], y2v[4];
   WaveIdx widx;
