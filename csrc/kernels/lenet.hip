@@ -42,12 +42,21 @@
 
 #include <algorithm>
 
+#ifndef MCC_LENET_Y1DMA
+#define MCC_LENET_Y1DMA 0  // backward: Y1 HBM -> LDS by LDS-DMA issued after the conv2 dW (A/B)
+#endif
+#ifndef MCC_LENET_ABL
+#define MCC_LENET_ABL 0  // phase ablations for timing studies only (tools/build_variant.sh); 0 in every build
+#endif
+
 namespace mcc {
 namespace gpu {
 namespace {
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(1))) void gvoid;
+typedef __attribute__((address_space(3))) void lvoid;
 
 // ---- geometry ----
 constexpr int kImgPix = 784;          // 28 x 28 u8
@@ -189,10 +198,13 @@ __device__ __forceinline__ bf16x8 tr8(const char* p0, const char* p1) {
 }
 
 // LDS hand-off between the lanes of the (single-wave) workgroup: a wave's LDS
-// operations execute in order, so the compiler only must not move LDS
-// accesses across this point.  (__syncthreads would also drain vmcnt: the
-// in-flight prefetch loads and epilogue stores.)
-__device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+// operations execute in issue order, so the compiler only must not move LDS
+// accesses across this point -- a compiler fence, no s_waitcnt: the wave
+// keeps issuing (reads of the next phase queue behind the writes of this one
+// instead of the wave idling until every outstanding LDS operation returned).
+// (__syncthreads would also drain vmcnt: the in-flight prefetch loads and
+// epilogue stores.)
+__device__ __forceinline__ void wave_lds_sync() { asm volatile("" ::: "memory"); }
 
 // Dataset index of the k-th image of this wave (images blockIdx.x + k*stride):
 // the indices of 64 consecutive iterations come in one vector load (lane k),
@@ -247,8 +259,11 @@ __global__ void __launch_bounds__(64) lenet_fwd_kernel(LenetFwdParams p) {
       for (int e = 0; e < 8; ++e) {
         const int kw = e - j;
         float v = 0.f;
-        if (n16 < 12 && (c == 0 || g == 0) && kw >= 0 && kw < 5) v = p.w1[co * 25 + kh * 5 + kw];
-        w1[c][e] = (bf16)v;
+        // unconditional loads of a clamped index, then a select: a load under
+        // a lane condition is a branch + load + vmcnt(0) each (serialised)
+        const bool ok = n16 < 12 && (c == 0 || g == 0) && kw >= 0 && kw < 5;
+        v = p.w1[ok ? co * 25 + kh * 5 + kw : 0];
+        w1[c][e] = (bf16)(ok ? v : 0.f);
       }
     }
     bias1 = n16 < 12 ? 255.f * p.b1[co] : 0.f;  // the tile holds raw integer pixels
@@ -262,7 +277,9 @@ __global__ void __launch_bounds__(64) lenet_fwd_kernel(LenetFwdParams p) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       float v = 0.f;
-      if (t < 25 && e < 6) v = p.w2[(n16 * 6 + e) * 25 + t];
+      const bool ok = t < 25 && e < 6;
+      v = p.w2[ok ? (n16 * 6 + e) * 25 + t : 0];
+      v = ok ? v : 0.f;
       w2[c][e] = (bf16)v;
     }
   }
@@ -354,6 +371,7 @@ __global__ void __launch_bounds__(64) lenet_fwd_kernel(LenetFwdParams p) {
     if (img + stride_w < p.B) load_img(kimg + 1);
 
     // ---- conv1 + ReLU + pool: the next tile's A fragments are read before this tile's epilogue ----
+    if constexpr (!(MCC_LENET_ABL & 16)) {
     bf16x8 fa, fb;
     {
       const int off = tabA[mblk];
@@ -395,7 +413,9 @@ __global__ void __launch_bounds__(64) lenet_fwd_kernel(LenetFwdParams p) {
       if (lane < 20) a1g[lane + 64] = *reinterpret_cast<const u32x4*>(a1s + a1src1);
     }
 
+    }
     // ---- conv2 + ReLU + pool: all seven A fragments in flight before the MFMA chain ----
+    if constexpr (!(MCC_LENET_ABL & 32)) {
     bf16* y2g = static_cast<bf16*>(p.y2) + (size_t)img * kY2Elems;
     uint8_t* a2g = p.a2 + (size_t)img * kY2Elems;
 #pragma unroll 1
@@ -419,6 +439,7 @@ __global__ void __launch_bounds__(64) lenet_fwd_kernel(LenetFwdParams p) {
         y2g[wo * 16 + n16] = yb;
         a2g[wo * 16 + n16] = (uint8_t)((float)yb > 0.f ? ((best & 3) ^ 3) : 4);
       }
+    }
     }
   }
 }
@@ -464,7 +485,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1)))
       for (int e = 0; e < 8; ++e) {
         const int co = 8 * (g & 1) + e;
         float w = 0.f;
-        if (n16 < 12 && kh >= 0 && kh < 5) w = p.w2[((co * 6 + ci) * 5 + kh) * 5 + kw];
+        const bool ok = n16 < 12 && kh >= 0 && kh < 5;
+        w = p.w2[ok ? ((co * 6 + ci) * 5 + kh) * 5 + kw : 0];
+        w = ok ? w : 0.f;
         wdx[c][e] = (bf16)w;
       }
     }
@@ -531,32 +554,51 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1)))
   auto load_img = [&](int k) {  // k-th image of this wave
     const int img = blockIdx.x + k * (int)gridDim.x;
     if ((k & 63) == 0 && k > 0) widx.load(p.idx, blockIdx.x, (int)gridDim.x, p.B, k);
-    if (lane < 50) {
-      dy = *reinterpret_cast<const u32x4*>(static_cast<const bf16*>(p.dy2) + (size_t)img * kY2Elems + zq * 16 + 8 * zh);
-      cw = *reinterpret_cast<const u32x2*>(p.a2 + (size_t)img * kY2Elems + zq * 16 + 8 * zh);
-    }
-    const bf16* y1g = static_cast<const bf16*>(p.y1) + (size_t)img * kY1Elems;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int px = min(lane + 64 * r, 195);
-      yv[r] = *reinterpret_cast<const u32x4*>(y1g + px * 8);
-    }
+    // the dataset image first: its address needs the index vector (a wait
+    // only when it was just reloaded); issued after the other loads, that
+    // wait also covered them -- a full memory latency on every image
     const uint8_t* xin = p.x + (size_t)widx.get(k) * kImgPix;
 #pragma unroll
     for (int it = 0; it < 4; ++it) {
       const int yy = it * 8 + srow;
       xw[it] = (yy < 28 && sk < 7) ? *reinterpret_cast<const uint32_t*>(xin + yy * 28 + sk * 4) : 0u;
     }
+    if (lane < 50) {
+      dy = *reinterpret_cast<const u32x4*>(static_cast<const bf16*>(p.dy2) + (size_t)img * kY2Elems + zq * 16 + 8 * zh);
+      cw = *reinterpret_cast<const u32x2*>(p.a2 + (size_t)img * kY2Elems + zq * 16 + 8 * zh);
+    }
+    if constexpr (!MCC_LENET_Y1DMA) {
+      const bf16* y1g = static_cast<const bf16*>(p.y1) + (size_t)img * kY1Elems;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int px = min(lane + 64 * r, 195);
+        yv[r] = *reinterpret_cast<const u32x4*>(y1g + px * 8);
+      }
+    }
     const uint8_t* a1g = p.a1 + (size_t)img * kA1Bytes + dxci * 224 + 4 * g;
 #pragma unroll
     for (int t = 0; t < 7; ++t) a1n[t] = *reinterpret_cast<const uint32_t*>(a1g + (2 * t + dxj) * 16);
   };
-  if ((int)blockIdx.x < p.B) load_img(0);
+  // Y1 of image img straight into its LDS region (16 B per lane, 4 pieces of
+  // 64 lanes; the Y1 region is free once the conv2 weight gradient has read it)
+  auto dma_y1 = [&](int img) {
+    const char* y1g = reinterpret_cast<const char*>(static_cast<const bf16*>(p.y1) + (size_t)img * kY1Elems);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int px = lane + 64 * r;
+      if (px < 196)
+        __builtin_amdgcn_global_load_lds((gvoid*)(y1g + px * 16), (lvoid*)(smem + kBY1 + 1024 * r), 16, 0, 0);
+    }
+  };
+  if ((int)blockIdx.x < p.B) {
+    load_img(0);
+    if constexpr (MCC_LENET_Y1DMA) dma_y1(blockIdx.x);
+  }
 
   for (int img = blockIdx.x, kimg = 0; img < p.B; img += (int)gridDim.x, ++kimg) {
     wave_lds_sync();  // previous image: every LDS read done
     // ---- stage dZ2 (unpool of dY2 by the argmax codes) ----
-    if (lane < 50) {
+    if (lane < 50 && !(MCC_LENET_ABL & 8)) {
       const u32x4 z = {0u, 0u, 0u, 0u};
       *reinterpret_cast<u32x4*>(smem + zbase) = z;
       *reinterpret_cast<u32x4*>(smem + zbase + 32) = z;
@@ -572,13 +614,13 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1)))
     }
     // ---- stage Y1 ----
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
+    for (int r = 0; r < ((MCC_LENET_ABL & 64) || MCC_LENET_Y1DMA ? 0 : 4); ++r) {
       const int px = lane + 64 * r;
       if (px < 196) *reinterpret_cast<u32x4*>(smem + kBY1 + px * 16) = yv[r];
     }
     // ---- stage X0: copy c holds Xpad[r][p + c] at position p ----
 #pragma unroll
-    for (int it = 0; it < 4; ++it) {
+    for (int it = 0; it < ((MCC_LENET_ABL & 128) ? 0 : 4); ++it) {
       const int yy = it * 8 + srow;
       uint32_t lo, hi;
       u8x4_ints(xw[it], lo, hi);
@@ -597,10 +639,11 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1)))
     for (int t = 0; t < 7; ++t) a1w[t] = a1n[t];
     wave_lds_sync();
     // next image's loads fly while this one computes
-    if (img + (int)gridDim.x < p.B) load_img(kimg + 1);
+    if (img + (int)gridDim.x < p.B && !(MCC_LENET_ABL & 256) && !MCC_LENET_Y1DMA) load_img(kimg + 1);
 
+    if constexpr (MCC_LENET_Y1DMA) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this image's Y1 landed
     // ---- conv2 weight gradient (operands of chunk c+1 read during chunk c) ----
-    {
+    if constexpr (!(MCC_LENET_ABL & 1)) {
       bf16x8 af[2], bfr[2][13];
       auto load_chunk = [&](int c, int buf) {
         af[buf] = tr8(smem + aw2[c][0], smem + aw2[c][1]);
@@ -622,24 +665,27 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1)))
       }
     }
 
+    if constexpr (MCC_LENET_Y1DMA) {
+      // every Y1 read of the weight gradient returned; then the next image's
+      // Y1 DMA and its register loads (issued here, not before the weight
+      // gradient, so the vmcnt(0) above waits for this image's DMA only)
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (img + (int)gridDim.x < p.B) {
+        dma_y1(img + (int)gridDim.x);
+        load_img(kimg + 1);
+      }
+    }
     // ---- conv2 data gradient -> dZ1 rows (unpool by the conv1 argmax) ----
-    {
+    if constexpr (!(MCC_LENET_ABL & 2)) {
       bf16x8 fr[15], nx[5];
 #pragma unroll
       for (int c = 0; c < 15; ++c)
         fr[c] = *reinterpret_cast<const bf16x8*>(smem + (dxwrap(c) ? hxb : hxa) + dxoff(c));
-#pragma unroll
-      for (int T = 0; T < 7; ++T) {
-        if (T + 1 < 7) {  // tile T+1 reuses fr[5..14] as its chunks 0..9; read its chunks 10..14 now
-#pragma unroll
-          for (int c = 10; c < 15; ++c)
-            nx[c - 10] = *reinterpret_cast<const bf16x8*>(smem + (dxwrap(c) ? hxb : hxa) + dxoff(c) + (T + 1) * 1280);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int c = 0; c < 15; ++c) acc = mma(acc, fr[c], wdx[c]);
-        __builtin_amdgcn_sched_barrier(0);
+      // software pipelined: tile T's 15 chained MFMAs are issued together with
+      // tile T-1's epilogue (unpool by the conv1 argmax, dZ1 row stores), so
+      // the epilogue's VALU / LDS work fills the MFMA dependency gaps
+      f32x4 accp = {0.f, 0.f, 0.f, 0.f};
+      auto epilogue = [&](int T, const f32x4& acc) {
         // lane (n = 2ci + j, g): rows px = 4g + i of dY1 row py = 2T + j
         uint32_t top[4], bot[4];
 #pragma unroll
@@ -656,16 +702,30 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1)))
           *reinterpret_cast<u32x4*>(d) = u32x4{top[0], top[1], top[2], top[3]};
           *reinterpret_cast<u32x4*>(d + 64) = u32x4{bot[0], bot[1], bot[2], bot[3]};
         }
+      };
+#pragma unroll
+      for (int T = 0; T < 7; ++T) {
+        if (T + 1 < 7) {  // tile T+1 reuses fr[5..14] as its chunks 0..9; read its chunks 10..14 now
+#pragma unroll
+          for (int c = 10; c < 15; ++c)
+            nx[c - 10] = *reinterpret_cast<const bf16x8*>(smem + (dxwrap(c) ? hxb : hxa) + dxoff(c) + (T + 1) * 1280);
+        }
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int c = 0; c < 15; ++c) acc = mma(acc, fr[c], wdx[c]);
+        if (T > 0) epilogue(T - 1, accp);
+        accp = acc;
 #pragma unroll
         for (int c = 0; c < 10; ++c) fr[c] = fr[c + 5];
 #pragma unroll
         for (int c = 10; c < 15; ++c) fr[c] = nx[c - 10];
       }
+      epilogue(6, accp);
     }
     wave_lds_sync();  // dZ1 complete
 
     // ---- conv1 weight gradient: one MFMA per output row (32 pixels), 4 rows of reads in flight ----
-    {
+    if constexpr (!(MCC_LENET_ABL & 4)) {
       constexpr int D = 4;
       bf16x8 a[D], b[D];
 #pragma unroll
