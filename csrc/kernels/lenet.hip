@@ -42,9 +42,6 @@
 
 #include <algorithm>
 
-#ifndef MCC_LENET_Y1DMA
-#define MCC_LENET_Y1DMA 0  // backward: Y1 HBM -> LDS by LDS-DMA issued after the conv2 dW (A/B)
-#endif
 #ifndef MCC_LENET_ABL
 #define MCC_LENET_ABL 0  // phase ablations for timing studies only (tools/build_variant.sh); 0 in every build
 #endif
@@ -55,8 +52,6 @@ namespace {
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-typedef __attribute__((address_space(1))) void gvoid;
-typedef __attribute__((address_space(3))) void lvoid;
 
 // ---- geometry ----
 constexpr int kImgPix = 784;          // 28 x 28 u8
@@ -567,33 +562,17 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1)))
       dy = *reinterpret_cast<const u32x4*>(static_cast<const bf16*>(p.dy2) + (size_t)img * kY2Elems + zq * 16 + 8 * zh);
       cw = *reinterpret_cast<const u32x2*>(p.a2 + (size_t)img * kY2Elems + zq * 16 + 8 * zh);
     }
-    if constexpr (!MCC_LENET_Y1DMA) {
-      const bf16* y1g = static_cast<const bf16*>(p.y1) + (size_t)img * kY1Elems;
+    const bf16* y1g = static_cast<const bf16*>(p.y1) + (size_t)img * kY1Elems;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int px = min(lane + 64 * r, 195);
-        yv[r] = *reinterpret_cast<const u32x4*>(y1g + px * 8);
-      }
+    for (int r = 0; r < 4; ++r) {
+      const int px = min(lane + 64 * r, 195);
+      yv[r] = *reinterpret_cast<const u32x4*>(y1g + px * 8);
     }
     const uint8_t* a1g = p.a1 + (size_t)img * kA1Bytes + dxci * 224 + 4 * g;
 #pragma unroll
     for (int t = 0; t < 7; ++t) a1n[t] = *reinterpret_cast<const uint32_t*>(a1g + (2 * t + dxj) * 16);
   };
-  // Y1 of image img straight into its LDS region (16 B per lane, 4 pieces of
-  // 64 lanes; the Y1 region is free once the conv2 weight gradient has read it)
-  auto dma_y1 = [&](int img) {
-    const char* y1g = reinterpret_cast<const char*>(static_cast<const bf16*>(p.y1) + (size_t)img * kY1Elems);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int px = lane + 64 * r;
-      if (px < 196)
-        __builtin_amdgcn_global_load_lds((gvoid*)(y1g + px * 16), (lvoid*)(smem + kBY1 + 1024 * r), 16, 0, 0);
-    }
-  };
-  if ((int)blockIdx.x < p.B) {
-    load_img(0);
-    if constexpr (MCC_LENET_Y1DMA) dma_y1(blockIdx.x);
-  }
+  if ((int)blockIdx.x < p.B) load_img(0);
 
   for (int img = blockIdx.x, kimg = 0; img < p.B; img += (int)gridDim.x, ++kimg) {
     wave_lds_sync();  // previous image: every LDS read done
@@ -614,7 +593,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1)))
     }
     // ---- stage Y1 ----
 #pragma unroll
-    for (int r = 0; r < ((MCC_LENET_ABL & 64) || MCC_LENET_Y1DMA ? 0 : 4); ++r) {
+    for (int r = 0; r < ((MCC_LENET_ABL & 64) ? 0 : 4); ++r) {
       const int px = lane + 64 * r;
       if (px < 196) *reinterpret_cast<u32x4*>(smem + kBY1 + px * 16) = yv[r];
     }
@@ -639,9 +618,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1)))
     for (int t = 0; t < 7; ++t) a1w[t] = a1n[t];
     wave_lds_sync();
     // next image's loads fly while this one computes
-    if (img + (int)gridDim.x < p.B && !(MCC_LENET_ABL & 256) && !MCC_LENET_Y1DMA) load_img(kimg + 1);
+    if (img + (int)gridDim.x < p.B && !(MCC_LENET_ABL & 256)) load_img(kimg + 1);
 
-    if constexpr (MCC_LENET_Y1DMA) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this image's Y1 landed
     // ---- conv2 weight gradient (operands of chunk c+1 read during chunk c) ----
     if constexpr (!(MCC_LENET_ABL & 1)) {
       bf16x8 af[2], bfr[2][13];
@@ -665,16 +643,6 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1)))
       }
     }
 
-    if constexpr (MCC_LENET_Y1DMA) {
-      // every Y1 read of the weight gradient returned; then the next image's
-      // Y1 DMA and its register loads (issued here, not before the weight
-      // gradient, so the vmcnt(0) above waits for this image's DMA only)
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      if (img + (int)gridDim.x < p.B) {
-        dma_y1(img + (int)gridDim.x);
-        load_img(kimg + 1);
-      }
-    }
     // ---- conv2 data gradient -> dZ1 rows (unpool by the conv1 argmax) ----
     if constexpr (!(MCC_LENET_ABL & 2)) {
       bf16x8 fr[15], nx[5];
