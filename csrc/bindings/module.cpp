@@ -435,18 +435,22 @@ PYBIND11_MODULE(_C, m) {
   // reference-model conv block (refnet.hip): raw launches for the kernel unit tests
   k.def("ref_forward",
         [](int B, uintptr_t x, uintptr_t idx, uintptr_t w1, uintptr_t b1, uintptr_t w2, uintptr_t b2, uintptr_t y2,
-           uintptr_t s) {
+           uintptr_t s, bool f32) {
           gpu::RefFwdParams p;
           p.B = B; p.x = reinterpret_cast<const uint8_t*>(x); p.idx = reinterpret_cast<const int32_t*>(idx);
           p.w1 = reinterpret_cast<const float*>(w1); p.b1 = reinterpret_cast<const float*>(b1);
           p.w2 = reinterpret_cast<const float*>(w2); p.b2 = reinterpret_cast<const float*>(b2);
           p.y2 = reinterpret_cast<void*>(y2);
+          p.f32 = f32;
           gpu::ref_forward(p, stream_of(s));
-        });
+        },
+        py::arg("B"), py::arg("x"), py::arg("idx"), py::arg("w1"), py::arg("b1"), py::arg("w2"), py::arg("b2"),
+        py::arg("y2"), py::arg("stream"), py::arg("f32") = false);
   k.def("ref_backward",
         [](int B, uintptr_t x, uintptr_t idx, uintptr_t w1, uintptr_t b1, uintptr_t w2, uintptr_t y2, uintptr_t dy2,
-           uintptr_t slab, uintptr_t gw1, uintptr_t gb1, uintptr_t gw2, uintptr_t gb2, uintptr_t s) {
+           uintptr_t slab, uintptr_t gw1, uintptr_t gb1, uintptr_t gw2, uintptr_t gb2, uintptr_t s, bool f32) {
           gpu::RefBwdParams p;
+          p.f32 = f32;
           p.B = B; p.x = reinterpret_cast<const uint8_t*>(x); p.idx = reinterpret_cast<const int32_t*>(idx);
           p.w1 = reinterpret_cast<const float*>(w1); p.b1 = reinterpret_cast<const float*>(b1);
           p.w2 = reinterpret_cast<const float*>(w2);
@@ -455,8 +459,11 @@ PYBIND11_MODULE(_C, m) {
           p.gw1 = reinterpret_cast<float*>(gw1); p.gb1 = reinterpret_cast<float*>(gb1);
           p.gw2 = reinterpret_cast<float*>(gw2); p.gb2 = reinterpret_cast<float*>(gb2);
           gpu::ref_backward(p, stream_of(s));
-        });
-  k.def("ref_slab_bytes", &gpu::ref_slab_bytes);
+        },
+        py::arg("B"), py::arg("x"), py::arg("idx"), py::arg("w1"), py::arg("b1"), py::arg("w2"), py::arg("y2"),
+        py::arg("dy2"), py::arg("slab"), py::arg("gw1"), py::arg("gb1"), py::arg("gw2"), py::arg("gb2"),
+        py::arg("stream"), py::arg("f32") = false);
+  k.def("ref_slab_bytes", &gpu::ref_slab_bytes, py::arg("f32") = false);
   k.def("lenet_slab_bytes", &gpu::lenet_slab_bytes);
   // device minibatch sampler (rand() % N semantics, cnn.c:455) with the step
   // counter in device memory: graph-capturable (a replay draws fresh indices)
@@ -487,6 +494,9 @@ PYBIND11_MODULE(_C, m) {
         py::arg("dtype"), py::arg("M"), py::arg("N"), py::arg("logits"), py::arg("ldl"), py::arg("labels"),
         py::arg("idx") = 0, py::arg("dlogits") = 0, py::arg("ldd") = 0, py::arg("scale") = 1.f, py::arg("stats") = 0,
         py::arg("probs") = 0, py::arg("pred") = 0, py::arg("stream") = 0);
+  k.def(
+      "cu_hold", [](int nwg, int lds_bytes, double usec, uintptr_t s) { gpu::cu_hold(nwg, lds_bytes, usec, stream_of(s)); },
+      py::arg("nwg"), py::arg("lds_bytes"), py::arg("usec"), py::arg("stream") = 0);
   k.attr("EPI_BIAS_ACT") = (int)gpu::EPI_BIAS_ACT;
   k.attr("EPI_LOGITS") = (int)gpu::EPI_LOGITS;
   k.attr("EPI_DACT") = (int)gpu::EPI_DACT;

@@ -71,9 +71,9 @@ struct GpuNet::Stage {
   // forward copy K-major) and the weight gradient on the implicit-GEMM dW
   // kernel as a 1x1 "conv" over the batch
   bool fc_big = false, fc_igdw = false;
-  // wide FC at a large batch (CIFAR-3conv FC1 2048 -> 256): forward / data
-  // gradient as a 1x1 implicit-GEMM "conv" over the batch (igemm.hip's
-  // 256-tile kernels) instead of the generic tiled GEMM
+  // wide FC at a large batch (CIFAR-3conv FC1 2048 -> 256, ref FC1
+  // 1568 -> 200): forward / data gradient as a 1x1 implicit-GEMM "conv" over
+  // the batch (igemm.hip) instead of the generic tiled GEMM
   bool fc_ig = false, fc_igdx = false;
   void* conv_buf = nullptr;      // pre-pool conv output (big + pooled)
   void* dz_buf = nullptr;        // pre-activation gradient at conv-output size (big)
@@ -360,7 +360,7 @@ void GpuNet::build() {
     }
     if (st.kind == Stage::FC) MCC_CHECK(st.in_ld % 8 == 0, "fc input leading dim must be a multiple of 8");
     if (st.kind == Stage::FC && dtype_ == DType::BF16 && !st.last && !st.fc_big && !no_igemm_ &&
-        max_batch_ >= 8192 && st.Kin % 64 == 0 && st.Nout % 64 == 0 &&
+        max_batch_ >= 8192 && st.Kin % 8 == 0 && st.Nout % 8 == 0 && st.Kin >= 512 &&
         st.in_ld == st.Kin && st.out_ld == st.Nout && !gpu::fc_supported(st.Nout, st.Kin)) {
       st.fc_ig = gpu::igemm_conv_supported(st.Kin, st.Nout, 1);
       // data gradient: pv's act' is a ReLU mask (FC) or nothing (conv: its staging applies it)
@@ -395,12 +395,12 @@ void GpuNet::build() {
                b.inC == 6 && b.C == 16 && b.pad == 0;
     }
   }
-  // ---- reference-model conv block (refnet.hip): conv 1->16 and 16->32, 3x3
-  // stride 2 pad 1 ReLU on 28x28, fused forward and fused backward
-  // (recomputed conv1, sub-pixel conv2 dX).
+  // ---- reference-model conv block (refnet.hip; fp32: refnet_f32.hip): conv
+  // 1->16 and 16->32, 3x3 stride 2 pad 1 ReLU on 28x28, fused forward and
+  // fused backward (recomputed conv1, sub-pixel conv2 dX).
   {
     refblk_ = false;
-    if (dtype_ == DType::BF16 && stages_.size() >= 3) {
+    if (stages_.size() >= 3) {
       const Stage& a = *stages_[0];
       const Stage& b = *stages_[1];
       auto s2 = [](const Stage& x) {
@@ -664,7 +664,7 @@ void GpuNet::build() {
   }
   if (lenet_) scratch = std::max(scratch, gpu::lenet_slab_bytes());
   if (fcchain_) scratch = std::max(scratch, gpu::lenet_fc_slab_bytes(Bm));
-  if (refblk_) scratch = std::max(scratch, gpu::ref_slab_bytes());
+  if (refblk_) scratch = std::max(scratch, gpu::ref_slab_bytes(dtype_ == DType::F32));
   scratch_bytes_ = scratch;
   for (int pass = 0; pass < 2; ++pass) {
     arena_used_ = 0;
@@ -868,7 +868,7 @@ void GpuNet::forward_stages(size_t first, bool defer_fc, hipStream_t s) {
       if (si == 1) continue;  // produced with stage 0 (stage 0's own output is never stored)
       const Stage& s1 = *stages_[1];
       gpu::RefFwdParams f;
-      f.B = B; f.x = images; f.idx = idx;
+      f.B = B; f.x = images; f.idx = idx; f.f32 = dtype_ == DType::F32;
       f.w1 = params_ + st.w_off; f.b1 = params_ + st.b_off; f.w2 = params_ + s1.w_off; f.b2 = params_ + s1.b_off;
       f.y2 = s1.act_buf;
       gpu::ref_forward(f, s);
@@ -1087,7 +1087,7 @@ void GpuNet::backward(int hi, int lo, hipStream_t s) {
       }
       const Stage& s0 = *stages_[0];
       gpu::RefBwdParams b;
-      b.B = B; b.x = images_; b.idx = idx_;
+      b.B = B; b.x = images_; b.idx = idx_; b.f32 = dtype_ == DType::F32;
       b.w1 = params_ + s0.w_off; b.b1 = params_ + s0.b_off; b.w2 = params_ + st.w_off;
       b.y2 = st.act_buf; b.dy2 = st.grad_buf;
       b.slab = scratch_;

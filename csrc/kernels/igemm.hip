@@ -224,7 +224,7 @@ __global__ void __launch_bounds__(kIgT, 2) igemm_conv_kernel(IgemmParams p) {
     }
   }
 
-  const int nk = cdiv(p.K, kIgBK);  // !U8: C % 32 == 0; pieces at k >= K read the zero page
+  const int nk = cdiv(p.K, kIgBK);  // !U8: C % 32 == 0 (KS = 1: C % 8); pieces at k >= K read the zero page
   auto stage = [&](int kt, int buf) {
     const int k0 = kt * kIgBK;
     bf16* A = smem + buf * IMG;
@@ -1187,8 +1187,10 @@ void launch_conv(const IgemmParams& p, hipStream_t s) {
 
 bool igemm_conv_supported(int C, int N, int KS) {
   // 128x128 kernel: C % 32 (a K-step spans <= 2 taps; K padded to 64 with
-  // zero pieces); the 256-tile kernels additionally need C % 64 (igemm_conv)
-  return C % 32 == 0 && N % 8 == 0 && KS <= 16;
+  // zero pieces) -- a 1x1 "conv" (an FC layer over the batch) has one tap, so
+  // 8-channel pieces suffice there (ref FC1 1568 -> 200 and its data gradient,
+  // K = 200); the 256-tile kernels additionally need C % 64 (igemm_conv)
+  return (KS == 1 ? C % 8 == 0 : C % 32 == 0) && N % 8 == 0 && KS <= 16;
 }
 
 void igemm_conv(const IgemmParams& p0, hipStream_t s) {
@@ -1198,7 +1200,7 @@ void igemm_conv(const IgemmParams& p0, hipStream_t s) {
                   (int64_t)p.KS * p.W * p.C < (1 << 22),
               "igemm_conv(u8): bad shapes");
   } else {
-    MCC_CHECK(igemm_conv_supported(p.C, p.N, p.KS), "igemm_conv: needs C % 32 == 0 and N % 8 == 0");
+    MCC_CHECK(igemm_conv_supported(p.C, p.N, p.KS), "igemm_conv: needs C % 32 == 0 (1x1: C % 8) and N % 8 == 0");
   }
   MCC_CHECK(p.K == p.KS * p.KS * p.C, "igemm_conv: K must be KS*KS*C");
   MCC_CHECK(p.M == p.B * p.OH * p.OW && p.M > 0, "igemm_conv: M must be B*OH*OW");

@@ -347,6 +347,7 @@ void lenet_backward(const LenetBwdParams& p, hipStream_t s);
 // recomputes conv1 per image and produces dW1, db1, dW2, db2.
 struct RefFwdParams {
   int B = 0;
+  bool f32 = false;  // fp32 block (refnet_f32.hip): y2 / dy2 are fp32
   const uint8_t* x = nullptr;
   const int32_t* idx = nullptr;
   const float *w1 = nullptr, *b1 = nullptr, *w2 = nullptr, *b2 = nullptr;  // fp32 masters (canonical OIHW)
@@ -354,6 +355,7 @@ struct RefFwdParams {
 };
 struct RefBwdParams {
   int B = 0;
+  bool f32 = false;
   const uint8_t* x = nullptr;
   const int32_t* idx = nullptr;
   const float *w1 = nullptr, *b1 = nullptr, *w2 = nullptr;
@@ -362,9 +364,13 @@ struct RefBwdParams {
   float* slab = nullptr;      // ref_slab_bytes()
   float *gw1 = nullptr, *gb1 = nullptr, *gw2 = nullptr, *gb2 = nullptr;  // canonical gradients (written)
 };
-size_t ref_slab_bytes();
+size_t ref_slab_bytes(bool f32 = false);
 void ref_forward(const RefFwdParams& p, hipStream_t s);
 void ref_backward(const RefBwdParams& p, hipStream_t s);
+// fp32 kernels (refnet_f32.hip); ref_forward / ref_backward dispatch on p.f32
+size_t ref32_slab_bytes();
+void ref32_forward(const RefFwdParams& p, hipStream_t s);
+void ref32_backward(const RefBwdParams& p, hipStream_t s);
 
 struct ConvDwRowsParams {
   int N = 0, SH = 0, SW = 0, OH = 0, OW = 0, KS = 1, pad = 0, Cout = 0;
@@ -627,6 +633,8 @@ void sample_indices(int32_t* idx, int B, int64_t lo, int64_t hi, uint64_t seed, 
 void seq_sample_indices(int32_t* idx, int B, int64_t offset, int64_t stride, int64_t n, const uint64_t* step,
                         hipStream_t s);
 void advance_counter(uint64_t* step, hipStream_t s);
+// contention probe: nwg workgroups holding lds_bytes of LDS each, spinning usec
+void cu_hold(int nwg, int lds_bytes, double usec, hipStream_t s);
 // idx[b] = start + b (sequential evaluation windows)
 void iota_i32(int32_t* idx, int B, int64_t start, hipStream_t s);
 void cast_f32(DType t, void* dst, const float* src, int64_t n, hipStream_t s);

@@ -564,6 +564,21 @@ __global__ void sample_kernel(int32_t* idx, int B, int64_t lo, int64_t span, uin
 
 __global__ void advance_kernel(uint64_t* step) { *step += 1; }
 
+// Contention probe (tools/probes/cu_contention.py): `nwg` workgroups of 256
+// threads that each hold `lds` bytes of LDS and spin for `ticks` wall-clock
+// ticks -- a stand-in for an RCCL kernel that occupies CUs while it waits for
+// its peers.  Stores only to LDS (the sink is never written in practice).
+__global__ void cu_hold_kernel(uint64_t ticks, float* sink) {
+  extern __shared__ float hold_lds[];
+  const uint64_t t0 = wall_clock64();
+  float a = (float)threadIdx.x;
+  while (wall_clock64() - t0 < ticks) {
+    hold_lds[threadIdx.x] = a;
+    a = a * 0.5f + hold_lds[(threadIdx.x + 64) & 255];
+  }
+  if (a == -1.f) sink[threadIdx.x] = a;
+}
+
 // Sequential global windows: at step t the global batch is dataset positions
 // t*stride .. t*stride + stride - 1 (mod n), and this rank takes the slice
 // starting at `offset` -- world ranks together draw exactly the batch one
@@ -691,6 +706,17 @@ void seq_sample_indices(int32_t* idx, int B, int64_t offset, int64_t stride, int
                         hipStream_t s) {
   MCC_CHECK(B > 0 && n > 0 && stride > 0 && offset >= 0, "seq_sample_indices: bad range");
   hipLaunchKernelGGL(seq_sample_kernel, dim3((unsigned)cdiv(B, 256)), dim3(256), 0, s, idx, B, offset, stride, n, step);
+}
+
+void cu_hold(int nwg, int lds_bytes, double usec, hipStream_t s) {
+  MCC_CHECK(nwg >= 1 && nwg <= 4096 && lds_bytes >= 1024 && lds_bytes <= 65536 && usec > 0 && usec < 1e5,
+            "cu_hold: bad arguments");
+  int dev = 0, khz = 0;
+  MCC_CHECK(hipGetDevice(&dev) == hipSuccess &&
+                hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) == hipSuccess,
+            "cu_hold: device query failed");
+  const uint64_t ticks = (uint64_t)(usec * 1e-3 * (khz > 0 ? khz : 100000));
+  hipLaunchKernelGGL(cu_hold_kernel, dim3((unsigned)nwg), dim3(256), (size_t)lds_bytes, s, ticks, nullptr);
 }
 
 void advance_counter(uint64_t* step, hipStream_t s) {

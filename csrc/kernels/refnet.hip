@@ -498,15 +498,17 @@ __global__ void __launch_bounds__(64 * kRedWaves) ref_bwd_reduce_kernel(RefBwdPa
 
 }  // namespace
 
-size_t ref_slab_bytes() { return (size_t)kBwdGrid * kSlab * 4; }
+size_t ref_slab_bytes(bool f32) { return f32 ? ref32_slab_bytes() : (size_t)kBwdGrid * kSlab * 4; }
 
 void ref_forward(const RefFwdParams& p, hipStream_t s) {
+  if (p.f32) return ref32_forward(p, s);
   if (p.B <= 0) return;
   const int grid = std::min(p.B, 256 * 14);
   hipLaunchKernelGGL(ref_fwd_kernel, dim3(grid), dim3(64), kFLds, s, p);
 }
 
 void ref_backward(const RefBwdParams& p, hipStream_t s) {
+  if (p.f32) return ref32_backward(p, s);
   if (p.B <= 0) return;
   hipLaunchKernelGGL(ref_bwd_kernel, dim3(kBwdGrid), dim3(64), kBLds, s, p);
   hipLaunchKernelGGL(ref_bwd_reduce_kernel, dim3(kSlab / 64), dim3(64 * kRedWaves), 0, s, p, kBwdGrid);

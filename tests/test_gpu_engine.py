@@ -320,13 +320,16 @@ def test_bench_batch_step_matches_small_batches(cuda):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("model,B,b,fc_plan", [("cifar3", 65024 + 37, 1024, "igemm[fwd dx]")])
+@pytest.mark.parametrize(
+    "model,B,b,fc_plan", [("cifar3", 65024 + 37, 1024, "igemm[fwd dx]"), ("ref", 163840 + 37, 2048, "igemm[fwd dx]")]
+)
 def test_fc_igemm_bench_batch_matches_small_batches(cuda, model, B, b, fc_plan):
-    """CIFAR-3conv at bench.py's per-GPU batch (+ a ragged tail): the wide FC1
-    (2048 -> 256) runs on the 1x1 implicit-GEMM path there (batch >= 8192)
-    and on the tiled GEMM in small chunks; logits and every layer's summed
-    gradient must agree (the chunked path is pinned to PyTorch by the other
-    tests)."""
+    """CIFAR-3conv and the reference model at bench.py's per-GPU batches (+ a
+    ragged tail): the wide FC1 (2048 -> 256, 1568 -> 200) runs on the 1x1
+    implicit-GEMM path there (batch >= 8192) and on the tiled GEMM in small
+    chunks, and the fused ref conv block's persistent loops run at full size;
+    logits and every layer's summed gradient must agree (the chunked path is
+    pinned to PyTorch by the other tests)."""
     spec = mcc.make_model(model)
     C, H, W = spec.input_shape()
     imgs, labels = mcc.synth_dataset(B, C, H, W, 10, seed=23)
