@@ -75,6 +75,9 @@ struct GpuNet::Stage {
   // 1568 -> 200): forward / data gradient as a 1x1 implicit-GEMM "conv" over
   // the batch (igemm.hip) instead of the generic tiled GEMM
   bool fc_ig = false, fc_igdx = false;
+  // ... narrow enough (Nout <= 224) for one tile row of the tall-skinny FC
+  // kernel (fc_tall.hip: ref FC1 1568 -> 200), forward / data gradient
+  bool fc_tall = false, fc_tall_dx = false;
   void* conv_buf = nullptr;      // pre-pool conv output (big + pooled)
   void* dz_buf = nullptr;        // pre-activation gradient at conv-output size (big)
   // persistent pipelined kernels (bf16 small-image layers; geometry planned
@@ -368,6 +371,18 @@ void GpuNet::build() {
       st.fc_igdx = st.fc_ig && pv &&
                    (pv->kind == Stage::CONV || pv->act == gpu::ACT_RELU || pv->act == gpu::ACT_NONE) &&
                    gpu::igemm_conv_supported(st.Nout, st.Kin, 1);
+      st.fc_tall = st.fc_ig && st.Nout <= 224 && gpu::fc_tall_supported(max_batch_, st.Nout, st.Kin);
+      st.fc_tall_dx = st.fc_tall && st.fc_igdx && (pv->kind == Stage::CONV || pv->act == gpu::ACT_NONE) &&
+                      gpu::fc_tall_supported(max_batch_, st.Kin, st.Nout);
+    }
+    // fp32 tall-skinny FC (ref FC1 at a large batch): exact f32 MFMA, same tiles
+    if (st.kind == Stage::FC && dtype_ == DType::F32 && !st.last && !st.fc_big && max_batch_ >= 8192 && s > 0 &&
+        st.Nout <= 224 && st.Kin >= 512 && st.Kin % 8 == 0 && st.in_ld == st.Kin && st.out_ld == st.Nout &&
+        gpu::fc_tall_supported(max_batch_, st.Nout, st.Kin)) {
+      const Stage* pv = stages_[s - 1];
+      st.fc_tall = true;
+      st.fc_tall_dx = (pv->kind == Stage::CONV || pv->act == gpu::ACT_NONE) &&
+                      gpu::fc_tall_supported(max_batch_, st.Kin, st.Nout);
     }
     st.head = st.kind == Stage::FC && st.last && s > 0 && dtype_ == DType::BF16 &&
               gpu::xent_head_supported(st.Nout, st.Kin, st.in_ld);
@@ -739,7 +754,9 @@ std::string GpuNet::plan() const {
       os << "\n";
     } else {
       os << "  [" << s << "] fc " << st.Kin << " -> " << st.Nout << (st.last ? " (logits)" : "")
-         << (st.permC ? " nhwc-flatten" : "") << (st.fc_ig ? (st.fc_igdx ? " igemm[fwd dx]" : " igemm[fwd]") : "")
+         << (st.permC ? " nhwc-flatten" : "")
+         << (st.fc_tall ? (st.fc_tall_dx ? " tall[fwd dx]" : " tall[fwd]")
+                        : st.fc_ig ? (st.fc_igdx ? " igemm[fwd dx]" : " igemm[fwd]") : "")
          << "\n";
     }
   }
@@ -947,6 +964,15 @@ void GpuNet::forward_stages(size_t first, bool defer_fc, hipStream_t s) {
       p.out = st.act_buf; p.out_arg = st.arg_buf;
      
       gpu::conv_forward(dtype_, p, s);
+    } else if (st.fc_tall) {
+      const Stage& pv = *stages_[si - 1];
+      gpu::FcTallParams t;
+      t.M = B; t.N = st.Nout; t.K = st.Kin; t.f32 = dtype_ == DType::F32;
+      t.A = pv.act_buf; t.lda = st.in_ld;
+      t.W = static_cast<const char*>(packed_) + es * st.pk_fwd; t.ldw = r8(st.Kin);
+      t.bias = params_ + st.b_off; t.act = st.act;
+      t.out = st.act_buf; t.ldo = st.out_ld;
+      gpu::fc_tall(t, s);
     } else if (st.fc_ig) {
       const Stage& pv = *stages_[si - 1];
       gpu::IgemmParams g;
@@ -1353,7 +1379,15 @@ void GpuNet::backward(int hi, int lo, hipStream_t s) {
       gpu::dw_reduce(r, ws);
       }
       // data gradient
-      if (si > 0 && st.fc_igdx) {
+      if (si > 0 && st.fc_tall_dx) {
+        gpu::FcTallParams t;
+        t.M = B; t.N = st.Kin; t.K = st.Nout; t.f32 = dtype_ == DType::F32;
+        t.A = st.grad_buf; t.lda = st.out_ld;
+        t.W = static_cast<const char*>(packed_) + es * st.pk_dx; t.ldw = st.out_ld;  // W^T [Kin][out_ld]
+        t.bias = nullptr; t.act = gpu::ACT_NONE;  // pv is a conv (its staging applies the ReLU mask) or linear
+        t.out = pv.grad_buf; t.ldo = st.in_ld;
+        gpu::fc_tall(t, s);
+      } else if (si > 0 && st.fc_igdx) {
         gpu::IgemmParams g;
         g.B = B; g.H = 1; g.W = 1; g.C = st.Nout;
         g.OH = 1; g.OW = 1; g.KS = 1; g.stride = 1; g.pad = 0;

@@ -1,0 +1,213 @@
+// Tall-skinny FC GEMM for a large batch and a long reduction whose weights do
+// not fit in LDS: the reference model's FC1 (1568 -> 200, cnn.c:416-428,
+// Layer_feedForw_full cnn.c:113-152) forward, and its data gradient
+// (200 -> 1568, Layer_feedBack_full cnn.c:154-173) as the same GEMM with the
+// W^T copy.
+//
+//   out[m][n] = epi( sum_k A[m][k] * W[n][k] )   m < M (batch), n < N, k < K
+//
+// Tile: 128 batch rows x 224 output columns (14 fragments: N = 200 wastes
+// 11 %, where the 128x128 implicit-GEMM kernel computed two N tiles and 22 %
+// padding), 8 waves = 4 (rows, 32 each) x 2 (columns, 112 each), 14
+// v_mfma_f32_16x16x32_bf16 accumulators per wave.  The MFMA orientation is
+// transposed -- rows = output columns, columns = batch rows -- so a lane
+// holds 4 consecutive outputs of one batch row and stores them as one 8-byte
+// write.  K moves in 32-deep stages (A rows then W rows, 24 KB) through a
+// 3-deep ring of LDS buffers filled by global->LDS DMA (16 B per lane,
+// wave-uniform destination): two stages in flight while one is multiplied,
+// one barrier per stage, and every iteration issues exactly 3 DMAs per wave
+// (past K: the zero page) so the wait is a fixed vmcnt(3).  73 KB of LDS:
+// two workgroups per CU, whose load / multiply phases interleave (a
+// persistent one-workgroup-per-CU variant with a 6-deep ring and deferred
+// epilogues measured 36 % slower: at 256 workgroups a CU still busy with the
+// previous kernel's tail delays its whole share).  Rows are 64 B with the
+// 16-byte segment XOR-swizzled by row bits 2..3: every 16-lane
+// ds_read_b128 phase covers all 64 banks once.  Batch rows past M (clamped)
+// and weight rows past N (the zero page) cost no branch.
+// fp32 (exact f32 products, f32 accumulate): the same 64-byte LDS rows hold
+// 16 floats, so a stage is 16 deep and a lane's 16-byte fragment read feeds
+// four v_mfma_f32_16x16x4_f32 (k = 4g .. 4g + 3); MFMA-bound at 32 cycles
+// per instruction.
+#include <algorithm>
+#include <type_traits>
+
+#include "kernels.h"
+#include "mfma.h"
+
+namespace mcc {
+namespace gpu {
+namespace {
+
+typedef __attribute__((address_space(1))) void gvoid;
+typedef __attribute__((address_space(3))) void lvoid;
+
+constexpr int kTT = 512;                 // threads (8 waves)
+constexpr int kTM = 128;                 // batch rows per tile
+constexpr int kTN = 224;                 // output columns per tile
+constexpr int kTWRows = 256;             // W rows staged per stage (224 + zero rows: 2 DMAs per wave)
+constexpr int kTNS = 3;                  // ring depth: 2 stages in flight
+constexpr int kTXBytes = kTM * 64, kTWBytes = kTWRows * 64;
+constexpr int kTStageB = kTXBytes + kTWBytes;     // 24 KB
+constexpr int kTLds = kTNS * kTStageB + kTN * 4;  // 74,624 B (+ the bias): two workgroups per CU
+
+__device__ __attribute__((aligned(64))) const unsigned short kTallZero[32] = {0};
+
+__device__ __forceinline__ int tswz(int row) { return (row >> 2) & 3; }
+
+template <typename T, int ACT, bool BIAS>
+__global__ void __launch_bounds__(kTT, 2) fc_tall_kernel(FcTallParams p) {
+  constexpr int EPR = 64 / (int)sizeof(T);  // elements per 64-byte row = K per stage
+  constexpr int EPS = 16 / (int)sizeof(T);  // elements per 16-byte segment
+  typedef typename std::conditional<sizeof(T) == 2, bf16x8, f32x4>::type V;
+  extern __shared__ __attribute__((aligned(16))) char tsm[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r16 = lane & 15, g = lane >> 4;
+  const int wm = wave & 3, wn = wave >> 2;
+  // XCD-aware order: consecutive column tiles of one row block share its A
+  // rows in the same L2
+  const int ntn = (p.N + kTN - 1) / kTN;
+  const int nwg = gridDim.x;
+  const int q8 = nwg >> 3, r8 = nwg & 7, xc = blockIdx.x & 7;
+  const int tile = (xc < r8 ? xc * (q8 + 1) : r8 * (q8 + 1) + (xc - r8) * q8) + (blockIdx.x >> 3);
+  const int tm = tile / ntn, tn = tile - tm * ntn;
+  const int m0 = tm * kTM, n0 = tn * kTN;
+  const T* zero = reinterpret_cast<const T*>(kTallZero);
+
+  // ---- DMA sources: A piece = rows 16 wave .. +15 of the tile, W pieces =
+  // rows 16 wave and 128 + 16 wave; lane -> row + (lane >> 2), physical
+  // segment lane & 3 ----
+  const T* src[3];
+  int sk[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const int row = i == 0 ? 16 * wave + (lane >> 2) : 16 * (wave + 8 * (i - 1)) + (lane >> 2);
+    const int seg = (lane & 3) ^ tswz(row);
+    sk[i] = seg * EPS;
+    if (i == 0) {
+      src[i] = static_cast<const T*>(p.A) + (size_t)min(m0 + row, p.M - 1) * p.lda + seg * EPS;
+    } else {
+      const int n = n0 + row;
+      src[i] = (row < kTN && n < p.N) ? static_cast<const T*>(p.W) + (size_t)n * p.ldw + seg * EPS : nullptr;
+    }
+  }
+  const int nk = (p.K + EPR - 1) / EPR;
+  auto stage = [&](int kt) {  // always 3 DMAs (past K: the zero page)
+    char* dst = tsm + (kt % kTNS) * kTStageB;
+    const int k0 = kt * EPR;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const T* s = (src[i] && k0 + sk[i] < p.K) ? src[i] + k0 : zero;
+      char* d = i == 0 ? dst + wave * 1024 : dst + kTXBytes + (wave + 8 * (i - 1)) * 1024;
+      __builtin_amdgcn_global_load_lds((gvoid*)s, (lvoid*)d, 16, 0, 0);
+    }
+  };
+
+  f32x4 acc[7][2];
+#pragma unroll
+  for (int f = 0; f < 7; ++f) acc[f][0] = acc[f][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int xrow0 = 32 * wm + r16;   // batch fragment b: A row xrow0 + 16 b
+  const int wrow0 = 112 * wn + r16;  // weight fragment f: W row wrow0 + 16 f
+
+  stage(0);
+  stage(1);
+  for (int kt = 0; kt < nk; ++kt) {
+    // one stage (3 DMAs) was issued after stage kt: vmcnt(3) = stage kt
+    // landed (in-order retirement); the barrier (an explicit s_barrier:
+    // __syncthreads() would drain vmcnt) makes every wave's pieces visible
+    // and frees the slot read in iteration kt - 1
+    asm volatile("s_waitcnt vmcnt(3)\n\ts_barrier" ::: "memory");
+    stage(kt + 2);
+    const char* xb_ = tsm + (kt % kTNS) * kTStageB;
+    const char* wb_ = xb_ + kTXBytes;
+    V xb[2], wf[7];
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      const int row = xrow0 + 16 * b;
+      xb[b] = *reinterpret_cast<const V*>(xb_ + row * 64 + ((g ^ tswz(row)) << 4));
+    }
+#pragma unroll
+    for (int f = 0; f < 7; ++f) {
+      const int row = wrow0 + 16 * f;
+      wf[f] = *reinterpret_cast<const V*>(wb_ + row * 64 + ((g ^ tswz(row)) << 4));
+    }
+    __builtin_amdgcn_sched_barrier(0);  // all nine reads in flight before the first MFMA
+    if constexpr (sizeof(T) == 2) {
+#pragma unroll
+      for (int f = 0; f < 7; ++f)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) acc[f][b] = mma(acc[f][b], wf[f], xb[b]);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int f = 0; f < 7; ++f)
+#pragma unroll
+          for (int b = 0; b < 2; ++b)
+            acc[f][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[f][j], xb[b][j], acc[f][b], 0, 0, 0);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the trailing zero-page DMAs
+
+  // ---- epilogue: C^T[4g + i][r] = out[m = batch col r][n = 4g + i] ----
+  T* out = static_cast<T*>(p.out);
+#pragma unroll
+  for (int f = 0; f < 7; ++f) {
+    const int n = n0 + 112 * wn + 16 * f + 4 * g;
+    if (n >= p.N) continue;
+    float bv[4] = {0.f, 0.f, 0.f, 0.f};
+    if (BIAS) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) bv[i] = p.bias[n + i];
+    }
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      const int m = m0 + 32 * wm + 16 * b + r16;
+      if (m >= p.M) continue;
+      float v[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float t = acc[f][b][i] + bv[i];
+        v[i] = ACT == ACT_RELU ? fmaxf(t, 0.f) : (ACT == ACT_TANH ? tanhf(t) : t);
+      }
+      if constexpr (sizeof(T) == 2) {
+        const uint32_t lo = (uint32_t)__builtin_bit_cast(unsigned short, (bf16)v[0]) |
+                            ((uint32_t)__builtin_bit_cast(unsigned short, (bf16)v[1]) << 16);
+        const uint32_t hi = (uint32_t)__builtin_bit_cast(unsigned short, (bf16)v[2]) |
+                            ((uint32_t)__builtin_bit_cast(unsigned short, (bf16)v[3]) << 16);
+        *reinterpret_cast<uint2*>(out + (size_t)m * p.ldo + n) = make_uint2(lo, hi);
+      } else {
+        *reinterpret_cast<float4*>(out + (size_t)m * p.ldo + n) = make_float4(v[0], v[1], v[2], v[3]);
+      }
+    }
+  }
+}
+
+}  // namespace
+
+bool fc_tall_supported(int M, int N, int K) {
+  return M > 0 && N > 0 && N % 4 == 0 && K > 0 && K % 8 == 0;
+}
+
+void fc_tall(const FcTallParams& p, hipStream_t s) {
+  MCC_CHECK(fc_tall_supported(p.M, p.N, p.K), "fc_tall: needs N % 4 == 0 and K % 8 == 0");
+  const int va = p.f32 ? 4 : 8;  // elements per 16 bytes
+  MCC_CHECK(p.lda % va == 0 && p.lda >= p.K && p.ldw % va == 0 && p.ldw >= p.K && p.ldo % 4 == 0 && p.ldo >= p.N,
+            "fc_tall: bad leading dims");
+  MCC_CHECK(reinterpret_cast<uintptr_t>(p.A) % 16 == 0 && reinterpret_cast<uintptr_t>(p.W) % 16 == 0 &&
+                reinterpret_cast<uintptr_t>(p.out) % (p.f32 ? 16 : 8) == 0,
+            "fc_tall: alignment");
+  MCC_CHECK(p.act == ACT_NONE || p.bias, "fc_tall: an activation needs the forward (bias) epilogue");
+  const int tiles = ((p.M + kTM - 1) / kTM) * ((p.N + kTN - 1) / kTN);
+  const dim3 grid((unsigned)tiles), block(kTT);
+  auto go = [&](auto t) {
+    using T = decltype(t);
+    if (!p.bias) hipLaunchKernelGGL((fc_tall_kernel<T, ACT_NONE, false>), grid, block, kTLds, s, p);
+    else if (p.act == ACT_TANH) hipLaunchKernelGGL((fc_tall_kernel<T, ACT_TANH, true>), grid, block, kTLds, s, p);
+    else if (p.act == ACT_RELU) hipLaunchKernelGGL((fc_tall_kernel<T, ACT_RELU, true>), grid, block, kTLds, s, p);
+    else hipLaunchKernelGGL((fc_tall_kernel<T, ACT_NONE, true>), grid, block, kTLds, s, p);
+  };
+  if (p.f32) go(float{}); else go(bf16{});
+}
+
+}  // namespace gpu
+}  // namespace mcc

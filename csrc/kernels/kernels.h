@@ -540,6 +540,24 @@ struct IgemmParams {
 bool igemm_conv_supported(int C, int N, int KS);
 void igemm_conv(const IgemmParams& p, hipStream_t s);
 
+// Tall-skinny FC GEMM (fc_tall.hip): out[m][n] = act(sum_k A[m][k] W[n][k] + b[n])
+// (bias null: plain store, the data gradient through a W^T copy), bf16 in /
+// out, fp32 accumulate; large M, K % 8 == 0, N % 4 == 0.
+struct FcTallParams {
+  int M = 0, N = 0, K = 0;
+  bool f32 = false;         // fp32 operands / output (exact f32 MFMA)
+  const void* A = nullptr;  // bf16 [M][lda]
+  int lda = 0;
+  const void* W = nullptr;  // bf16 [N][ldw]
+  int ldw = 0;
+  const float* bias = nullptr;
+  int act = ACT_NONE;
+  void* out = nullptr;      // bf16 [M][ldo]
+  int ldo = 0;
+};
+bool fc_tall_supported(int M, int N, int K);
+void fc_tall(const FcTallParams& p, hipStream_t s);
+
 // Weight gradient: dW[co][k] = sum_m dz[m][co] in(m, k), db[co] = sum_m dz[m][co],
 // split-K over m into fp32 slabs [splitk][kf+1][Cout], then reduced into the
 // canonical gw[Cout][C][KS][KS], gb[Cout] (grad = beta*grad + sum).

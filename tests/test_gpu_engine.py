@@ -321,12 +321,12 @@ def test_bench_batch_step_matches_small_batches(cuda):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize(
-    "model,B,b,fc_plan", [("cifar3", 65024 + 37, 1024, "igemm[fwd dx]"), ("ref", 163840 + 37, 2048, "igemm[fwd dx]")]
+    "model,B,b,fc_plan", [("cifar3", 65024 + 37, 1024, "igemm[fwd dx]"), ("ref", 163840 + 37, 2048, "tall[fwd dx]")]
 )
 def test_fc_igemm_bench_batch_matches_small_batches(cuda, model, B, b, fc_plan):
     """CIFAR-3conv and the reference model at bench.py's per-GPU batches (+ a
-    ragged tail): the wide FC1 (2048 -> 256, 1568 -> 200) runs on the 1x1
-    implicit-GEMM path there (batch >= 8192) and on the tiled GEMM in small
+    ragged tail): the wide FC1 (2048 -> 256: 1x1 implicit GEMM; 1568 -> 200:
+    the tall-skinny FC kernel) runs on those paths there (batch >= 8192) and on the tiled GEMM in small
     chunks, and the fused ref conv block's persistent loops run at full size;
     logits and every layer's summed gradient must agree (the chunked path is
     pinned to PyTorch by the other tests)."""
@@ -348,7 +348,7 @@ def test_fc_igemm_bench_batch_matches_small_batches(cuda, model, B, b, fc_plan):
     logits, grads = big.get_logits(B), big.get_grads()
     del big
     small = mcc.GpuNet(spec, "bf16", b)
-    assert "igemm[fwd" not in small.plan()
+    assert "igemm[fwd" not in small.plan() and "tall[fwd" not in small.plan()
     small.set_params(params)
     ref_logits = np.empty_like(logits)
     ref_grads = np.zeros_like(grads, dtype=np.float64)

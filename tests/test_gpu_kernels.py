@@ -179,3 +179,33 @@ def test_ops_softmax_xent_and_sgd(cuda):
     torch.testing.assert_close(w, w0 - 0.1 * (gr + 0.01 * w0), atol=1e-6, rtol=1e-6)
     with pytest.raises(RuntimeError):
         ops.linear(torch.zeros(4, 8), torch.zeros(4, 8))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", ["bf16", "fp32"])
+@pytest.mark.parametrize("M,N,K,act", [(1000, 200, 1568, "tanh"), (4096 + 37, 200, 1568, "none"),
+                                       (300, 1568, 200, "nobias"), (2 * 128 + 5, 224 + 8, 64 + 8, "nobias"),
+                                       (2 * 128 + 5, 216, 64 + 8, "relu")])
+def test_fc_tall_kernel(cuda, M, N, K, act, dtype):
+    """fc_tall.hip (the reference model's FC1 forward and data gradient): every
+    epilogue, ragged batch rows, a K tail, N spanning two column tiles (the
+    data-gradient form; the bias epilogue covers one tile), several tiles per
+    persistent workgroup (1568 = 7 column tiles);
+    fp32 is exact f32 MFMA (checked tight against an fp64 product)."""
+    g = torch.Generator().manual_seed(M + N)
+    t = TDT[dtype]
+    a = torch.randn(M, K, generator=g).to(t).to(cuda)
+    w = (torch.randn(N, K, generator=g) / K**0.5).to(t).to(cuda)
+    b = torch.randn(N, generator=g).to(cuda)
+    out = torch.full((M, N), 7.0, dtype=t, device=cuda)
+    code = {"none": K_.ACT_NONE, "relu": K_.ACT_RELU, "tanh": K_.ACT_TANH, "nobias": K_.ACT_NONE}[act]
+    K_.fc_tall(M, N, K, a.data_ptr(), K, w.data_ptr(), K, 0 if act == "nobias" else b.data_ptr(), code,
+               out.data_ptr(), N, _s(), f32=dtype == "fp32")
+    torch.cuda.synchronize()
+    ref = a.double() @ w.double().t()
+    if act != "nobias":
+        ref = ref + b.double()
+    ref = {"relu": torch.relu, "tanh": torch.tanh}.get(act, lambda x: x)(ref)
+    err = float((out.double() - ref).norm() / ref.norm())
+    assert err < (1e-5 if dtype == "fp32" else 1e-2), err
+    assert float((out.double() - ref).abs().max()) < (1e-4 if dtype == "fp32" else 0.05) * float(ref.abs().max())
