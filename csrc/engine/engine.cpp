@@ -375,9 +375,10 @@ void GpuNet::build() {
       st.fc_tall_dx = st.fc_tall && st.fc_igdx && (pv->kind == Stage::CONV || pv->act == gpu::ACT_NONE) &&
                       gpu::fc_tall_supported(max_batch_, st.Kin, st.Nout);
     }
-    // fp32 tall-skinny FC (ref FC1 at a large batch): exact f32 MFMA, same tiles
+    // fp32 tall-skinny FC (ref FC1 1568 -> 200, LeNet-5 FC1 400 -> 120 at a
+    // large batch): exact f32 MFMA, same tiles
     if (st.kind == Stage::FC && dtype_ == DType::F32 && !st.last && !st.fc_big && max_batch_ >= 8192 && s > 0 &&
-        st.Nout <= 224 && st.Kin >= 512 && st.Kin % 8 == 0 && st.in_ld == st.Kin && st.out_ld == st.Nout &&
+        st.Nout <= 224 && st.Kin >= 256 && st.Kin % 8 == 0 && st.in_ld == st.Kin && st.out_ld == st.Nout &&
         gpu::fc_tall_supported(max_batch_, st.Nout, st.Kin)) {
       const Stage* pv = stages_[s - 1];
       st.fc_tall = true;

@@ -43,19 +43,27 @@ typedef __attribute__((address_space(3))) void lvoid;
 
 constexpr int kTT = 512;                 // threads (8 waves)
 constexpr int kTM = 128;                 // batch rows per tile
-constexpr int kTN = 224;                 // output columns per tile
-constexpr int kTWRows = 256;             // W rows staged per stage (224 + zero rows: 2 DMAs per wave)
 constexpr int kTNS = 3;                  // ring depth: 2 stages in flight
-constexpr int kTXBytes = kTM * 64, kTWBytes = kTWRows * 64;
-constexpr int kTStageB = kTXBytes + kTWBytes;     // 24 KB
-constexpr int kTLds = kTNS * kTStageB + kTN * 4;  // 74,624 B (+ the bias): two workgroups per CU
+constexpr int kTXBytes = kTM * 64;
+// NF fragments per wave column: tile width TN = 32 NF output columns (7: 224
+// for the ref model's FC1; 4: 128 for LeNet-5's FC1 120), W rows staged per
+// stage rounded up to 128 (one DMA round of the 8 waves), LDS per workgroup
+template <int NF> struct TallGeom {
+  static constexpr int TN = 32 * NF;
+  static constexpr int WR = (TN + 127) / 128 * 128;
+  static constexpr int DMAS = 1 + WR / 128;  // per wave per stage
+  static constexpr int STAGE = kTXBytes + WR * 64;
+  static constexpr int LDS = kTNS * STAGE;   // 73,728 B (NF 7) / 49,152 B (NF 4)
+};
 
 __device__ __attribute__((aligned(64))) const unsigned short kTallZero[32] = {0};
 
 __device__ __forceinline__ int tswz(int row) { return (row >> 2) & 3; }
 
-template <typename T, int ACT, bool BIAS>
+template <typename T, int NF, int ACT, bool BIAS>
 __global__ void __launch_bounds__(kTT, 2) fc_tall_kernel(FcTallParams p) {
+  using Gm = TallGeom<NF>;
+  constexpr int kTN = Gm::TN, DM = Gm::DMAS;
   constexpr int EPR = 64 / (int)sizeof(T);  // elements per 64-byte row = K per stage
   constexpr int EPS = 16 / (int)sizeof(T);  // elements per 16-byte segment
   typedef typename std::conditional<sizeof(T) == 2, bf16x8, f32x4>::type V;
@@ -76,10 +84,10 @@ __global__ void __launch_bounds__(kTT, 2) fc_tall_kernel(FcTallParams p) {
   // ---- DMA sources: A piece = rows 16 wave .. +15 of the tile, W pieces =
   // rows 16 wave and 128 + 16 wave; lane -> row + (lane >> 2), physical
   // segment lane & 3 ----
-  const T* src[3];
-  int sk[3];
+  const T* src[DM];
+  int sk[DM];
 #pragma unroll
-  for (int i = 0; i < 3; ++i) {
+  for (int i = 0; i < DM; ++i) {
     const int row = i == 0 ? 16 * wave + (lane >> 2) : 16 * (wave + 8 * (i - 1)) + (lane >> 2);
     const int seg = (lane & 3) ^ tswz(row);
     sk[i] = seg * EPS;
@@ -91,56 +99,57 @@ __global__ void __launch_bounds__(kTT, 2) fc_tall_kernel(FcTallParams p) {
     }
   }
   const int nk = (p.K + EPR - 1) / EPR;
-  auto stage = [&](int kt) {  // always 3 DMAs (past K: the zero page)
-    char* dst = tsm + (kt % kTNS) * kTStageB;
+  auto stage = [&](int kt) {  // always DM DMAs (past K: the zero page)
+    char* dst = tsm + (kt % kTNS) * Gm::STAGE;
     const int k0 = kt * EPR;
 #pragma unroll
-    for (int i = 0; i < 3; ++i) {
+    for (int i = 0; i < DM; ++i) {
       const T* s = (src[i] && k0 + sk[i] < p.K) ? src[i] + k0 : zero;
       char* d = i == 0 ? dst + wave * 1024 : dst + kTXBytes + (wave + 8 * (i - 1)) * 1024;
       __builtin_amdgcn_global_load_lds((gvoid*)s, (lvoid*)d, 16, 0, 0);
     }
   };
 
-  f32x4 acc[7][2];
+  f32x4 acc[NF][2];
 #pragma unroll
-  for (int f = 0; f < 7; ++f) acc[f][0] = acc[f][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int xrow0 = 32 * wm + r16;   // batch fragment b: A row xrow0 + 16 b
-  const int wrow0 = 112 * wn + r16;  // weight fragment f: W row wrow0 + 16 f
+  for (int f = 0; f < NF; ++f) acc[f][0] = acc[f][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int xrow0 = 32 * wm + r16;          // batch fragment b: A row xrow0 + 16 b
+  const int wrow0 = 16 * NF * wn + r16;     // weight fragment f: W row wrow0 + 16 f
 
   stage(0);
   stage(1);
   for (int kt = 0; kt < nk; ++kt) {
-    // one stage (3 DMAs) was issued after stage kt: vmcnt(3) = stage kt
+    // one stage (DM DMAs) was issued after stage kt: vmcnt(DM) = stage kt
     // landed (in-order retirement); the barrier (an explicit s_barrier:
     // __syncthreads() would drain vmcnt) makes every wave's pieces visible
     // and frees the slot read in iteration kt - 1
-    asm volatile("s_waitcnt vmcnt(3)\n\ts_barrier" ::: "memory");
+    if constexpr (DM == 3) asm volatile("s_waitcnt vmcnt(3)\n\ts_barrier" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(2)\n\ts_barrier" ::: "memory");
     stage(kt + 2);
-    const char* xb_ = tsm + (kt % kTNS) * kTStageB;
+    const char* xb_ = tsm + (kt % kTNS) * Gm::STAGE;
     const char* wb_ = xb_ + kTXBytes;
-    V xb[2], wf[7];
+    V xb[2], wf[NF];
 #pragma unroll
     for (int b = 0; b < 2; ++b) {
       const int row = xrow0 + 16 * b;
       xb[b] = *reinterpret_cast<const V*>(xb_ + row * 64 + ((g ^ tswz(row)) << 4));
     }
 #pragma unroll
-    for (int f = 0; f < 7; ++f) {
+    for (int f = 0; f < NF; ++f) {
       const int row = wrow0 + 16 * f;
       wf[f] = *reinterpret_cast<const V*>(wb_ + row * 64 + ((g ^ tswz(row)) << 4));
     }
-    __builtin_amdgcn_sched_barrier(0);  // all nine reads in flight before the first MFMA
+    __builtin_amdgcn_sched_barrier(0);  // all fragment reads in flight before the first MFMA
     if constexpr (sizeof(T) == 2) {
 #pragma unroll
-      for (int f = 0; f < 7; ++f)
+      for (int f = 0; f < NF; ++f)
 #pragma unroll
         for (int b = 0; b < 2; ++b) acc[f][b] = mma(acc[f][b], wf[f], xb[b]);
     } else {
 #pragma unroll
       for (int j = 0; j < 4; ++j)
 #pragma unroll
-        for (int f = 0; f < 7; ++f)
+        for (int f = 0; f < NF; ++f)
 #pragma unroll
           for (int b = 0; b < 2; ++b)
             acc[f][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[f][j], xb[b][j], acc[f][b], 0, 0, 0);
@@ -151,8 +160,8 @@ __global__ void __launch_bounds__(kTT, 2) fc_tall_kernel(FcTallParams p) {
   // ---- epilogue: C^T[4g + i][r] = out[m = batch col r][n = 4g + i] ----
   T* out = static_cast<T*>(p.out);
 #pragma unroll
-  for (int f = 0; f < 7; ++f) {
-    const int n = n0 + 112 * wn + 16 * f + 4 * g;
+  for (int f = 0; f < NF; ++f) {
+    const int n = n0 + 16 * NF * wn + 16 * f + 4 * g;
     if (n >= p.N) continue;
     float bv[4] = {0.f, 0.f, 0.f, 0.f};
     if (BIAS) {
@@ -197,16 +206,24 @@ void fc_tall(const FcTallParams& p, hipStream_t s) {
                 reinterpret_cast<uintptr_t>(p.out) % (p.f32 ? 16 : 8) == 0,
             "fc_tall: alignment");
   MCC_CHECK(p.act == ACT_NONE || p.bias, "fc_tall: an activation needs the forward (bias) epilogue");
-  const int tiles = ((p.M + kTM - 1) / kTM) * ((p.N + kTN - 1) / kTN);
-  const dim3 grid((unsigned)tiles), block(kTT);
-  auto go = [&](auto t) {
+  // narrow layers (N <= 128, e.g. LeNet-5 FC1 120) on 128-column tiles, the
+  // rest on 224-column tiles
+  auto go = [&](auto t, auto nf) {
     using T = decltype(t);
-    if (!p.bias) hipLaunchKernelGGL((fc_tall_kernel<T, ACT_NONE, false>), grid, block, kTLds, s, p);
-    else if (p.act == ACT_TANH) hipLaunchKernelGGL((fc_tall_kernel<T, ACT_TANH, true>), grid, block, kTLds, s, p);
-    else if (p.act == ACT_RELU) hipLaunchKernelGGL((fc_tall_kernel<T, ACT_RELU, true>), grid, block, kTLds, s, p);
-    else hipLaunchKernelGGL((fc_tall_kernel<T, ACT_NONE, true>), grid, block, kTLds, s, p);
+    constexpr int NF = decltype(nf)::value;
+    using Gm = TallGeom<NF>;
+    const int tiles = ((p.M + kTM - 1) / kTM) * ((p.N + Gm::TN - 1) / Gm::TN);
+    const dim3 grid((unsigned)tiles), block(kTT);
+    if (!p.bias) hipLaunchKernelGGL((fc_tall_kernel<T, NF, ACT_NONE, false>), grid, block, Gm::LDS, s, p);
+    else if (p.act == ACT_TANH) hipLaunchKernelGGL((fc_tall_kernel<T, NF, ACT_TANH, true>), grid, block, Gm::LDS, s, p);
+    else if (p.act == ACT_RELU) hipLaunchKernelGGL((fc_tall_kernel<T, NF, ACT_RELU, true>), grid, block, Gm::LDS, s, p);
+    else hipLaunchKernelGGL((fc_tall_kernel<T, NF, ACT_NONE, true>), grid, block, Gm::LDS, s, p);
   };
-  if (p.f32) go(float{}); else go(bf16{});
+  const bool narrow = p.N <= 128;
+  using N4 = std::integral_constant<int, 4>;
+  using N7 = std::integral_constant<int, 7>;
+  if (p.f32) { if (narrow) go(float{}, N4{}); else go(float{}, N7{}); }
+  else { if (narrow) go(bf16{}, N4{}); else go(bf16{}, N7{}); }
 }
 
 }  // namespace gpu

@@ -321,15 +321,18 @@ def test_bench_batch_step_matches_small_batches(cuda):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize(
-    "model,B,b,fc_plan", [("cifar3", 65024 + 37, 1024, "igemm[fwd dx]"), ("ref", 163840 + 37, 2048, "tall[fwd dx]")]
+    "model,B,b,fc_plan,dtype",
+    [("cifar3", 65024 + 37, 1024, "igemm[fwd dx]", "bf16"), ("ref", 163840 + 37, 2048, "tall[fwd dx]", "bf16"),
+     ("ref", 163840 + 37, 4096, "tall[fwd dx]", "fp32"), ("lenet5", 163840 + 37, 4096, "tall[fwd dx]", "fp32")],
 )
-def test_fc_igemm_bench_batch_matches_small_batches(cuda, model, B, b, fc_plan):
-    """CIFAR-3conv and the reference model at bench.py's per-GPU batches (+ a
-    ragged tail): the wide FC1 (2048 -> 256: 1x1 implicit GEMM; 1568 -> 200:
-    the tall-skinny FC kernel) runs on those paths there (batch >= 8192) and on the tiled GEMM in small
-    chunks, and the fused ref conv block's persistent loops run at full size;
-    logits and every layer's summed gradient must agree (the chunked path is
-    pinned to PyTorch by the other tests)."""
+def test_fc_igemm_bench_batch_matches_small_batches(cuda, model, B, b, fc_plan, dtype):
+    """CIFAR-3conv, the reference model and fp32 LeNet-5 at bench.py's per-GPU
+    batches (+ a ragged tail): the wide FC1 (2048 -> 256: 1x1 implicit GEMM;
+    1568 -> 200 and fp32 400 -> 120: the tall-skinny FC kernel) runs on those
+    paths there (batch >= 8192) and on the tiled GEMM in small chunks, and the
+    fused conv blocks' persistent loops run at full size; logits and every
+    layer's summed gradient must agree (the chunked path is pinned to PyTorch
+    by the other tests; fp32 to rounding, bf16 to its rounding points)."""
     spec = mcc.make_model(model)
     C, H, W = spec.input_shape()
     imgs, labels = mcc.synth_dataset(B, C, H, W, 10, seed=23)
@@ -337,7 +340,7 @@ def test_fc_igemm_bench_batch_matches_small_batches(cuda, model, B, b, fc_plan):
     d_img = torch.from_numpy(imgs).to(cuda)
     d_lab = torch.from_numpy(labels).to(cuda)
     s = torch.cuda.current_stream().cuda_stream
-    big = mcc.GpuNet(spec, "bf16", B)
+    big = mcc.GpuNet(spec, dtype, B)
     assert fc_plan in big.plan(), big.plan()
     big.set_params(params)
     big.zero_stats(s)
@@ -347,7 +350,7 @@ def test_fc_igemm_bench_batch_matches_small_batches(cuda, model, B, b, fc_plan):
     torch.cuda.synchronize()
     logits, grads = big.get_logits(B), big.get_grads()
     del big
-    small = mcc.GpuNet(spec, "bf16", b)
+    small = mcc.GpuNet(spec, dtype, b)
     assert "igemm[fwd" not in small.plan() and "tall[fwd" not in small.plan()
     small.set_params(params)
     ref_logits = np.empty_like(logits)
@@ -361,13 +364,14 @@ def test_fc_igemm_bench_batch_matches_small_batches(cuda, model, B, b, fc_plan):
         torch.cuda.synchronize()
         ref_logits[i : i + nb] = small.get_logits(nb)
         ref_grads += small.get_grads()
-    assert _relerr(logits, ref_logits) < 1e-2
+    tl, tg = (1e-5, 1e-4) if dtype == "fp32" else (1e-2, 2e-2)
+    assert _relerr(logits, ref_logits) < tl
     for L in spec.layers():
         if L["nweights"] == 0:
             continue
         for off, n, what in ((L["w_off"], L["nweights"], "W"), (L["b_off"], L["nbiases"], "b")):
             err = _relerr(grads[off : off + n], ref_grads[off : off + n])
-            assert err < 2e-2, f"layer {L['kind']} C={L['C']} {what} grad rel err {err:.3e}"
+            assert err < tg, f"layer {L['kind']} C={L['C']} {what} grad rel err {err:.3e}"
 
 
 @pytest.mark.gpu
@@ -403,13 +407,14 @@ def test_vgg11_bench_batch_matches_small_batches(cuda):
         torch.cuda.synchronize()
         ref_logits[i : i + b] = small.get_logits(b)
         ref_grads += small.get_grads()
-    assert _relerr(logits, ref_logits) < 1e-2
+    tl, tg = (1e-5, 1e-4) if dtype == "fp32" else (1e-2, 2e-2)
+    assert _relerr(logits, ref_logits) < tl
     for L in spec.layers():
         if L["nweights"] == 0:
             continue
         for off, n, what in ((L["w_off"], L["nweights"], "W"), (L["b_off"], L["nbiases"], "b")):
             err = _relerr(grads[off : off + n], ref_grads[off : off + n])
-            assert err < 2e-2, f"layer {L['kind']} C={L['C']} {what} grad rel err {err:.3e}"
+            assert err < tg, f"layer {L['kind']} C={L['C']} {what} grad rel err {err:.3e}"
 
 
 @pytest.mark.gpu
