@@ -62,6 +62,11 @@ $(OBJ)/kernels/%.o: csrc/kernels/%.hip $(HDRS)
 # lenet.hip: MFMA results in VGPRs (no v_accvgpr_read per accumulator in the
 # VALU-bound epilogues; the register file is unified on gfx950)
 $(OBJ)/kernels/lenet.o: HIPFLAGS += -mllvm -amdgpu-mfma-vgpr-form=1
+# conv_direct.hip: the packed-FMA kernels use explicit float2 vectors; the SLP
+# vectorizer would pair the scatter dX kernel's 98 scalar accumulators into
+# v_pk_fma_f32 register pairs (866 moves and 165 spilled registers; 151
+# VGPRs and no spills without it)
+$(OBJ)/kernels/conv_direct.o: HIPFLAGS += -fno-slp-vectorize
 
 $(OBJ)/engine/%.o: csrc/engine/%.cpp $(HDRS)
 	@mkdir -p $(dir $@)

@@ -422,89 +422,111 @@ __global__ void __launch_bounds__(kDW3T) __attribute__((amdgpu_waves_per_eu(3)))
   }
 }
 
-// Data gradient of a pooled 5x5 conv (stride 1, no padding): dX = full
-// correlation of dZ = unpool(dY, argmax) with the flipped weights.  Item =
-// (image, 2x2 block of dX pixels); its 6x6 dZ patch is exactly 3x3 pooling
-// windows (the block is 2-aligned and the halo KS-1 = 4 is even), so the
-// patch is decoded from the group's pooled dY / argmax in LDS (value at the
-// argmax position, zeros elsewhere; argmax 4 routes nothing) instead of
-// staging the 4x larger unpooled tensor.  Then 4*KS*KS packed FMAs per
-// (dZ channel, dX channel pair) with scalar-loaded weight pairs from the
-// flipped tap-major copy wd [CI][KS*KS][CO] (wd[i][t][c] = w[i][c][KK-1-t]).
-constexpr int kDxImgs = 16;
-template <int KS, int CI, int CO>  // CI: dZ channels (forward Cout), CO: dX channels (forward Cin)
-__global__ void __launch_bounds__(kDT) __attribute__((amdgpu_waves_per_eu(4))) conv_direct_dx_kernel(Conv1DirectParams p, const float* __restrict__ wd,
-                                                           float* __restrict__ out) {
-  static_assert(KS == 5, "the 3x3-window patch decode assumes KS - 1 == 4");
-  static_assert(CO % 2 == 0, "channel pairs");
-  constexpr int CP = CO / 2;
-  extern __shared__ __attribute__((aligned(16))) float dys[];
-  const int PHW = p.PH * p.PW;  // pooled grid of dY
-  const int BH = p.H / 2, BW = p.W / 2, nb = BH * BW;  // 2x2 blocks of the dX grid (H x W)
-  uint8_t* args = reinterpret_cast<uint8_t*>(dys + kDxImgs * PHW * CI);
-  const int ngroups = (p.N + kDxImgs - 1) / kDxImgs;
-  for (int grp = blockIdx.x; grp < ngroups; grp += gridDim.x) {
-    const int img0 = grp * kDxImgs, nimg = min(kDxImgs, p.N - img0);
-    __syncthreads();
-    {
-      const int n4 = nimg * PHW * CI / 4;
-      const float4* g = reinterpret_cast<const float4*>(p.dy + (size_t)img0 * PHW * CI);
-      const uint32_t* ga = reinterpret_cast<const uint32_t*>(p.arg + (size_t)img0 * PHW * CI);
-      for (int i = threadIdx.x; i < n4; i += kDT) {
+// Data gradient of LeNet-5's pooled conv2 (6 -> 16, 5x5, stride 1, no
+// padding: 14x14x6 -> 10x10x16 -> pool -> 5x5x16) in SCATTER form:
+// dZ = unpool(dY, argmax) is nonzero only at each pooling window's argmax, so
+// dX = sum over (channel co, window) of dY x W[co][ci] placed at the argmax
+// position.  A lane owns one (image, ci) pair and one half of its 14x14 dX
+// plane (7 rows x 14 = 98 accumulators in registers); the placement depends
+// on the argmax class (ay, ax) of the window, so every class is applied with
+// a mask (dY where the argmax is that class, else 0) -- static register
+// indices, no branches, only the taps that land in the lane's half.  240 K
+// FMAs per image instead of the 470 K of the full correlation over the
+// unpooled grid (the zeros of three unpooled positions and the border taps);
+// an LDS-atomic scatter of only the nonzero terms (60 K) measured 15x slower
+// (ds_add_f32 retires about one lane per clock).
+// Workgroup = 4 waves = 2 image groups x 2 halves: waves 2k, 2k+1 share group
+// k's staged dY / argmax codes (10 images, lanes 0..59 = image x ci); the
+// weights are staged once per workgroup as [co][ci][28] (16-byte rows).
+constexpr int kDxImgW = 10;                    // images per group
+constexpr int kDxWRow = 28;                    // floats per (co, ci) weight row
+constexpr int kDxWFloats = 16 * 6 * kDxWRow;   // 2688
+constexpr int kDxImgF = 25 * 16;               // dY floats per image (5 x 5 windows x 16 channels)
+constexpr int kDxGrpF = kDxImgW * kDxImgF + kDxImgW * kDxImgF / 4;   // dY + argmax bytes: 5,000 floats
+constexpr int kDxLds = (kDxWFloats + 2 * kDxGrpF) * 4;               // 50,752 B
+template <int HALF>
+__device__ __forceinline__ void dx_half(const float* __restrict__ ws, const float* dimg, const uint8_t* aimg, int ci,
+                                        float (&acc)[7][14]) {
+#pragma unroll
+  for (int y = 0; y < 7; ++y)
+#pragma unroll
+    for (int x = 0; x < 14; ++x) acc[y][x] = 0.f;
+#pragma unroll 1
+  for (int co = 0; co < 16; ++co) {
+    float w[28];
+    const float4* wr = reinterpret_cast<const float4*>(ws + (co * 6 + ci) * kDxWRow);
+#pragma unroll
+    for (int q = 0; q < 7; ++q) {
+      const float4 v = wr[q];
+      w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w;
+    }
+#pragma unroll
+    for (int py = 0; py < 5; ++py) {
+      // rows 2py + ay + kh (ay <= 1, kh <= 4) must meet this half's rows
+      if (2 * py + 5 < 7 * HALF || 2 * py > 7 * HALF + 6) continue;
+#pragma unroll
+      for (int px = 0; px < 5; ++px) {
+        const int o = (py * 5 + px) * 16 + co;
+        const float gv = dimg[o];
+        const int a = aimg[o];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const float m = a == c ? gv : 0.f;  // argmax 4 (ReLU-inactive): nothing
+          const int y0 = 2 * py + (c >> 1) - 7 * HALF, x0 = 2 * px + (c & 1);
+#pragma unroll
+          for (int kh = 0; kh < 5; ++kh) {
+            if (y0 + kh < 0 || y0 + kh >= 7) continue;
+#pragma unroll
+            for (int kw = 0; kw < 5; ++kw)
+              acc[y0 + kh][x0 + kw] = __builtin_fmaf(w[kh * 5 + kw], m, acc[y0 + kh][x0 + kw]);
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);  // one window at a time (register budget)
+      }
+    }
+  }
+}
+__global__ void __launch_bounds__(256, 2) conv_direct_dx_kernel(Conv1DirectParams p, const float* __restrict__ wd,
+                                                               float* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) float dxs[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int grp = wave >> 1, half = wave & 1;
+  float* ws = dxs;                                  // [co][ci][28]
+  float* dys = dxs + kDxWFloats + grp * kDxGrpF;    // [img][window][co]
+  const uint8_t* ags = reinterpret_cast<const uint8_t*>(dys + kDxImgW * kDxImgF);
+  for (int i = tid; i < 16 * 6 * 25; i += 256) {
+    const int co = i / 150, r = i - co * 150, ci = r / 25, t = r - ci * 25;
+    ws[(co * 6 + ci) * kDxWRow + t] = wd[(co * 25 + 24 - t) * 6 + ci];  // W[co][ci][t] (wd is flipped tap-major)
+  }
+  const int im = lane / 6, ci = lane - 6 * im;  // lane -> (image of the group, input channel)
+  const int ngroups = (p.N + kDxImgW - 1) / kDxImgW;
+  const int npairs = (ngroups + 1) / 2;
+  for (int pi = blockIdx.x; pi < npairs; pi += gridDim.x) {
+    const int gi = 2 * pi + grp;
+    const int img0 = gi * kDxImgW, nimg = max(0, min(kDxImgW, p.N - img0));
+    __syncthreads();  // the previous groups' reads are done (and, first time, the weights are staged)
+    if (half == 0) {
+      const float4* g = reinterpret_cast<const float4*>(p.dy + (size_t)img0 * kDxImgF);
+      const uint32_t* ga = reinterpret_cast<const uint32_t*>(p.arg + (size_t)img0 * kDxImgF);
+      const int n4 = nimg * kDxImgF / 4;
+      for (int i = lane; i < n4; i += 64) {
         reinterpret_cast<float4*>(dys)[i] = g[i];
-        reinterpret_cast<uint32_t*>(args)[i] = ga[i];
+        reinterpret_cast<uint32_t*>(dys + kDxImgW * kDxImgF)[i] = ga[i];
       }
     }
     __syncthreads();
-    for (int it = threadIdx.x; it < nimg * nb; it += kDT) {
-      const int m = it / nb, b = it - m * nb;
-      const int by = b / BW, bx = b - by * BW;
-      f2 acc[CP][4];
+    const bool live = lane < 6 * kDxImgW && im < nimg;
+    const float* dimg = dys + (live ? im : 0) * kDxImgF;
+    const uint8_t* aimg = ags + (live ? im : 0) * kDxImgF;
+    float acc[7][14];
+    if (half == 0) dx_half<0>(ws, dimg, aimg, ci, acc);
+    else dx_half<1>(ws, dimg, aimg, ci, acc);
+    if (live) {
+      float* d = out + ((size_t)(img0 + im) * 196 + 98 * half) * 6 + ci;
 #pragma unroll
-      for (int c = 0; c < CP; ++c) acc[c][0] = acc[c][1] = acc[c][2] = acc[c][3] = f2{0.f, 0.f};
-      const float* dimg = dys + m * PHW * CI;
-      const uint8_t* aimg = args + m * PHW * CI;
-      for (int i = 0; i < CI; ++i) {
-        f2 P[KS + 1][(KS + 1) / 2];  // row pairs: window wc's two columns are one pair
+      for (int y = 0; y < 7; ++y)
 #pragma unroll
-        for (int wr = 0; wr < 3; ++wr) {
-#pragma unroll
-          for (int wc = 0; wc < 3; ++wc) {
-            const int wy = by - 2 + wr, wx = bx - 2 + wc;
-            const bool ok = (unsigned)wy < (unsigned)p.PH && (unsigned)wx < (unsigned)p.PW;
-            const int o = ok ? (wy * p.PW + wx) * CI + i : 0;
-            const float g = ok ? dimg[o] : 0.f;
-            const int a = ok ? aimg[o] : 4;
-            P[2 * wr][wc] = f2{a == 0 ? g : 0.f, a == 1 ? g : 0.f};
-            P[2 * wr + 1][wc] = f2{a == 2 ? g : 0.f, a == 3 ? g : 0.f};
-          }
-        }
-        const float* wi = wd + i * KS * KS * CO;  // wave-uniform: scalar loads
-#pragma unroll
-        for (int kh = 0; kh < KS; ++kh) {
-#pragma unroll
-          for (int kw = 0; kw < KS; ++kw) {
-#pragma unroll
-            for (int c = 0; c < CP; ++c) {
-              const f2 wv = *reinterpret_cast<const f2*>(wi + (kh * KS + kw) * CO + 2 * c);
-              acc[c][0] = pfma(wv, MCC_PS(P[kh], kw), acc[c][0]);
-              acc[c][1] = pfma(wv, MCC_PS(P[kh], kw + 1), acc[c][1]);
-              acc[c][2] = pfma(wv, MCC_PS(P[kh + 1], kw), acc[c][2]);
-              acc[c][3] = pfma(wv, MCC_PS(P[kh + 1], kw + 1), acc[c][3]);
-            }
-          }
-        }
-      }
-      // dX pixels (2by + r, 2bx + q), CO channels each: two rows of 2*CO contiguous floats
-#pragma unroll
-      for (int r = 0; r < 2; ++r) {
-        float* d = out + (((size_t)(img0 + m) * p.H + 2 * by + r) * p.W + 2 * bx) * CO;
-#pragma unroll
-        for (int c = 0; c < CP; ++c) {
-          *reinterpret_cast<float2*>(d + 2 * c) = make_float2(acc[c][2 * r].x, acc[c][2 * r].y);
-          *reinterpret_cast<float2*>(d + CO + 2 * c) = make_float2(acc[c][2 * r + 1].x, acc[c][2 * r + 1].y);
-        }
-      }
+        for (int x = 0; x < 14; ++x) d[(y * 14 + x) * 6] = acc[y][x];
     }
   }
 }
@@ -677,17 +699,18 @@ bool conv_direct_fwd_supported(const Conv1DirectParams& p) {
 
 // dX geometry: p.H x p.W = the forward input (dX) grid, p.PH x p.PW = pooled dY
 bool conv_direct_dx_supported(const Conv1DirectParams& p) {
-  return p.KS == 5 && p.pad == 0 && p.Cin == 6 && p.C == 16 && p.OH == p.H - 4 && p.OW == p.W - 4 &&
-         p.H % 2 == 0 && p.W % 2 == 0 && p.PH == p.OH / 2 && p.PW == p.OW / 2 && (p.PH * p.PW * p.C) % 4 == 0 &&
-         (size_t)kDxImgs * p.PH * p.PW * p.C * 5 <= 64 * 1024;
+  // the scatter kernel is specialised to LeNet-5's conv2 (14x14x6 -> 10x10x16 -> 5x5x16)
+  return p.KS == 5 && p.pad == 0 && p.Cin == 6 && p.C == 16 && p.H == 14 && p.W == 14 && p.OH == 10 && p.OW == 10 &&
+         p.PH == 5 && p.PW == 5;
 }
 
 void conv_direct_dx(const Conv1DirectParams& p, float* dx, hipStream_t s) {
   MCC_CHECK(conv_direct_dx_supported(p) && p.wd && p.dy && p.arg && dx, "conv_direct_dx: bad params");
-  const int ngroups = (p.N + kDxImgs - 1) / kDxImgs;
-  const dim3 grid((unsigned)std::max(1, std::min(ngroups, 256 * 4))), block(kDT);
-  const size_t lds = (size_t)kDxImgs * p.PH * p.PW * p.C * 5;
-  hipLaunchKernelGGL((conv_direct_dx_kernel<5, 16, 6>), grid, block, lds, s, p, p.wd, dx);
+  MCC_CHECK(reinterpret_cast<uintptr_t>(p.dy) % 16 == 0 && reinterpret_cast<uintptr_t>(p.arg) % 4 == 0,
+            "conv_direct_dx: dY / argmax alignment");
+  const int npairs = ((p.N + kDxImgW - 1) / kDxImgW + 1) / 2;
+  const dim3 grid((unsigned)std::max(1, std::min(npairs, 256 * 2))), block(256);
+  hipLaunchKernelGGL(conv_direct_dx_kernel, grid, block, kDxLds, s, p, p.wd, dx);
 }
 
 bool conv1_direct_dw_supported(const Conv1DirectParams& p) {
