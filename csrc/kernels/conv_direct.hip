@@ -434,7 +434,9 @@ __global__ void __launch_bounds__(kDW3T) __attribute__((amdgpu_waves_per_eu(3)))
 // FMAs per image instead of the 470 K of the full correlation over the
 // unpooled grid (the zeros of three unpooled positions and the border taps);
 // an LDS-atomic scatter of only the nonzero terms (60 K) measured 15x slower
-// (ds_add_f32 retires about one lane per clock).
+// (ds_add_f32 retires about one lane per clock), and a v_pk_fma_f32 variant
+// over input-channel pairs (thirds of the plane, one kernel row of weights
+// at a time) 1.8x slower (2,020 vs 1,099 us).
 // Workgroup = 4 waves = 2 image groups x 2 halves: waves 2k, 2k+1 share group
 // k's staged dY / argmax codes (10 images, lanes 0..59 = image x ci); the
 // weights are staged once per workgroup as [co][ci][28] (16-byte rows).
@@ -443,7 +445,7 @@ constexpr int kDxWRow = 28;                    // floats per (co, ci) weight row
 constexpr int kDxWFloats = 16 * 6 * kDxWRow;   // 2688
 constexpr int kDxImgF = 25 * 16;               // dY floats per image (5 x 5 windows x 16 channels)
 constexpr int kDxGrpF = kDxImgW * kDxImgF + kDxImgW * kDxImgF / 4;   // dY + argmax bytes: 5,000 floats
-constexpr int kDxLds = (kDxWFloats + 2 * kDxGrpF) * 4;               // 50,752 B
+constexpr int kDxLds = (kDxWFloats + 2 * kDxGrpF) * 4;               // 50,752 B: three workgroups per CU
 template <int HALF>
 __device__ __forceinline__ void dx_half(const float* __restrict__ ws, const float* dimg, const uint8_t* aimg, int ci,
                                         float (&acc)[7][14]) {
@@ -486,7 +488,7 @@ __device__ __forceinline__ void dx_half(const float* __restrict__ ws, const floa
     }
   }
 }
-__global__ void __launch_bounds__(256, 2) conv_direct_dx_kernel(Conv1DirectParams p, const float* __restrict__ wd,
+__global__ void __launch_bounds__(256, 3) conv_direct_dx_kernel(Conv1DirectParams p, const float* __restrict__ wd,
                                                                float* __restrict__ out) {
   extern __shared__ __attribute__((aligned(16))) float dxs[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -709,7 +711,7 @@ void conv_direct_dx(const Conv1DirectParams& p, float* dx, hipStream_t s) {
   MCC_CHECK(reinterpret_cast<uintptr_t>(p.dy) % 16 == 0 && reinterpret_cast<uintptr_t>(p.arg) % 4 == 0,
             "conv_direct_dx: dY / argmax alignment");
   const int npairs = ((p.N + kDxImgW - 1) / kDxImgW + 1) / 2;
-  const dim3 grid((unsigned)std::max(1, std::min(npairs, 256 * 2))), block(256);
+  const dim3 grid((unsigned)std::max(1, std::min(npairs, 256 * 3))), block(256);
   hipLaunchKernelGGL(conv_direct_dx_kernel, grid, block, kDxLds, s, p, p.wd, dx);
 }
 
