@@ -207,7 +207,7 @@ __device__ __forceinline__ void wave_lds_sync() { asm volatile("" ::: "memory");
 struct WaveIdx {
   int v = 0;
   __device__ __forceinline__ void load(const int32_t* idx, int first, int stride, int B, int k0) {
-    const int i = first + (k0 + (int)threadIdx.x) * stride;
+    const int i = first + (k0 + (int)(threadIdx.x & 63)) * stride;
     v = idx ? idx[min(i, B - 1)] : min(i, B - 1);
   }
   __device__ __forceinline__ int get(int k) const { return __builtin_amdgcn_readlane(v, k & 63); }
@@ -450,159 +450,54 @@ __host__ __device__ constexpr int tapoff2(int t) { return ((t / 5) * 14 + t % 5)
 __host__ __device__ constexpr int dxoff(int c) { return (((2 * c) / 5) * 20 + (2 * c) % 5) * 32; }
 __host__ __device__ constexpr bool dxwrap(int c) { return (2 * c) % 5 == 4; }
 
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1))) lenet_bwd_kernel(LenetBwdParams p) {
+// Two waves per image (a 128-thread workgroup, four per CU: two waves per
+// SIMD, where the single-wave version ran one and exposed every LDS / VALU
+// latency of its phases):
+//   wave 0 (weight gradients): conv2 dW (reads dZ2, Y1), then conv1 dW
+//     (reads dZ1, X0); owns the dW accumulators and the slab;
+//   wave 1 (data gradient + staging): conv2 dX -> dZ1 (reads dZ2), then the
+//     NEXT image's dZ2 and Y1 (their last readers are done) while wave 0
+//     runs conv1 dW.
+// Both stage their half of X0.  Three barriers per image: B1 (X0, dZ2, Y1
+// staged), B2 (dZ1 complete, dZ2 / Y1 free), B3 (conv1 dW done: X0 and dZ1
+// free).  Barriers are explicit s_barrier after lgkmcnt(0) (the LDS writes),
+// never __syncthreads(), which would also drain the in-flight prefetch loads.
+__device__ __forceinline__ void wg_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+__global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2, 2))) lenet_bwd_kernel(LenetBwdParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int lane = threadIdx.x;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int n16 = lane & 15, g = lane >> 4;
   const int tq = (lane >> 2) & 3, tp = lane & 3;  // transposed-read roles (row q, column quad p)
+  const int sk = lane & 7, srow = lane >> 3;      // X0 staging items
 
-  zero_wave_lds(smem, kBLds);
-  wave_lds_sync();
-  {  // bf16 ones: the dW2 bias pixel and the dW1 bias rows (cols 0..31 of 30 rows)
+  {
+    const u32x4 z = {0u, 0u, 0u, 0u};
+    for (int i = threadIdx.x * 16; i < kBLds; i += 128 * 16) *reinterpret_cast<u32x4*>(smem + i) = z;
+  }
+  wg_barrier();
+  if (wv == 0) {  // bf16 ones: the dW2 bias pixel and the dW1 bias rows (cols 0..31 of 30 rows)
     const uint32_t one2 = 0x3f803f80u;
     if (lane < 4) *reinterpret_cast<uint32_t*>(smem + kBOne2 + 4 * lane) = one2;
     for (int i = lane; i < 30 * 16; i += 64)
       *reinterpret_cast<uint32_t*>(smem + kBOne1 + (i >> 4) * 80 + (i & 15) * 4) = one2;
   }
 
-  // ---- conv2 data-gradient weights in registers ----
-  // lane (n, kgroup g): k = 32c + 8g + e -> tap t = 2c + (g>>1) = (u', v),
-  // output channel co = 8(g&1) + e; column n = 2*ci + j (ci < 6):
-  // B = W2[co][ci][4 + j - u'][4 - v] where the row is in range.
-  bf16x8 wdx[15];
-  {
-    const int ci = n16 >> 1, j = n16 & 1;
+  // X0 staging of rows it*8 + srow (it = 2 wv, 2 wv + 1): copy c holds Xpad[r][p + c] at position p
+  uint32_t xw[2];
+  auto load_x = [&](const uint8_t* xin) {
 #pragma unroll
-    for (int c = 0; c < 15; ++c) {
-      const int t = 2 * c + (g >> 1), u = t / 5, v = t % 5;
-      const int kh = 4 + j - u, kw = 4 - v;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const int co = 8 * (g & 1) + e;
-        float w = 0.f;
-        const bool ok = n16 < 12 && kh >= 0 && kh < 5;
-        w = p.w2[ok ? ((co * 6 + ci) * 5 + kh) * 5 + kw : 0];
-        w = ok ? w : 0.f;
-        wdx[c][e] = (bf16)w;
-      }
+    for (int h = 0; h < 2; ++h) {
+      const int yy = (2 * wv + h) * 8 + srow;
+      xw[h] = (yy < 28 && sk < 7) ? *reinterpret_cast<const uint32_t*>(xin + yy * 28 + sk * 4) : 0u;
     }
-  }
-
-  // ---- per-lane LDS bases (image independent) ----
-  // dW2: transposed reads, K position 32c + 8g + 4hf + tq holds pixel kZPos[.]
-  int aw2[4][2], bw2a[4][2], bw2b[4][2], bw2c[4][2];
-#pragma unroll
-  for (int c = 0; c < 4; ++c)
-#pragma unroll
-    for (int hf = 0; hf < 2; ++hf) {
-      const int v = kZPos[32 * c + 8 * g + 4 * hf + tq];
-      const bool ok = v < 100;
-      const int z = ok ? v : v - 128;
-      const int zy = z / 10, zx = z % 10;
-      aw2[c][hf] = ok ? kBDz2 + ((zy + 4) * 20 + zx + 4) * 32 + 8 * tp : kBDz2 + 8 * tp;
-      const int yb = kBY1 + (zy * 14 + zx) * 16 + 8 * (tp & 1);
-      bw2a[c][hf] = yb + (tp >> 1) * 16;
-      bw2b[c][hf] = yb + (tp >> 1) * 160;
-      bw2c[c][hf] = (tp >> 1) ? kBOne2 + 8 * (tp & 1) - tapoff2(24) : yb;
-    }
-  // dX2: A rows px = n16, k-group g: chunk tap parity (g>>1), channel half (g&1)
-  const int hxa = kBDz2 + n16 * 32 + 16 * (g & 1) + (g >> 1) * 32;
-  const int hxb = kBDz2 + n16 * 32 + 16 * (g & 1) + (g >> 1) * 512;
-  // dW1: A row m = (kDw1Co[m], kDw1S[m]) (rows 12..15 repeat 0..3), B column
-  // n = 5*kh' + kw (15 = ones).  Row zy + 2 - 2s of the swizzled dZ1 plane:
-  // its chunk bit is (zy >> 1) ^ 1 ^ s, so two bases by the parity of zy >> 1.
-  int a1b[2];
-  {
-    const int m = n16 < 12 ? n16 : n16 - 12, co = kDw1Co[m], s = kDw1S[m];
-    const int base = kBDz1 + co * kBDz1Plane + (2 - 2 * s) * 64;
-    a1b[0] = base + 16 * (g ^ 1 ^ s);
-    a1b[1] = base + 16 * (g ^ s);
-  }
-  int b1b;
-  {
-    if (n16 == 15) b1b = kBOne1 + 16 * g;
-    else {
-      const int kh = n16 / 5, kw = n16 % 5, c = kw & 3;
-      b1b = kBXs + c * kBxCopy + (kh * 40 + 8 * g + kw - c) * 2;
-    }
-  }
-
-  f32x4 acc2[13];
-#pragma unroll
-  for (int t = 0; t < 13; ++t) acc2[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-  f32x4 acc1 = {0.f, 0.f, 0.f, 0.f};
-
-  const int sk = lane & 7, srow = lane >> 3;  // X0 staging items
-  const int zq = lane >> 1, zh = lane & 1;    // dZ2 staging items (lane < 50)
-  const int zqy = (zq * 205) >> 10, zqx = zq - 5 * zqy;
-  const int zbase = kBDz2 + ((2 * zqy + 4) * 20 + 2 * zqx + 4) * 32 + 16 * zh;
-  const int dxci = n16 < 12 ? n16 >> 1 : 5, dxj = n16 & 1;
-
-  // Per-image global loads, issued one image ahead (one wave per SIMD: nothing
-  // else would hide their latency): dY2 + argmax codes of conv2 (lanes < 50),
-  // Y1 (196 x 16 B), the u8 image (8 lanes per row), conv1 codes per dX tile.
-  u32x4 dy = {0u, 0u, 0u, 0u}, yv[4];
-  u32x2 cw = {0u, 0u};
-  uint32_t xw[4], a1n[7], a1w[7];
-  WaveIdx widx;
-  widx.load(p.idx, blockIdx.x, (int)gridDim.x, p.B, 0);
-  auto load_img = [&](int k) {  // k-th image of this wave
-    const int img = blockIdx.x + k * (int)gridDim.x;
-    if ((k & 63) == 0 && k > 0) widx.load(p.idx, blockIdx.x, (int)gridDim.x, p.B, k);
-    // the dataset image first: its address needs the index vector (a wait
-    // only when it was just reloaded); issued after the other loads, that
-    // wait also covered them -- a full memory latency on every image
-    const uint8_t* xin = p.x + (size_t)widx.get(k) * kImgPix;
-#pragma unroll
-    for (int it = 0; it < 4; ++it) {
-      const int yy = it * 8 + srow;
-      xw[it] = (yy < 28 && sk < 7) ? *reinterpret_cast<const uint32_t*>(xin + yy * 28 + sk * 4) : 0u;
-    }
-    if (lane < 50) {
-      dy = *reinterpret_cast<const u32x4*>(static_cast<const bf16*>(p.dy2) + (size_t)img * kY2Elems + zq * 16 + 8 * zh);
-      cw = *reinterpret_cast<const u32x2*>(p.a2 + (size_t)img * kY2Elems + zq * 16 + 8 * zh);
-    }
-    const bf16* y1g = static_cast<const bf16*>(p.y1) + (size_t)img * kY1Elems;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int px = min(lane + 64 * r, 195);
-      yv[r] = *reinterpret_cast<const u32x4*>(y1g + px * 8);
-    }
-    const uint8_t* a1g = p.a1 + (size_t)img * kA1Bytes + dxci * 224 + 4 * g;
-#pragma unroll
-    for (int t = 0; t < 7; ++t) a1n[t] = *reinterpret_cast<const uint32_t*>(a1g + (2 * t + dxj) * 16);
   };
-  if ((int)blockIdx.x < p.B) load_img(0);
-
-  for (int img = blockIdx.x, kimg = 0; img < p.B; img += (int)gridDim.x, ++kimg) {
-    wave_lds_sync();  // previous image: every LDS read done
-    // ---- stage dZ2 (unpool of dY2 by the argmax codes) ----
-    if (lane < 50 && !(MCC_LENET_ABL & 8)) {
-      const u32x4 z = {0u, 0u, 0u, 0u};
-      *reinterpret_cast<u32x4*>(smem + zbase) = z;
-      *reinterpret_cast<u32x4*>(smem + zbase + 32) = z;
-      *reinterpret_cast<u32x4*>(smem + zbase + 640) = z;
-      *reinterpret_cast<u32x4*>(smem + zbase + 672) = z;
+  auto stage_x = [&]() {
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const uint32_t code = (cw[i >> 2] >> (8 * (i & 3))) & 0xffu;
-        const uint32_t v = (dy[i >> 1] >> (16 * (i & 1))) & 0xffffu;
-        const int off = ((code & 2u) ? 640 : 0) + ((code & 1u) ? 32 : 0);  // code 4: value 0 at TL
-        *reinterpret_cast<unsigned short*>(smem + zbase + off + 2 * i) = (unsigned short)(code < 4u ? v : 0u);
-      }
-    }
-    // ---- stage Y1 ----
-#pragma unroll
-    for (int r = 0; r < ((MCC_LENET_ABL & 64) ? 0 : 4); ++r) {
-      const int px = lane + 64 * r;
-      if (px < 196) *reinterpret_cast<u32x4*>(smem + kBY1 + px * 16) = yv[r];
-    }
-    // ---- stage X0: copy c holds Xpad[r][p + c] at position p ----
-#pragma unroll
-    for (int it = 0; it < ((MCC_LENET_ABL & 128) ? 0 : 4); ++it) {
-      const int yy = it * 8 + srow;
+    for (int h = 0; h < ((MCC_LENET_ABL & 128) ? 0 : 2); ++h) {
+      const int yy = (2 * wv + h) * 8 + srow;
       uint32_t lo, hi;
-      u8x4_ints(xw[it], lo, hi);
+      u8x4_ints(xw[h], lo, hi);
       const uint32_t phi = from_left(hi);
       const uint32_t rlo = from_right(lo);
       const uint32_t nlo = sk == 7 ? 0u : rlo;
@@ -614,115 +509,261 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1)))
         *reinterpret_cast<u32x2*>(d + 3 * kBxCopy) = u32x2{mid16(lo, hi), mid16(hi, nlo)};
       }
     }
-#pragma unroll
-    for (int t = 0; t < 7; ++t) a1w[t] = a1n[t];
-    wave_lds_sync();
-    // next image's loads fly while this one computes
-    if (img + (int)gridDim.x < p.B && !(MCC_LENET_ABL & 256)) load_img(kimg + 1);
+  };
+  WaveIdx widx;
+  widx.load(p.idx, blockIdx.x, (int)gridDim.x, p.B, 0);
+  auto image_x = [&](int k) {  // dataset image of this workgroup's k-th image
+    if ((k & 63) == 0 && k > 0) widx.load(p.idx, blockIdx.x, (int)gridDim.x, p.B, k);
+    return p.x + (size_t)widx.get(k) * kImgPix;
+  };
 
-    // ---- conv2 weight gradient (operands of chunk c+1 read during chunk c) ----
-    if constexpr (!(MCC_LENET_ABL & 1)) {
-      bf16x8 af[2], bfr[2][13];
-      auto load_chunk = [&](int c, int buf) {
-        af[buf] = tr8(smem + aw2[c][0], smem + aw2[c][1]);
-#pragma unroll
-        for (int t = 0; t < 13; ++t) {
-          const int o = tapoff2(2 * t);
-          const int* base = t == 12 ? bw2c[c] : ((2 * t) % 5 == 4 ? bw2b[c] : bw2a[c]);
-          bfr[buf][t] = tr8(smem + base[0] + o, smem + base[1] + o);
-        }
-      };
-      load_chunk(0, 0);
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        if (c + 1 < 4) load_chunk(c + 1, (c + 1) & 1);
-        __builtin_amdgcn_sched_barrier(0);  // keep the reads of chunk c+1 ahead of chunk c's MFMAs
-#pragma unroll
-        for (int t = 0; t < 13; ++t) acc2[t] = mma(acc2[t], af[c & 1], bfr[c & 1][t]);
-        __builtin_amdgcn_sched_barrier(0);
-      }
+  // conv1 dW (wave 0, all 30 output rows: splitting the rows between the two
+  // waves measured no faster and costs a second slab half): A row m = (kDw1Co[m], kDw1S[m]) (rows 12..15 repeat 0..3), B column n =
+  // 5*kh' + kw (15 = ones).  Row zy + 2 - 2s of the swizzled dZ1 plane: its
+  // chunk bit is (zy >> 1) ^ 1 ^ s, so two bases by the parity of zy >> 1.
+  int a1b[2];
+  {
+    const int m = n16 < 12 ? n16 : n16 - 12, co = kDw1Co[m], s2 = kDw1S[m];
+    const int base = kBDz1 + co * kBDz1Plane + (2 - 2 * s2) * 64;
+    a1b[0] = base + 16 * (g ^ 1 ^ s2);
+    a1b[1] = base + 16 * (g ^ s2);
+  }
+  int b1b;
+  {
+    if (n16 == 15) b1b = kBOne1 + 16 * g;
+    else {
+      const int kh = n16 / 5, kw = n16 % 5, c = kw & 3;
+      b1b = kBXs + c * kBxCopy + (kh * 40 + 8 * g + kw - c) * 2;
     }
-
-    // ---- conv2 data gradient -> dZ1 rows (unpool by the conv1 argmax) ----
-    if constexpr (!(MCC_LENET_ABL & 2)) {
-      bf16x8 fr[15], nx[5];
-#pragma unroll
-      for (int c = 0; c < 15; ++c)
-        fr[c] = *reinterpret_cast<const bf16x8*>(smem + (dxwrap(c) ? hxb : hxa) + dxoff(c));
-      // software pipelined: tile T's 15 chained MFMAs are issued together with
-      // tile T-1's epilogue (unpool by the conv1 argmax, dZ1 row stores), so
-      // the epilogue's VALU / LDS work fills the MFMA dependency gaps
-      f32x4 accp = {0.f, 0.f, 0.f, 0.f};
-      auto epilogue = [&](int T, const f32x4& acc) {
-        // lane (n = 2ci + j, g): rows px = 4g + i of dY1 row py = 2T + j
-        uint32_t top[4], bot[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const uint32_t code = (a1w[T] >> (8 * i)) & 0xffu;
-          const uint64_t h = code < 4u ? (uint64_t)bf16_bits(acc[i]) : 0ull;
-          const uint64_t w = h << (16u * (code & 3u));
-          top[i] = (uint32_t)w;
-          bot[i] = (uint32_t)(w >> 32);
-        }
-        if (n16 < 12) {
-          // rows 4T + 2dxj + 2 and + 3: swizzle bit (2T + dxj + 1) & 1 = 1 - dxj
-          char* d = smem + kBDz1 + dxci * kBDz1Plane + (4 * T + 2 * dxj + 2) * 64 + 16 * (g ^ (1 - dxj));
-          *reinterpret_cast<u32x4*>(d) = u32x4{top[0], top[1], top[2], top[3]};
-          *reinterpret_cast<u32x4*>(d + 64) = u32x4{bot[0], bot[1], bot[2], bot[3]};
-        }
-      };
-#pragma unroll
-      for (int T = 0; T < 7; ++T) {
-        if (T + 1 < 7) {  // tile T+1 reuses fr[5..14] as its chunks 0..9; read its chunks 10..14 now
-#pragma unroll
-          for (int c = 10; c < 15; ++c)
-            nx[c - 10] = *reinterpret_cast<const bf16x8*>(smem + (dxwrap(c) ? hxb : hxa) + dxoff(c) + (T + 1) * 1280);
-        }
-        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int c = 0; c < 15; ++c) acc = mma(acc, fr[c], wdx[c]);
-        if (T > 0) epilogue(T - 1, accp);
-        accp = acc;
-#pragma unroll
-        for (int c = 0; c < 10; ++c) fr[c] = fr[c + 5];
-#pragma unroll
-        for (int c = 10; c < 15; ++c) fr[c] = nx[c - 10];
-      }
-      epilogue(6, accp);
-    }
-    wave_lds_sync();  // dZ1 complete
-
-    // ---- conv1 weight gradient: one MFMA per output row (32 pixels), 4 rows of reads in flight ----
+  }
+  f32x4 acc1 = {0.f, 0.f, 0.f, 0.f};
+  auto dw1 = [&]() {  // one MFMA per output row (32 pixels), 4 rows of reads in flight
     if constexpr (!(MCC_LENET_ABL & 4)) {
-      constexpr int D = 4;
+      constexpr int D = 4, NR = 30;
+      const int z0 = 0;
       bf16x8 a[D], b[D];
 #pragma unroll
-      for (int zy = 0; zy < D; ++zy) {
-        a[zy] = *reinterpret_cast<const bf16x8*>(smem + a1b[(zy >> 1) & 1] + zy * 64);
-        b[zy] = lds8(smem + b1b + zy * 80);
+      for (int i = 0; i < D; ++i) {
+        const int zy = z0 + i;
+        a[i] = *reinterpret_cast<const bf16x8*>(smem + a1b[(zy >> 1) & 1] + zy * 64);
+        b[i] = lds8(smem + b1b + zy * 80);
       }
 #pragma unroll
-      for (int zy = 0; zy < 30; ++zy) {
-        const bf16x8 ca = a[zy % D], cb = b[zy % D];
-        if (zy + D < 30) {
-          a[zy % D] = *reinterpret_cast<const bf16x8*>(smem + a1b[((zy + D) >> 1) & 1] + (zy + D) * 64);
-          b[zy % D] = lds8(smem + b1b + (zy + D) * 80);
+      for (int i = 0; i < NR; ++i) {
+        const bf16x8 ca = a[i % D], cb = b[i % D];
+        if (i + D < NR) {
+          const int zy = z0 + i + D;
+          a[i % D] = *reinterpret_cast<const bf16x8*>(smem + a1b[(zy >> 1) & 1] + zy * 64);
+          b[i % D] = lds8(smem + b1b + zy * 80);
         }
         __builtin_amdgcn_sched_barrier(0);
         acc1 = mma(acc1, ca, cb);
         __builtin_amdgcn_sched_barrier(0);
       }
     }
-  }
+  };
 
-  // ---- per-wave slab (accumulator order) ----
-  float* slab = p.slab + (size_t)blockIdx.x * kSlab;
+  if (wv == 0) {
+    // ======================= wave 0: conv2 dW, conv1 dW =======================
+    // dW2: transposed reads, K position 32c + 8g + 4hf + tq holds pixel kZPos[.]
+    int aw2[4][2], bw2a[4][2], bw2b[4][2], bw2c[4][2];
 #pragma unroll
-  for (int t = 0; t < 13; ++t)
+    for (int c = 0; c < 4; ++c)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) slab[(t * 4 + i) * 64 + lane] = acc2[t][i];
+      for (int hf = 0; hf < 2; ++hf) {
+        const int v = kZPos[32 * c + 8 * g + 4 * hf + tq];
+        const bool ok = v < 100;
+        const int z = ok ? v : v - 128;
+        const int zy = z / 10, zx = z % 10;
+        aw2[c][hf] = ok ? kBDz2 + ((zy + 4) * 20 + zx + 4) * 32 + 8 * tp : kBDz2 + 8 * tp;
+        const int yb = kBY1 + (zy * 14 + zx) * 16 + 8 * (tp & 1);
+        bw2a[c][hf] = yb + (tp >> 1) * 16;
+        bw2b[c][hf] = yb + (tp >> 1) * 160;
+        bw2c[c][hf] = (tp >> 1) ? kBOne2 + 8 * (tp & 1) - tapoff2(24) : yb;
+      }
+    f32x4 acc2[13];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) slab[kSlabW2 + i * 64 + lane] = acc1[i];
+    for (int t = 0; t < 13; ++t) acc2[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    if ((int)blockIdx.x < p.B) load_x(image_x(0));
+    for (int img = blockIdx.x, kimg = 0; img < p.B; img += (int)gridDim.x, ++kimg) {
+      stage_x();
+      wg_barrier();  // B1
+      if (img + (int)gridDim.x < p.B && !(MCC_LENET_ABL & 256)) load_x(image_x(kimg + 1));
+
+      // ---- conv2 weight gradient (operands of chunk c+1 read during chunk c) ----
+      if constexpr (!(MCC_LENET_ABL & 1)) {
+        bf16x8 af[2], bfr[2][13];
+        auto load_chunk = [&](int c, int buf) {
+          af[buf] = tr8(smem + aw2[c][0], smem + aw2[c][1]);
+#pragma unroll
+          for (int t = 0; t < 13; ++t) {
+            const int o = tapoff2(2 * t);
+            const int* base = t == 12 ? bw2c[c] : ((2 * t) % 5 == 4 ? bw2b[c] : bw2a[c]);
+            bfr[buf][t] = tr8(smem + base[0] + o, smem + base[1] + o);
+          }
+        };
+        load_chunk(0, 0);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          if (c + 1 < 4) load_chunk(c + 1, (c + 1) & 1);
+          __builtin_amdgcn_sched_barrier(0);  // keep the reads of chunk c+1 ahead of chunk c's MFMAs
+#pragma unroll
+          for (int t = 0; t < 13; ++t) acc2[t] = mma(acc2[t], af[c & 1], bfr[c & 1][t]);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+      wg_barrier();  // B2: dZ1 complete
+      dw1();
+      wg_barrier();  // B3: X0 and dZ1 free
+    }
+
+    // ---- per-workgroup slab (accumulator order) ----
+    float* slab = p.slab + (size_t)blockIdx.x * kSlab;
+#pragma unroll
+    for (int t = 0; t < 13; ++t)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) slab[(t * 4 + i) * 64 + lane] = acc2[t][i];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) slab[kSlabW2 + i * 64 + lane] = acc1[i];
+  } else {
+    // ================ wave 1: conv2 dX -> dZ1, dZ2 / Y1 staging ================
+    // conv2 data-gradient weights in registers: lane (n, kgroup g): k = 32c +
+    // 8g + e -> tap t = 2c + (g>>1) = (u', v), output channel co = 8(g&1) + e;
+    // column n = 2*ci + j (ci < 6): B = W2[co][ci][4 + j - u'][4 - v] where the
+    // row is in range.
+    bf16x8 wdx[15];
+    {
+      const int ci = n16 >> 1, j = n16 & 1;
+#pragma unroll
+      for (int c = 0; c < 15; ++c) {
+        const int t = 2 * c + (g >> 1), u = t / 5, v = t % 5;
+        const int kh = 4 + j - u, kw = 4 - v;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int co = 8 * (g & 1) + e;
+          const bool ok = n16 < 12 && kh >= 0 && kh < 5;
+          float w = p.w2[ok ? ((co * 6 + ci) * 5 + kh) * 5 + kw : 0];
+          w = ok ? w : 0.f;
+          wdx[c][e] = (bf16)w;
+        }
+      }
+    }
+    // A rows px = n16, k-group g: chunk tap parity (g>>1), channel half (g&1)
+    const int hxa = kBDz2 + n16 * 32 + 16 * (g & 1) + (g >> 1) * 32;
+    const int hxb = kBDz2 + n16 * 32 + 16 * (g & 1) + (g >> 1) * 512;
+    const int zq = lane >> 1, zh = lane & 1;  // dZ2 staging items (lane < 50)
+    const int zqy = (zq * 205) >> 10, zqx = zq - 5 * zqy;
+    const int zbase = kBDz2 + ((2 * zqy + 4) * 20 + 2 * zqx + 4) * 32 + 16 * zh;
+    const int dxci = n16 < 12 ? n16 >> 1 : 5, dxj = n16 & 1;
+
+    // per-image loads, issued one image ahead: dY2 + argmax codes of conv2
+    // (lanes < 50), Y1 (196 x 16 B), the u8 image rows of this wave, conv1
+    // codes per dX tile
+    u32x4 dy = {0u, 0u, 0u, 0u}, yv[4];
+    u32x2 cw = {0u, 0u};
+    uint32_t a1n[7], a1w[7];
+    auto load_img = [&](int k) {
+      const int img = blockIdx.x + k * (int)gridDim.x;
+      load_x(image_x(k));  // first: the address needs the index vector
+      if (lane < 50) {
+        dy = *reinterpret_cast<const u32x4*>(static_cast<const bf16*>(p.dy2) + (size_t)img * kY2Elems + zq * 16 + 8 * zh);
+        cw = *reinterpret_cast<const u32x2*>(p.a2 + (size_t)img * kY2Elems + zq * 16 + 8 * zh);
+      }
+      const bf16* y1g = static_cast<const bf16*>(p.y1) + (size_t)img * kY1Elems;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int px = min(lane + 64 * r, 195);
+        yv[r] = *reinterpret_cast<const u32x4*>(y1g + px * 8);
+      }
+      const uint8_t* a1g = p.a1 + (size_t)img * kA1Bytes + dxci * 224 + 4 * g;
+#pragma unroll
+      for (int t = 0; t < 7; ++t) a1n[t] = *reinterpret_cast<const uint32_t*>(a1g + (2 * t + dxj) * 16);
+    };
+    auto stage_dz2_y1 = [&]() {
+      if (lane < 50 && !(MCC_LENET_ABL & 8)) {  // dZ2 = unpool of dY2 by the argmax codes
+        const u32x4 z = {0u, 0u, 0u, 0u};
+        *reinterpret_cast<u32x4*>(smem + zbase) = z;
+        *reinterpret_cast<u32x4*>(smem + zbase + 32) = z;
+        *reinterpret_cast<u32x4*>(smem + zbase + 640) = z;
+        *reinterpret_cast<u32x4*>(smem + zbase + 672) = z;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const uint32_t code = (cw[i >> 2] >> (8 * (i & 3))) & 0xffu;
+          const uint32_t v = (dy[i >> 1] >> (16 * (i & 1))) & 0xffffu;
+          const int off = ((code & 2u) ? 640 : 0) + ((code & 1u) ? 32 : 0);  // code 4: value 0 at TL
+          *reinterpret_cast<unsigned short*>(smem + zbase + off + 2 * i) = (unsigned short)(code < 4u ? v : 0u);
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < ((MCC_LENET_ABL & 64) ? 0 : 4); ++r) {
+        const int px = lane + 64 * r;
+        if (px < 196) *reinterpret_cast<u32x4*>(smem + kBY1 + px * 16) = yv[r];
+      }
+    };
+    if ((int)blockIdx.x < p.B) {
+      load_img(0);
+      stage_dz2_y1();
+    }
+    for (int img = blockIdx.x, kimg = 0; img < p.B; img += (int)gridDim.x, ++kimg) {
+      stage_x();
+#pragma unroll
+      for (int t = 0; t < 7; ++t) a1w[t] = a1n[t];
+      wg_barrier();  // B1
+      const bool more = img + (int)gridDim.x < p.B;
+      if (more && !(MCC_LENET_ABL & 256)) load_img(kimg + 1);
+
+      // ---- conv2 data gradient -> dZ1 rows (unpool by the conv1 argmax) ----
+      if constexpr (!(MCC_LENET_ABL & 2)) {
+        bf16x8 fr[15], nx[5];
+#pragma unroll
+        for (int c = 0; c < 15; ++c)
+          fr[c] = *reinterpret_cast<const bf16x8*>(smem + (dxwrap(c) ? hxb : hxa) + dxoff(c));
+        // software pipelined: tile T's 15 chained MFMAs are issued together with
+        // tile T-1's epilogue (unpool by the conv1 argmax, dZ1 row stores)
+        f32x4 accp = {0.f, 0.f, 0.f, 0.f};
+        auto epilogue = [&](int T, const f32x4& acc) {
+          // lane (n = 2ci + j, g): rows px = 4g + i of dY1 row py = 2T + j
+          uint32_t top[4], bot[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const uint32_t code = (a1w[T] >> (8 * i)) & 0xffu;
+            const uint64_t h = code < 4u ? (uint64_t)bf16_bits(acc[i]) : 0ull;
+            const uint64_t w = h << (16u * (code & 3u));
+            top[i] = (uint32_t)w;
+            bot[i] = (uint32_t)(w >> 32);
+          }
+          if (n16 < 12) {
+            // rows 4T + 2dxj + 2 and + 3: swizzle bit (2T + dxj + 1) & 1 = 1 - dxj
+            char* d = smem + kBDz1 + dxci * kBDz1Plane + (4 * T + 2 * dxj + 2) * 64 + 16 * (g ^ (1 - dxj));
+            *reinterpret_cast<u32x4*>(d) = u32x4{top[0], top[1], top[2], top[3]};
+            *reinterpret_cast<u32x4*>(d + 64) = u32x4{bot[0], bot[1], bot[2], bot[3]};
+          }
+        };
+#pragma unroll
+        for (int T = 0; T < 7; ++T) {
+          if (T + 1 < 7) {  // tile T+1 reuses fr[5..14] as its chunks 0..9; read its chunks 10..14 now
+#pragma unroll
+            for (int c = 10; c < 15; ++c)
+              nx[c - 10] = *reinterpret_cast<const bf16x8*>(smem + (dxwrap(c) ? hxb : hxa) + dxoff(c) + (T + 1) * 1280);
+          }
+          f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int c = 0; c < 15; ++c) acc = mma(acc, fr[c], wdx[c]);
+          if (T > 0) epilogue(T - 1, accp);
+          accp = acc;
+#pragma unroll
+          for (int c = 0; c < 10; ++c) fr[c] = fr[c + 5];
+#pragma unroll
+          for (int c = 10; c < 15; ++c) fr[c] = nx[c - 10];
+        }
+        epilogue(6, accp);
+      }
+      wg_barrier();  // B2: dZ1 complete; dZ2 and Y1 free
+      if (more) stage_dz2_y1();  // the next image's, while wave 0 runs conv1 dW
+      wg_barrier();  // B3
+    }
+  }
 }
 
 // Fixed-order sum of the per-wave slabs, mapped to the canonical gradients.
@@ -780,7 +821,7 @@ void lenet_forward(const LenetFwdParams& p, hipStream_t s) {
 void lenet_backward(const LenetBwdParams& p, hipStream_t s) {
   if (p.B <= 0) return;
   const int grid = lenet_bwd_grid();
-  hipLaunchKernelGGL(lenet_bwd_kernel, dim3(grid), dim3(64), kBLds, s, p);
+  hipLaunchKernelGGL(lenet_bwd_kernel, dim3(grid), dim3(128), kBLds, s, p);
   hipLaunchKernelGGL(lenet_bwd_reduce_kernel, dim3(kSlab / 64), dim3(64 * kRedWaves), 0, s, p, grid);
 }
 
