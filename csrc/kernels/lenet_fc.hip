@@ -74,6 +74,7 @@ static_assert(OW2 % 16 == 0 && OW3 % 16 == 0 && OY % 16 == 0 && OH1 % 16 == 0 &&
 // canonical slab layout = the flat parameter range of the three FC layers
 constexpr int kSlabW1 = 0, kSlabB1 = N1 * K0, kSlabW2 = kSlabB1 + N1, kSlabB2 = kSlabW2 + N2 * N1,
               kSlabW3 = kSlabB2 + N2, kSlabB3 = kSlabW3 + N3 * N2, kSlab = kSlabB3 + N3;  // 59,134
+constexpr int kSlabP = (kSlab + 3) & ~3;  // slab stride (16-byte rows for the float4 reduce)
 
 // image row m of a tile -> LDS row (bits 2 and 3 swapped: the 8 rows of a
 // transposed read {0..3, 8..11} land in 8 different 32-byte bank slots)
@@ -472,7 +473,7 @@ __global__ void __launch_bounds__(kThreads, 1) lenet_fc_kernel(LenetFcParams P) 
   }
 
   // ---- this workgroup's weight-gradient slab (canonical layout) ----
-  float* slab = P.slab + (size_t)blockIdx.x * kSlab;
+  float* slab = P.slab + (size_t)blockIdx.x * kSlabP;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int n1 = 16 * w + 4 * g + i;
@@ -522,21 +523,32 @@ __global__ void __launch_bounds__(kThreads, 1) lenet_fc_kernel(LenetFcParams P) 
 // out[i] = sum over the workgroup slabs in order; 16 waves per 64 positions
 constexpr int kRedWaves = 16;
 __global__ void __launch_bounds__(64 * kRedWaves) lenet_fc_reduce_kernel(const float* slab, int nslabs, float* out) {
-  __shared__ float part[kRedWaves][64];
+  // float4 per lane (1 KB per wave load): wave w sums slabs w, w + 16, ... of
+  // positions 4 (blk * 64 + lane) .. + 3, then wave 0 adds the 16 partials in order
+  __shared__ float4 part[kRedWaves][64];
   const int l = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int pos = blockIdx.x * 64 + l;
-  float s = 0.f;
-  if (pos < kSlab) {
+  const int p4 = blockIdx.x * 64 + l;
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (4 * p4 < kSlab) {
 #pragma unroll 8
-    for (int k = wv; k < nslabs; k += kRedWaves) s += slab[(size_t)k * kSlab + pos];
+    for (int k = wv; k < nslabs; k += kRedWaves) {
+      const float4 v = *reinterpret_cast<const float4*>(slab + (size_t)k * kSlabP + 4 * p4);
+      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    }
   }
   part[wv][l] = s;
   __syncthreads();
-  if (wv != 0 || pos >= kSlab) return;
-  float v = part[0][l];
+  if (wv != 0 || 4 * p4 >= kSlab) return;
+  float4 v = part[0][l];
 #pragma unroll
-  for (int i = 1; i < kRedWaves; ++i) v += part[i][l];
-  out[pos] = v;
+  for (int i = 1; i < kRedWaves; ++i) {
+    const float4 t = part[i][l];
+    v.x += t.x; v.y += t.y; v.z += t.z; v.w += t.w;
+  }
+  const float r[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    if (4 * p4 + i < kSlab) out[4 * p4 + i] = r[i];
 }
 
 int fc_grid(int B) { return std::min((B + TM - 1) / TM, 256); }
@@ -544,7 +556,7 @@ int fc_grid(int B) { return std::min((B + TM - 1) / TM, 256); }
 }  // namespace
 
 bool lenet_fc_supported(int kin, int n1, int n2, int n3) { return kin == K0 && n1 == N1 && n2 == N2 && n3 == N3; }
-size_t lenet_fc_slab_bytes(int max_batch) { return (size_t)fc_grid(max_batch) * kSlab * 4; }
+size_t lenet_fc_slab_bytes(int max_batch) { return (size_t)fc_grid(max_batch) * kSlabP * 4; }
 int lenet_fc_grad_count() { return kSlab; }
 
 void lenet_fc(const LenetFcParams& p, float* grads, hipStream_t s) {
@@ -556,7 +568,7 @@ void lenet_fc(const LenetFcParams& p, float* grads, hipStream_t s) {
             "lenet_fc: leading dimensions");
   const int grid = fc_grid(p.B);
   hipLaunchKernelGGL(lenet_fc_kernel, dim3(grid), dim3(kThreads), 0, s, p);
-  hipLaunchKernelGGL(lenet_fc_reduce_kernel, dim3((kSlab + 63) / 64), dim3(64 * kRedWaves), 0, s, p.slab, grid, grads);
+  hipLaunchKernelGGL(lenet_fc_reduce_kernel, dim3((kSlab + 255) / 256), dim3(64 * kRedWaves), 0, s, p.slab, grid, grads);
 }
 
 }  // namespace gpu
