@@ -111,6 +111,12 @@ def main():
         raise SystemExit(f"bench: --gpus {args.gpus} but WORLD_SIZE={world}: the JSON line would not describe "
                          "the requested run")
 
+    # Native libraries write banners to stdout (RCCL prints its version block
+    # at communicator init): route fd 1 to stderr for the run and keep a
+    # duplicate of the real stdout for the one JSON line.
+    json_fd = os.dup(1)
+    os.dup2(2, 1)
+
     import torch
     import torch.distributed as dist
 
@@ -251,7 +257,8 @@ def main():
                 "launch": graph_note,
             },
         }
-        print(json.dumps(out), flush=True)
+        sys.stdout.flush()
+        os.write(json_fd, (json.dumps(out) + "\n").encode())
     if dist.is_initialized():
         dist.destroy_process_group()
 

@@ -52,7 +52,7 @@ inline void usage(const char* prog) {
   std::fprintf(stderr,
                "usage: %s train-images train-labels test-images test-labels\n"
                "  [--model ref|lenet5|cifar3|vgg11] [--epochs N] [--batch B] [--lr X]\n"
-               "  [--momentum X] [--weight-decay X] [--seed S] [--dtype bf16|fp32]\n"
+               "  [--momentum X] [--weight-decay X] [--seed S] [--dtype bf16|fp32|fp64]\n"
                "  [--ref-compat] [--fp32] [--save W] [--load W] [--max-train N]\n"
                "  [--bucket-mb MB] [--log-every N] [--profile] [--no-graph] [--json PATH|-]\n"
                "  [--comm rccl|host|local]   (cnn_dist: RCCL; host shared memory for several ranks\n"

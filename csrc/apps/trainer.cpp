@@ -127,6 +127,8 @@ int run_gpu_training(const CliArgs& a, Comm& comm, const char* program) {
   HIPCHK(hipGetDeviceCount(&ndev));
   if (ndev < 1) { std::fprintf(stderr, "%s: no GPU\n", program); return 111; }
   HIPCHK(hipSetDevice(comm.local_rank() % ndev));
+  MCC_CHECK(a.dtype == "bf16" || a.dtype == "fp32",
+            "--dtype " + a.dtype + ": the data-parallel engine runs bf16 | fp32 (fp64: cnn_hip --dtype fp64)");
   const DType dt = a.dtype == "fp32" ? DType::F32 : DType::BF16;
 
   // ---- model + initial weights (identical on every rank, then broadcast) ----

@@ -15,6 +15,7 @@
 #include "mcc/engine.h"
 #include "mcc/io.h"
 #include "mcc/model.h"
+#include "mcc/net64.h"
 
 namespace py = pybind11;
 using namespace mcc;
@@ -218,6 +219,65 @@ PYBIND11_MODULE(_C, m) {
 
   bind_cpu_net<double>(m, "CpuNet64");
   bind_cpu_net<float>(m, "CpuNet32");
+
+  // fp64 on the GPU, CpuNet64's API (host arrays in and out) plus device
+  // pointers for zero-copy use
+  auto stats_dict = [](const StepStats& s) {
+    py::dict d;
+    d["loss_sum"] = s.loss_sum; d["mse_sum"] = s.mse_sum; d["correct"] = s.correct; d["count"] = s.count;
+    return d;
+  };
+  using F64 = py::array_t<double, py::array::c_style | py::array::forcecast>;
+  py::class_<GpuNet64>(m, "GpuNet64")
+      .def(py::init<const ModelSpec&, bool, int, int>(), py::arg("spec"), py::arg("ref_compat") = false,
+           py::arg("max_batch") = 256, py::arg("device") = -1)
+      .def_property_readonly("nparams", &GpuNet64::nparams)
+      .def_property_readonly("ref_compat", &GpuNet64::ref_compat)
+      .def_property_readonly("max_batch", &GpuNet64::max_batch)
+      .def_property_readonly("device_bytes", &GpuNet64::device_bytes)
+      .def_property_readonly("params_ptr", [](const GpuNet64& n) { return reinterpret_cast<uintptr_t>(n.device_params()); })
+      .def_property_readonly("grads_ptr", [](const GpuNet64& n) { return reinterpret_cast<uintptr_t>(n.device_grads()); })
+      .def_property_readonly("stream", [](const GpuNet64& n) { return reinterpret_cast<uintptr_t>(n.stream()); })
+      .def("get_params", [](const GpuNet64& n) { py::array_t<double> a(n.nparams()); n.get_params(a.mutable_data()); return a; })
+      .def("get_grads", [](const GpuNet64& n) { py::array_t<double> a(n.nparams()); n.get_grads(a.mutable_data()); return a; })
+      .def("set_params", [](GpuNet64& n, F64 a) {
+        MCC_CHECK((int64_t)a.size() == n.nparams(), "set_params: size mismatch");
+        n.set_params(a.data());
+      })
+      .def("set_grads", [](GpuNet64& n, F64 a) {
+        MCC_CHECK((int64_t)a.size() == n.nparams(), "set_grads: size mismatch");
+        n.set_grads(a.data());
+      })
+      .def("forward", [](GpuNet64& n, F64 x) {
+        const int64_t in = n.spec().input_nodes();
+        MCC_CHECK(x.size() % in == 0, "forward: input size not a multiple of the input shape");
+        const int B = (int)(x.size() / in);
+        const double* p;
+        {
+          py::gil_scoped_release rel;
+          n.forward(x.data(), B);
+          p = n.probs();
+        }
+        return py::array_t<double>({B, n.spec().num_classes()}, p);
+      })
+      .def("forward_device", [](GpuNet64& n, uintptr_t x, int B) { n.forward_device(ptr<const double>(x), B); },
+           py::arg("x"), py::arg("B"))
+      .def("backward", [stats_dict](GpuNet64& n, py::array_t<int, py::array::c_style | py::array::forcecast> labels,
+                                    double scale) {
+        MCC_CHECK(labels.size() >= n.batch(), "backward: fewer labels than the forward batch");
+        StepStats s;
+        {
+          py::gil_scoped_release rel;
+          s = n.backward(labels.data(), scale);
+        }
+        return stats_dict(s);
+      }, py::arg("labels"), py::arg("scale") = 1.0)
+      .def("evaluate", [stats_dict](GpuNet64& n, py::array_t<int, py::array::c_style | py::array::forcecast> labels) {
+        MCC_CHECK(labels.size() >= n.batch(), "evaluate: fewer labels than the forward batch");
+        return stats_dict(n.evaluate(labels.data()));
+      })
+      .def("sgd", [](GpuNet64& n, double lr) { n.sgd(lr); })
+      .def("zero_grads", &GpuNet64::zero_grads);
 
   // --------------------------------------------------------------- engine
   py::class_<GpuNet>(m, "GpuNet")

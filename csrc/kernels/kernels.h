@@ -658,5 +658,46 @@ void iota_i32(int32_t* idx, int B, int64_t start, hipStream_t s);
 void cast_f32(DType t, void* dst, const float* src, int64_t n, hipStream_t s);
 void to_f32(DType t, float* dst, const void* src, int64_t n, hipStream_t s);
 
+// ---- fp64 executor (f64.hip; GpuNet64, the reference's precision) ----
+// C[m][n] (+)= act(sum_k A(m,k) B(k,n) + bias_m[m] + bias_n[n]) with
+// A(m,k) = A[m*sam + k*sak], B(k,n) = B[k*sbk + n*sbn] (v_mfma_f64_16x16x4).
+// P > 0 stores C in the conv activation layout: n = b*P + p -> C[b][m][p].
+// `accumulate` adds to C after the activation (weight gradients: act none).
+struct Gemm64Params {
+  int M = 0, N = 0;
+  int64_t K = 0;
+  const double* A = nullptr;
+  int64_t sam = 0, sak = 0;
+  const double* B = nullptr;
+  int64_t sbk = 0, sbn = 0;
+  double* C = nullptr;
+  int64_t ldc = 0;
+  int P = 0;
+  const double* bias_m = nullptr;
+  const double* bias_n = nullptr;
+  int act = ACT_NONE;
+  bool accumulate = false;
+  double* part = nullptr;  // set by gemm64
+  int64_t kchunk = 0;      // set by gemm64
+};
+// split-K slab count for an (M, N, K) product (shape-only: deterministic)
+int gemm64_slabs(int M, int N, int64_t K);
+// `part` (>= gemm64_slabs * M * N doubles) enables fixed-order split-K; nullptr: one slab
+void gemm64(const Gemm64Params& p, double* part, hipStream_t s);
+struct Conv64Geom { int Ci, H, W, k, s, pad, OH, OW; };
+struct Pool64Geom { int C, H, W, k, s, OH, OW; };
+void im2col64(const Conv64Geom& g, const double* x, double* col, int B, hipStream_t s);
+void col2im64(const Conv64Geom& g, const double* dcol, double* dx, int B, hipStream_t s);
+void weff64(const double* w, double* weff, int C, int Ci, int kk, hipStream_t s);
+void fold64(const double* full, double* gw, int C, int Ci, int kk, hipStream_t s);
+void dz64(const double* err, const double* y, double* dzT, int B, int C, int P, int act, hipStream_t s);
+void rowsum64(const double* dzT, double* gb, int rows, int64_t n, hipStream_t s);
+void pool64_fwd(const Pool64Geom& g, const double* x, double* y, int32_t* arg, int B, hipStream_t s);
+void pool64_bwd(const Pool64Geom& g, const double* er, const int32_t* arg, double* dx, int B, hipStream_t s);
+void softmax64(double* z, int B, int C, bool ref_compat, hipStream_t s);
+void out_err64(const double* p, const int32_t* labels, double* err, double* stats, int B, int C, double scale,
+               hipStream_t s);
+void sgd64(double* w, double* g, double lr, int64_t n, hipStream_t s);
+
 }  // namespace gpu
 }  // namespace mcc
