@@ -49,6 +49,9 @@ typedef __attribute__((address_space(3))) void lvoid;
 constexpr int kIgT = 256;  // threads per workgroup
 constexpr int kIgBM = 128;
 constexpr int kIgBK = 64;
+// weight-gradient kernel (128 x 128 tiles): 32-pixel K-steps through a
+// 4-deep LDS ring (64 KB, two workgroups per CU)
+constexpr int kDwBK = 32, kDwStages = 4;
 
 // zero page (and a bf16 "1, 0 x 7" piece for the ones column), >= 16 bytes each
 __device__ __attribute__((aligned(64))) const unsigned short kIgZero[32] = {0};
@@ -703,11 +706,21 @@ __global__ void __launch_bounds__(kBigT, 1) igemm_big_kernel(IgemmParams p) {
 // ---------------------------------------------------------------------------
 // weight gradient (split-K over pixels)
 // ---------------------------------------------------------------------------
+// Pipeline: K-step ks lands in ring slot (ks - ks0) % 4 and is issued three
+// steps ahead; every step issues exactly 2J DMAs per thread (past the split:
+// harmless pieces into a slot nobody reads), so "stage ks landed" is the fixed
+// `s_waitcnt vmcnt(8)` (in-order retirement) followed by an explicit
+// s_barrier -- __syncthreads() would drain the lookahead.  The barrier also
+// retires the reads of the slot the next DMA overwrites (read one step ago).
+// (Round 3 ran 64-pixel steps double-buffered with a full drain per step:
+// one compute step of lookahead, latency-bound at ~2 TB/s on the reference
+// model's FC1 gradient, 286 us.)
 __global__ void __launch_bounds__(kIgT, 2) igemm_dw_kernel(IgemmDwParams p) {
-  constexpr int BM = 128, BN = 128, BK = 64;  // co x k x pixels
-  constexpr int J = BK * 16 / kIgT;            // glds per thread per operand (4)
+  constexpr int BM = 128, BN = 128, BK = kDwBK;  // co x k x pixels
+  constexpr int J = BK * 16 / kIgT;               // glds per thread per operand (2)
   constexpr int IMG = (BM + BN) * BK;
-  __shared__ __attribute__((aligned(16))) bf16 smem[2 * IMG];
+  static_assert(2 * J * (kDwStages - 2) == 8, "the s_waitcnt below");
+  __shared__ __attribute__((aligned(16))) bf16 smem[kDwStages * IMG];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r16 = lane & 15, g = lane >> 4;
@@ -800,41 +813,50 @@ __global__ void __launch_bounds__(kIgT, 2) igemm_dw_kernel(IgemmDwParams p) {
 
   // transpose-read of a [BK][128] image: 4 consecutive K rows (pixels) of
   // 16 columns; lane 4q+p of a 16-lane group addresses row kr+q, columns 4p..
-  auto tr = [&](const bf16* img, int kr, int col0) {
+  auto tra = [&](const bf16* img, int kr, int col0) {  // (inline asm: see tr4_async)
     const int row = kr + q;
     const int col = col0 + 4 * pp;
-    return tr4(img + row * 128 + (((col >> 3) ^ swz128(row)) << 3) + (col & 7));
+    return tr4_async(img + row * 128 + (((col >> 3) ^ swz128(row)) << 3) + (col & 7));
   };
 
   if (ks0 < ks1) {
-    stage(0);
-    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < kDwStages - 1; ++i) stage(i);
     for (int ks = ks0; ks < ks1; ++ks) {
-      const int buf = (ks - ks0) & 1;
-      if (ks + 1 < ks1) stage(buf ^ 1);
-      const bf16* D = smem + buf * IMG;
+      const int it = ks - ks0;
+      asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
+      stage((it + kDwStages - 1) % kDwStages);
+      const bf16* D = smem + (it % kDwStages) * IMG;
       const bf16* X = D + BK * BM;
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
+      for (int h = 0; h < BK / 32; ++h) {
         const int kr = 32 * h + 8 * g;
-        bf16x8 a[4], b[4];
+        bf16x4 al[4], ah[4], bl[4], bh[4];
 #pragma unroll
         for (int f = 0; f < 4; ++f) {
-          const bf16x4 lo = tr(D, kr, wm * 64 + f * 16), hi = tr(D, kr + 4, wm * 64 + f * 16);
-          a[f] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+          al[f] = tra(D, kr, wm * 64 + f * 16);
+          ah[f] = tra(D, kr + 4, wm * 64 + f * 16);
         }
 #pragma unroll
         for (int f = 0; f < 4; ++f) {
-          const bf16x4 lo = tr(X, kr, wn * 64 + f * 16), hi = tr(X, kr + 4, wn * 64 + f * 16);
-          b[f] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+          bl[f] = tra(X, kr, wn * 64 + f * 16);
+          bh[f] = tra(X, kr + 4, wn * 64 + f * 16);
+        }
+        lds_wait(al[0], al[1], al[2], al[3], ah[0], ah[1], ah[2], ah[3], bl[0], bl[1], bl[2], bl[3], bh[0], bh[1],
+                 bh[2], bh[3]);
+        bf16x8 a[4], b[4];
+#pragma unroll
+        for (int f = 0; f < 4; ++f) {
+          a[f] = __builtin_shufflevector(al[f], ah[f], 0, 1, 2, 3, 4, 5, 6, 7);
+          b[f] = __builtin_shufflevector(bl[f], bh[f], 0, 1, 2, 3, 4, 5, 6, 7);
         }
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
           for (int j = 0; j < 4; ++j) acc[i][j] = mma(acc[i][j], a[i], b[j]);
       }
-      __syncthreads();
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the DMAs issued past the split
   }
 
   if (p.direct) {
@@ -1060,32 +1082,56 @@ __global__ void __launch_bounds__(kBigT, 1) igemm_dwbig_kernel(IgemmDwParams p) 
   for (int e = 0; e < 8; ++e) ones[e] = (bf16)1.0f;
 
   // transposed fragment: 4 consecutive pixel rows of 16 columns per call
+  // transposed reads as inline asm (tr4_async): with the builtin the compiler
+  // put an s_waitcnt vmcnt(0) in front of every quarter's reads, draining the
+  // quarter pipeline's DMA lookahead (measured: the ISA showed vmcnt(4),
+  // s_barrier, vmcnt(0) per quarter)
   auto tr = [&](const bf16* img, int ncols, int kr, int col0) {
     const int row = kr + q;
     const int col = col0 + 4 * pp;
     const int sw = ncols == 128 ? swz128(row) : swz_tr64(row);
-    return tr4(img + row * ncols + (((col >> 3) ^ sw) << 3) + (col & 7));
+    return tr4_async(img + row * ncols + (((col >> 3) ^ sw) << 3) + (col & 7));
   };
   bf16x8 fa[FA][2], fb0[2][2], fb1[2][2];
   auto read_a = [&](const bf16* img, int h) {
+    bf16x4 lo[FA][2], hi[FA][2];
 #pragma unroll
     for (int f = 0; f < FA; ++f)
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
         const int kr = 32 * ks + 8 * g, c0 = wr * (CA / 2) + f * 16;
-        const bf16x4 lo = tr(img + h * QA, CA, kr, c0), hi = tr(img + h * QA, CA, kr + 4, c0);
-        fa[f][ks] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+        lo[f][ks] = tr(img + h * QA, CA, kr, c0);
+        hi[f][ks] = tr(img + h * QA, CA, kr + 4, c0);
+      }
+    lds_wait();
+#pragma unroll
+    for (int f = 0; f < FA; ++f)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        lds_pin(lo[f][ks]);
+        lds_pin(hi[f][ks]);
+        fa[f][ks] = __builtin_shufflevector(lo[f][ks], hi[f][ks], 0, 1, 2, 3, 4, 5, 6, 7);
       }
   };
   auto read_b = [&](const bf16* img, int h, bf16x8 (&fb)[2][2]) {
+    bf16x4 lo[2][2], hi[2][2];
 #pragma unroll
     for (int e = 0; e < 2; ++e)
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
         const int kr = 32 * ks + 8 * g, c0 = wc * 32 + e * 16;
         const bf16* base = img + 2 * QA + h * QB;
-        const bf16x4 lo = tr(base, CB, kr, c0), hi = tr(base, CB, kr + 4, c0);
-        fb[e][ks] = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+        lo[e][ks] = tr(base, CB, kr, c0);
+        hi[e][ks] = tr(base, CB, kr + 4, c0);
+      }
+    lds_wait();
+#pragma unroll
+    for (int e = 0; e < 2; ++e)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        lds_pin(lo[e][ks]);
+        lds_pin(hi[e][ks]);
+        fb[e][ks] = __builtin_shufflevector(lo[e][ks], hi[e][ks], 0, 1, 2, 3, 4, 5, 6, 7);
       }
   };
   auto mfma_q = [&](int ha, int hb, const bf16x8 (&fb)[2][2]) {
@@ -1283,8 +1329,9 @@ int igemm_dw_splitk(int M, int Cout, int kf, int tile) {
     return std::max(1, std::min(cap, 2048 / tiles));
   }
   const int tiles = cdiv(Cout, 128) * cdiv(kf + 1, 128);
-  int sk = std::max(1, 1024 / tiles);         // ~4 workgroups per CU in flight
-  sk = std::min(sk, std::max(1, nks / 4));    // >= 4 K-steps per slice
+  const int nks32 = cdiv(M, kDwBK);
+  int sk = std::max(1, 1024 / tiles);          // ~4 workgroups per CU in flight
+  sk = std::min(sk, std::max(1, nks32 / 8));   // >= 8 K-steps per slice (the ring is 4 deep)
   return std::min(sk, 1024);
 }
 
@@ -1304,15 +1351,16 @@ void igemm_dw(const IgemmDwParams& p0, float* gw, float* gb, float beta, hipStre
             "igemm_dw: bad permutation");
   p.div_ohw = magic(p.OH * p.OW);
   p.div_ow = magic(p.OW);
-  {  // +kIgBK output pixels as (ox, oy, b) increments with carries (igemm_dw_kernel)
-    const int q = kIgBK / p.OW;
-    p.adv_x = kIgBK % p.OW;
+  const int ba = dw_big_ba(p.Cout, p.kf, p.tile);
+  {  // +BK output pixels per K-step as (ox, oy, b) increments with carries
+    const int bk = ba ? kIgBK : kDwBK;
+    const int q = bk / p.OW;
+    p.adv_x = bk % p.OW;
     p.adv_y = q % p.OH;
     p.adv_b = q / p.OH;
   }
   p.gw = gw;
   p.gb = gb;
-  const int ba = dw_big_ba(p.Cout, p.kf, p.tile);
   if (ba) {
     MCC_CHECK(p.KS < 16, "igemm_dw: 256-column kernel packs ky, kx in 4 bits");
     p.direct = p.splitk == 1 && p.KS == 1 && p.perm_c == 0 && beta == 0.f;

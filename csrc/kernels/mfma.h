@@ -115,6 +115,28 @@ __device__ __forceinline__ bf16x4 tr4(const bf16* p) {
   return __builtin_bit_cast(bf16x4, __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(const_cast<bf16*>(p))));
 }
 
+// The same read as inline asm, for loops that keep LDS-DMA (global_load_lds)
+// prefetches in flight: the compiler cannot disambiguate the builtin's LDS
+// access from pending DMAs and puts an `s_waitcnt vmcnt(0)` in front of it,
+// which drains the whole lookahead every step.  The asm result is NOT
+// tracked: issue the reads, then lds_wait(...) before using them.
+__device__ __forceinline__ bf16x4 tr4_async(const bf16* p) {
+  v4s r;
+  const uint32_t a = (uint32_t)(uintptr_t)((const __attribute__((address_space(3))) bf16*)(p));
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(a));
+  return __builtin_bit_cast(bf16x4, r);
+}
+// wait for every outstanding LDS read and pin the given fragments after it
+template <typename F>
+__device__ __forceinline__ void lds_pin(F& f) { asm volatile("" : "+v"(f)); }
+__device__ __forceinline__ void lds_wait() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+template <typename F0, typename... F>
+__device__ __forceinline__ void lds_wait(F0& f0, F&... f) {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  lds_pin(f0);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  (lds_pin(f), ...);
+}
 
 }  // namespace gpu
 }  // namespace mcc
