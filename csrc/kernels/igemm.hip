@@ -50,8 +50,8 @@ constexpr int kIgT = 256;  // threads per workgroup
 constexpr int kIgBM = 128;
 constexpr int kIgBK = 64;
 // weight-gradient kernel (128 x 128 tiles): 32-pixel K-steps through a
-// 4-deep LDS ring (64 KB, two workgroups per CU)
-constexpr int kDwBK = 32, kDwStages = 4;
+// LDS ring (igemm_dw_kernel)
+constexpr int kDwBK = 32;
 
 // zero page (and a bf16 "1, 0 x 7" piece for the ones column), >= 16 bytes each
 __device__ __attribute__((aligned(64))) const unsigned short kIgZero[32] = {0};
@@ -706,21 +706,29 @@ __global__ void __launch_bounds__(kBigT, 1) igemm_big_kernel(IgemmParams p) {
 // ---------------------------------------------------------------------------
 // weight gradient (split-K over pixels)
 // ---------------------------------------------------------------------------
-// Pipeline: K-step ks lands in ring slot (ks - ks0) % 4 and is issued three
-// steps ahead; every step issues exactly 2J DMAs per thread (past the split:
-// harmless pieces into a slot nobody reads), so "stage ks landed" is the fixed
-// `s_waitcnt vmcnt(8)` (in-order retirement) followed by an explicit
-// s_barrier -- __syncthreads() would drain the lookahead.  The barrier also
-// retires the reads of the slot the next DMA overwrites (read one step ago).
-// (Round 3 ran 64-pixel steps double-buffered with a full drain per step:
-// one compute step of lookahead, latency-bound at ~2 TB/s on the reference
-// model's FC1 gradient, 286 us.)
+// Pipeline: K-step ks lands in ring slot (ks - ks0) % NST and is issued
+// NST - 1 steps ahead; every step issues exactly JD + JX DMAs per thread (past
+// the split: harmless pieces into a slot nobody reads), so "stage ks landed"
+// is a fixed `s_waitcnt vmcnt((NST - 2) * (JD + JX))` (in-order retirement)
+// followed by an explicit s_barrier -- __syncthreads() would drain the
+// lookahead.  The barrier also retires the reads of the slot the next DMA
+// overwrites (read one step ago).
+// BM = 128: 128 x 128 tiles, 4-deep ring (64 KB); BM = 256 (129..256 output
+// channels, e.g. the reference model's FC1: 200): one tile covers every
+// output channel, so the streamed X rows are not shared between co tiles and
+// each ring slot carries twice the unique HBM bytes (3-deep ring, 72 KB).
+// (Round 3 ran 64-pixel steps double-buffered with a full drain per step.)
+template <int BM, int NST>
 __global__ void __launch_bounds__(kIgT, 2) igemm_dw_kernel(IgemmDwParams p) {
-  constexpr int BM = 128, BN = 128, BK = kDwBK;  // co x k x pixels
-  constexpr int J = BK * 16 / kIgT;               // glds per thread per operand (2)
+  constexpr int BN = 128, BK = kDwBK;             // co x k x pixels
+  constexpr int JD = BK * BM / 8 / kIgT;          // dZ glds per thread per step
+  constexpr int JX = BK * BN / 8 / kIgT;          // X glds per thread per step
+  constexpr int SD = BM / 8;                      // 16-byte slots per dZ row
   constexpr int IMG = (BM + BN) * BK;
-  static_assert(2 * J * (kDwStages - 2) == 8, "the s_waitcnt below");
-  __shared__ __attribute__((aligned(16))) bf16 smem[kDwStages * IMG];
+  constexpr int VM = (NST - 2) * (JD + JX);
+  constexpr int FM = BM / 32;                     // co fragments per wave
+  static_assert(VM == 8 || VM == 6, "the s_waitcnt below");
+  __shared__ __attribute__((aligned(16))) bf16 smem[NST * IMG];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r16 = lane & 15, g = lane >> 4;
@@ -746,18 +754,25 @@ __global__ void __launch_bounds__(kIgT, 2) igemm_dw_kernel(IgemmDwParams p) {
   const bf16* ones = reinterpret_cast<const bf16*>(kIgOnes);
 
   // per-thread staging geometry: row (pixel within the K-step) and the
-  // logical 16-byte slot (8 output channels / 8 im2col columns).  The row's
-  // pixel (b, oy, ox) is decoded once and then advanced by BK pixels per
-  // K-step with carries (the K-steps of a split are staged in order), and
+  // logical 16-byte slot (8 output channels / 8 im2col columns).  The X
+  // row's pixel (b, oy, ox) is decoded once and then advanced by BK pixels
+  // per K-step with carries (the K-steps of a split are staged in order), and
   // every source is picked by selects: no per-step divisions, no branches.
-  int d_col[J], m_[J], b_[J], oy_[J], ox_[J];
-  int x_ky[J], x_kx[J], x_c[J], x_kind[J];  // kind: 0 tap, 1 ones, 2 zero
+  int d_col[JD], dm_[JD];
 #pragma unroll
-  for (int j = 0; j < J; ++j) {
+  for (int j = 0; j < JD; ++j) {
+    const int s = j * kIgT + tid;
+    const int row = s / SD;
+    d_col[j] = co0 + ((s % SD) ^ swz128(row)) * 8;
+    dm_[j] = ks0 * BK + row;
+  }
+  int m_[JX], b_[JX], oy_[JX], ox_[JX];
+  int x_ky[JX], x_kx[JX], x_c[JX], x_kind[JX];  // kind: 0 tap, 1 ones, 2 zero
+#pragma unroll
+  for (int j = 0; j < JX; ++j) {
     const int s = j * kIgT + tid;
     const int row = s >> 4;
     const int ls = (s & 15) ^ swz128(row);
-    d_col[j] = co0 + ls * 8;
     const int k = k0 + ls * 8;
     if (k < p.kf) {
       const int tap = k / p.C;
@@ -782,11 +797,16 @@ __global__ void __launch_bounds__(kIgT, 2) igemm_dw_kernel(IgemmDwParams p) {
     bf16* D = smem + buf * IMG;
     bf16* X = D + BK * BM;
 #pragma unroll
-    for (int j = 0; j < J; ++j) {
-      const bool mok = m_[j] < p.M;
-      const uint64_t dz_u = reinterpret_cast<uint64_t>(dz + (size_t)m_[j] * p.ldz + d_col[j]);
+    for (int j = 0; j < JD; ++j) {
+      const bool mok = dm_[j] < p.M;
+      const uint64_t dz_u = reinterpret_cast<uint64_t>(dz + (size_t)dm_[j] * p.ldz + d_col[j]);
       const bf16* dsrc = reinterpret_cast<const bf16*>((mok && d_col[j] < p.Cout) ? dz_u : zero_u);  // piece may span the pad
       glds16(dsrc, D + (j * kIgT + wave * 64) * 8);
+      dm_[j] += BK;
+    }
+#pragma unroll
+    for (int j = 0; j < JX; ++j) {
+      const bool mok = m_[j] < p.M;
       const int iy = oy_[j] * p.stride - p.pad + x_ky[j], ix = ox_[j] * p.stride - p.pad + x_kx[j];
       const bool tap_ok = mok && x_kind[j] == 0 && (unsigned)iy < (unsigned)p.H && (unsigned)ix < (unsigned)p.W;
       const int off = ((b_[j] * p.H + iy) * p.W + ix) * p.C + x_c[j];  // < 2^31 (host check); unused if !tap_ok
@@ -805,53 +825,60 @@ __global__ void __launch_bounds__(kIgT, 2) igemm_dw_kernel(IgemmDwParams p) {
     }
   };
 
-  f32x4 acc[4][4];
+  f32x4 acc[FM][4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < FM; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // transpose-read of a [BK][128] image: 4 consecutive K rows (pixels) of
+  // transpose-read of a [BK][ncols] image: 4 consecutive K rows (pixels) of
   // 16 columns; lane 4q+p of a 16-lane group addresses row kr+q, columns 4p..
-  auto tra = [&](const bf16* img, int kr, int col0) {  // (inline asm: see tr4_async)
+  auto tra = [&](const bf16* img, int ncols, int kr, int col0) {  // (inline asm: see tr4_async)
     const int row = kr + q;
     const int col = col0 + 4 * pp;
-    return tr4_async(img + row * 128 + (((col >> 3) ^ swz128(row)) << 3) + (col & 7));
+    return tr4_async(img + row * ncols + (((col >> 3) ^ swz128(row)) << 3) + (col & 7));
   };
 
   if (ks0 < ks1) {
 #pragma unroll
-    for (int i = 0; i < kDwStages - 1; ++i) stage(i);
+    for (int i = 0; i < NST - 1; ++i) stage(i);
     for (int ks = ks0; ks < ks1; ++ks) {
       const int it = ks - ks0;
-      asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
-      stage((it + kDwStages - 1) % kDwStages);
-      const bf16* D = smem + (it % kDwStages) * IMG;
+      if constexpr (VM == 8) asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(6)\n\ts_barrier" ::: "memory");
+      stage((it + NST - 1) % NST);
+      const bf16* D = smem + (it % NST) * IMG;
       const bf16* X = D + BK * BM;
 #pragma unroll
       for (int h = 0; h < BK / 32; ++h) {
         const int kr = 32 * h + 8 * g;
-        bf16x4 al[4], ah[4], bl[4], bh[4];
+        bf16x4 al[FM], ah[FM], bl[4], bh[4];
 #pragma unroll
-        for (int f = 0; f < 4; ++f) {
-          al[f] = tra(D, kr, wm * 64 + f * 16);
-          ah[f] = tra(D, kr + 4, wm * 64 + f * 16);
+        for (int f = 0; f < FM; ++f) {
+          al[f] = tra(D, BM, kr, wm * (BM / 2) + f * 16);
+          ah[f] = tra(D, BM, kr + 4, wm * (BM / 2) + f * 16);
         }
 #pragma unroll
         for (int f = 0; f < 4; ++f) {
-          bl[f] = tra(X, kr, wn * 64 + f * 16);
-          bh[f] = tra(X, kr + 4, wn * 64 + f * 16);
+          bl[f] = tra(X, BN, kr, wn * 64 + f * 16);
+          bh[f] = tra(X, BN, kr + 4, wn * 64 + f * 16);
         }
-        lds_wait(al[0], al[1], al[2], al[3], ah[0], ah[1], ah[2], ah[3], bl[0], bl[1], bl[2], bl[3], bh[0], bh[1],
-                 bh[2], bh[3]);
-        bf16x8 a[4], b[4];
+        lds_wait();
+        bf16x8 a[FM], b[4];
 #pragma unroll
-        for (int f = 0; f < 4; ++f) {
+        for (int f = 0; f < FM; ++f) {
+          lds_pin(al[f]);
+          lds_pin(ah[f]);
           a[f] = __builtin_shufflevector(al[f], ah[f], 0, 1, 2, 3, 4, 5, 6, 7);
+        }
+#pragma unroll
+        for (int f = 0; f < 4; ++f) {
+          lds_pin(bl[f]);
+          lds_pin(bh[f]);
           b[f] = __builtin_shufflevector(bl[f], bh[f], 0, 1, 2, 3, 4, 5, 6, 7);
         }
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+        for (int i = 0; i < FM; ++i)
 #pragma unroll
           for (int j = 0; j < 4; ++j) acc[i][j] = mma(acc[i][j], a[i], b[j]);
       }
@@ -865,13 +892,13 @@ __global__ void __launch_bounds__(kIgT, 2) igemm_dw_kernel(IgemmDwParams p) {
     // consecutive k of one row: 64-byte runs
     const int kreal = p.kreal > 0 ? p.kreal : p.kf;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < FM; ++i) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int k = k0 + wn * 64 + j * 16 + r16;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          const int co = co0 + wm * 64 + i * 16 + 4 * g + e;
+          const int co = co0 + wm * (BM / 2) + i * 16 + 4 * g + e;
           if (co >= p.Cout) continue;
           if (k < kreal) p.gw[(size_t)co * kreal + k] = acc[i][j][e];
           else if (k == p.kf) p.gb[co] = acc[i][j][e];
@@ -883,8 +910,8 @@ __global__ void __launch_bounds__(kIgT, 2) igemm_dw_kernel(IgemmDwParams p) {
   // slab[split][k][co]: lane holds co 4g..4g+3 of column k = r16
   float* slab = p.slab + (size_t)split * p.slab_stride;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int co = co0 + wm * 64 + i * 16 + 4 * g;
+  for (int i = 0; i < FM; ++i) {
+    const int co = co0 + wm * (BM / 2) + i * 16 + 4 * g;
     if (co >= p.Cout) continue;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -1313,6 +1340,10 @@ static int dw_big_ba(int Cout, int kf, int tile) {
   return (Cout % 256 == 0 && mode != 128) ? 256 : 128;
 }
 
+// co tile of the 128-column weight-gradient kernel: one tile for 129..256
+// output channels (see igemm_dw_kernel)
+static int dw_bm(int Cout) { return Cout > 128 ? 256 : 128; }
+
 int igemm_dw_splitk(int M, int Cout, int kf, int tile) {
   const int nks = cdiv(M, kIgBK);
   const int ba = dw_big_ba(Cout, kf, tile);
@@ -1328,7 +1359,7 @@ int igemm_dw_splitk(int M, int Cout, int kf, int tile) {
     }
     return std::max(1, std::min(cap, 2048 / tiles));
   }
-  const int tiles = cdiv(Cout, 128) * cdiv(kf + 1, 128);
+  const int tiles = cdiv(Cout, dw_bm(Cout)) * cdiv(kf + 1, 128);
   const int nks32 = cdiv(M, kDwBK);
   int sk = std::max(1, 1024 / tiles);          // ~4 workgroups per CU in flight
   sk = std::min(sk, std::max(1, nks32 / 8));   // >= 8 K-steps per slice (the ring is 4 deep)
@@ -1369,9 +1400,11 @@ void igemm_dw(const IgemmDwParams& p0, float* gw, float* gb, float beta, hipStre
     else hipLaunchKernelGGL((igemm_dwbig_kernel<128>), dim3((unsigned)nwg), dim3(kBigT), 0, s, p);
     if (p.direct) return;
   } else {
-    const int nwg = cdiv(p.Cout, 128) * cdiv(p.kf + 1, 128) * p.splitk;
+    const int bm = dw_bm(p.Cout);
+    const int nwg = cdiv(p.Cout, bm) * cdiv(p.kf + 1, 128) * p.splitk;
     p.direct = p.splitk == 1 && p.KS == 1 && p.perm_c == 0 && beta == 0.f;
-    hipLaunchKernelGGL(igemm_dw_kernel, dim3((unsigned)nwg), dim3(kIgT), 0, s, p);
+    if (bm == 256) hipLaunchKernelGGL((igemm_dw_kernel<256, 3>), dim3((unsigned)nwg), dim3(kIgT), 0, s, p);
+    else hipLaunchKernelGGL((igemm_dw_kernel<128, 4>), dim3((unsigned)nwg), dim3(kIgT), 0, s, p);
     if (p.direct) return;
   }
   const int64_t total4 = (int64_t)(p.kf + 1) * p.Cout / 4;  // Cout % 8 == 0

@@ -24,6 +24,8 @@ CASES = [
     (3, 16, 16, 32, 64, 3, 1, 1),    # C = 32: a K-step spans two taps, K = 288 (tail K-step half zero)
     (2, 14, 14, 32, 48, 5, 1, 2),    # C = 32, 5x5: K = 800
     (2, 12, 10, 96, 40, 3, 1, 1),    # C = 96: channel wrap at c0 = 64
+    (4, 8, 8, 96, 200, 1, 1, 0),     # 129..256 output channels: the 256-channel dW tile (ref FC1 shape class)
+    (3, 7, 7, 32, 160, 3, 1, 1),     # ... with taps
 ]
 
 
