@@ -1361,7 +1361,9 @@ int igemm_dw_splitk(int M, int Cout, int kf, int tile) {
   }
   const int tiles = cdiv(Cout, dw_bm(Cout)) * cdiv(kf + 1, 128);
   const int nks32 = cdiv(M, kDwBK);
-  int sk = std::max(1, 1024 / tiles);          // ~4 workgroups per CU in flight
+  // BM = 128: ~4 workgroups per CU over the launch; BM = 256 (twice the work
+  // per K-step): one round of two per CU -- fewer slabs to write and reduce
+  int sk = std::max(1, (dw_bm(Cout) == 256 ? 512 : 1024) / tiles);
   sk = std::min(sk, std::max(1, nks32 / 8));   // >= 8 K-steps per slice (the ring is 4 deep)
   return std::min(sk, 1024);
 }
