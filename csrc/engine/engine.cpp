@@ -1465,6 +1465,10 @@ const void* GpuNet::stage_output(int stage, int64_t& per_sample, const uint8_t**
   // recomputed in the backward); its buffer is not the standard NCHW output.
   MCC_CHECK(!((lenet_ || refblk_) && stage == 0),
             "stage_output: stage 0 is internal to the fused conv block (no standard-layout output)");
+  // the fused LeNet classifier chain keeps FC1 / FC2 activations in LDS when
+  // it ran forward + backward in one kernel (loss() of a training step)
+  MCC_CHECK(!(fcchain_ && fc_bwd_done_ && (stage == 2 || stage == 3)),
+            "stage_output: FC activations of the fused classifier chain were not written (training step)");
   per_sample = st.out_elems;
   if (argmax) *argmax = st.pooled ? st.arg_buf : nullptr;
   return st.act_buf;
