@@ -150,7 +150,15 @@ NP    ?= 2
 SYN   ?= 20000
 DATA  ?= --synthetic $(SYN)
 RUNFLAGS ?=
-.PHONY: run_serial run_mpi run_hip run_dist run_bench
+.PHONY: run_serial run_mpi run_hip run_dist run_bench data
+# the four IDX files under data/ (the reference's get_mnist, Makefile:12-35,
+# without network): MNIST_SRC=DIR takes local MNIST files (raw or .gz), else
+# the synthetic MNIST-shaped set; then e.g. make run_serial DATA="$$(cat data/files)"
+data:
+	@mkdir -p data
+	$(PYTHON) tools/get_mnist.py --out data $(if $(MNIST_SRC),--src $(MNIST_SRC),--synthetic $(SYN)) > data/files.tmp
+	mv data/files.tmp data/files
+	@cat data/files
 run_serial: build/bin/cnn
 	build/bin/cnn $(DATA) $(RUNFLAGS)
 run_mpi: build/bin/cnnmpi

@@ -181,3 +181,39 @@ def test_bench_refuses_world_mismatch():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "1"],
                        capture_output=True, text=True, timeout=120, env=env)
     assert r.returncode != 0 and "WORLD_SIZE=3" in r.stderr, r.stderr
+
+
+def test_get_mnist_local_and_synthetic(cnn_bin, tmp_path):
+    """tools/get_mnist.py (the reference's get_mnist rule, Makefile:12-35,
+    offline): local MNIST files in the dotted / gzipped spellings are checked
+    and normalised; without a source the synthetic set is written; `cnn`
+    trains on the result."""
+    import gzip
+
+    tool = os.path.join(ROOT, "tools", "get_mnist.py")
+    syn = tmp_path / "syn"
+    r = subprocess.run([sys.executable, tool, "--out", str(syn), "--synthetic", "500"], capture_output=True, text=True,
+                       timeout=120)
+    assert r.returncode == 0, r.stderr
+    paths = r.stdout.split()
+    assert [os.path.basename(p) for p in paths] == ["train-images-idx3-ubyte", "train-labels-idx1-ubyte",
+                                                    "t10k-images-idx3-ubyte", "t10k-labels-idx1-ubyte"]
+    src = tmp_path / "src"
+    src.mkdir()
+    for p in paths:  # as distributed: dotted names, gzipped
+        with open(p, "rb") as fi, gzip.open(src / (os.path.basename(p).replace("-idx", ".idx") + ".gz"), "wb") as fo:
+            fo.write(fi.read())
+    out = tmp_path / "out"
+    r2 = subprocess.run([sys.executable, tool, "--src", str(src), "--out", str(out)], capture_output=True, text=True,
+                        timeout=120)
+    assert r2.returncode == 0, r2.stderr
+    for a, b in zip(paths, r2.stdout.split()):
+        assert open(a, "rb").read() == open(b, "rb").read()
+    bad = tmp_path / "bad"
+    bad.mkdir()
+    for p in paths:
+        (bad / os.path.basename(p)).write_bytes(b"\x01\x02\x03\x04")
+    assert subprocess.run([sys.executable, tool, "--src", str(bad), "--out", str(tmp_path / "o2")],
+                          capture_output=True).returncode != 0
+    r3 = subprocess.run([cnn_bin] + r2.stdout.split() + ["--epochs", "1"], capture_output=True, text=True, timeout=300)
+    assert r3.returncode == 0 and r3.stderr.strip().splitlines()[-1].startswith("ntests=100, ")
