@@ -18,6 +18,7 @@ from ._C import (  # noqa: F401
     ModelSpec,
     CpuNet32,
     CpuNet64,
+    GpuNet64,
     GpuNet,
     MccError,
     init_params,
@@ -37,6 +38,7 @@ __all__ = [
     "ModelSpec",
     "CpuNet32",
     "CpuNet64",
+    "GpuNet64",
     "GpuNet",
     "MccError",
     "init_params",
