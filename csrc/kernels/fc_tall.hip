@@ -43,26 +43,26 @@ typedef __attribute__((address_space(3))) void lvoid;
 
 constexpr int kTT = 512;                 // threads (8 waves)
 constexpr int kTM = 128;                 // batch rows per tile
-constexpr int kTNS = 3;                  // ring depth: 2 stages in flight
+constexpr int kTNS = 3;                  // ring depth: 2 stages in flight (bf16 forward: 4, see fc_tall)
 constexpr int kTXBytes = kTM * 64;
 // NF fragments per wave column: tile width TN = 32 NF output columns (7: 224
 // for the ref model's FC1; 4: 128 for LeNet-5's FC1 120), W rows staged per
 // stage rounded up to 128 (one DMA round of the 8 waves), LDS per workgroup
-template <int NF> struct TallGeom {
+template <int NF, int NS = kTNS> struct TallGeom {
   static constexpr int TN = 32 * NF;
   static constexpr int WR = (TN + 127) / 128 * 128;
   static constexpr int DMAS = 1 + WR / 128;  // per wave per stage
   static constexpr int STAGE = kTXBytes + WR * 64;
-  static constexpr int LDS = kTNS * STAGE;   // 73,728 B (NF 7) / 49,152 B (NF 4)
+  static constexpr int LDS = NS * STAGE;     // 3 stages: 73,728 B (NF 7) / 49,152 B (NF 4)
 };
 
 __device__ __attribute__((aligned(64))) const unsigned short kTallZero[32] = {0};
 
 __device__ __forceinline__ int tswz(int row) { return (row >> 2) & 3; }
 
-template <typename T, int NF, int ACT, bool BIAS>
-__global__ void __launch_bounds__(kTT, 2) fc_tall_kernel(FcTallParams p) {
-  using Gm = TallGeom<NF>;
+template <typename T, int NF, int ACT, bool BIAS, int NS>
+__global__ void __launch_bounds__(kTT, NS == 3 ? 2 : 1) fc_tall_kernel(FcTallParams p) {
+  using Gm = TallGeom<NF, NS>;
   constexpr int kTN = Gm::TN, DM = Gm::DMAS;
   constexpr int EPR = 64 / (int)sizeof(T);  // elements per 64-byte row = K per stage
   constexpr int EPS = 16 / (int)sizeof(T);  // elements per 16-byte segment
@@ -100,7 +100,7 @@ __global__ void __launch_bounds__(kTT, 2) fc_tall_kernel(FcTallParams p) {
   }
   const int nk = (p.K + EPR - 1) / EPR;
   auto stage = [&](int kt) {  // always DM DMAs (past K: the zero page)
-    char* dst = tsm + (kt % kTNS) * Gm::STAGE;
+    char* dst = tsm + (kt % NS) * Gm::STAGE;
     const int k0 = kt * EPR;
 #pragma unroll
     for (int i = 0; i < DM; ++i) {
@@ -116,17 +116,20 @@ __global__ void __launch_bounds__(kTT, 2) fc_tall_kernel(FcTallParams p) {
   const int xrow0 = 32 * wm + r16;          // batch fragment b: A row xrow0 + 16 b
   const int wrow0 = 16 * NF * wn + r16;     // weight fragment f: W row wrow0 + 16 f
 
-  stage(0);
-  stage(1);
+#pragma unroll
+  for (int i = 0; i < NS - 1; ++i) stage(i);
   for (int kt = 0; kt < nk; ++kt) {
-    // one stage (DM DMAs) was issued after stage kt: vmcnt(DM) = stage kt
-    // landed (in-order retirement); the barrier (an explicit s_barrier:
-    // __syncthreads() would drain vmcnt) makes every wave's pieces visible
-    // and frees the slot read in iteration kt - 1
-    if constexpr (DM == 3) asm volatile("s_waitcnt vmcnt(3)\n\ts_barrier" ::: "memory");
+    // NS - 2 stages (DM DMAs each) were issued after stage kt: vmcnt((NS-2)
+    // DM) = stage kt landed (in-order retirement); the barrier (an explicit
+    // s_barrier: __syncthreads() would drain vmcnt) makes every wave's pieces
+    // visible and frees the slot read in iteration kt - 1
+    constexpr int VM = (NS - 2) * DM;
+    static_assert(VM == 2 || VM == 3 || VM == 6, "the s_waitcnt below");
+    if constexpr (VM == 6) asm volatile("s_waitcnt vmcnt(6)\n\ts_barrier" ::: "memory");
+    else if constexpr (VM == 3) asm volatile("s_waitcnt vmcnt(3)\n\ts_barrier" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(2)\n\ts_barrier" ::: "memory");
-    stage(kt + 2);
-    const char* xb_ = tsm + (kt % kTNS) * Gm::STAGE;
+    stage(kt + NS - 1);
+    const char* xb_ = tsm + (kt % NS) * Gm::STAGE;
     const char* wb_ = xb_ + kTXBytes;
     V xb[2], wf[NF];
 #pragma unroll
@@ -208,16 +211,31 @@ void fc_tall(const FcTallParams& p, hipStream_t s) {
   MCC_CHECK(p.act == ACT_NONE || p.bias, "fc_tall: an activation needs the forward (bias) epilogue");
   // narrow layers (N <= 128, e.g. LeNet-5 FC1 120) on 128-column tiles, the
   // rest on 224-column tiles
+  // The bf16 forward of the wide (224-column) tiles runs a 4-deep ring at one
+  // workgroup per CU (three stages in flight: ref FC1 forward 240 -> 224 us,
+  // profiles/fc_tall_ab_r4.txt v1); the data gradients and fp32 keep 3 deep
+  // at two per CU (v1 lost there: 290 -> 348 us bf16 dX, 986 -> 1010 fp32).
   auto go = [&](auto t, auto nf) {
     using T = decltype(t);
     constexpr int NF = decltype(nf)::value;
     using Gm = TallGeom<NF>;
+    using G4 = TallGeom<NF, 4>;
+    constexpr bool kDeep = sizeof(T) == 2 && NF == 7;
     const int tiles = ((p.M + kTM - 1) / kTM) * ((p.N + Gm::TN - 1) / Gm::TN);
     const dim3 grid((unsigned)tiles), block(kTT);
-    if (!p.bias) hipLaunchKernelGGL((fc_tall_kernel<T, NF, ACT_NONE, false>), grid, block, Gm::LDS, s, p);
-    else if (p.act == ACT_TANH) hipLaunchKernelGGL((fc_tall_kernel<T, NF, ACT_TANH, true>), grid, block, Gm::LDS, s, p);
-    else if (p.act == ACT_RELU) hipLaunchKernelGGL((fc_tall_kernel<T, NF, ACT_RELU, true>), grid, block, Gm::LDS, s, p);
-    else hipLaunchKernelGGL((fc_tall_kernel<T, NF, ACT_NONE, true>), grid, block, Gm::LDS, s, p);
+    if (!p.bias) {
+      hipLaunchKernelGGL((fc_tall_kernel<T, NF, ACT_NONE, false, 3>), grid, block, Gm::LDS, s, p);
+      return;
+    }
+    if constexpr (kDeep) {
+      if (p.act == ACT_TANH) hipLaunchKernelGGL((fc_tall_kernel<T, NF, ACT_TANH, true, 4>), grid, block, G4::LDS, s, p);
+      else if (p.act == ACT_RELU) hipLaunchKernelGGL((fc_tall_kernel<T, NF, ACT_RELU, true, 4>), grid, block, G4::LDS, s, p);
+      else hipLaunchKernelGGL((fc_tall_kernel<T, NF, ACT_NONE, true, 4>), grid, block, G4::LDS, s, p);
+      return;
+    }
+    if (p.act == ACT_TANH) hipLaunchKernelGGL((fc_tall_kernel<T, NF, ACT_TANH, true, 3>), grid, block, Gm::LDS, s, p);
+    else if (p.act == ACT_RELU) hipLaunchKernelGGL((fc_tall_kernel<T, NF, ACT_RELU, true, 3>), grid, block, Gm::LDS, s, p);
+    else hipLaunchKernelGGL((fc_tall_kernel<T, NF, ACT_NONE, true, 3>), grid, block, Gm::LDS, s, p);
   };
   const bool narrow = p.N <= 128;
   using N4 = std::integral_constant<int, 4>;
