@@ -20,7 +20,9 @@
 // two workgroups per CU, whose load / multiply phases interleave (a
 // persistent one-workgroup-per-CU variant with a 6-deep ring and deferred
 // epilogues measured 36 % slower: at 256 workgroups a CU still busy with the
-// previous kernel's tail delays its whole share).  Rows are 64 B with the
+// previous kernel's tail delays its whole share).  The bf16 forward of the
+// 224-column tiles is the exception: a 4-deep ring at one workgroup per CU
+// (98 KB, three stages in flight) reads the streamed rows 12 % faster.  Rows are 64 B with the
 // 16-byte segment XOR-swizzled by row bits 2..3: every 16-lane
 // ds_read_b128 phase covers all 64 banks once.  Batch rows past M (clamped)
 // and weight rows past N (the zero page) cost no branch.
