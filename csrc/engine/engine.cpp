@@ -102,10 +102,15 @@ static inline int r16(int x) { return (x + 15) & ~15; }
 static inline int r32(int x) { return (x + 31) & ~31; }
 // Split-K factor for a weight-gradient GEMM [M x N] reduced over K rows:
 // aim for ~512 workgroups of 64x64 tiles, each slice >= 128 rows.
-static inline int dw_splitk(int M, int N, int64_t K) {
+static inline int dw_splitk(int M, int N, int64_t K, int target = 512) {
   const int64_t tiles = ceil_div(M, 64) * ceil_div(N, 64);
-  int64_t sk = std::max<int64_t>(1, std::min<int64_t>(512 / std::max<int64_t>(1, tiles), K / 64));
+  int64_t sk = std::max<int64_t>(1, std::min<int64_t>(target / std::max<int64_t>(1, tiles), K / 64));
   return (int)std::min<int64_t>(sk, 256);
+}
+// FC weight gradients on the generic GEMM: fp32 aims at ~5 workgroups per CU
+// (its one-chunk register prefetch leaves each workgroup latency-bound)
+static inline int fc_dw_splitk(int M, int N, int64_t K, DType t) {
+  return dw_splitk(M, N, K, t == DType::F32 ? 1280 : 512);
 }
 
 static inline int act_kind(Act a) {
@@ -669,7 +674,7 @@ void GpuNet::build() {
     } else if (st.fc_igdw) {
       scratch = std::max(scratch, gpu::igemm_dw_slab_bytes(st.Nout, st.in_ld, gpu::igemm_dw_splitk(Bm, st.Nout, st.in_ld)));
     } else {
-      scratch = std::max(scratch, (size_t)dw_splitk(st.Nout, st.Kin + 1, Bm) * st.Nout * st.ldp * 4);
+      scratch = std::max(scratch, (size_t)fc_dw_splitk(st.Nout, st.Kin + 1, Bm, dtype_) * st.Nout * st.ldp * 4);
     }
   }
   for (Stage* sp : stages_) {
@@ -1368,7 +1373,7 @@ void GpuNet::backward(int hi, int lo, hipStream_t s) {
       w.A = st.grad_buf; w.lda = st.out_ld; w.ta = true;
       w.B = pv.act_buf; w.ldb = st.in_ld; w.tb = true; w.ones_col = st.Kin;
       w.epi = gpu::EPI_PARTIAL; w.Cf = scratch_; w.ldc = st.ldp;
-      const int sk = dw_splitk(st.Nout, st.Kin + 1, B);
+      const int sk = fc_dw_splitk(st.Nout, st.Kin + 1, B, dtype_);
       w.splitk = sk;
       w.partial_stride = (int64_t)st.Nout * st.ldp;
       gpu::gemm(dtype_, w, ws);
