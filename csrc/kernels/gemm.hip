@@ -42,14 +42,20 @@ __device__ __forceinline__ float ld_elem(const T* base, int ld, bool trans, int 
 }
 
 // One operand tile (ROWS x 32) moving global -> registers -> LDS.
-// Layout in LDS: !TRANS or !TR: [ROWS][LDK] (k contiguous);
-//                TRANS && TR:   [32][ROWS + 8] (rows of k, read by ds_read_b64_tr_b16).
+// Layout in LDS: !TRANS:        [ROWS][LDK] (k contiguous);
+//                TRANS && TR:   [32][ROWS + 8] (rows of k, read by ds_read_b64_tr_b16);
+//                TRANS && !TR (fp32): [32][ROWS + 4] (rows of k as they sit in
+//                  memory, 16-byte stores; a fragment is 8 ds_read_b32 down a
+//                  column -- the f32 MFMA takes one k per lane per instruction,
+//                  so nothing needs transposing.  Until round 4 these tiles
+//                  were transposed by 8 scalar LDS stores per vector, 4-way
+//                  bank-conflicted: ref fp32 FC1 weight gradient 2.1 ms.)
 template <typename T, int ROWS, bool TRANS, bool TR>
 struct Operand {
   typedef typename Vec8<T>::type V8;
   static constexpr int LDK = 32 + (sizeof(T) == 2 ? 8 : 4);
-  static constexpr int LDM = ROWS + 8;
-  static constexpr int ELEMS = (TRANS && TR) ? 32 * LDM : ROWS * LDK;
+  static constexpr int LDM = ROWS + (TR ? 8 : 4);
+  static constexpr int ELEMS = TRANS ? 32 * LDM : ROWS * LDK;
   static constexpr int NVEC = ROWS * 4;  // 8-element vectors per tile
   static constexpr int PER = (NVEC + 255) / 256;
   V8 r[PER];
@@ -94,12 +100,7 @@ struct Operand {
       } else {
         constexpr int RV = ROWS / 8;
         const int kr = v / RV, rv = (v - kr * RV) * 8;
-        if (TR) {
-          store8(lds + kr * LDM + rv, r[j]);
-        } else {
-#pragma unroll
-          for (int e = 0; e < 8; ++e) lds[(rv + e) * LDK + kr] = r[j][e];
-        }
+        store8(lds + kr * LDM + rv, r[j]);
       }
     }
   }
@@ -114,6 +115,11 @@ struct Operand {
       const bf16x4 lo = __builtin_bit_cast(bf16x4, ds_tr16(b + (8 * g + q) * LDM + row0 + 4 * pp));
       const bf16x4 hi = __builtin_bit_cast(bf16x4, ds_tr16(b + (8 * g + 4 + q) * LDM + row0 + 4 * pp));
       return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    } else if constexpr (TRANS) {
+      V8 v;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = lds[(8 * g + e) * LDM + row0 + r16];
+      return v;
     } else {
       return load8(lds + (row0 + r16) * LDK + 8 * g);
     }
