@@ -382,9 +382,11 @@ void GpuNet::build() {
     }
     // fp32 tall-skinny FC (ref FC1 1568 -> 200, LeNet-5 FC1 400 -> 120 at a
     // large batch): exact f32 MFMA, same tiles
+    // (also the narrow FC2s: LeNet-5 120 -> 84 writes 84 of its 88-column
+    // rows, as the generic GEMM did; ref 200 -> 200)
     if (st.kind == Stage::FC && dtype_ == DType::F32 && !st.last && !st.fc_big && max_batch_ >= 8192 && s > 0 &&
-        st.Nout <= 224 && st.Kin >= 256 && st.Kin % 8 == 0 && st.in_ld == st.Kin && st.out_ld == st.Nout &&
-        gpu::fc_tall_supported(max_batch_, st.Nout, st.Kin)) {
+        st.Nout <= 224 && st.Kin >= 64 && st.Kin % 8 == 0 && st.in_ld == st.Kin && st.out_ld >= st.Nout &&
+        st.out_ld % 4 == 0 && gpu::fc_tall_supported(max_batch_, st.Nout, st.Kin)) {
       const Stage* pv = stages_[s - 1];
       st.fc_tall = true;
       st.fc_tall_dx = (pv->kind == Stage::CONV || pv->act == gpu::ACT_NONE) &&
