@@ -154,6 +154,28 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmParams p) {
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  // EPI_DACT: the act' operand (4 outputs per fragment per lane) is requested
+  // before the K loop, so its latency hides behind the GEMM instead of
+  // stalling the epilogue (short-K data gradients: K = 10..120 is 1-4 chunks)
+  constexpr bool kPreAux = FM * FN <= 4;
+  float auxv[kPreAux ? FM : 1][kPreAux ? FN : 1][4];
+  if constexpr (kPreAux) {
+    if (p.epi == EPI_DACT && p.act != ACT_NONE) {
+      const T* aux = static_cast<const T*>(p.aux);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          const int col = n0 + wn * WTN + j * 16 + r16;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int row = m0 + wm * WTM + i * 16 + 4 * g + e;
+            auxv[i][j][e] = (col < p.N && row < p.M) ? to_f(aux[(size_t)row * p.ldaux + col]) : 0.f;
+          }
+        }
+    }
+  }
+
   OpA la;
   OpB lb;
   if (kc0 < kc1) {
@@ -210,7 +232,12 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmParams p) {
             break;
           case EPI_DACT: {
             float d = 1.f;
-            if (p.act != ACT_NONE) d = act_grad_y(p.act, to_f(aux[(size_t)row * p.ldaux + col]));
+            if (p.act != ACT_NONE) {
+              float y;
+              if constexpr (kPreAux) y = auxv[i][j][e];
+              else y = to_f(aux[(size_t)row * p.ldaux + col]);
+              d = act_grad_y(p.act, y);
+            }
             C[(size_t)row * p.ldc + col] = from_f<T>(v * d);
             break;
           }
