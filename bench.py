@@ -11,6 +11,11 @@ does the full work: device-side sampling, forward, softmax-CE, backward, the
 bucketed gradient all-reduce and the SGD update.  The timed region is K
 steps bracketed by barrier + device synchronize on both sides; the reported
 time is the max over ranks.
+
+At N = 1 the same run also times LeNet-5 in fp32 (BASELINE.json config 2,
+"LeNet-5 fp32 on one MI355X") as a second region with the same K / W and
+reports it under "fp32" in the one JSON line.  The optimizer defaults to the
+reference's plain SGD at lr 0.1 (cnn.c:303-314, 446).
 """
 
 import argparse
@@ -54,6 +59,109 @@ def metric_for(model):
     return METRIC if model == "lenet5" else f"images/sec (whole node), {model}, at 1/2/4/8 MI355X"
 
 
+def timed_run(args, spec, dtype, B, d_img, d_lab, dev, dev_idx, rank, world, multi):
+    """Build a trainer, warm up, time exactly args.steps steps between
+    barrier + device synchronize on both sides (max over ranks), free it."""
+    import torch
+    import torch.distributed as dist
+
+    import mpi_cuda_cnn_amd as mcc
+    from mpi_cuda_cnn_amd.trainer import GpuTrainer
+
+    tr = GpuTrainer(
+        spec,
+        dtype=dtype,
+        batch=B,
+        device=dev_idx,
+        seed=0,
+        lr=args.lr,
+        momentum=args.momentum,
+        init="fast",
+        bucket_bytes=int(args.bucket_mb * (1 << 20)),
+        force_reduce=args.force_reduce,
+    )
+    # device minibatch sampler (rand() % N semantics, cnn.c:455): indices and
+    # its step counter live on the GPU, so a graph replay draws a fresh batch
+    K = mcc._C.kernels
+    idx_buf = torch.empty(B, dtype=torch.int32, device=dev)
+    counter = torch.zeros(1, dtype=torch.int64, device=dev)
+    seed = 0x5EED0000 + rank
+
+    def step_launch():
+        s = torch.cuda.current_stream(dev).cuda_stream
+        K.sample_indices(idx_buf.data_ptr(), B, 0, args.dataset, seed, counter.data_ptr(), s)
+        tr.step(d_img, d_lab, idx_buf)
+        K.advance_counter(counter.data_ptr(), s)
+
+    # host-side rank agreement (capture consensus, the barriers around the
+    # timed loop, the MAX of the per-rank times) only where there are ranks
+    # to agree with: at world 1 a barrier / MAX is the identity, and no eager
+    # collective then follows the graph capture (see ddp.init_process_group)
+    step = step_launch
+    graph_note = "per-kernel launches" + (" (--graph off)" if args.graph == "off" else "")
+    coll_graph = None
+    g = None
+    tr.zero_stats()
+    step_launch()  # eager first: code objects loaded, RCCL communicator warmed up
+    torch.cuda.synchronize()
+    if args.graph == "on" or (args.graph == "auto" and world == 1):
+        from mpi_cuda_cnn_amd.trainer import capture_step
+
+        issued_before = tr.sync.issued
+        g, why = capture_step(step_launch)
+        ok = torch.tensor([1 if g is not None else 0], device=dev, dtype=torch.int32)
+        if multi:  # every rank replays or none does (collectives inside)
+            dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        if int(ok.item()) == 1:
+            coll_graph = tr.sync.issued - issued_before
+            step = g.replay
+            graph_note = "hip graph: whole step captured once (torch.cuda.CUDAGraph), replayed per step"
+        else:
+            if args.graph == "on":
+                raise RuntimeError(f"--graph on: capture failed: {why}")
+            graph_note = f"off (capture failed: {why})"
+    for _ in range(max(0, args.warmup - 1)):
+        step()
+    torch.cuda.synchronize()
+    if multi:
+        dist.barrier()
+    torch.cuda.synchronize()
+    tr.zero_stats()
+    issued0 = tr.sync.issued
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if multi:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    coll_per_step = (tr.sync.issued - issued0) / max(1, args.steps) if coll_graph is None else coll_graph
+    if multi:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    st = tr.net.get_stats()
+    nb = len(tr.sync.buckets)
+    res = {
+        "elapsed": elapsed,
+        "loss": round(st["loss_sum"] / (B * args.steps), 4),
+        "launch": graph_note,
+        "optimizer": ("sgd lr={} (plain SGD, the reference's Layer_update, cnn.c:303-314)".format(args.lr)
+                      if args.momentum == 0 else f"sgd lr={args.lr} momentum={args.momentum}"),
+        "allreduce": (f"{'rccl' if args.dist_backend == 'nccl' else 'gloo (rehearsal)'}: {coll_per_step:g} "
+                      f"all-reduce(s)/step over {nb} bucket(s) <= {args.bucket_mb} MiB, async on RCCL's stream, "
+                      "joined before SGD"
+                      + ("; at one rank RCCL elides the in-place SUM: no reduction kernel runs"
+                         " (--force-reduce runs one)" if tr.sync.elided else "")
+                      + ("; forced one-rank reduction kernel (AVG)" if args.force_reduce and world == 1 else "")
+                      if coll_per_step else "none (--no-dist)"),
+    }
+    del step, g, tr
+    torch.cuda.synchronize()
+    return res
+
+
 def _self_launch(n: int) -> int:
     """Run this script under torch.distributed.run with n ranks on this node
     (rendezvous on 127.0.0.1, a free port) as a child process; rank 0's JSON
@@ -81,8 +189,12 @@ def main():
     ap.add_argument("--dataset", type=int, default=0,
                     help="synthetic samples resident per GPU (default 65536; 8 batches for large images)")
     ap.add_argument("--bucket-mb", type=float, default=4.0)
-    ap.add_argument("--lr", type=float, default=0.05)
-    ap.add_argument("--momentum", type=float, default=0.9)
+    # the reference's optimizer: plain SGD at lr 0.1 (cnn.c:303-314,446)
+    ap.add_argument("--lr", type=float, default=0.1)
+    ap.add_argument("--momentum", type=float, default=0.0)
+    ap.add_argument("--fp32-extra", choices=["auto", "on", "off"], default="auto",
+                    help="also time LeNet-5 fp32 (BASELINE config 2) in the same run and report it under "
+                         "\"fp32\" in the JSON line; auto = on at N=1 for a bf16 LeNet-5 run")
     ap.add_argument("--no-dist", action="store_true",
                     help="N=1 only: no process group, no collectives (A/B against the RCCL path)")
     ap.add_argument("--graph", choices=["auto", "on", "off"], default="auto",
@@ -135,7 +247,6 @@ def main():
         init_process_group(args.dist_backend, dev)
 
     import mpi_cuda_cnn_amd as mcc
-    from mpi_cuda_cnn_amd.trainer import GpuTrainer
 
     spec = mcc.make_model(args.model)
     C, H, W = spec.input_shape()
@@ -148,83 +259,18 @@ def main():
     imgs, labels = mcc.synth_dataset(args.dataset, C, H, W, spec.num_classes(), seed=1234 + rank)
     d_img = torch.from_numpy(imgs).to(dev)
     d_lab = torch.from_numpy(labels).to(dev)
-    tr = GpuTrainer(
-        spec,
-        dtype=args.dtype,
-        batch=B,
-        device=dev_idx,
-        seed=0,
-        lr=args.lr,
-        momentum=args.momentum,
-        init="fast",
-        bucket_bytes=int(args.bucket_mb * (1 << 20)),
-        force_reduce=args.force_reduce,
-    )
-    # device minibatch sampler (rand() % N semantics, cnn.c:455): indices and
-    # its step counter live on the GPU, so a graph replay draws a fresh batch
-    K = mcc._C.kernels
-    idx_buf = torch.empty(B, dtype=torch.int32, device=dev)
-    counter = torch.zeros(1, dtype=torch.int64, device=dev)
-    seed = 0x5EED0000 + rank
-
-    def step_launch():
-        s = torch.cuda.current_stream(dev).cuda_stream
-        K.sample_indices(idx_buf.data_ptr(), B, 0, args.dataset, seed, counter.data_ptr(), s)
-        tr.step(d_img, d_lab, idx_buf)
-        K.advance_counter(counter.data_ptr(), s)
-
-    # host-side rank agreement (capture consensus, the barriers around the
-    # timed loop, the MAX of the per-rank times) only where there are ranks
-    # to agree with: at world 1 a barrier / MAX is the identity, and no eager
-    # collective then follows the graph capture (see ddp.init_process_group)
     multi = dist.is_initialized() and world > 1
-    step = step_launch
-    graph_note = "per-kernel launches" + (" (--graph off)" if args.graph == "off" else "")
-    coll_graph = None
-    tr.zero_stats()
-    step_launch()  # eager first: code objects loaded, RCCL communicator warmed up
-    torch.cuda.synchronize()
-    if args.graph == "on" or (args.graph == "auto" and world == 1):
-        from mpi_cuda_cnn_amd.trainer import capture_step
 
-        issued_before = tr.sync.issued
-        g, why = capture_step(step_launch)
-        ok = torch.tensor([1 if g is not None else 0], device=dev, dtype=torch.int32)
-        if multi:  # every rank replays or none does (collectives inside)
-            dist.all_reduce(ok, op=dist.ReduceOp.MIN)
-        if int(ok.item()) == 1:
-            coll_graph = tr.sync.issued - issued_before
-            step = g.replay
-            graph_note = "hip graph: whole step captured once (torch.cuda.CUDAGraph), replayed per step"
-        else:
-            if args.graph == "on":
-                raise RuntimeError(f"--graph on: capture failed: {why}")
-            graph_note = f"off (capture failed: {why})"
-    for _ in range(max(0, args.warmup - 1)):
-        step()
-    torch.cuda.synchronize()
-    if multi:
-        dist.barrier()
-    torch.cuda.synchronize()
-    tr.zero_stats()
-    issued0 = tr.sync.issued
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    if multi:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    coll_per_step = (tr.sync.issued - issued0) / max(1, args.steps) if coll_graph is None else coll_graph
-    if multi:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    st = tr.net.get_stats()
+    head = timed_run(args, spec, args.dtype, B, d_img, d_lab, dev, dev_idx, rank, world, multi)
+    # BASELINE config 2 ("LeNet-5 fp32 on one MI355X") in the same run: a
+    # second trainer after the first is freed, same graph replay, same K / W
+    extra = None
+    if args.fp32_extra == "on" or (args.fp32_extra == "auto" and world == 1 and args.model == "lenet5"
+                                   and args.dtype != "fp32"):
+        extra = timed_run(args, spec, "fp32", B, d_img, d_lab, dev, dev_idx, rank, world, multi)
+
     if rank == 0:
-        total_imgs = B * world * args.steps
-        value = total_imgs / elapsed
+        value = B * world * args.steps / head["elapsed"]
         out = {
             "metric": metric_for(args.model),
             "value": round(value, 1),
@@ -232,7 +278,7 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": round(1000.0 * elapsed / args.steps, 4),
+            "ms_per_step": round(1000.0 * head["elapsed"] / args.steps, 4),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": round(value / BASELINE_IMG_S, 2) if args.model == "lenet5" else None,
@@ -245,18 +291,26 @@ def main():
                 "parallelism": f"dp{world}",
                 "batch_per_gpu": B,
                 "input_shape": f"{C}x{H}x{W}",
-                "optimizer": f"sgd lr={args.lr} momentum={args.momentum}",
-                "allreduce": (f"{'rccl' if args.dist_backend == 'nccl' else 'gloo (rehearsal)'}: {coll_per_step:g} all-reduce(s)/step over {len(tr.sync.buckets)} "
-                              f"bucket(s) <= {args.bucket_mb} MiB, async on RCCL's stream, joined before SGD"
-                              + ("; at one rank RCCL elides the in-place SUM: no reduction kernel runs"
-                                 " (--force-reduce runs one)" if tr.sync.elided else "")
-                              + ("; forced one-rank reduction kernel (AVG)" if args.force_reduce and world == 1
-                                 else "")
-                              if coll_per_step else "none (--no-dist)"),
-                "train_loss_last": round(st["loss_sum"] / (B * args.steps), 4),
-                "launch": graph_note,
+                "optimizer": head["optimizer"],
+                "allreduce": head["allreduce"],
+                "train_loss_last": head["loss"],
+                "launch": head["launch"],
             },
         }
+        if extra is not None:
+            v32 = B * world * args.steps / extra["elapsed"]
+            out["fp32"] = {
+                "config": f"BASELINE config 2: {args.model} fp32 (exact f32 MFMA / fp32 VALU), dp{world}, "
+                          f"batch_per_gpu {B}, same data, second timed region of this run",
+                "value": round(v32, 1),
+                "unit": "images/s",
+                "ms_per_step": round(1000.0 * extra["elapsed"] / args.steps, 4),
+                "steps": args.steps,
+                "warmup": args.warmup,
+                "vs_baseline": round(v32 / BASELINE_IMG_S, 2) if args.model == "lenet5" else None,
+                "train_loss_last": extra["loss"],
+                "launch": extra["launch"],
+            }
         sys.stdout.flush()
         os.write(json_fd, (json.dumps(out) + "\n").encode())
     if dist.is_initialized():

@@ -13,6 +13,7 @@
 #include <memory>
 #include <set>
 #include <thread>
+#include <vector>
 
 #include "mcc/common.h"
 
@@ -91,21 +92,65 @@ void serve_blob(const void* blob, size_t n, int clients, const BootstrapAddr& ad
   // connection (no or a malformed hello) is dropped without the blob, and a
   // rank that reconnects (e.g. after its own receive timed out) gets the blob
   // again without taking another rank's slot.
+  //
+  // Connections are served concurrently: every accepted socket waits for its
+  // hello in one poll() set with the listening socket (at most 2 s each), so
+  // silent connectors (port scanners, leftovers of a dead job) cannot hold up
+  // the real ranks queued behind them.
+  struct Pending {
+    int fd;
+    Clock::time_point until;
+    int32_t hello[2];
+    size_t got;
+  };
+  std::vector<Pending> pend;
+  auto drop = [&](size_t i) {
+    ::close(pend[i].fd);
+    pend[i] = pend.back();
+    pend.pop_back();
+  };
   std::set<int32_t> served;
-  while ((int)served.size() < clients) {
-    pollfd pf{srv.fd, POLLIN, 0};
-    const int left = ms_left(deadline);
-    if (left <= 0 || ::poll(&pf, 1, left) <= 0)
-      throw Error("bootstrap: timed out waiting for ranks (" + std::to_string(served.size()) + " of " +
-                  std::to_string(clients) + " served)");
-    Fd c(::accept(srv.fd, nullptr, nullptr));
-    if (c.fd < 0) continue;
-    int32_t hello[2] = {0, -1};
-    const auto hello_deadline = std::min(deadline, Clock::now() + std::chrono::seconds(5));
-    if (!recv_all(c.fd, reinterpret_cast<char*>(hello), sizeof(hello), hello_deadline)) continue;
-    if (hello[0] != kHelloMagic || hello[1] < 1 || hello[1] > clients) continue;
-    if (send_all(c.fd, static_cast<const char*>(blob), n)) served.insert(hello[1]);
+  try {
+    while ((int)served.size() < clients) {
+      const int left = ms_left(deadline);
+      if (left <= 0)
+        throw Error("bootstrap: timed out waiting for ranks (" + std::to_string(served.size()) + " of " +
+                    std::to_string(clients) + " served)");
+      std::vector<pollfd> pf(1 + pend.size());
+      pf[0] = pollfd{srv.fd, POLLIN, 0};
+      int wait = std::min(left, 100);
+      for (size_t i = 0; i < pend.size(); ++i) {
+        pf[1 + i] = pollfd{pend[i].fd, POLLIN, 0};
+        wait = std::max(0, std::min(wait, ms_left(pend[i].until)));
+      }
+      ::poll(pf.data(), pf.size(), wait);
+      // hellos first (indices shift on drop: walk backwards)
+      for (size_t i = pend.size(); i-- > 0;) {
+        Pending& q = pend[i];
+        if (pf[1 + i].revents & (POLLIN | POLLHUP | POLLERR)) {
+          const ssize_t k = ::recv(q.fd, reinterpret_cast<char*>(q.hello) + q.got, sizeof(q.hello) - q.got, 0);
+          if (k <= 0) { drop(i); continue; }
+          q.got += (size_t)k;
+          if (q.got == sizeof(q.hello)) {
+            if (q.hello[0] == kHelloMagic && q.hello[1] >= 1 && q.hello[1] <= clients &&
+                send_all(q.fd, static_cast<const char*>(blob), n))
+              served.insert(q.hello[1]);
+            drop(i);
+            continue;
+          }
+        }
+        if (Clock::now() >= q.until) drop(i);
+      }
+      if (pf[0].revents & POLLIN) {
+        const int c = ::accept(srv.fd, nullptr, nullptr);
+        if (c >= 0) pend.push_back(Pending{c, std::min(deadline, Clock::now() + std::chrono::seconds(2)), {0, -1}, 0});
+      }
+    }
+  } catch (...) {
+    for (auto& q : pend) ::close(q.fd);
+    throw;
   }
+  for (auto& q : pend) ::close(q.fd);
 }
 
 void fetch_blob(void* blob, size_t n, int rank, const BootstrapAddr& addr) {

@@ -315,6 +315,10 @@ PYBIND11_MODULE(_C, m) {
       .def("get_logits",
            [](const GpuNet& n, int B) {
              MCC_CHECK(B > 0 && B <= n.max_batch(), "get_logits: bad batch");
+             // forward() may have been enqueued on any (non-blocking) stream:
+             // the deferred FC forward runs on the null stream only after the
+             // whole device is idle, and is itself waited for before the copy
+             if (hipDeviceSynchronize() != hipSuccess) throw Error("hipDeviceSynchronize failed");
              n.flush_forward(nullptr);
              const int nc = n.spec().num_classes(), ld = n.logits_ld();
              std::vector<float> tmp((size_t)B * ld);
@@ -330,6 +334,10 @@ PYBIND11_MODULE(_C, m) {
            [](const GpuNet& n, int stage, int B) {
              // (float32 copy of the stored activation, argmax bytes or None)
              MCC_CHECK(B > 0 && B <= n.max_batch(), "stage_output: bad batch");
+             // a deferred LeNet-5 FC forward (forward() alone) is run first, on
+             // the null stream after the device is idle, so stages 2-4 are current
+             if (hipDeviceSynchronize() != hipSuccess) throw Error("hipDeviceSynchronize failed");
+             n.flush_forward(nullptr);
              int64_t per = 0;
              const uint8_t* arg = nullptr;
              const void* y = n.stage_output(stage, per, &arg);

@@ -1476,6 +1476,8 @@ const void* GpuNet::stage_output(int stage, int64_t& per_sample, const uint8_t**
   // it ran forward + backward in one kernel (loss() of a training step)
   MCC_CHECK(!(fcchain_ && fc_bwd_done_ && (stage == 2 || stage == 3)),
             "stage_output: FC activations of the fused classifier chain were not written (training step)");
+  MCC_CHECK(!(fcchain_ && fc_pending_ && stage >= 2),
+            "stage_output: the FC forward of the fused classifier chain is still pending (call flush_forward)");
   per_sample = st.out_elems;
   if (argmax) *argmax = st.pooled ? st.arg_buf : nullptr;
   return st.act_buf;

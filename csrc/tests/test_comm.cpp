@@ -191,6 +191,48 @@ static void test_bootstrap_stray_connections() {
   std::printf("bootstrap stray connections ok\n");
 }
 
+// Silent connectors (connect, send nothing, hold the socket) must not stall
+// the real ranks: hellos are awaited concurrently, each for at most 2 s.
+static void test_bootstrap_silent_connectors() {
+  BootstrapAddr a;
+  a.port = free_port();
+  a.timeout_s = 20;
+  constexpr int kSilent = 5;
+  auto rcs = run_procs(3 + kSilent, [&](int r) {
+    char b[16] = {};
+    if (r == 0) {
+      std::strcpy(b, "token");
+      serve_blob(b, sizeof(b), 2, a);
+      return 0;
+    }
+    if (r >= 3) {  // a silent connector: holds its connection for 6 s
+      for (int t = 0; t < 400; ++t) {
+        int fd = ::socket(AF_INET, SOCK_STREAM, 0);
+        sockaddr_in sa{};
+        sa.sin_family = AF_INET;
+        sa.sin_port = htons((uint16_t)a.port);
+        sa.sin_addr.s_addr = htonl(0x7f000001);
+        if (::connect(fd, reinterpret_cast<sockaddr*>(&sa), sizeof(sa)) == 0) {
+          ::usleep(6000000);
+          ::close(fd);
+          return 0;
+        }
+        ::close(fd);
+        ::usleep(5000);
+      }
+      return 0;
+    }
+    ::usleep(300000);  // the real ranks arrive after the silent ones
+    const auto t0 = Clock::now();
+    fetch_blob(b, sizeof(b), r, a);
+    const double s = std::chrono::duration<double>(Clock::now() - t0).count();
+    if (s > 3.0) return 7;  // served behind the silent connectors
+    return std::strcmp(b, "token") == 0 ? 0 : 4;
+  });
+  for (int rc : rcs) CHECK(rc == 0);
+  std::printf("bootstrap silent connectors ok\n");
+}
+
 static uint64_t token() {
   std::random_device rd;
   return ((uint64_t)rd() << 32) ^ rd() ^ (uint64_t)::getpid();
@@ -302,6 +344,7 @@ int main() {
   test_bootstrap_world4();
   test_bootstrap_timeouts();
   test_bootstrap_stray_connections();
+  test_bootstrap_silent_connectors();
   test_shm_collectives();
   test_shm_dead_peer_and_poison();
   std::printf("comm ok\n");

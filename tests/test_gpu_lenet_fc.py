@@ -133,3 +133,13 @@ def test_fused_fc_chain_eval_and_logits_without_backward(cuda):
     assert _relerr(l_train[:, :10], l_eval[:, :10]) < 1e-5
     assert st_eval["correct"] == st_train["correct"]
     assert abs(st_eval["loss_sum"] - st_train["loss_sum"]) < 1e-4 * max(1.0, st_eval["loss_sum"])
+    # forward() on a non-blocking side stream: get_logits() / stage_output()
+    # order the deferred FC forward after it (device-wide synchronisation)
+    side = torch.cuda.Stream()
+    for k in range(3):
+        net.forward(d_img.data_ptr(), 0, B, side.cuda_stream)
+        l_side = net.get_logits(B)
+        np.testing.assert_array_equal(l_side, l_fwd)
+    net.forward(d_img.data_ptr(), 0, B, side.cuda_stream)
+    y3, _ = net.stage_output(3, B)
+    assert np.isfinite(y3).all() and np.abs(y3).max() > 0

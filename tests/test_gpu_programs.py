@@ -141,3 +141,22 @@ def test_bench_self_launch_without_launcher():
     assert len(lines) == 1, r.stdout
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "dp2", d
+
+
+@pytest.mark.gpu
+def test_bench_one_gpu_reports_fp32_config():
+    """At N = 1 the headline (bf16) line also carries BASELINE config 2 (LeNet-5
+    fp32 on one MI355X) as a second timed region of the same run, and both
+    regions report the reference optimizer (plain SGD, lr 0.1)."""
+    import json
+
+    r = _run([sys.executable, "bench.py", "--steps", "3", "--warmup", "2", "--batch-per-gpu", "4096"], cwd=ROOT)
+    assert r.returncode == 0, r.stderr
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["dtype"] == "bf16" and d["n_gpus"] == 1 and d["value"] > 0, d
+    assert "plain SGD" in d["config"]["optimizer"] and "lr=0.1" in d["config"]["optimizer"], d
+    f = d["fp32"]
+    assert f["steps"] == 3 and f["warmup"] == 2 and f["value"] > 0 and f["ms_per_step"] > 0, f
+    assert abs(f["value"] * f["ms_per_step"] / 1000.0 - 4096) < 1.0, f

@@ -48,6 +48,7 @@ def _check_idx(path: str, want_dims: int) -> None:
 
 def from_local(src: str, out: str) -> list[str]:
     paths = []
+    copied = False
     for name in NAMES:
         found = next((p for p in _candidates(src, name) if os.path.exists(p)), None)
         if found is None:
@@ -57,9 +58,14 @@ def from_local(src: str, out: str) -> list[str]:
         if found.endswith(".gz"):
             with gzip.open(found, "rb") as fi, open(dst, "wb") as fo:
                 shutil.copyfileobj(fi, fo)
-        else:
+            copied = True
+        elif not (os.path.exists(dst) and os.path.samefile(found, dst)):
             shutil.copyfile(found, dst)
+            copied = True
         paths.append(dst)
+    marker = os.path.join(out, "SYNTHETIC")
+    if copied and os.path.exists(marker):  # files from elsewhere replace an earlier synthetic set
+        os.remove(marker)
     return paths
 
 
@@ -73,6 +79,13 @@ def synthetic(out: str, n: int) -> list[str]:
         mcc.idx_write(pi, imgs.reshape(count, 28, 28))
         mcc.idx_write(pl, labels)
         paths += [pi, pl]
+    # the synthetic set uses the real MNIST file names: leave a marker so a
+    # later run's accuracy / loss log is not mistaken for a real-MNIST one
+    with open(os.path.join(out, "SYNTHETIC"), "w") as f:
+        f.write(f"synthetic MNIST-shaped stripe images (mcc.synth_dataset), {n} train / {max(1, n // 5)} test;"
+                " not real MNIST\n")
+    print(f"get_mnist: no --src given: wrote a SYNTHETIC MNIST-shaped set under {out} "
+          f"(marker {os.path.join(out, 'SYNTHETIC')})", file=sys.stderr)
     return paths
 
 
