@@ -39,9 +39,25 @@
 //   (the FC input, NHWC flatten), A2 [B][25][16] u8.
 #include "kernels.h"
 #include "mfma.h"
+#include "mcc/ab.h"
 
 #include <algorithm>
 
+#ifndef MCC_LENET_STAMP
+#define MCC_LENET_STAMP 0  // per-phase s_memtime stamps of lenet_bwd4 (diagnostic builds only)
+#endif
+#ifndef MCC_BWD4_SPLIT
+#define MCC_BWD4_SPLIT 1  // conv2 dX tiles: 0 = w1 0-2 / w2 3-5 / w3 6 (+ dW1); 1 = w1 0-3 / w2 4-6 / w3 dW1 only
+#endif
+#ifndef MCC_BWD4_STAGE
+#define MCC_BWD4_STAGE 1  // 1: w1 stages Y1 and w2 dZ2 (swapped); X0 row groups [0, MCC_BWD4_XW0) on w0, the rest on w3
+#endif
+#ifndef MCC_BWD4_XW0
+#define MCC_BWD4_XW0 3
+#endif
+#ifndef MCC_DW1_D
+#define MCC_DW1_D 8  // conv1 dW operand read lookahead (MFMAs)
+#endif
 #ifndef MCC_LENET_ABL
 #define MCC_LENET_ABL 0  // phase ablations for timing studies only (tools/build_variant.sh); 0 in every build
 #endif
@@ -439,6 +455,234 @@ __global__ void __launch_bounds__(64) lenet_fwd_kernel(LenetFwdParams p) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// Forward, round 5: conv1 with whole pooling windows in a lane.
+//
+// The kernel above spends ~60 % of its time in the conv1 epilogue (phase
+// ablation: conv1 266 of 433 us): its MFMA rows are pixel pairs, so a 2x2
+// window is split over two lanes (DPP swap + selects), and every tile reads
+// three index tables (A offsets, Y1 / A1 epilogue offsets) whose values feed
+// the next tile's address math (26 VALU + 2 dependent LDS table reads per
+// tile).  Here:
+//   * MFMA row m = 4w + i is POSITION i = (dy, dx) = (i >> 1, i & 1) of window
+//     slot w, so lane (n, g) holds the four positions of window slot g in its
+//     accumulator: the pool is two v_max3 (keys with the position in the low
+//     bits, as before, and the ReLU clamp folded in);
+//   * column n = 2 co + s computes channel co of the window s = 0 / 1 pooled
+//     columns to the right (taps shifted by two inside the 8-wide K window):
+//     12 of 16 columns useful, as before;
+//   * a tile's four window slots are the 2x2 block of even-column windows
+//     (py0 + (w >> 1), px0 + 2 (w & 1)), so with the s shift a tile covers
+//     2 pooled rows x 4 pooled columns and every operand / result address is
+//     a per-lane constant plus a per-tile immediate: no tables, no address
+//     VALU.  28 tiles (7 row pairs x 4 column blocks; the last block's
+//     columns 14, 15 land in junk columns of the LDS Y1 / A1 rows) vs 25;
+//   * the odd-position rows read a second copy of the padded input shifted by
+//     ONE element (copies: shift 0 and 1), so every A fragment is two aligned
+//     ds_read_b64;
+//   * conv2's pooled outputs are staged in LDS (in the dead input copies) and
+//     leave as 16-byte rows instead of 2-byte / 1-byte scattered stores.
+constexpr int kGxPitch = 36;                      // elements (72 B: rows on distinct bank pairs)
+constexpr int kGxCopy = kGxPitch * 32 * 2 + 16;   // 2320 (copy 1 on banks 4 dwords off copy 0)
+// Y1 keeps the compact HWC-8 layout of the global tensor (14-pixel rows: the
+// conv2 operand reads were bank-annealed for it; 16-pixel rows measured 701
+// conflict cycles per image, tools/lds_banks.py lenet_fwd2), so the windows of
+// the last column block that fall past column 13 are masked at the Y1 store.
+constexpr int kGY1 = 2 * kGxCopy;                 // 4640: Y1 HWC-8, 196 x 16 B
+constexpr int kGA1 = kGY1 + 196 * 16;             // 7776: A1 [7][14][16] u8 (plane 6: columns co 6, 7)
+constexpr int kGA1Plane = 240;
+constexpr int kGTab2 = kGA1 + 7 * kGA1Plane;      // 9456: u16 [112] conv2 row -> Y1 byte offset
+constexpr int kGLds = kGTab2 + 224;               // 9680
+static_assert(16 * kGLds <= 163840, "lenet_fwd2: 16 waves per CU");
+static_assert(kGY1 % 16 == 0 && kGY1 >= 2 * kGxCopy, "lenet_fwd2 layout");
+// conv2 pooled outputs staged over A1 (copied out before conv2; the next
+// image's conv1 rewrites every byte of A1 that is copied out).  Not over the
+// input copies: their zero padding rows / columns are written only once.
+constexpr int kGY2 = kGA1;                        // Y2 [25][16] bf16 = 800 B
+constexpr int kGA2 = kGA1 + 800;                  // A2 [25][16] u8 = 400 B
+static_assert(kGA2 + 400 <= kGA1 + 7 * kGA1Plane, "Y2 / A2 staging fits in A1");
+
+// 8 bf16 from two 8-byte LDS reads that the compiler must not fuse into one
+// ds_read2_b64 (8 cycles at 32 banks vs 2 x 2 cycles)
+typedef __attribute__((address_space(3))) const volatile bf16x4 lds_vbf16x4;
+__device__ __forceinline__ bf16x8 lds8v(const char* p) {
+  const auto* q = (const __attribute__((address_space(3))) char*)(p);
+  const bf16x4 lo = *reinterpret_cast<lds_vbf16x4*>(q);
+  const bf16x4 hi = *reinterpret_cast<lds_vbf16x4*>(q + 8);
+  return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+
+__global__ void __launch_bounds__(64) lenet_fwd2_kernel(LenetFwdParams p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = threadIdx.x;
+  const int n16 = lane & 15, g = lane >> 4;
+  const int co = n16 >> 1, sh = n16 & 1;
+
+  // ---- weights: conv1 B[k][n = 2 co + s] = W1[co][kh][kw' - 2 s] ----
+  bf16x8 w1[2];
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const int kh = c == 0 ? g : 4;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int kw = e - 2 * sh;
+      const bool ok = n16 < 12 && (c == 0 || g == 0) && kw >= 0 && kw < 5;
+      const float v = p.w1[ok ? co * 25 + kh * 5 + kw : 0];
+      w1[c][e] = (bf16)(ok ? v : 0.f);
+    }
+  }
+  const float bias1 = n16 < 12 ? 255.f * p.b1[co] : 0.f;  // the tile holds raw integer pixels
+  bf16x8 w2[7];
+  int koff2[7];
+#pragma unroll
+  for (int c = 0; c < 7; ++c) {
+    const int t = kC2Tap[4 * c + g], kh = t < 25 ? t / 5 : 0, kw = t < 25 ? t % 5 : 0;
+    koff2[c] = (kh * 14 + kw) * 16;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const bool ok = t < 25 && e < 6;
+      const float v = p.w2[ok ? (n16 * 6 + e) * 25 + t : 0];
+      w2[c][e] = (bf16)(ok ? v : 0.f);
+    }
+  }
+  const float bias2 = p.b2[n16];
+
+  char* xf = smem;
+  char* y1s = smem + kGY1;
+  char* a1s = smem + kGA1;
+  zero_wave_lds(smem, kGLds);
+  wave_lds_sync();
+  for (int r = lane; r < 112; r += 64) {
+    const int wr = kC2Win[4 * (r >> 4) + ((r & 15) >> 2)], w = wr < 0 ? 24 : wr, pos = r & 3;
+    reinterpret_cast<unsigned short*>(smem + kGTab2)[r] =
+        (unsigned short)(((2 * (w / 5) + (pos >> 1)) * 14 + 2 * (w % 5) + (pos & 1)) * 16);
+  }
+  uint32_t c2win[2] = {0u, 0u};
+#pragma unroll
+  for (int T = 0; T < 7; ++T) c2win[T >> 2] |= (uint32_t)(kC2Win[4 * T + g] + 1) << (8 * (T & 3));
+  const unsigned short* tab2 = reinterpret_cast<const unsigned short*>(smem + kGTab2);
+
+  // conv1 A operand of this lane: row m = n16 = 4 wa + ia, k-group g (kernel row g; chunk 1: row 4)
+  const int wa = n16 >> 2, ia = n16 & 3;
+  const int abase = (ia & 1) * kGxCopy + (2 * (wa >> 1) + (ia >> 1) + g) * kGxPitch * 2 + 8 * (wa & 1);
+  // epilogue of this lane: window slot g, column shift sh, channel co
+  const int ey1 = ((g >> 1) * 14 + 2 * (g & 1) + sh) * 16 + co * 2;
+  const bool y1last = (g & 1) == 0;  // in the last column block (px0 = 12) only slots 0, 2 are columns < 14
+  const int ea1 = min(co, 6) * kGA1Plane + (g >> 1) * 16 + 2 * (g & 1) + sh;
+
+  const int sk = lane & 7, srow = lane >> 3;
+  const int stride_w = (int)gridDim.x;
+  uint32_t xw[4];
+  WaveIdx widx;
+  widx.load(p.idx, blockIdx.x, stride_w, p.B, 0);
+  auto load_img = [&](int k) {
+    if ((k & 63) == 0 && k > 0) widx.load(p.idx, blockIdx.x, stride_w, p.B, k);
+    const uint8_t* xin = p.x + (size_t)widx.get(k) * kImgPix;
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      const int yy = it * 8 + srow;
+      xw[it] = (yy < 28 && sk < 7) ? *reinterpret_cast<const uint32_t*>(xin + yy * 28 + sk * 4) : 0u;
+    }
+  };
+  if ((int)blockIdx.x < p.B) load_img(0);
+  // A1 bulk copy: chunk i = (plane i / 14, row i % 14)
+  const int a1src0 = (lane / 14) * kGA1Plane + (lane % 14) * 16;
+  const int a1src1 = ((lane + 64) / 14) * kGA1Plane + ((lane + 64) % 14) * 16;
+
+  for (int img = blockIdx.x, kimg = 0; img < p.B; img += stride_w, ++kimg) {
+    wave_lds_sync();  // the previous image's LDS reads (incl. the Y2 / A2 copy-out) are done
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      const int yy = it * 8 + srow;
+      uint32_t lo, hi;
+      u8x4_ints(xw[it], lo, hi);
+      const uint32_t phi = from_left(hi);
+      if (yy < 28) {
+        char* d = xf + ((yy + 2) * kGxPitch + 4 * sk) * 2;
+        *reinterpret_cast<u32x2*>(d) = u32x2{phi, lo};                                    // Xpad cols 4k .. 4k+3
+        *reinterpret_cast<u32x2*>(d + kGxCopy) = u32x2{mid16(phi, lo), mid16(lo, hi)};    // Xpad cols 4k+1 .. 4k+4
+      }
+    }
+    wave_lds_sync();
+    if (img + stride_w < p.B) load_img(kimg + 1);
+
+    // ---- conv1 + ReLU + pool: 28 tiles, operand reads of tile T+1 before tile T's epilogue ----
+    if constexpr (!(MCC_LENET_ABL & 16)) {
+      auto tile_a = [](int T) { return (2 * (T >> 2)) * 2 * kGxPitch * 2 + 4 * (4 * (T & 3)); };  // py0 = 2 (T/4), px0 = 4 (T%4)
+      auto tile_y = [](int T) { return ((2 * (T >> 2)) * 14 + 4 * (T & 3)) * 16; };               // Y1 (py0, px0)
+      auto tile_c = [](int T) { return (2 * (T >> 2)) * 16 + 4 * (T & 3); };                      // A1 (py0, px0)
+      bf16x8 fa = lds8v(xf + abase + tile_a(0));
+      bf16x8 fb = lds8v(xf + abase + tile_a(0) + 4 * kGxPitch * 2);
+#pragma unroll
+      for (int T = 0; T < 28; ++T) {
+        f32x4 acc = {bias1, bias1, bias1, bias1};
+        acc = mma(acc, fa, w1[0]);
+        acc = mma(acc, fb, w1[1]);
+        if (T + 1 < 28) {
+          fa = lds8v(xf + abase + tile_a(T + 1));
+          fb = lds8v(xf + abase + tile_a(T + 1) + 4 * kGxPitch * 2);
+        }
+        const int k0 = (__float_as_int(acc[0]) & ~3) | 3;
+        const int k1 = (__float_as_int(acc[1]) & ~3) | 2;
+        const int k2 = (__float_as_int(acc[2]) & ~3) | 1;
+        const int k3 = __float_as_int(acc[3]) & ~3;
+        const int best = imax(imax(imax(k0, k1), imax(k2, k3)), 0);
+        // the two code bits left in the value perturb it by < 2^-21: below the bf16 rounding
+        const bf16 yb = (bf16)(__int_as_float(best) * (1.f / 255.f));
+        if ((T & 3) != 3 || y1last) *reinterpret_cast<bf16*>(y1s + ey1 + tile_y(T)) = yb;
+        a1s[ea1 + tile_c(T)] = (uint8_t)(best > 3 ? (~best & 3) : 4);
+      }
+    }
+    wave_lds_sync();  // pooled conv1 output and codes complete in LDS
+    {  // bulk copies to HBM: Y1 (196 x 16 B), A1 (84 x 16 B)
+      u32x4* y1g = reinterpret_cast<u32x4*>(static_cast<bf16*>(p.y1) + (size_t)img * kY1Elems);
+      u32x4* a1g = reinterpret_cast<u32x4*>(p.a1 + (size_t)img * kA1Bytes);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int i = lane + 64 * r;
+        if (i < 196) y1g[i] = *reinterpret_cast<const u32x4*>(y1s + i * 16);
+      }
+      a1g[lane] = *reinterpret_cast<const u32x4*>(a1s + a1src0);
+      if (lane < 20) a1g[lane + 64] = *reinterpret_cast<const u32x4*>(a1s + a1src1);
+    }
+
+    // ---- conv2 + ReLU + pool -> Y2 / A2 staged in LDS (over A1) ----
+    if constexpr (!(MCC_LENET_ABL & 32)) {
+#pragma unroll 1
+      for (int T = 0; T < 7; ++T) {
+        const char* pa = y1s + tab2[16 * T + n16];
+        bf16x8 af[7];
+#pragma unroll
+        for (int c = 0; c < 7; ++c) af[c] = *reinterpret_cast<const bf16x8*>(pa + koff2[c]);
+        __builtin_amdgcn_sched_barrier(0);
+        f32x4 acc = {bias2, bias2, bias2, bias2};
+#pragma unroll
+        for (int c = 0; c < 7; ++c) acc = mma(acc, af[c], w2[c]);
+        const int wo = (int)(((T < 4 ? c2win[0] : c2win[1]) >> (8 * (T & 3))) & 0xffu) - 1;
+        const int k0 = __float_as_int(acc[0]) | 3;
+        const int k1 = (__float_as_int(acc[1]) & ~3) | 2;
+        const int k2 = (__float_as_int(acc[2]) & ~3) | 1;
+        const int k3 = __float_as_int(acc[3]) & ~3;
+        const int best = imax(imax(imax(k0, k1), imax(k2, k3)), 0);
+        const bf16 yb = (bf16)__int_as_float(best);
+        if (wo >= 0) {
+          *reinterpret_cast<bf16*>(smem + kGY2 + (wo * 16 + n16) * 2) = yb;
+          smem[kGA2 + wo * 16 + n16] = (uint8_t)(best > 3 ? (~best & 3) : 4);
+        }
+      }
+    }
+    wave_lds_sync();
+    {  // Y2: 50 x 16 B, A2: 25 x 16 B
+      u32x4* y2g = reinterpret_cast<u32x4*>(static_cast<bf16*>(p.y2) + (size_t)img * kY2Elems);
+      u32x4* a2g = reinterpret_cast<u32x4*>(p.a2 + (size_t)img * kY2Elems);
+      // chunks 0..74 = Y2 0..49, A2 0..24 over lanes 0..63, then 64..74
+      if (lane < 50) y2g[lane] = *reinterpret_cast<const u32x4*>(smem + kGY2 + lane * 16);
+      else a2g[lane - 50] = *reinterpret_cast<const u32x4*>(smem + kGA2 + (lane - 50) * 16);
+      if (lane < 11) a2g[lane + 14] = *reinterpret_cast<const u32x4*>(smem + kGA2 + (lane + 14) * 16);
+    }
+  }
+}
+
 // ============================================================================
 // Backward
 // ============================================================================
@@ -766,6 +1010,403 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2, 2))
   }
 }
 
+// ---------------------------------------------------------------------------
+// Four waves per image (round 5).  The two-wave kernel above serialises each
+// image as [dW2 | dX2 (105 MFMAs)] -> [dW1 (30)] -> staging, so wave 1's 105
+// MFMAs + wave 0's 30 are its critical path and the staging loads / LDS
+// writes sit between barriers.  Here a 256-thread workgroup (two per CU: two
+// waves per SIMD) gives every wave ~1/4 of an image's 187 MFMAs:
+//   w0: conv2 dW (52)
+//   w1: conv2 dX tiles 0..2 (45)      w2: conv2 dX tiles 3..5 (45)
+//   w3: conv1 dW of the PREVIOUS image (30) + conv2 dX tile 6 (15)
+// conv1 dW lags one image, so dZ1 and X0 are double-buffered; per image two
+// barriers: A (image k's dZ2 / Y1 / X0 staged) and B (everything that reads
+// dZ2 / Y1 done: stage image k+1; dZ1[(k-1)&1] and X0[(k-1)&1] free).  The
+// staging is split over w0 (X0 rows 0..15), w1 (dZ2), w2 (Y1), w3 (X0 rows
+// 16..27); every wave's global loads for image k+1 are issued at the start of
+// phase A and land during its MFMAs.  Buffer strides are multiples of 256 B,
+// so both buffers keep the bank-model layout of the single-buffer version.
+constexpr int kQXs = kBXs;                   // 14720: X0 [2][4 copies]
+constexpr int kQXbuf = 41 * 256;             // 10496 (>= 4 * kBxCopy = 10336)
+constexpr int kQOne1 = kQXs + kQXbuf + 4 * kBxCopy;  // 35552 (== 224 mod 256, as kBOne1)
+constexpr int kQDz1 = kQOne1 + 30 * 80;      // dZ1 [2][6 planes]  (== 64 mod 256, as kBDz1)
+constexpr int kQDz1buf = 49 * 256;           // 12544 (>= 6 * kBDz1Plane = 12480)
+constexpr int kQLds = kQDz1 + 2 * kQDz1buf;
+static_assert(kQOne1 % 256 == kBOne1 % 256 && kQDz1 % 256 == kBDz1 % 256, "bank-model offsets");
+static_assert(kQXs % 256 == kBXs % 256, "bank-model offsets");
+static_assert(2 * kQLds <= 163840, "lenet_bwd4: two workgroups per CU");
+constexpr int kXw0 = MCC_BWD4_XW0;  // X0 row groups (of 8 rows) staged by w0; the rest by w3
+static_assert(kXw0 >= 1 && kXw0 <= 3, "X0 staging split");
+
+template <int T0, int T1>
+__device__ __forceinline__ void lenet_dx2_tiles(char* smem, const bf16x8 (&wdx)[15], const uint32_t* a1w, int hxa,
+                                                int hxb, int n16, int g, int dxci, int dxj, int dz1) {
+  bf16x8 fr[15], nx[5];
+#pragma unroll
+  for (int c = 0; c < 15; ++c)
+    fr[c] = *reinterpret_cast<const bf16x8*>(smem + (dxwrap(c) ? hxb : hxa) + dxoff(c) + T0 * 1280);
+  f32x4 accp = {0.f, 0.f, 0.f, 0.f};
+  auto epilogue = [&](int T, const f32x4& acc) {
+    uint32_t top[4], bot[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const uint32_t code = (a1w[T - T0] >> (8 * i)) & 0xffu;
+      const uint64_t h = code < 4u ? (uint64_t)bf16_bits(acc[i]) : 0ull;
+      const uint64_t w = h << (16u * (code & 3u));
+      top[i] = (uint32_t)w;
+      bot[i] = (uint32_t)(w >> 32);
+    }
+    if (n16 < 12) {
+      char* d = smem + dz1 + dxci * kBDz1Plane + (4 * T + 2 * dxj + 2) * 64 + 16 * (g ^ (1 - dxj));
+      *reinterpret_cast<u32x4*>(d) = u32x4{top[0], top[1], top[2], top[3]};
+      *reinterpret_cast<u32x4*>(d + 64) = u32x4{bot[0], bot[1], bot[2], bot[3]};
+    }
+  };
+#pragma unroll
+  for (int T = T0; T < T1; ++T) {
+    if (T + 1 < T1) {
+#pragma unroll
+      for (int c = 10; c < 15; ++c)
+        nx[c - 10] = *reinterpret_cast<const bf16x8*>(smem + (dxwrap(c) ? hxb : hxa) + dxoff(c) + (T + 1) * 1280);
+    }
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int c = 0; c < 15; ++c) acc = mma(acc, fr[c], wdx[c]);
+    if (T > T0) epilogue(T - 1, accp);
+    accp = acc;
+#pragma unroll
+    for (int c = 0; c < 10; ++c) fr[c] = fr[c + 5];
+#pragma unroll
+    for (int c = 10; c < 15; ++c) fr[c] = nx[c - 10];
+  }
+  epilogue(T1 - 1, accp);
+}
+
+// X0 staging shared by the w0 / w3 roles of lenet_bwd4_kernel (NH row groups
+// of 8 rows from group XG): loads into xw[], LDS copies c = 0..3 of buffer buf.
+#define LENET_LOAD_X(XG, NH)                                                                       \
+  if ((k & 63) == 0 && k > 0) widx.load(p.idx, blockIdx.x, grid, p.B, k);                         \
+  {                                                                                                \
+    const uint8_t* xin = p.x + (size_t)widx.get(k) * kImgPix;                                      \
+    _Pragma("unroll") for (int h = 0; h < (NH); ++h) {                                             \
+      const int yy = ((XG) + h) * 8 + srow;                                                        \
+      xw[h] = (yy < 28 && sk < 7) ? *reinterpret_cast<const uint32_t*>(xin + yy * 28 + sk * 4) : 0u; \
+    }                                                                                              \
+  }
+#define LENET_STAGE_X(XG, NH)                                                                      \
+  _Pragma("unroll") for (int h = 0; h < ((MCC_LENET_ABL & 128) ? 0 : (NH)); ++h) {                 \
+    const int yy = ((XG) + h) * 8 + srow;                                                          \
+    uint32_t lo, hi;                                                                               \
+    u8x4_ints(xw[h], lo, hi);                                                                      \
+    const uint32_t phi = from_left(hi);                                                            \
+    const uint32_t rlo = from_right(lo);                                                           \
+    const uint32_t nlo = sk == 7 ? 0u : rlo;                                                       \
+    if (yy < 28) {                                                                                 \
+      char* d = smem + kQXs + buf * kQXbuf + ((yy + 2) * 40 + 4 * sk) * 2;                         \
+      *reinterpret_cast<u32x2*>(d) = u32x2{phi, lo};                                               \
+      *reinterpret_cast<u32x2*>(d + kBxCopy) = u32x2{mid16(phi, lo), mid16(lo, hi)};               \
+      *reinterpret_cast<u32x2*>(d + 2 * kBxCopy) = u32x2{lo, hi};                                  \
+      *reinterpret_cast<u32x2*>(d + 3 * kBxCopy) = u32x2{mid16(lo, hi), mid16(hi, nlo)};           \
+    }                                                                                              \
+  }
+
+// One role's per-image loop: every wave runs the same barrier sequence, but
+// each role is its own inlined loop, so its registers (w0's 52 dW2
+// accumulators, w1..w3's 60 dX2 weight registers) are not live in the others.
+template <typename Load, typename Begin, typename Compute, typename Stage>
+__device__ __forceinline__ int lenet_bwd4_loop(const LenetBwdParams& p, Load&& load, Begin&& begin, Compute&& compute,
+                                               Stage&& stage) {
+  const int grid = (int)gridDim.x;
+  if ((int)blockIdx.x < p.B) {
+    load(0);
+    stage(0);
+  }
+  int k = 0;
+#if MCC_LENET_STAMP
+  // diagnostic build only: per-phase s_memtime sums (wave-uniform, in SGPRs),
+  // written once at the end into the unused second half of the slab buffer
+  // (tools/probes/lenet_stamp_probe.py); no memory traffic inside the loop
+  unsigned long long tprev = 0, tsum[4] = {0, 0, 0, 0};
+  auto stamp = [&](int, int e) {
+    const unsigned long long t = __builtin_amdgcn_s_memtime();
+    if (e > 0) tsum[e - 1] += t - tprev;
+    tprev = t;
+  };
+#else
+  auto stamp = [](int, int) {};
+#endif
+  for (int img = blockIdx.x; img < p.B; img += grid, ++k) {
+    stamp(k, 0);
+    wg_barrier();  // A: image k staged (dZ2, Y1, X0[k & 1])
+    stamp(k, 1);
+    begin();
+    const bool more = img + grid < p.B;
+    if (more && !(MCC_LENET_ABL & 256)) load(k + 1);
+    compute(k);
+    stamp(k, 2);
+    wg_barrier();  // B: dZ2 / Y1 / X0[(k - 1) & 1] / dZ1[(k - 1) & 1] free
+    stamp(k, 3);
+    if (more) stage((k + 1) & 1);
+    stamp(k, 4);
+  }
+#if MCC_LENET_STAMP
+  if ((threadIdx.x & 63) == 0) {
+    unsigned long long* st = reinterpret_cast<unsigned long long*>(p.slab + (size_t)512 * kSlab) +
+                             (size_t)(blockIdx.x * 4 + (threadIdx.x >> 6)) * 5;
+    for (int e = 0; e < 4; ++e) st[e] = tsum[e];
+    st[4] = (unsigned long long)k;
+  }
+#endif
+  return k;
+}
+
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) lenet_bwd4_kernel(LenetBwdParams p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int n16 = lane & 15, g = lane >> 4;
+  const int sk = lane & 7, srow = lane >> 3;
+  const int grid = (int)gridDim.x;
+
+  {
+    const u32x4 z = {0u, 0u, 0u, 0u};
+    for (int i = threadIdx.x * 16; i < kQLds; i += 256 * 16) *reinterpret_cast<u32x4*>(smem + i) = z;
+  }
+  wg_barrier();
+  if (wv == 0) {  // bf16 ones: the dW2 bias pixel and the dW1 bias rows
+    const uint32_t one2 = 0x3f803f80u;
+    if (lane < 4) *reinterpret_cast<uint32_t*>(smem + kBOne2 + 4 * lane) = one2;
+    for (int i = lane; i < 30 * 16; i += 64)
+      *reinterpret_cast<uint32_t*>(smem + kQOne1 + (i >> 4) * 80 + (i & 15) * 4) = one2;
+  }
+  float* slab = p.slab + (size_t)blockIdx.x * kSlab;
+  auto nothing = [] {};
+
+
+  if (wv == 0) {
+    // ======================= w0: conv2 dW; X0 rows 0..15 =======================
+    const int tq = (lane >> 2) & 3, tp = lane & 3;
+    int aw2[4][2], bw2a[4][2], bw2b[4][2], bw2c[4][2];
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int hf = 0; hf < 2; ++hf) {
+        const int v = kZPos[32 * c + 8 * g + 4 * hf + tq];
+        const bool ok = v < 100;
+        const int z = ok ? v : v - 128;
+        const int zy = z / 10, zx = z % 10;
+        aw2[c][hf] = ok ? kBDz2 + ((zy + 4) * 20 + zx + 4) * 32 + 8 * tp : kBDz2 + 8 * tp;
+        const int yb = kBY1 + (zy * 14 + zx) * 16 + 8 * (tp & 1);
+        bw2a[c][hf] = yb + (tp >> 1) * 16;
+        bw2b[c][hf] = yb + (tp >> 1) * 160;
+        bw2c[c][hf] = (tp >> 1) ? kBOne2 + 8 * (tp & 1) - tapoff2(24) : yb;
+      }
+    f32x4 acc2[13];
+#pragma unroll
+    for (int t = 0; t < 13; ++t) acc2[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    uint32_t xw[kXw0] = {};
+    WaveIdx widx;
+    widx.load(p.idx, blockIdx.x, grid, p.B, 0);
+    auto load = [&](int k) { LENET_LOAD_X(0, kXw0) };
+    auto stage = [&](int buf) { LENET_STAGE_X(0, kXw0) };
+    auto compute = [&](int) {
+      if constexpr (!(MCC_LENET_ABL & 1)) {
+        bf16x8 af[2], bfr[2][13];
+        auto load_chunk = [&](int c, int buf) {
+          af[buf] = tr8(smem + aw2[c][0], smem + aw2[c][1]);
+#pragma unroll
+          for (int t = 0; t < 13; ++t) {
+            const int o = tapoff2(2 * t);
+            const int* base = t == 12 ? bw2c[c] : ((2 * t) % 5 == 4 ? bw2b[c] : bw2a[c]);
+            bfr[buf][t] = tr8(smem + base[0] + o, smem + base[1] + o);
+          }
+        };
+        load_chunk(0, 0);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          if (c + 1 < 4) load_chunk(c + 1, (c + 1) & 1);
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int t = 0; t < 13; ++t) acc2[t] = mma(acc2[t], af[c & 1], bfr[c & 1][t]);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+    };
+    lenet_bwd4_loop(p, load, nothing, compute, stage);
+#pragma unroll
+    for (int t = 0; t < 13; ++t)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) slab[(t * 4 + i) * 64 + lane] = acc2[t][i];
+    return;
+  }
+
+  // ================= w1..w3: conv2 dX (w1 tiles 0-2, w2 3-5, w3 6) =================
+  bf16x8 wdx[15];
+  {
+    const int ci = n16 >> 1, j = n16 & 1;
+#pragma unroll
+    for (int c = 0; c < 15; ++c) {
+      const int t = 2 * c + (g >> 1), u = t / 5, v = t % 5;
+      const int kh = 4 + j - u, kw = 4 - v;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int co = 8 * (g & 1) + e;
+        const bool ok = n16 < 12 && kh >= 0 && kh < 5;
+        float w = p.w2[ok ? ((co * 6 + ci) * 5 + kh) * 5 + kw : 0];
+        wdx[c][e] = (bf16)(ok ? w : 0.f);
+      }
+    }
+  }
+  const int hxa = kBDz2 + n16 * 32 + 16 * (g & 1) + (g >> 1) * 32;
+  const int hxb = kBDz2 + n16 * 32 + 16 * (g & 1) + (g >> 1) * 512;
+  const int dxci = n16 < 12 ? n16 >> 1 : 5, dxj = n16 & 1;
+  constexpr int kT1 = MCC_BWD4_SPLIT ? 4 : 3, kT2 = MCC_BWD4_SPLIT ? 7 : 6;  // w1: [0, kT1), w2: [kT1, kT2), w3: [kT2, 7)
+  const int t_lo = wv == 1 ? 0 : wv == 2 ? kT1 : kT2;
+  uint32_t a1n[4] = {0u, 0u, 0u, 0u}, a1w[4] = {0u, 0u, 0u, 0u};
+  auto load_codes = [&](int k, int nt) {
+    const int img = blockIdx.x + k * grid;
+    const uint8_t* a1g = p.a1 + (size_t)img * kA1Bytes + dxci * 224 + 4 * g;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+      if (t < nt) a1n[t] = *reinterpret_cast<const uint32_t*>(a1g + (2 * (t_lo + t) + dxj) * 16);
+  };
+  auto begin = [&] {
+#pragma unroll
+    for (int t = 0; t < 4; ++t) a1w[t] = a1n[t];
+  };
+  auto dz1_of = [](int k) { return kQDz1 + (k & 1) * kQDz1buf; };
+
+  // dZ2 = unpool of dY2 (lanes < 50) and Y1: staged by w1 / w2, or swapped
+  // (MCC_BWD4_STAGE: the wave with more dX tiles takes the cheaper Y1 copy)
+  const int zq = lane >> 1, zh = lane & 1;
+  const int zqy = (zq * 205) >> 10, zqx = zq - 5 * zqy;
+  const int zbase = kBDz2 + ((2 * zqy + 4) * 20 + 2 * zqx + 4) * 32 + 16 * zh;
+  u32x4 dy = {0u, 0u, 0u, 0u};
+  u32x2 cw = {0u, 0u};
+  auto load_dz2 = [&](int k) {
+    const int img = blockIdx.x + k * grid;
+    if (lane < 50) {
+      dy = *reinterpret_cast<const u32x4*>(static_cast<const bf16*>(p.dy2) + (size_t)img * kY2Elems + zq * 16 + 8 * zh);
+      cw = *reinterpret_cast<const u32x2*>(p.a2 + (size_t)img * kY2Elems + zq * 16 + 8 * zh);
+    }
+  };
+  auto stage_dz2 = [&] {
+    if (lane < 50 && !(MCC_LENET_ABL & 8)) {
+      const u32x4 z = {0u, 0u, 0u, 0u};
+      *reinterpret_cast<u32x4*>(smem + zbase) = z;
+      *reinterpret_cast<u32x4*>(smem + zbase + 32) = z;
+      *reinterpret_cast<u32x4*>(smem + zbase + 640) = z;
+      *reinterpret_cast<u32x4*>(smem + zbase + 672) = z;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const uint32_t code = (cw[i >> 2] >> (8 * (i & 3))) & 0xffu;
+        const uint32_t v = (dy[i >> 1] >> (16 * (i & 1))) & 0xffffu;
+        const int off = ((code & 2u) ? 640 : 0) + ((code & 1u) ? 32 : 0);  // code 4: value 0 at TL
+        *reinterpret_cast<unsigned short*>(smem + zbase + off + 2 * i) = (unsigned short)(code < 4u ? v : 0u);
+      }
+    }
+  };
+  u32x4 yv[4];
+  auto load_y1 = [&](int k) {
+    const int img = blockIdx.x + k * grid;
+    const bf16* y1g = static_cast<const bf16*>(p.y1) + (size_t)img * kY1Elems;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) yv[r] = *reinterpret_cast<const u32x4*>(y1g + min(lane + 64 * r, 195) * 8);
+  };
+  auto stage_y1 = [&] {
+    if constexpr (!(MCC_LENET_ABL & 64)) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int px = lane + 64 * r;
+        if (px < 196) *reinterpret_cast<u32x4*>(smem + kBY1 + px * 16) = yv[r];
+      }
+    }
+  };
+
+  if (wv == 1) {
+    // ---- w1: dX tiles [0, kT1); stages dZ2 (or Y1) ----
+    auto load = [&](int k) {
+      if constexpr (MCC_BWD4_STAGE) load_y1(k); else load_dz2(k);
+      load_codes(k, kT1);
+    };
+    auto stage = [&](int) {
+      if constexpr (MCC_BWD4_STAGE) stage_y1(); else stage_dz2();
+    };
+    auto compute = [&](int k) {
+      if constexpr (!(MCC_LENET_ABL & 2)) lenet_dx2_tiles<0, kT1>(smem, wdx, a1w, hxa, hxb, n16, g, dxci, dxj, dz1_of(k));
+    };
+    lenet_bwd4_loop(p, load, begin, compute, stage);
+  } else if (wv == 2) {
+    // ---- w2: dX tiles [kT1, kT2); stages Y1 (or dZ2) ----
+    auto load = [&](int k) {
+      if constexpr (MCC_BWD4_STAGE) load_dz2(k); else load_y1(k);
+      load_codes(k, kT2 - kT1);
+    };
+    auto stage = [&](int) {
+      if constexpr (MCC_BWD4_STAGE) stage_dz2(); else stage_y1();
+    };
+    auto compute = [&](int k) {
+      if constexpr (!(MCC_LENET_ABL & 2)) lenet_dx2_tiles<kT1, kT2>(smem, wdx, a1w, hxa, hxb, n16, g, dxci, dxj, dz1_of(k));
+    };
+    lenet_bwd4_loop(p, load, begin, compute, stage);
+  } else {
+    // ---- w3: conv1 dW of the previous image + dX tile 6; X0 rows 16..27 ----
+    int a1b[2], b1b;
+    {
+      const int m = n16 < 12 ? n16 : n16 - 12, co = kDw1Co[m], s2 = kDw1S[m];
+      const int base = kQDz1 + co * kBDz1Plane + (2 - 2 * s2) * 64;
+      a1b[0] = base + 16 * (g ^ 1 ^ s2);
+      a1b[1] = base + 16 * (g ^ s2);
+      if (n16 == 15) b1b = kQOne1 + 16 * g;
+      else {
+        const int kh = n16 / 5, kw = n16 % 5, c = kw & 3;
+        b1b = kQXs + c * kBxCopy + (kh * 40 + 8 * g + kw - c) * 2;
+      }
+    }
+    f32x4 acc1 = {0.f, 0.f, 0.f, 0.f};
+    auto dw1 = [&](int buf) {  // conv1 dW of the image staged in buffer `buf`
+      if constexpr (!(MCC_LENET_ABL & 4)) {
+        constexpr int D = MCC_DW1_D, NR = 30;
+        const int ao = buf * kQDz1buf, bo = n16 == 15 ? 0 : buf * kQXbuf;
+        bf16x8 a[D], b[D];
+#pragma unroll
+        for (int i = 0; i < D; ++i) {
+          a[i] = *reinterpret_cast<const bf16x8*>(smem + a1b[(i >> 1) & 1] + ao + i * 64);
+          b[i] = lds8(smem + b1b + bo + i * 80);
+        }
+#pragma unroll
+        for (int i = 0; i < NR; ++i) {
+          const bf16x8 ca = a[i % D], cb = b[i % D];
+          if (i + D < NR) {
+            const int zy = i + D;
+            a[i % D] = *reinterpret_cast<const bf16x8*>(smem + a1b[(zy >> 1) & 1] + ao + zy * 64);
+            b[i % D] = lds8(smem + b1b + bo + zy * 80);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+          acc1 = mma(acc1, ca, cb);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+    };
+    uint32_t xw[4 - kXw0] = {};
+    WaveIdx widx;
+    widx.load(p.idx, blockIdx.x, grid, p.B, 0);
+    auto load = [&](int k) {
+      LENET_LOAD_X(kXw0, 4 - kXw0)
+      if constexpr (kT2 < 7) load_codes(k, 7 - kT2);
+    };
+    auto stage = [&](int buf) { LENET_STAGE_X(kXw0, 4 - kXw0) };
+    auto compute = [&](int k) {
+      if (k > 0) dw1((k - 1) & 1);
+      if constexpr (!(MCC_LENET_ABL & 2) && kT2 < 7)
+        lenet_dx2_tiles<kT2, 7>(smem, wdx, a1w, hxa, hxb, n16, g, dxci, dxj, dz1_of(k));
+    };
+    const int n = lenet_bwd4_loop(p, load, begin, compute, stage);
+    if (n > 0) dw1((n - 1) & 1);  // the last image's conv1 dW
+#pragma unroll
+    for (int i = 0; i < 4; ++i) slab[kSlabW2 + i * 64 + lane] = acc1[i];
+  }
+}
+
 // Fixed-order sum of the per-wave slabs, mapped to the canonical gradients.
 // Block = 1024 threads over 64 slab positions: wave w sums slabs w, w+16, ...
 // of position blk*64 + lane (16 loads in flight per lane), then wave 0 adds
@@ -807,21 +1448,24 @@ __global__ void __launch_bounds__(64 * kRedWaves) lenet_bwd_reduce_kernel(LenetB
 
 }  // namespace
 
-int lenet_bwd_grid() { return 1024; }
-size_t lenet_slab_bytes() { return (size_t)lenet_bwd_grid() * kSlab * 4; }
+// two-wave kernel: 4 workgroups per CU; four-wave kernel: 2
+int lenet_bwd_grid() { return ab_flag("lenet_bwd2") ? 1024 : 512; }
+size_t lenet_slab_bytes() { return (size_t)1024 * kSlab * 4; }  // the larger of the two grids
 int lenet_y1_elems() { return kY1Elems; }
 int lenet_a1_bytes() { return kA1Bytes; }
 
 void lenet_forward(const LenetFwdParams& p, hipStream_t s) {
   if (p.B <= 0) return;
   const int grid = std::min(p.B, 256 * 16);
-  hipLaunchKernelGGL(lenet_fwd_kernel, dim3(grid), dim3(64), kFLds, s, p);
+  if (ab_flag("lenet_fwd1")) hipLaunchKernelGGL(lenet_fwd_kernel, dim3(grid), dim3(64), kFLds, s, p);
+  else hipLaunchKernelGGL(lenet_fwd2_kernel, dim3(grid), dim3(64), kGLds, s, p);
 }
 
 void lenet_backward(const LenetBwdParams& p, hipStream_t s) {
   if (p.B <= 0) return;
   const int grid = lenet_bwd_grid();
-  hipLaunchKernelGGL(lenet_bwd_kernel, dim3(grid), dim3(128), kBLds, s, p);
+  if (ab_flag("lenet_bwd2")) hipLaunchKernelGGL(lenet_bwd_kernel, dim3(grid), dim3(128), kBLds, s, p);
+  else hipLaunchKernelGGL(lenet_bwd4_kernel, dim3(grid), dim3(256), kQLds, s, p);
   hipLaunchKernelGGL(lenet_bwd_reduce_kernel, dim3(kSlab / 64), dim3(64 * kRedWaves), 0, s, p, grid);
 }
 

@@ -60,8 +60,10 @@ def _pool_codes(z):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("B", [1, 37, 300])
+@pytest.mark.parametrize("B", [1, 37, 300, 5000])
 def test_lenet_forward_matches_oracle(cuda, B):
+    """(B = 5000 > the 4096-wave grid: waves that take a second image reuse
+    their LDS tiles and the prefetched pixels)"""
     d = _case(B, 7 + B, cuda)
     _run_fwd(d, B)
     xs = d["x"].cpu()[d["idx"].cpu().long()].to(torch.float64)[:, None] / 255.0
@@ -100,8 +102,11 @@ def _unpool(dy, codes):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("B", [1, 37, 300])
+@pytest.mark.parametrize("B", [1, 37, 300, 1500, 2900])
 def test_lenet_backward_matches_oracle(cuda, B):
+    """(B > 512: several images per workgroup of the four-wave kernel, so its
+    one-image conv1-dW lag and double-buffered dZ1 / X0 are exercised, with a
+    ragged tail)"""
     d = _case(B, 100 + B, cuda)
     _run_fwd(d, B)
     g = torch.Generator().manual_seed(B)

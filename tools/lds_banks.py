@@ -400,3 +400,91 @@ def lenet_fwd_report(**kw):
 
 if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "lenet_fwd":
     lenet_fwd_report()
+
+
+# ---------------------------------------------------------------- lenet_fwd2 (round 5)
+def lenet_fwd2_accesses(FXP=36, CB=2320, P=16, c2win=None, c2tap=None, y1x=None):
+    """LDS instructions of one image of lenet.hip's lenet_fwd2_kernel: conv1 with
+    whole windows in a lane, 28 tiles of 2 pooled rows x 4 pooled columns, Y1 rows
+    of P pixel slots (16 B each), y1x(py, px) = extra byte offset (swizzle)."""
+    c2win = c2win or C2WIN
+    c2tap = c2tap or C2TAP
+    y1x = y1x or (lambda py, px: 0)
+    kY1 = 2 * CB
+    kA1 = kY1 + 14 * P * 16
+    L = range(64)
+    acc = []
+
+    def y1(py, px):
+        return kY1 + (py * P + px) * 16 + y1x(py, px)
+
+    for it in range(4):
+        for cp in range(2):
+            addrs = []
+            for l in L:
+                sk, srow = l & 7, l >> 3
+                yy = it * 8 + srow
+                addrs.append(((yy + 2) * FXP + 4 * sk) * 2 + cp * CB if yy < 28 else None)
+            acc.append(("x stage", "write_b64", addrs, 1))
+    for T in range(28):
+        py0, px0 = 2 * (T >> 2), 4 * (T & 3)
+        for part in range(4):
+            addrs = []
+            for l in L:
+                n16, g = l & 15, l >> 4
+                wa, ia = n16 >> 2, n16 & 3
+                a = (ia & 1) * CB + (2 * (wa >> 1) + (ia >> 1) + g) * FXP * 2 + 8 * (wa & 1)
+                a += py0 * 2 * FXP * 2 + 4 * px0
+                a += (4 * FXP * 2 if part >= 2 else 0) + (8 if part & 1 else 0)
+                addrs.append(a)
+            acc.append(("conv1 A", "read_b64", addrs, 1))
+        ya, aa = [], []
+        for l in L:
+            n16, g = l & 15, l >> 4
+            co, sh = n16 >> 1, n16 & 1
+            py, px = py0 + (g >> 1), px0 + 2 * (g & 1) + sh
+            ya.append(y1(py, px) + co * 2)
+            aa.append(kA1 + min(co, 6) * 240 + py * 16 + px)
+        acc.append(("y1 write", "write_b16", ya, 1))
+        acc.append(("a1 write", "write_b16", aa, 1))
+    for rr in range(4):
+        acc.append(("y1 bulk", "read_b128",
+                    [y1((l + 64 * rr) // 14, (l + 64 * rr) % 14) if l + 64 * rr < 196 else None for l in L], 1))
+    for T in range(7):
+        for c in range(7):
+            addrs = []
+            for l in L:
+                n16, g = l & 15, l >> 4
+                r = 16 * T + n16
+                wr = c2win[4 * (r >> 4) + ((r & 15) >> 2)]
+                w = 24 if wr < 0 else wr
+                pos = r & 3
+                t = c2tap[4 * c + g]
+                kh, kw = (t // 5, t % 5) if t < 25 else (0, 0)
+                addrs.append(y1(2 * (w // 5) + (pos >> 1) + kh, 2 * (w % 5) + (pos & 1) + kw))
+            acc.append(("conv2 A", "read_b128", addrs, 1))
+    return acc
+
+
+def lenet_fwd2_report(**kw):
+    acc = lenet_fwd2_accesses(**kw)
+    rows = {}
+    tot = ex = 0
+    for name, kind, addrs, n in acc:
+        c = cycles(kind, addrs)
+        e = c - ideal(kind)
+        r = rows.setdefault(name, [0, 0, 0])
+        r[0] += n
+        r[1] += n * c
+        r[2] += n * e
+        tot += n * c
+        ex += n * e
+    print(f"per image: {tot:.0f} LDS-array cycles, {ex:.0f} conflict cycles  {kw if kw else ''}")
+    for k, (n, c, e) in rows.items():
+        print(f"  {k:10s} {n:5.0f} instr {c:6.0f} cycles {e:5.0f} extra")
+    return tot, ex
+
+
+if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "lenet_fwd2":
+    for P in (16, 17, 18, 20):
+        lenet_fwd2_report(P=P)
