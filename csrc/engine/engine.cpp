@@ -1488,10 +1488,24 @@ std::vector<GpuBucket> GpuNet::buckets(int64_t bucket_bytes) const {
   for (const Bucket& b : plan_buckets(spec_, bucket_bytes)) {
     GpuBucket g;
     g.stage_hi = b.stage_hi; g.stage_lo = b.stage_lo; g.off = b.off; g.count = b.count;
-    // A fused conv block (lenet_bwd / ref_bwd) finishes stage 0's gradient in
-    // the same kernel as stage 1's: a separate stage-0 bucket would only add a
-    // second latency-bound collective at the end of the step.  Merge it into
-    // the bucket that holds stage 1 (parameters are contiguous, stage 0 first).
+    // A fused conv block (lenet_bwd / ref_bwd) produces stage 0's and stage
+    // 1's gradients in ONE kernel that runs after every later stage's
+    // backward (LeNet-5: the FC chain's gradients are final when loss()
+    // returns).  Cut the bucket that spans the block boundary so the later
+    // stages' all-reduce (LeNet-5: 96 % of the gradient bytes) is issued
+    // BEFORE the block's backward kernel and overlaps it on RCCL's stream;
+    // the block's own small bucket is the only collective left after it.
+    if ((lenet_ || refblk_) && b.stage_hi >= 2 && b.stage_lo <= 1) {
+      int64_t off2 = 0, cnt2 = 0;
+      stage_param_range(2, off2, cnt2);
+      GpuBucket hi = g, lo = g;
+      hi.stage_lo = 2; hi.off = off2; hi.count = b.off + b.count - off2;
+      lo.stage_hi = 1; lo.count = off2 - b.off;
+      out.push_back(hi);
+      g = lo;
+    }
+    // ... and stage 0 joins the block's bucket (same kernel; a separate
+    // stage-0 bucket would only add another latency-bound collective)
     if ((lenet_ || refblk_) && b.stage_hi == 0 && !out.empty() && out.back().stage_lo == 1 &&
         b.off + b.count == out.back().off) {
       out.back().stage_lo = 0;

@@ -1449,7 +1449,12 @@ __global__ void __launch_bounds__(64 * kRedWaves) lenet_bwd_reduce_kernel(LenetB
 }  // namespace
 
 // two-wave kernel: 4 workgroups per CU; four-wave kernel: 2
-int lenet_bwd_grid() { return ab_flag("lenet_bwd2") ? 1024 : 512; }
+// MCC_AB=bwd_reserve_cus=k leaves k CUs without a backward workgroup, for an
+// RCCL kernel that overlaps it (profiles/cu_contention_r5.txt)
+int lenet_bwd_grid() {
+  const int k = std::max(0, std::min(ab_int("bwd_reserve_cus", 0), 128));
+  return ab_flag("lenet_bwd2") ? 4 * (256 - k) : 2 * (256 - k);
+}
 size_t lenet_slab_bytes() { return (size_t)1024 * kSlab * 4; }  // the larger of the two grids
 int lenet_y1_elems() { return kY1Elems; }
 int lenet_a1_bytes() { return kA1Bytes; }

@@ -762,3 +762,17 @@ def test_dz_fused_into_next_dgrad_bit_equal(cuda, monkeypatch):
     for m in ("2",):
         np.testing.assert_array_equal(out[m][1], out["0"][1])
         np.testing.assert_array_equal(out[m][2], out["0"][2])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("model", ["lenet5", "ref"])
+def test_fused_block_buckets_split_at_block(cuda, model):
+    """The fused conv block's backward runs after every FC stage's: its
+    gradient is a bucket of its own, so the FC bucket's all-reduce is issued
+    before the block's backward kernel (overlap on RCCL's stream)."""
+    spec = mcc.make_model(model)
+    net = mcc.GpuNet(spec, "bf16", 256)
+    b = net.buckets(4 << 20)
+    assert [(hi, lo) for hi, lo, _, _ in b] == [(4, 2), (1, 0)], b
+    assert sum(c for _, _, _, c in b) == spec.nparams
+    assert b[1][2] == 0 and b[0][2] == b[1][3], b  # contiguous, stage 0 first in the flat buffer

@@ -36,6 +36,8 @@ def main() -> int:
     ap.add_argument("--batch", type=int, default=163840)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--model", default="lenet5")
+    ap.add_argument("--reserve-sweep", action="store_true",
+                    help="sweep MCC_AB=bwd_reserve_cus over 0/2/4/8 with holds during the backward")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     spec = mcc.make_model(a.model)
@@ -90,6 +92,21 @@ def main() -> int:
         torch.cuda.synchronize()
         print(f"cu_hold alone: 32 WG x 40 KB, {us:.0f} us requested -> {e0.elapsed_time(e1) * 1e3:.1f} us", flush=True)
 
+    if a.reserve_sweep:
+        # round 5: the FC bucket's all-reduce is issued before lenet_bwd; a
+        # backward grid that leaves k CUs free keeps a peer-waiting RCCL
+        # kernel off the static partition.  Per k: undisturbed step, holds
+        # during the backward.
+        for k in (0, 2, 4, 8):
+            os.environ["MCC_AB"] = f"bwd_reserve_cus={k}"
+            base = min(timed(None) for _ in range(3))
+            line = f"reserve {k} CUs: undisturbed {base:.4f} ms"
+            for nwg, us in ((4, 20.0), (4, 50.0), (16, 50.0)):
+                t = timed(("bwd", nwg, 40960, us))
+                line += f" | hold {nwg:2d} WG x {us:.0f} us {t:.4f} ({(t - base) * 1e3:+.1f} us)"
+            print(line, flush=True)
+        os.environ.pop("MCC_AB", None)
+        return 0
     base = [timed(None) for _ in range(2)]
     ref = min(base)
     print(f"model {a.model} batch {B}: undisturbed step {base[0]:.4f} / {base[1]:.4f} ms", flush=True)
