@@ -730,8 +730,13 @@ static int direct_grid(const Conv1DirectParams& p) {
 static int dw3_grid(const Conv1DirectParams& p) {
   return std::max(1, std::min((p.N + kDW3Imgs - 1) / kDW3Imgs, 256 * 4));
 }
+// LeNet-5's conv1 (28x28 u8, pad 2, 6 channels): the sparse kernel of lenet_f32.hip
+static bool lenet32_dw1_shape(const Conv1DirectParams& p) {
+  return p.Cin == 1 && p.C == 6 && p.KS == 5 && p.pad == 2 && p.H == 28 && p.W == 28 && p.PH == 14 && p.PW == 14;
+}
 size_t conv1_direct_slab_bytes(const Conv1DirectParams& p) {
-  return (size_t)std::max(direct_grid(p), dw3_grid(p)) * p.C * (p.KS * p.KS + 1) * 4;
+  const int g = std::max(std::max(direct_grid(p), dw3_grid(p)), lenet32_dw1_shape(p) ? lenet32_dw1_grid(p.N) : 0);
+  return (size_t)g * p.C * (p.KS * p.KS + 1) * 4;
 }
 
 void conv_direct_forward(const Conv1DirectParams& p, hipStream_t s) {
@@ -755,6 +760,11 @@ void conv1_direct_dw(const Conv1DirectParams& p, float* gw, float* gb, hipStream
   MCC_CHECK(conv1_direct_dw_supported(p) && p.x && p.dy && p.arg && p.slab, "conv1_direct_dw: bad params");
   const int grid = direct_grid(p);
   const dim3 g((unsigned)grid), b(kDT);
+  if (lenet32_dw1_shape(p) && !ab_flag("f32_dense_dw")) {
+    lenet32_dw1(p, s);
+    dw_reduce(p, lenet32_dw1_grid(p.N), gw, gb, s);
+    return;
+  }
   if (p.KS == 5 && p.C == 6) {
     const int g3 = dw3_grid(p);
     const size_t lds = (size_t)kDW3Imgs * d_tile(p).IMG * 4 + (size_t)kDW3Imgs * p.PH * p.PW * p.C * 5;
@@ -780,10 +790,15 @@ bool conv_direct_dw_supported(const Conv1DirectParams& p) {
          (p.PH * p.PW * p.C) % 4 == 0 && dw2_lds(p) <= 64 * 1024;
 }
 size_t conv_direct_dw_slab_bytes(const Conv1DirectParams& p) {
-  return (size_t)dw2_grid(p) * p.C * (p.Cin * p.KS * p.KS + 1) * 4;
+  return (size_t)std::max(dw2_grid(p), lenet32_dw2_grid(p.N)) * p.C * (p.Cin * p.KS * p.KS + 1) * 4;
 }
 void conv_direct_dw(const Conv1DirectParams& p, float* gw, float* gb, hipStream_t s) {
   MCC_CHECK(conv_direct_dw_supported(p) && p.xf && p.dy && p.arg && p.slab, "conv_direct_dw: bad params");
+  if (p.H == 14 && p.W == 14 && !ab_flag("f32_dense_dw")) {  // LeNet-5's conv2: sparse kernel (lenet_f32.hip)
+    lenet32_dw2(p, s);
+    dw_reduce(p, lenet32_dw2_grid(p.N), gw, gb, s);
+    return;
+  }
   const int grid = dw2_grid(p);
   // one channel pair per thread (NP = 1): 1,274 us at B = 131072 vs 1,409 us
   // with two pairs (fewer patch reads, but 158 registers and 3 waves per SIMD)

@@ -249,6 +249,13 @@ void conv1_direct_dw(const Conv1DirectParams& p, float* gw, float* gb, hipStream
 bool conv_direct_dw_supported(const Conv1DirectParams& p);
 size_t conv_direct_dw_slab_bytes(const Conv1DirectParams& p);
 void conv_direct_dw(const Conv1DirectParams& p, float* gw, float* gb, hipStream_t s);
+// LeNet-5 shapes: sparse (argmax-only) fp32 weight gradients, slab layout of
+// conv1_direct_dw's reduce (lenet_f32.hip); used by conv1_direct_dw /
+// conv_direct_dw unless MCC_AB=f32_dense_dw
+int lenet32_dw1_grid(int N);
+int lenet32_dw2_grid(int N);
+void lenet32_dw1(const Conv1DirectParams& p, hipStream_t s);
+void lenet32_dw2(const Conv1DirectParams& p, hipStream_t s);
 
 // Forward of the u8 RGB first conv (C = 3, 3x3, stride 1, pad 1, bias + ReLU
 // + 2x2/2 max-pool fused), bf16 MFMA, output pooled NHWC [N][H/2][W/2][Cout]

@@ -776,3 +776,37 @@ def test_fused_block_buckets_split_at_block(cuda, model):
     assert [(hi, lo) for hi, lo, _, _ in b] == [(4, 2), (1, 0)], b
     assert sum(c for _, _, _, c in b) == spec.nparams
     assert b[1][2] == 0 and b[0][2] == b[1][3], b  # contiguous, stage 0 first in the flat buffer
+
+
+@pytest.mark.gpu
+def test_fp32_lenet_sparse_dw_matches_dense(cuda, monkeypatch):
+    """fp32 LeNet-5's conv weight gradients from the argmax-only sparse kernels
+    (lenet_f32.hip) vs the masked dense direct kernels (MCC_AB=f32_dense_dw):
+    the same sums in a different order, per output channel to fp32 rounding.
+    B = 4099: several staged groups per workgroup and a ragged last group."""
+    spec = mcc.make_model("lenet5")
+    B = 4099
+    imgs, labels = mcc.synth_dataset(B, 1, 28, 28, 10, seed=21)
+    params = mcc.init_params(spec, seed=4, mode="fast").astype(np.float32)
+    d_img = torch.from_numpy(imgs).to(cuda)
+    d_lab = torch.from_numpy(labels).to(cuda)
+    idx = torch.randperm(B, device=cuda).to(torch.int32)
+
+    def grads(ab):
+        monkeypatch.setenv("MCC_AB", ab)
+        net = mcc.GpuNet(spec, "fp32", B)
+        net.set_params(params)
+        s = torch.cuda.current_stream().cuda_stream
+        net.forward(d_img.data_ptr(), idx.data_ptr(), B, s)
+        net.loss(d_lab.data_ptr(), idx.data_ptr(), 1.0 / B, True, s)
+        net.backward_all(s)
+        torch.cuda.synchronize()
+        return net.get_grads()
+
+    g_sparse, g_dense = grads(""), grads("f32_dense_dw")
+    for L in spec.layers()[:3]:
+        if L["nweights"] == 0:
+            continue
+        for off, n, what in ((L["w_off"], L["nweights"], "W"), (L["b_off"], L["nbiases"], "b")):
+            e, c = _per_channel_err(g_sparse[off : off + n], g_dense[off : off + n], L["C"], floor_frac=1e-3)
+            assert e < 1e-5, f"conv C={L['C']} {what}: channel {c} rel err {e:.3e}"
