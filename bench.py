@@ -162,6 +162,48 @@ def timed_run(args, spec, dtype, B, d_img, d_lab, dev, dev_idx, rank, world, mul
     return res
 
 
+def timed_run64(args, spec, B, d_img, d_lab, dev):
+    """The reference precision (fp64 throughout, cnn.c:22-30) on the GPU:
+    GpuNet64 (v_mfma_f64_16x16x4_f64 GEMMs, f64.hip) with a device-resident
+    batch (u8 gather by the device sampler's indices, /255 in fp64), forward,
+    softmax-CE, backward and SGD per step; no collectives (one GPU)."""
+    import torch
+
+    import mpi_cuda_cnn_amd as mcc
+
+    net = mcc._C.GpuNet64(spec, False, B)
+    net.set_params(mcc.init_params(spec, seed=0, mode="fast").astype("float64"))
+    K = mcc._C.kernels
+    idx_buf = torch.empty(B, dtype=torch.int32, device=dev)
+    counter = torch.zeros(1, dtype=torch.int64, device=dev)
+    s = net.stream  # GpuNet64's own stream: the sampler runs there too
+
+    def step():
+        K.sample_indices(idx_buf.data_ptr(), B, 0, args.dataset, 0x5EED0000, counter.data_ptr(), s)
+        net.forward_u8(d_img.data_ptr(), d_lab.data_ptr(), idx_buf.data_ptr(), B)
+        net.backward_device(1.0 / B)
+        net.sgd(args.lr)
+        K.advance_counter(counter.data_ptr(), s)
+
+    for _ in range(max(1, args.warmup)):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    loss = net.loss_sum() / B
+    del net
+    return {
+        "elapsed": elapsed,
+        "loss": round(loss, 4),
+        "launch": "per-kernel launches on GpuNet64's stream (fp64 GEMMs on v_mfma_f64_16x16x4_f64)",
+        "optimizer": f"sgd lr={args.lr} (plain SGD, the reference's Layer_update, cnn.c:303-314)",
+        "allreduce": "none (fp64 reference-precision path: one GPU)",
+    }
+
+
 def _self_launch(n: int) -> int:
     """Run this script under torch.distributed.run with n ranks on this node
     (rendezvous on 127.0.0.1, a free port) as a child process; rank 0's JSON
@@ -239,7 +281,7 @@ def main():
     dev_idx = local_rank % max(1, ndev)
     torch.cuda.set_device(dev_idx)
     dev = torch.device("cuda", dev_idx)
-    if world > 1 or not args.no_dist:
+    if (world > 1 or not args.no_dist) and args.dtype != "fp64":
         # RCCL process group at every N, 1 included: the N=1 step runs the
         # same broadcast + bucketed all-reduce on RCCL's stream as N=8
         from mpi_cuda_cnn_amd.parallel.ddp import init_process_group
@@ -253,7 +295,7 @@ def main():
     if args.model in SIDE_STREAM:
         ab = os.environ.get("MCC_AB", "")
         os.environ["MCC_AB"] = ",".join(x for x in (ab, "side_stream") if x)
-    B = args.batch_per_gpu or DEFAULT_BATCH.get(args.model, 1024)
+    B = args.batch_per_gpu or (16384 if args.dtype == "fp64" else DEFAULT_BATCH.get(args.model, 1024))
     if not args.dataset:
         args.dataset = max(65536, B) if H * W <= 32 * 32 else max(256, 8 * B)
     imgs, labels = mcc.synth_dataset(args.dataset, C, H, W, spec.num_classes(), seed=1234 + rank)
@@ -261,7 +303,13 @@ def main():
     d_lab = torch.from_numpy(labels).to(dev)
     multi = dist.is_initialized() and world > 1
 
-    head = timed_run(args, spec, args.dtype, B, d_img, d_lab, dev, dev_idx, rank, world, multi)
+    if args.dtype == "fp64":
+        if world > 1:
+            raise SystemExit("bench: --dtype fp64 (the reference precision, GpuNet64) runs on one GPU")
+        head = timed_run64(args, spec, B, d_img, d_lab, dev)
+        args.fp32_extra = "off"
+    else:
+        head = timed_run(args, spec, args.dtype, B, d_img, d_lab, dev, dev_idx, rank, world, multi)
     # BASELINE config 2 ("LeNet-5 fp32 on one MI355X") in the same run: a
     # second trainer after the first is freed, same graph replay, same K / W
     extra = None

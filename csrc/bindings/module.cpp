@@ -238,6 +238,26 @@ PYBIND11_MODULE(_C, m) {
       .def_property_readonly("params_ptr", [](const GpuNet64& n) { return reinterpret_cast<uintptr_t>(n.device_params()); })
       .def_property_readonly("grads_ptr", [](const GpuNet64& n) { return reinterpret_cast<uintptr_t>(n.device_grads()); })
       .def_property_readonly("stream", [](const GpuNet64& n) { return reinterpret_cast<uintptr_t>(n.stream()); })
+      .def("forward_u8",
+           [](GpuNet64& n, uintptr_t data, uintptr_t labels, uintptr_t idx, int B) {
+             n.forward_u8(reinterpret_cast<const uint8_t*>(data), reinterpret_cast<const uint8_t*>(labels),
+                          reinterpret_cast<const int32_t*>(idx), B);
+           },
+           py::arg("data"), py::arg("labels"), py::arg("idx"), py::arg("B"),
+           "device-resident batch: rows idx[0..B) of the u8 dataset (/255) and their labels; no host sync")
+      .def("backward_device", &GpuNet64::backward_device, py::arg("scale"),
+           "backward of the last forward_u8 with device labels; per-sample stats stay on the device")
+      .def("loss_sum",
+           [](const GpuNet64& n) {
+             // sum of -log p_label over the last backward's batch (synchronises)
+             std::vector<double> st(3 * (size_t)n.batch());
+             if (hipDeviceSynchronize() != hipSuccess) throw Error("hipDeviceSynchronize failed");
+             if (hipMemcpy(st.data(), n.device_stats(), 8 * st.size(), hipMemcpyDeviceToHost) != hipSuccess)
+               throw Error("hipMemcpy failed");
+             double s = 0.0;
+             for (int b = 0; b < n.batch(); ++b) s += st[3 * b];
+             return s;
+           })
       .def("get_params", [](const GpuNet64& n) { py::array_t<double> a(n.nparams()); n.get_params(a.mutable_data()); return a; })
       .def("get_grads", [](const GpuNet64& n) { py::array_t<double> a(n.nparams()); n.get_grads(a.mutable_data()); return a; })
       .def("set_params", [](GpuNet64& n, F64 a) {

@@ -198,11 +198,25 @@ StepStats GpuNet64::evaluate(const int* labels) {
   return read_stats();
 }
 
+void GpuNet64::forward_u8(const uint8_t* data, const uint8_t* labels, const int32_t* idx, int B) {
+  MCC_CHECK(B > 0 && B <= max_batch_, "GpuNet64::forward_u8: bad batch");
+  const int npix = (int)spec_.input_nodes();
+  // the input layer's activation buffer holds the normalised batch
+  gpu::u8_batch64(data, labels, idx, act_[0], labels_, B, npix, stream_);
+  forward_device(act_[0], B);
+}
+
 StepStats GpuNet64::backward(const int* labels, double scale) {
+  MCC_CHECK(B_ > 0, "GpuNet64::backward before forward");
+  upload_labels(labels);
+  backward_device(scale);
+  return read_stats();
+}
+
+void GpuNet64::backward_device(double scale) {
   MCC_CHECK(B_ > 0, "GpuNet64::backward before forward");
   const int B = B_;
   const size_t n = spec_.layers.size();
-  upload_labels(labels);
   gpu::out_err64(act_.back(), labels_, err_.back(), stats_, B, spec_.num_classes(), scale, stream_);
   for (size_t li = n - 1; li >= 1; --li) {
     const LayerSpec& L = spec_.layers[li];
@@ -215,7 +229,7 @@ StepStats GpuNet64::backward(const int* labels, double scale) {
       const int kk = L.ks * L.ks, P = L.H * L.W;
       const int64_t K = (int64_t)L.inC * kk, BP = (int64_t)B * P;
       gpu::dz64(err_[li], act_[li], dz_, B, L.C, P, act_kind(L.act), stream_);
-      gpu::rowsum64(dz_, gb, L.C, BP, stream_);
+      gpu::rowsum64(dz_, gb, L.C, BP, part_, stream_);
       // gW[C][K] += dZ^T[C][BP] col^T[BP][K]
       gpu::Gemm64Params p;
       p.M = L.C; p.N = (int)K; p.K = BP;
@@ -249,7 +263,7 @@ StepStats GpuNet64::backward(const int* labels, double scale) {
       const bool last = li + 1 == n;
       const int64_t nin = L.in_nodes();
       gpu::dz64(err_[li], act_[li], dz_, B, L.C, 1, last ? gpu::ACT_NONE : act_kind(L.act), stream_);
-      gpu::rowsum64(dz_, gb, L.C, B, stream_);
+      gpu::rowsum64(dz_, gb, L.C, B, part_, stream_);
       // gW[C][nin] += dZ^T[C][B] X[B][nin]
       gpu::Gemm64Params p;
       p.M = L.C; p.N = (int)nin; p.K = B;
@@ -269,7 +283,6 @@ StepStats GpuNet64::backward(const int* labels, double scale) {
     }
   }
   HIP_OK(hipGetLastError());
-  return read_stats();
 }
 
 void GpuNet64::sgd(double lr) {

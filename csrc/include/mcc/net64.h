@@ -58,6 +58,13 @@ class GpuNet64 {
   StepStats backward(const int* labels, double scale);
   StepStats evaluate(const int* labels);
   void sgd(double lr);  // params -= lr * grads; grads = 0
+  // Device-resident training step pieces without host synchronisation (the
+  // throughput path, bench.py --dtype fp64): forward of the u8 dataset rows
+  // idx[0..B) (/255 in fp64), and the backward with the labels gathered on the
+  // device; per-sample stats stay on the device (device_stats).
+  void forward_u8(const uint8_t* data, const uint8_t* labels, const int32_t* idx, int B);
+  void backward_device(double scale);
+  const double* device_stats() const { return stats_; }
   void zero_grads();
 
  private:

@@ -13,6 +13,8 @@
 // slabs instead of atomics, gathers instead of scatters (col2im, unpool).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "kernels.h"
 
 namespace mcc {
@@ -22,7 +24,7 @@ namespace {
 
 using f64x4 = __attribute__((ext_vector_type(4))) double;
 
-constexpr int kTM = 64, kTN = 64, kTK = 16;
+constexpr int kTK = 16;
 constexpr int kPitch = 80;  // LDS row pitch (doubles): the 4 k rows a 16x16x4 operand read touches sit 128 B apart
 
 __device__ __forceinline__ double act_f(int act, double v) {
@@ -42,49 +44,56 @@ __device__ __forceinline__ void g64_store(const Gemm64Params& p, int m, int n, d
   *dst = v;
 }
 
-// 64x64 output tile per 256-thread workgroup; wave w owns the 32x32 quadrant
-// (w >> 1, w & 1) as 2x2 MFMA blocks.  Operands are staged k-major in LDS
-// ([k][m], [k][n]) with register prefetch of the next k tile; the global load
-// order follows whichever operand dimension is unit-stride.
+// TS x TS output tile per 256-thread workgroup (TS = 64 or 32); wave w owns
+// the (TS/2)^2 quadrant (w >> 1, w & 1) as (TS/32)^2 MFMA blocks.  Operands
+// are staged k-major in LDS ([k][m], [k][n]) with register prefetch of the
+// next k tile; the global load order follows whichever operand dimension is
+// unit-stride.  TS = 32 serves the skinny weight-gradient products (the
+// reference model's conv1 dW is 16 x 9 over K = B * 196: a 64-tile computed
+// 28x the useful MACs).
+template <int TS>
 __global__ void __launch_bounds__(256) gemm64_kernel(Gemm64Params p) {
-  __shared__ double As[kTK][kPitch];
-  __shared__ double Bs[kTK][kPitch];
+  constexpr int NB = TS / 32;             // MFMA blocks per wave dimension
+  constexpr int NL = TS * kTK / 256;      // staged elements per thread per operand
+  constexpr int PITCH = TS == 64 ? kPitch : 48;
+  __shared__ double As[kTK][PITCH];
+  __shared__ double Bs[kTK][PITCH];
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-  const int m0 = blockIdx.y * kTM, n0 = blockIdx.x * kTN;
+  const int m0 = blockIdx.y * TS, n0 = blockIdx.x * TS;
   const int64_t kbeg = (int64_t)blockIdx.z * p.kchunk;
   const int64_t kend = kbeg + p.kchunk < p.K ? kbeg + p.kchunk : p.K;
   const bool a_kfast = p.sak == 1, b_nfast = p.sbn == 1;
 
-  double ra[4], rb[4];
+  double ra[NL], rb[NL];
   auto fetch = [&](int64_t k0) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < NL; ++j) {
       const int e = t + 256 * j;
       int m, k;
-      if (a_kfast) { k = e & 15; m = e >> 4; } else { m = e & 63; k = e >> 6; }
+      if (a_kfast) { k = e & 15; m = e >> 4; } else { m = e % TS; k = e / TS; }
       const int64_t gk = k0 + k;
       ra[j] = (m0 + m < p.M && gk < kend) ? p.A[(int64_t)(m0 + m) * p.sam + gk * p.sak] : 0.0;
       int n;
-      if (b_nfast) { n = e & 63; k = e >> 6; } else { k = e & 15; n = e >> 4; }
+      if (b_nfast) { n = e % TS; k = e / TS; } else { k = e & 15; n = e >> 4; }
       const int64_t gk2 = k0 + k;
       rb[j] = (n0 + n < p.N && gk2 < kend) ? p.B[gk2 * p.sbk + (int64_t)(n0 + n) * p.sbn] : 0.0;
     }
   };
   auto stash = [&]() {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < NL; ++j) {
       const int e = t + 256 * j;
-      if (a_kfast) As[e & 15][e >> 4] = ra[j]; else As[e >> 6][e & 63] = ra[j];
-      if (b_nfast) Bs[e >> 6][e & 63] = rb[j]; else Bs[e & 15][e >> 4] = rb[j];
+      if (a_kfast) As[e & 15][e >> 4] = ra[j]; else As[e / TS][e % TS] = ra[j];
+      if (b_nfast) Bs[e / TS][e % TS] = rb[j]; else Bs[e & 15][e >> 4] = rb[j];
     }
   };
 
-  f64x4 acc[2][2];
+  f64x4 acc[NB][NB];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < NB; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = f64x4{0.0, 0.0, 0.0, 0.0};
-  const int wm = (wave >> 1) * 32, wn = (wave & 1) * 32;
+    for (int j = 0; j < NB; ++j) acc[i][j] = f64x4{0.0, 0.0, 0.0, 0.0};
+  const int wm = (wave >> 1) * (TS / 2), wn = (wave & 1) * (TS / 2);
   const int r = lane & 15, q = lane >> 4;
 
   if (kbeg < kend) fetch(kbeg);
@@ -95,19 +104,23 @@ __global__ void __launch_bounds__(256) gemm64_kernel(Gemm64Params p) {
     if (k0 + kTK < kend) fetch(k0 + kTK);
 #pragma unroll
     for (int s = 0; s < kTK / 4; ++s) {
-      const double a0 = As[4 * s + q][wm + r], a1 = As[4 * s + q][wm + 16 + r];
-      const double b0 = Bs[4 * s + q][wn + r], b1 = Bs[4 * s + q][wn + 16 + r];
-      acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc[0][0], 0, 0, 0);
-      acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, acc[0][1], 0, 0, 0);
-      acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, acc[1][0], 0, 0, 0);
-      acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[1][1], 0, 0, 0);
+      double a[NB], bb[NB];
+#pragma unroll
+      for (int i = 0; i < NB; ++i) {
+        a[i] = As[4 * s + q][wm + 16 * i + r];
+        bb[i] = Bs[4 * s + q][wn + 16 * i + r];
+      }
+#pragma unroll
+      for (int i = 0; i < NB; ++i)
+#pragma unroll
+        for (int j = 0; j < NB; ++j) acc[i][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[i], bb[j], acc[i][j], 0, 0, 0);
     }
   }
   // f64 C/D map: col = lane & 15, row = (lane >> 4) + 4 * reg
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < NB; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < NB; ++j)
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const int m = m0 + wm + 16 * i + q + 4 * g, n = n0 + wn + 16 * j + r;
@@ -192,20 +205,32 @@ __global__ void dz64_kernel(const double* err, const double* y, double* dzT, int
   dzT[(int64_t)o * B * P + (int64_t)b * P + pp] = err[e] * act_g(act, y[e]);
 }
 
-// gb[o] += sum_n dzT[o][n]: one workgroup per row, fixed-order strided
-// partials and a fixed tree
-__global__ void __launch_bounds__(256) rowsum64_kernel(const double* dzT, double* gb, int64_t n) {
-  __shared__ double part[256];
-  const double* row = dzT + blockIdx.x * n;
+// gb[o] += sum_n dzT[o][n] in two fixed-order levels: S workgroups per row
+// each sum a contiguous chunk (strided partials + a fixed tree) into
+// part[o][s], then one thread per row adds its S partials in slab order.
+// (One workgroup per row left the reference model's conv1 bias -- 16 rows of
+// B * 196 -- on 16 CUs: 5 ms of a 13 ms fp64 step at B = 16384.)
+__global__ void __launch_bounds__(256) rowsum64_kernel(const double* dzT, double* part, int64_t n, int64_t chunk) {
+  __shared__ double red[256];
+  const int row = blockIdx.y, sl = blockIdx.x;
+  const double* src = dzT + (int64_t)row * n;
+  const int64_t j0 = (int64_t)sl * chunk, j1 = j0 + chunk < n ? j0 + chunk : n;
   double v = 0.0;
-  for (int64_t j = threadIdx.x; j < n; j += 256) v += row[j];
-  part[threadIdx.x] = v;
+  for (int64_t j = j0 + threadIdx.x; j < j1; j += 256) v += src[j];
+  red[threadIdx.x] = v;
   __syncthreads();
   for (int w = 128; w > 0; w >>= 1) {
-    if ((int)threadIdx.x < w) part[threadIdx.x] += part[threadIdx.x + w];
+    if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
     __syncthreads();
   }
-  if (threadIdx.x == 0) gb[blockIdx.x] += part[0];
+  if (threadIdx.x == 0) part[(int64_t)row * gridDim.x + sl] = red[0];
+}
+__global__ void rowsum64_finish_kernel(const double* part, double* gb, int rows, int S) {
+  const int o = blockIdx.x * blockDim.x + threadIdx.x;
+  if (o >= rows) return;
+  double v = 0.0;
+  for (int s = 0; s < S; ++s) v += part[(int64_t)o * S + s];
+  gb[o] += v;
 }
 
 // max pool, first maximum wins (cpu_net.cpp pool_fwd); arg = flat input index
@@ -279,6 +304,17 @@ __global__ void out_err64_kernel(const double* p, const int32_t* labels, double*
   stats[3 * b + 2] = mj == lab ? 1.0 : 0.0;
 }
 
+// device-resident batch: x[b] = dataset[idx[b]] / 255 (cnn.c:457), labels[b] = lab[idx[b]]
+__global__ void u8_batch64_kernel(const uint8_t* data, const uint8_t* lab, const int32_t* idx, double* x,
+                                  int32_t* labels, int B, int npix) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= (int64_t)B * npix) return;
+  const int b = (int)(e / npix), i = (int)(e - (int64_t)b * npix);
+  const int src = idx ? idx[b] : b;
+  x[e] = (double)data[(int64_t)src * npix + i] / 255.0;
+  if (i == 0) labels[b] = lab[src];
+}
+
 __global__ void sgd64_kernel(double* w, double* g, double lr, int64_t n) {
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= n) return;
@@ -290,26 +326,41 @@ unsigned blocks(int64_t n, int t = 256) { return (unsigned)((n + t - 1) / t); }
 
 }  // namespace
 
+void u8_batch64(const uint8_t* data, const uint8_t* lab, const int32_t* idx, double* x, int32_t* labels, int B,
+                int npix, hipStream_t s) {
+  hipLaunchKernelGGL(u8_batch64_kernel, dim3(blocks((int64_t)B * npix)), dim3(256), 0, s, data, lab, idx, x, labels,
+                     B, npix);
+}
+
+static int gemm64_tile(int M, int N);
+
 int gemm64_slabs(int M, int N, int64_t K) {
   // enough (tile, slab) workgroups to cover the 256 CUs twice, slabs of at
   // least 256 k; a function of the shape only (deterministic results)
-  const int64_t tiles = (int64_t)((M + kTM - 1) / kTM) * ((N + kTN - 1) / kTN);
+  const int TS = gemm64_tile(M, N);
+  const int64_t tiles = (int64_t)((M + TS - 1) / TS) * ((N + TS - 1) / TS);
   int64_t s = 512 / tiles;
   const int64_t kmax = (K + 255) / 256;
   if (s > kmax) s = kmax;
   return s < 1 ? 1 : (int)s;
 }
 
+// 32-tiles when either output dimension is at most 32 (skinny weight
+// gradients / FC layers with few outputs), else 64-tiles
+static int gemm64_tile(int M, int N) { return (M <= 32 || N <= 32) ? 32 : 64; }
+
 void gemm64(const Gemm64Params& p0, double* part, hipStream_t s) {
   Gemm64Params p = p0;
+  const int TS = gemm64_tile(p.M, p.N);
   const int nslab = part ? gemm64_slabs(p.M, p.N, p.K) : 1;
   int64_t kc = (p.K + nslab - 1) / nslab;
   kc = (kc + kTK - 1) / kTK * kTK;
   const int z = (int)((p.K + kc - 1) / kc);
   p.kchunk = kc;
   p.part = z > 1 ? part : nullptr;
-  dim3 grid((unsigned)((p.N + kTN - 1) / kTN), (unsigned)((p.M + kTM - 1) / kTM), (unsigned)(z > 0 ? z : 1));
-  hipLaunchKernelGGL(gemm64_kernel, grid, dim3(256), 0, s, p);
+  dim3 grid((unsigned)((p.N + TS - 1) / TS), (unsigned)((p.M + TS - 1) / TS), (unsigned)(z > 0 ? z : 1));
+  if (TS == 32) hipLaunchKernelGGL(gemm64_kernel<32>, grid, dim3(256), 0, s, p);
+  else hipLaunchKernelGGL(gemm64_kernel<64>, grid, dim3(256), 0, s, p);
   if (z > 1) hipLaunchKernelGGL(gemm64_reduce_kernel, dim3(blocks((int64_t)p.M * p.N)), dim3(256), 0, s, p, z);
 }
 
@@ -330,8 +381,14 @@ void fold64(const double* full, double* gw, int C, int Ci, int kk, hipStream_t s
 void dz64(const double* err, const double* y, double* dzT, int B, int C, int P, int act, hipStream_t s) {
   hipLaunchKernelGGL(dz64_kernel, dim3(blocks((int64_t)B * C * P)), dim3(256), 0, s, err, y, dzT, B, C, P, act);
 }
-void rowsum64(const double* dzT, double* gb, int rows, int64_t n, hipStream_t s) {
-  hipLaunchKernelGGL(rowsum64_kernel, dim3(rows), dim3(256), 0, s, dzT, gb, n);
+void rowsum64(const double* dzT, double* gb, int rows, int64_t n, double* part, hipStream_t s) {
+  // slabs per row: ~1024 workgroups in all, chunks of at least 4096 (a
+  // function of the shape only: deterministic)
+  int64_t S = std::max<int64_t>(1, std::min<int64_t>(1024 / std::max(rows, 1), (n + 4095) / 4096));
+  const int64_t chunk = (n + S - 1) / S;
+  S = (n + chunk - 1) / chunk;
+  hipLaunchKernelGGL(rowsum64_kernel, dim3((unsigned)S, (unsigned)rows), dim3(256), 0, s, dzT, part, n, chunk);
+  hipLaunchKernelGGL(rowsum64_finish_kernel, dim3(blocks(rows)), dim3(256), 0, s, part, gb, rows, (int)S);
 }
 void pool64_fwd(const Pool64Geom& g, const double* x, double* y, int32_t* arg, int B, hipStream_t s) {
   hipLaunchKernelGGL(pool64_fwd_kernel, dim3(blocks((int64_t)B * g.C * g.OH * g.OW)), dim3(256), 0, s, g, x, y, arg, B);

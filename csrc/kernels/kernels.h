@@ -698,13 +698,16 @@ void col2im64(const Conv64Geom& g, const double* dcol, double* dx, int B, hipStr
 void weff64(const double* w, double* weff, int C, int Ci, int kk, hipStream_t s);
 void fold64(const double* full, double* gw, int C, int Ci, int kk, hipStream_t s);
 void dz64(const double* err, const double* y, double* dzT, int B, int C, int P, int act, hipStream_t s);
-void rowsum64(const double* dzT, double* gb, int rows, int64_t n, hipStream_t s);
+void rowsum64(const double* dzT, double* gb, int rows, int64_t n, double* part, hipStream_t s);
 void pool64_fwd(const Pool64Geom& g, const double* x, double* y, int32_t* arg, int B, hipStream_t s);
 void pool64_bwd(const Pool64Geom& g, const double* er, const int32_t* arg, double* dx, int B, hipStream_t s);
 void softmax64(double* z, int B, int C, bool ref_compat, hipStream_t s);
 void out_err64(const double* p, const int32_t* labels, double* err, double* stats, int B, int C, double scale,
                hipStream_t s);
 void sgd64(double* w, double* g, double lr, int64_t n, hipStream_t s);
+// x[b] = data[idx[b]] / 255 (doubles), labels[b] = lab[idx[b]] (idx nullable)
+void u8_batch64(const uint8_t* data, const uint8_t* lab, const int32_t* idx, double* x, int32_t* labels, int B,
+                int npix, hipStream_t s);
 
 }  // namespace gpu
 }  // namespace mcc
