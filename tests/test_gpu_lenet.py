@@ -59,9 +59,18 @@ def _pool_codes(z):
     return v, pos, gap
 
 
+@pytest.fixture(params=["", "lenet_fwd1,lenet_bwd2"], ids=["round5", "round4"])
+def kernel_gen(request, monkeypatch):
+    """The default kernels (window-in-lane forward lenet_fwd2, four-wave
+    backward lenet_bwd4) and, under MCC_AB=lenet_fwd1,lenet_bwd2, the round-4
+    pair they replaced: both against the same oracle."""
+    monkeypatch.setenv("MCC_AB", request.param)
+    return request.param
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("B", [1, 37, 300, 5000])
-def test_lenet_forward_matches_oracle(cuda, B):
+def test_lenet_forward_matches_oracle(cuda, B, kernel_gen):
     """(B = 5000 > the 4096-wave grid: waves that take a second image reuse
     their LDS tiles and the prefetched pixels)"""
     d = _case(B, 7 + B, cuda)
@@ -103,7 +112,7 @@ def _unpool(dy, codes):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("B", [1, 37, 300, 1500, 2900])
-def test_lenet_backward_matches_oracle(cuda, B):
+def test_lenet_backward_matches_oracle(cuda, B, kernel_gen):
     """(B > 512: several images per workgroup of the four-wave kernel, so its
     one-image conv1-dW lag and double-buffered dZ1 / X0 are exercised, with a
     ragged tail)"""
