@@ -31,8 +31,16 @@
 //    per wave, reduced in a fixed order (deterministic).
 #include "kernels.h"
 #include "mfma.h"
+#include "mcc/ab.h"
 
 #include <algorithm>
+
+// ref_bwd2 phase ablations (timing studies only; tools/build_variant.sh):
+// 1 = wave 0 skips conv1 + dW2, 2 = wave 1 skips everything, 4 = wave 0 skips
+// dW2, 8 = wave 1 skips conv1 dW
+#ifndef MCC_REF_ABL
+#define MCC_REF_ABL 0
+#endif
 
 namespace mcc {
 namespace gpu {
@@ -84,7 +92,14 @@ __device__ __forceinline__ uint32_t from_left(uint32_t v) {
   return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, true);
 }
 __device__ __forceinline__ uint32_t mid16(uint32_t a, uint32_t b) { return __builtin_amdgcn_alignbit(b, a, 16); }
+#ifndef MCC_REF_FENCE
+#define MCC_REF_FENCE 0
+#endif
+#if MCC_REF_FENCE
+__device__ __forceinline__ void wave_lds_sync() { asm volatile("" ::: "memory"); }
+#else
 __device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+#endif
 __device__ __forceinline__ bf16x8 tr8(const char* p0, const char* p1) {
   const bf16x4 a = tr4(reinterpret_cast<const bf16*>(p0));
   const bf16x4 b = tr4(reinterpret_cast<const bf16*>(p1));
@@ -93,8 +108,21 @@ __device__ __forceinline__ bf16x8 tr8(const char* p0, const char* p1) {
 __device__ __forceinline__ bf16x8 join(const bf16x4& a, const bf16x4& b) {
   return __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
 }
-__device__ __forceinline__ u32x2 pack4(float a, float b, float c, float d) {
-  return u32x2{bf16_bits(a) | (bf16_bits(b) << 16), bf16_bits(c) | (bf16_bits(d) << 16)};
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+// two floats -> two bf16 (RNE) in one v_cvt_pk_bf16_f32
+__device__ __forceinline__ uint32_t cvt2(float a, float b) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2{a, b}), bf16x2));
+}
+__device__ __forceinline__ u32x2 pack4(float a, float b, float c, float d) { return u32x2{cvt2(a, b), cvt2(c, d)}; }
+// ReLU on the bit pattern (one v_max_i32, no NaN canonicalisation): negative
+// values and -0 become +0, so a stored zero is always +0
+__device__ __forceinline__ float relu(float v) { return __builtin_bit_cast(float, max(__builtin_bit_cast(int, v), 0)); }
+// nonzero bits of four non-negative bf16 (two packed words): h + 0x7fff
+// carries into bit 15 of its half iff h != 0, never across halves (h <= 0x7fc0)
+__device__ __forceinline__ uint32_t nz4(u32x2 v) {
+  const uint32_t t0 = v.x + 0x7fff7fffu, t1 = v.y + 0x7fff7fffu;
+  return ((t0 >> 15) & 1u) | ((t0 >> 30) & 2u) | ((t1 >> 13) & 4u) | ((t1 >> 28) & 8u);
 }
 
 struct WaveIdx {
@@ -241,8 +269,8 @@ __global__ void __launch_bounds__(64) ref_fwd_kernel(RefFwdParams p) {
       f32x4 acc = {b1v[0], b1v[1], b1v[2], b1v[3]};
       acc = mma(acc, w1, pb);
       // lane (pixel, g): channels 4g .. 4g+3
-      const u32x2 v = pack4(fmaxf(acc[0], 0.f) * (1.f / 255.f), fmaxf(acc[1], 0.f) * (1.f / 255.f),
-                            fmaxf(acc[2], 0.f) * (1.f / 255.f), fmaxf(acc[3], 0.f) * (1.f / 255.f));
+      const u32x2 v = pack4(relu(acc[0]) * (1.f / 255.f), relu(acc[1]) * (1.f / 255.f),
+                            relu(acc[2]) * (1.f / 255.f), relu(acc[3]) * (1.f / 255.f));
       if (16 * T + n16 < 196) *reinterpret_cast<u32x2*>(smem + kFY1 + ((y + 1) * 15 + x + 1) * 32 + 8 * g) = v;
     }
     wave_lds_sync();
@@ -268,7 +296,7 @@ __global__ void __launch_bounds__(64) ref_fwd_kernel(RefFwdParams p) {
 #pragma unroll
         for (int mt = 0; mt < 2; ++mt)
           *reinterpret_cast<u32x2*>(y2g + q * 32 + 16 * mt + 4 * g) =
-              pack4(fmaxf(acc[mt][0], 0.f), fmaxf(acc[mt][1], 0.f), fmaxf(acc[mt][2], 0.f), fmaxf(acc[mt][3], 0.f));
+              pack4(relu(acc[mt][0]), relu(acc[mt][1]), relu(acc[mt][2]), relu(acc[mt][3]));
       }
     }
   }
@@ -387,8 +415,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1)))
         const bf16x8 pb = conv1_patch(smem, kBX0, kBX2, ok ? y : 0, ok ? x : 0, g);
         f32x4 acc = {b1v[0], b1v[1], b1v[2], b1v[3]};
         acc = mma(acc, w1, pb);
-        const float v0 = fmaxf(acc[0], 0.f) * (1.f / 255.f), v1 = fmaxf(acc[1], 0.f) * (1.f / 255.f);
-        const float v2 = fmaxf(acc[2], 0.f) * (1.f / 255.f), v3 = fmaxf(acc[3], 0.f) * (1.f / 255.f);
+        const float v0 = relu(acc[0]) * (1.f / 255.f), v1 = relu(acc[1]) * (1.f / 255.f);
+        const float v2 = relu(acc[2]) * (1.f / 255.f), v3 = relu(acc[3]) * (1.f / 255.f);
         const u32x2 v = pack4(v0, v1, v2, v3);
         // mask on the stored (bf16) value, as the forward's consumer saw it
         const uint32_t bits = ((v.x & 0xffffu) ? 1u : 0u) | ((v.x >> 16) ? 2u : 0u) | ((v.y & 0xffffu) ? 4u : 0u) |
@@ -467,6 +495,285 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1)))
   for (int i = 0; i < 4; ++i) slab[kSlabW2 + i * 64 + lane] = acc1[i];
 }
 
+// ---- two-wave backward ----
+// ref_bwd_kernel runs one wave per SIMD (its 80 dW2 accumulators plus the 36
+// dX weight registers do not fit two waves), so every LDS / MFMA latency of
+// the image's serial chain is exposed. Here a workgroup of two waves shares
+// one image at a time, the roles split by register set:
+//   wave 0: accumulates conv2 dW / db of image k (40 MFMAs), then stages
+//           image k+1 (global loads issued before image k's compute, LDS
+//           writes after it) and recomputes ITS conv1 (16 MFMAs) -> Y1
+//           (wave-private) and the ReLU mask bits, which it hands to wave 1
+//           through LDS (the mask lanes are wave 1's dX output lanes);
+//   wave 1: conv2 dX -> dZ1 (wave-private), conv1 dW / db (36 + 7 MFMAs).
+// (Recomputing conv1 in both waves cost wave 1 -- the critical one -- ~90 us
+// per step.) The column-parity planes, dZ2 and the mask are double-buffered,
+// so the waves meet at ONE barrier per image. 2 waves per SIMD.
+constexpr int kB2X0 = 0, kB2X2 = kXCopy;      // integer X copies (wave 0 only)
+constexpr int kB2Buf = 2 * kXCopy;             // 3840: two buffers of [Xc | dZ2 | mask]
+constexpr int kB2Xc = 0;                       // + buffer: column-parity planes E / O / Os
+constexpr int kB2Dz2 = 3 * kXcPlane;           // + buffer: dZ2 HWC 9 x 9 x 64 B (2880), see dz2_chunk
+constexpr int kB2Mask = kB2Dz2 + 81 * 64;      // + buffer: ReLU mask, 64 lanes x 8 B (8064)
+constexpr int kB2BufBytes = kB2Mask + 64 * 8;  // 8576
+// Y1 / dZ1: 40-B pixels (8-B channel quads, one 8-B pad), rows of 624 / 640 B,
+// quad q of row r stored at quad q ^ ((r >> 1) & 1); dZ2: the 16-B channel
+// chunk c of row i at chunk c ^ 2 (i & 1). With these, the phase-order Y1 /
+// dZ1 writes (16 lanes of one quad at pixels 2 apart: 8-way conflicts on
+// 32-B HWC pixels), the conv2 dX reads and the transposed dW reads are
+// (nearly) conflict-free: 1,459 -> 510 LDS cycles per image, 1,039 -> 90 of
+// them conflicts (python tools/lds_banks.py refbwd).
+constexpr int kY1Px = 40, kY1Row = 624, kZ1Px = 40, kZ1Row = 640;
+constexpr int kB2Y1 = kB2Buf + 2 * kB2BufBytes;  // 20992: Y1, 15 x 15 pixels (pad row / column 0) (wave 0)
+constexpr int kB2Dz1 = kB2Y1 + 15 * kY1Row;      // 30352: dZ1, 14 x 16 pixels (columns 14, 15 pads) (wave 1)
+constexpr int kB2Ones = kB2Dz1 + 14 * kZ1Row;    // 39312
+constexpr int kB2Lds = kB2Ones + 32;             // 39344
+__host__ __device__ constexpr int y1_at(int yy, int xx, int quad) {
+  return yy * kY1Row + xx * kY1Px + 8 * (quad ^ ((yy >> 1) & 1));
+}
+__host__ __device__ constexpr int z1_at(int y, int x, int quad) {
+  return y * kZ1Row + x * kZ1Px + 8 * (quad ^ ((y >> 1) & 1));
+}
+__host__ __device__ constexpr int dz2_at(int i, int j, int chunk) { return (i * 9 + j) * 64 + 16 * (chunk ^ (2 * (i & 1))); }
+static_assert(4 * kB2Lds <= 163840, "ref_bwd2: four workgroups per CU");
+static_assert(kB2BufBytes % 16 == 0 && kB2Dz2 % 16 == 0, "16-B aligned buffers");
+constexpr int kBwd2Grid = 256 * 4;
+static_assert(kBwd2Grid == kBwdGrid, "ref_slab_bytes covers both backward kernels");
+
+__device__ __forceinline__ void wg_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+// a wave's own LDS operations execute in issue order: a compiler fence suffices
+__device__ __forceinline__ void lds_fence() { asm volatile("" ::: "memory"); }
+
+// Wave 0's conv1 recompute in the data gradient's phase order (see
+// ref_bwd_kernel): Y1 stores and the ReLU mask bits of the stored bf16 values.
+// Every address is a per-lane base + an immediate: output pixel (y, x) =
+// (4T + 2a + p, 2j + q) for tile T of phase (p, q), lane n16 = 8a + j. The
+// K-padding lanes (g >= 2, and g = 1's second window) read real X rows
+// against zero weights -- finite, so their products are exact zeros -- and
+// the invalid pixels (i = 7 or j = 7) only feed their own, unstored columns.
+__device__ __forceinline__ void ref_conv1_y1_mask(char* smem, const bf16x8& w1, const float (&b1v)[4], int n16, int g,
+                                                  uint32_t (&mask)[2]) {
+  const int a = n16 >> 3, j = n16 & 7;
+  const int xa = 4 * a * kXPitch + 8 * j + (g == 0 ? 0 : 2 * kXPitch);  // window row kh = 0 (g = 0) / 2
+  const int xb = 4 * a * kXPitch + 8 * j + kXPitch;                     // window row kh = 1
+  // Y1 (yy, xx) = (y + 1, x + 1): quad swizzle ((yy >> 1) & 1) = (a + p) & 1
+  const int yl[2] = {kB2Y1 + 2 * a * kY1Row + 2 * j * kY1Px + 8 * (g ^ (a & 1)),
+                     kB2Y1 + 2 * a * kY1Row + 2 * j * kY1Px + 8 * (g ^ ((a + 1) & 1))};
+  const bool jok = j < 7, aok = a == 0;
+  mask[0] = mask[1] = 0u;
+#pragma unroll
+  for (int ph = 0; ph < 4; ++ph)
+#pragma unroll
+    for (int T = 0; T < 4; ++T) {
+      const int p = ph >> 1, q = ph & 1;
+      const int cb = (q ? kB2X2 + 8 : kB2X0) + (8 * T + 2 * p) * kXPitch;
+      const bf16x4 va = *reinterpret_cast<const bf16x4*>(smem + xa + cb);
+      const bf16x4 vb = *reinterpret_cast<const bf16x4*>(smem + xb + cb);
+      f32x4 acc = {b1v[0], b1v[1], b1v[2], b1v[3]};
+      acc = mma(acc, w1, join(va, vb));
+      const u32x2 v = pack4(relu(acc[0]) * (1.f / 255.f), relu(acc[1]) * (1.f / 255.f), relu(acc[2]) * (1.f / 255.f),
+                            relu(acc[3]) * (1.f / 255.f));
+      const bool ok = jok && (T < 3 || aok);
+      const uint32_t bits = nz4(v);
+      mask[(ph * 4 + T) >> 3] |= (ok ? bits : 0u) << (4 * ((ph * 4 + T) & 7));
+      if (ok) *reinterpret_cast<u32x2*>(smem + yl[p] + (4 * T + p + 1) * kY1Row + (q + 1) * kY1Px) = v;
+    }
+}
+
+__global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2, 2))) ref_bwd2_kernel(RefBwdParams p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int n16 = lane & 15, g = lane >> 4;
+  const int tq = (lane >> 2) & 3, tp = lane & 3;
+  const int grid = (int)gridDim.x;
+
+  {
+    const u32x4 z = {0u, 0u, 0u, 0u};
+    for (int i = (int)threadIdx.x * 16; i < kB2Lds; i += 128 * 16) *reinterpret_cast<u32x4*>(smem + i) = z;
+  }
+  wg_barrier();
+  if (threadIdx.x < 8) *reinterpret_cast<uint32_t*>(smem + kB2Ones + 4 * threadIdx.x) = 0x3f803f80u;
+  float* slab = p.slab + (size_t)blockIdx.x * kSlab;
+  auto buf = [](int k) { return kB2Buf + (k & 1) * kB2BufBytes; };
+
+  if (wv == 0) {
+    const bf16x8 w1 = conv1_weights(p.w1, lane);
+    float b1v[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) b1v[i] = 255.f * p.b1[4 * g + i];
+    f32x4 acc2[2][10];
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int t = 0; t < 10; ++t) acc2[mt][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // conv2 dW operands: q = 32c + 8g + 4h + tq (q >= 49: a zero dZ2 pad pixel / any Y1 pixel)
+    int adz[2][2], ay1[2][2][2];  // ay1[.][.][kh >> 1]
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int q = 32 * c + 8 * g + 4 * h + tq;
+        const int oy = q < 49 ? q / 7 : 8, ox = q < 49 ? q % 7 : 8;
+        adz[c][h] = dz2_at(oy, ox, tp >> 1) + 8 * (tp & 1);  // + buffer + kB2Dz2; ^ 32: channels 16..31
+        const int yy = q < 49 ? 2 * oy : 0, xx = q < 49 ? 2 * ox : 0;
+        ay1[c][h][0] = kB2Y1 + y1_at(yy, xx, tp);          // taps kh = 0, 1 (+ kh * row + kw * pixel)
+        ay1[c][h][1] = kB2Y1 + y1_at(yy + 2, xx, tp) - 2 * kY1Row;  // kh = 2
+      }
+
+    uint32_t xw[4];
+    u32x4 dyv[4], y2v[4];
+    WaveIdx widx;
+    widx.load(p.idx, blockIdx.x, grid, p.B, 0);
+    auto load = [&](int k) {
+      const int img = (int)blockIdx.x + k * grid;
+      if ((k & 63) == 0 && k > 0) widx.load(p.idx, blockIdx.x, grid, p.B, k);
+      load_x(xw, p.x + (size_t)widx.get(k) * kImgPix, lane);
+      const u32x4* dyg = reinterpret_cast<const u32x4*>(static_cast<const bf16*>(p.dy2) + (size_t)img * kY2Elems);
+      const u32x4* y2g = reinterpret_cast<const u32x4*>(static_cast<const bf16*>(p.y2) + (size_t)img * kY2Elems);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int w = min(lane + 64 * r, 195);
+        dyv[r] = dyg[w];
+        y2v[r] = y2g[w];
+      }
+    };
+    // image k: X copies + planes, dZ2 = dY2 * (Y2 > 0); then conv1 -> Y1 and the mask
+    auto stage = [&](int k) {
+      const int bo = buf(k);
+      stage_x(smem, kB2X0, kB2X2, bo + kB2Xc, xw, lane);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int w = lane + 64 * r;
+        if (w < 196) {
+          u32x4 z;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const uint32_t yv = y2v[r][e], dv = dyv[r][e];
+            const uint32_t lo = (int)(short)(yv & 0xffffu) > 0 ? (dv & 0xffffu) : 0u;
+            const uint32_t hi = (int)yv > 0x0000ffff ? (dv & 0xffff0000u) : 0u;  // upper bf16 > 0
+            z[e] = lo | hi;
+          }
+          const int q = w >> 2, oy = (q * 37) >> 8, ox = q - 7 * oy;
+          *reinterpret_cast<u32x4*>(smem + bo + kB2Dz2 + dz2_at(oy, ox, w & 3)) = z;
+        }
+      }
+      lds_fence();
+      if (MCC_REF_ABL & 1) return;
+      uint32_t mask[2];
+      ref_conv1_y1_mask(smem, w1, b1v, n16, g, mask);
+      *reinterpret_cast<u32x2*>(smem + bo + kB2Mask + 8 * lane) = u32x2{mask[0], mask[1]};
+    };
+    if ((int)blockIdx.x < p.B) {
+      load(0);
+      stage(0);
+    }
+    for (int img = blockIdx.x, k = 0; img < p.B; img += grid, ++k) {
+      wg_barrier();  // image k staged; wave 1 done with the other buffer (image k-1)
+      const bool more = img + grid < p.B;
+      if (more) load(k + 1);
+      const int bo = buf(k);
+      if (!(MCC_REF_ABL & 5)) {
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          bf16x8 a[2];
+#pragma unroll
+          for (int mt = 0; mt < 2; ++mt)
+            a[mt] = tr8(smem + bo + kB2Dz2 + (adz[c][0] ^ (32 * mt)), smem + bo + kB2Dz2 + (adz[c][1] ^ (32 * mt)));
+          // taps in two halves of 5 (t = 9: the ones column): 20 fewer live registers
+#pragma unroll
+          for (int t0 = 0; t0 < 10; t0 += 5) {
+            bf16x8 b[5];
+#pragma unroll
+            for (int u = 0; u < 5; ++u) {
+              const int t = t0 + u;
+              const int kh = t / 3, kw = t % 3, to = kh * kY1Row + kw * kY1Px;
+              b[u] = t < 9 ? tr8(smem + ay1[c][0][kh >> 1] + to, smem + ay1[c][1][kh >> 1] + to)
+                           : tr8(smem + kB2Ones + 8 * (tp & 1), smem + kB2Ones + 8 * (tp & 1));
+            }
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+              for (int u = 0; u < 5; ++u) acc2[mt][t0 + u] = mma(acc2[mt][t0 + u], a[mt], b[u]);
+          }
+        }
+      }
+      lds_fence();
+      if (more) stage(k + 1);  // Y1 rewritten after this wave's dW2 reads (issue order)
+    }
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int t = 0; t < 10; ++t)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) slab[((mt * 10 + t) * 4 + i) * 64 + lane] = acc2[mt][t][i];
+  } else {
+    // conv2 dX A operand per tap: rows = input channel ci = n16, K slot 8g + e = output channel
+    bf16x8 wdx[9];
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) wdx[t][e] = (bf16)p.w2[((8 * g + e) * 16 + n16) * 9 + t];
+    f32x4 acc1 = {0.f, 0.f, 0.f, 0.f};
+    // conv1 dW: A = dZ1 rows (y = 2c + (g >> 1), x0 = 8 (g & 1)), B = X planes (tap n16; 9: ones)
+    // (row 2c + (g >> 1): quad swizzle c & 1)
+    const int adz1[2] = {kB2Dz1 + z1_at(g >> 1, 8 * (g & 1) + tq, tp), kB2Dz1 + z1_at(g >> 1, 8 * (g & 1) + tq, tp ^ 1)};
+    // conv2 dX: dZ2 row i + di has parity ((n16 >> 3) ^ di) & 1
+    const int zc[2] = {16 * (g ^ (2 * ((n16 >> 3) & 1))), 16 * (g ^ (2 * (((n16 >> 3) & 1) ^ 1)))};
+    int bx1 = -1;
+    if (n16 < 9) {
+      const int kh = n16 / 3, kw = n16 % 3;
+      const int plane = kw == 1 ? 0 : kw == 2 ? 1 : 2;  // E / O / Os
+      bx1 = kB2Xc + plane * kXcPlane + ((g >> 1) * 2 + kh) * 32 + 16 * (g & 1);  // + buffer
+    }
+    for (int img = blockIdx.x, k = 0; img < p.B; img += grid, ++k) {
+      wg_barrier();
+      if (MCC_REF_ABL & 2) continue;
+      const int bo = buf(k);
+      const u32x2 mk = *reinterpret_cast<const u32x2*>(smem + bo + kB2Mask + 8 * lane);
+      const uint32_t mask[2] = {mk.x, mk.y};
+#pragma unroll
+      for (int ph = 0; ph < 4; ++ph) {
+        const int py = ph >> 1, pxx = ph & 1;
+#pragma unroll
+        for (int T = 0; T < 4; ++T) {
+          const int i = 2 * T + (n16 >> 3), j = n16 & 7;
+          const char* zb = smem + bo + kB2Dz2 + (i * 9 + j) * 64;
+          f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int a = 0; a < 2; ++a) {
+            if (py == 0 && a == 1) continue;
+            const int kh = py == 0 ? 1 : (a == 0 ? 0 : 2), di = py == 1 && a == 0 ? 1 : 0;
+#pragma unroll
+            for (int b = 0; b < 2; ++b) {
+              if (pxx == 0 && b == 1) continue;
+              const int kw = pxx == 0 ? 1 : (b == 0 ? 0 : 2), dj = pxx == 1 && b == 0 ? 1 : 0;
+              const bf16x8 zf = *reinterpret_cast<const bf16x8*>(zb + (di * 9 + dj) * 64 + zc[di]);
+              acc = mma(acc, wdx[kh * 3 + kw], zf);
+            }
+          }
+          const uint32_t mb = (mask[(ph * 4 + T) >> 3] >> (4 * ((ph * 4 + T) & 7))) & 15u;
+          const u32x2 v = pack4((mb & 1u) ? acc[0] : 0.f, (mb & 2u) ? acc[1] : 0.f, (mb & 4u) ? acc[2] : 0.f,
+                                (mb & 8u) ? acc[3] : 0.f);
+          const int y = 2 * i + py, x = 2 * j + pxx;
+          if (i < 7) *reinterpret_cast<u32x2*>(smem + kB2Dz1 + z1_at(y, x, g)) = v;  // (no rows 14, 15)
+        }
+      }
+      lds_fence();
+      if (MCC_REF_ABL & 8) continue;
+      const char* xb = smem + (bx1 >= 0 ? bo + bx1 : kB2Ones);
+      const int xstep = bx1 >= 0 ? 128 : 0;
+#pragma unroll
+      for (int c = 0; c < 7; ++c) {
+        const int za = adz1[c & 1] + c * 2 * kZ1Row;
+        const bf16x8 a = tr8(smem + za, smem + za + 4 * kZ1Px);
+        const bf16x8 b = *reinterpret_cast<const bf16x8*>(xb + c * xstep);
+        acc1 = mma(acc1, a, b);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) slab[kSlabW2 + i * 64 + lane] = acc1[i];
+  }
+}
+
 // Fixed-order sum of the per-wave slabs -> canonical gradients.
 constexpr int kRedWaves = 16;
 __global__ void __launch_bounds__(64 * kRedWaves) ref_bwd_reduce_kernel(RefBwdParams p, int nslabs) {
@@ -510,7 +817,8 @@ void ref_forward(const RefFwdParams& p, hipStream_t s) {
 void ref_backward(const RefBwdParams& p, hipStream_t s) {
   if (p.f32) return ref32_backward(p, s);
   if (p.B <= 0) return;
-  hipLaunchKernelGGL(ref_bwd_kernel, dim3(kBwdGrid), dim3(64), kBLds, s, p);
+  if (ab_flag("ref_bwd1")) hipLaunchKernelGGL(ref_bwd_kernel, dim3(kBwdGrid), dim3(64), kBLds, s, p);
+  else hipLaunchKernelGGL(ref_bwd2_kernel, dim3(kBwd2Grid), dim3(128), kB2Lds, s, p);
   hipLaunchKernelGGL(ref_bwd_reduce_kernel, dim3(kSlab / 64), dim3(64 * kRedWaves), 0, s, p, kBwdGrid);
 }
 

@@ -8,11 +8,12 @@ cd "$(dirname "$0")/.."
 name=$1; shift
 EXT=$(python3 -c "import sysconfig;print(sysconfig.get_config_var('EXT_SUFFIX'))")
 out=build/var_$name
+base=$(basename ${SRC:-csrc/kernels/lenet.hip} .hip)  # SRC: the kernel file rebuilt with the defines
 mkdir -p $out/obj $out/mpi_cuda_cnn_amd
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++20 -fPIC -Icsrc/include -Icsrc/kernels -Wall -Wno-unused-result \
-  -mllvm -amdgpu-mfma-vgpr-form=1 "$@" -c ${SRC:-csrc/kernels/lenet.hip} -o $out/obj/lenet.o
-objs=$(ls build/obj/bindings/module.o build/obj/core/*.o build/obj/kernels/*.o build/obj/engine/*.o | grep -v "kernels/lenet.o")
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o $out/mpi_cuda_cnn_amd/_C$EXT $objs $out/obj/lenet.o \
+  -mllvm -amdgpu-mfma-vgpr-form=1 "$@" -c ${SRC:-csrc/kernels/lenet.hip} -o $out/obj/$base.o
+objs=$(ls build/obj/bindings/module.o build/obj/core/*.o build/obj/kernels/*.o build/obj/engine/*.o | grep -v "kernels/$base.o")
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o $out/mpi_cuda_cnn_amd/_C$EXT $objs $out/obj/$base.o \
   -L/opt/rocm/lib -lamdhip64 -Wl,-rpath,/opt/rocm/lib
 (cd mpi_cuda_cnn_amd && find . -name '*.py' -exec install -D -m 644 {} ../$out/mpi_cuda_cnn_amd/{} \;)
 echo "built $out"

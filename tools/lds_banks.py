@@ -488,3 +488,114 @@ def lenet_fwd2_report(**kw):
 if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "lenet_fwd2":
     for P in (16, 17, 18, 20):
         lenet_fwd2_report(P=P)
+
+
+# ---------------------------------------------------------------- ref_bwd2 (refnet.hip)
+def refbwd_accesses(dz=None, y1=None, dz1=None):
+    """Every LDS access of one image of ref_bwd2_kernel, (name, kind, addrs,
+    count). Layout functions (bytes, one region each; regions never share an
+    instruction): dz(i, j, c16) -> dZ2 pixel (i, j) 16-B chunk c16 (channels
+    8 c16 .. +7), i, j in 0..8; y1(yy, xx, c16) -> Y1 padded pixel (yy, xx)
+    in 0..14, chunk 0..1; dz1(y, x, c8) -> dZ1 pixel (y, x) in 0..15, 8-B
+    piece c8 (channels 4 c8 .. +3)."""
+    dz = dz or (lambda i, j, c: (i * 9 + j) * 64 + 16 * c)
+    y1 = y1 or (lambda yy, xx, c: (yy * 15 + xx) * 32 + 16 * c)
+    dz1 = dz1 or (lambda y, x, c: (y * 16 + x) * 32 + 8 * c)
+    L = range(64)
+    acc = []
+    # wave 0: dZ2 staging (b128 per lane: pixel q = w >> 2, chunk w & 3)
+    for r in range(4):
+        a = []
+        for l in L:
+            w = l + 64 * r
+            if w >= 196:
+                a.append(None)
+                continue
+            q = w >> 2
+            a.append(dz(q // 7, q % 7, w & 3))
+        acc.append(("dZ2 stage", "write_b128", a, 1))
+    # conv1 -> Y1 writes (lane: pixel (y, x), channels 4g..4g+3), 16 tiles
+    for ph in range(4):
+        for T in range(4):
+            a = []
+            for l in L:
+                n16, g = l & 15, l >> 4
+                i, j = 2 * T + (n16 >> 3), n16 & 7
+                y, x = 2 * i + (ph >> 1), 2 * j + (ph & 1)
+                a.append(y1(y + 1, x + 1, g >> 1) + 8 * (g & 1) if i < 7 and j < 7 else None)
+            acc.append(("Y1 write", "write_b64", a, 1))
+    # dW2: A = dZ2 (tr, q = 32c + 8g + 4h + tq, 8-B piece tp of 32-B half mt)
+    for c in range(2):
+        for h in range(2):
+            for mt in range(2):
+                a = []
+                for l in L:
+                    g, tq, tp = l >> 4, (l >> 2) & 3, l & 3
+                    q = 32 * c + 8 * g + 4 * h + tq
+                    oy, ox = (q // 7, q % 7) if q < 49 else (8, 8)
+                    a.append(dz(oy, ox, 2 * mt + (tp >> 1)) + 8 * (tp & 1))
+                acc.append(("dW2 A (dZ2)", "tr_b16", a, 1))
+            for t in range(9):
+                kh, kw = t // 3, t % 3
+                a = []
+                for l in L:
+                    g, tq, tp = l >> 4, (l >> 2) & 3, l & 3
+                    q = 32 * c + 8 * g + 4 * h + tq
+                    oy, ox = (q // 7, q % 7) if q < 49 else (0, 0)
+                    a.append(y1(2 * oy + kh, 2 * ox + kw, tp >> 1) + 8 * (tp & 1))
+                acc.append(("dW2 B (Y1)", "tr_b16", a, 1))
+    # wave 1: dX reads (lane: dZ2 pixel (i + di, j + dj), chunk g)
+    for ph in range(4):
+        py, px = ph >> 1, ph & 1
+        taps = [(di, dj) for di in ((0,) if py == 0 else (1, 0)) for dj in ((0,) if px == 0 else (1, 0))]
+        for T in range(4):
+            for di, dj in taps:
+                a = []
+                for l in L:
+                    n16, g = l & 15, l >> 4
+                    i, j = 2 * T + (n16 >> 3), n16 & 7
+                    a.append(dz(i + di, j + dj, g) if (i + di) * 9 + j + dj < 81 else dz(8, 8, g))
+                acc.append(("dX (dZ2)", "read_b128", a, 1))
+            a = []
+            for l in L:
+                n16, g = l & 15, l >> 4
+                i, j = 2 * T + (n16 >> 3), n16 & 7
+                a.append(dz1(2 * i + py, 2 * j + px, g))
+            acc.append(("dZ1 write", "write_b64", a, 1))
+    # conv1 dW: A = dZ1 rows (tr), y = 2c + (g >> 1), x = 8 (g & 1) + tq + 4 (half)
+    for c in range(7):
+        for hh in range(2):
+            a = []
+            for l in L:
+                g, tq, tp = l >> 4, (l >> 2) & 3, l & 3
+                a.append(dz1(2 * c + (g >> 1), 8 * (g & 1) + tq + 4 * hh, tp))
+            acc.append(("dW1 A (dZ1)", "tr_b16", a, 1))
+    return acc
+
+
+def refbwd_report(**kw):
+    acc = refbwd_accesses(**kw)
+    rows = {}
+    tot = ex = 0
+    for name, kind, addrs, n in acc:
+        c = cycles(kind, addrs)
+        e = c - ideal(kind)
+        r = rows.setdefault(name, [0, 0, 0])
+        r[0] += n
+        r[1] += n * c
+        r[2] += n * e
+        tot += n * c
+        ex += n * e
+    print(f"per image: {tot:.0f} LDS-array cycles, {ex:.0f} conflict cycles")
+    for k, (n, c, e) in rows.items():
+        print(f"  {k:12s} {n:5.0f} instr {c:6.0f} cycles {e:5.0f} extra")
+    return tot, ex
+
+
+if __name__ == "__main__" and len(sys.argv) > 1 and sys.argv[1] == "refbwd":
+    print("32-B HWC pixels, 9 x 9 dZ2 (round-5 first cut):")
+    refbwd_report()
+    print("refnet.hip layouts (y1_at / z1_at / dz2_at):")
+    refbwd_report(dz=lambda i, j, c: (i * 9 + j) * 64 + 16 * (c ^ (2 * (i & 1))),
+                  y1=lambda yy, xx, c: yy * 624 + xx * 40 + 8 * ((2 * c) ^ ((yy >> 1) & 1)),
+                  dz1=lambda y, x, c: y * 640 + x * 40 + 8 * (c ^ ((y >> 1) & 1)))

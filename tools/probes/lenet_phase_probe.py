@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Time the LeNet-5 step's three parts (forward() = lenet_fwd, loss() = the
 fused FC chain, backward_all() = lenet_bwd) with HIP events, for the
-in-tree module or ablation builds (tools/build_variant.sh):
+in-tree module or ablation builds (tools/build_variant.sh); PROBE_MODEL picks
+another model (e.g. ref: fwd = ref_fwd, bwd = FC backward + ref_bwd):
 
     python tools/probes/lenet_phase_probe.py [variant_dir ...]
 
@@ -22,7 +23,7 @@ def run_one(path):
 
     assert os.path.dirname(mcc.__file__).startswith(os.path.abspath(path)), mcc.__file__
     B = int(os.environ.get("PROBE_B", "163840"))
-    spec = mcc.make_model("lenet5")
+    spec = mcc.make_model(os.environ.get("PROBE_MODEL", "lenet5"))
     imgs, labels = mcc.synth_dataset(65536, 1, 28, 28, 10, seed=1)
     dev = torch.device("cuda", 0)
     d_img, d_lab = torch.from_numpy(imgs).to(dev), torch.from_numpy(labels).to(dev)
