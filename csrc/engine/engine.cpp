@@ -677,6 +677,8 @@ void GpuNet::build() {
       scratch = std::max(scratch, gpu::igemm_dw_slab_bytes(st.Nout, st.in_ld, gpu::igemm_dw_splitk(Bm, st.Nout, st.in_ld)));
     } else {
       scratch = std::max(scratch, (size_t)fc_dw_splitk(st.Nout, st.Kin + 1, Bm, dtype_) * st.Nout * st.ldp * 4);
+      if (dtype_ == DType::F32)
+        scratch = std::max(scratch, (size_t)gpu::fc_dw32_splitk(st.Nout, st.Kin, Bm) * st.Nout * st.ldp * 4);
     }
   }
   for (Stage* sp : stages_) {
@@ -1368,6 +1370,24 @@ void GpuNet::backward(int hi, int lo, hipStream_t s) {
         w.slab = scratch_; w.slab_stride = (int64_t)(st.in_ld + 1) * st.Nout;
         MCC_CHECK(gpu::igemm_dw_slab_bytes(st.Nout, st.in_ld, w.splitk) <= scratch_bytes_, "fc dW scratch too small");
         gpu::igemm_dw(w, grads_ + st.w_off, grads_ + st.b_off, 0.f, ws);
+      } else if (dtype_ == DType::F32 && !ab_flag("no_fc_dw32") &&
+                 gpu::fc_dw32_supported(st.Nout, st.Kin, st.out_ld, st.in_ld)) {
+        // fp32 skinny-output weight gradient: all Nout rows per workgroup
+        gpu::FcDw32Params w;
+        w.M = st.Nout; w.N = st.Kin; w.K = B;
+        w.dz = static_cast<const float*>(st.grad_buf); w.ldz = st.out_ld;
+        w.x = static_cast<const float*>(pv.act_buf); w.ldx = st.in_ld;
+        w.slab = scratch_; w.ldp = st.ldp;
+        w.splitk = gpu::fc_dw32_splitk(st.Nout, st.Kin, B);
+        w.slab_stride = (int64_t)st.Nout * st.ldp;
+        MCC_CHECK((size_t)w.splitk * w.slab_stride * 4 <= scratch_bytes_, "fc dW scratch too small");
+        gpu::fc_dw32(w, ws);
+        gpu::DwReduceParams r;
+        r.S = w.splitk; r.Nout = st.Nout; r.kfeat = st.Kin; r.ldp = st.ldp; r.part = scratch_;
+        r.partial_stride = w.slab_stride;
+        r.gw = grads_ + st.w_off; r.gb = grads_ + st.b_off;
+        r.permC = 0; r.permHW = 0;
+        gpu::dw_reduce(r, ws);
       } else {
       // weight + bias gradient: [Nout][Kin+1] = dZ^T [X | 1], split-K over the batch
       gpu::GemmParams w;

@@ -565,6 +565,21 @@ struct FcTallParams {
 bool fc_tall_supported(int M, int N, int K);
 void fc_tall(const FcTallParams& p, hipStream_t s);
 
+// fp32 FC weight gradient for skinny outputs (fc_dw32.hip): split-K partials
+// part[s][m][ldp] of dW[m][n] = sum_k dz[k][m] x[k][n] (m < M <= 208, n < N)
+// and db[m] in column N; reduced by dw_reduce.
+struct FcDw32Params {
+  int M = 0, N = 0, K = 0;
+  const float* dz = nullptr; int ldz = 0;  // [K][ldz]
+  const float* x = nullptr; int ldx = 0;   // [K][ldx]
+  float* slab = nullptr; int ldp = 0;      // [splitk][M][ldp]
+  int64_t slab_stride = 0;
+  int splitk = 1;
+};
+bool fc_dw32_supported(int M, int N, int ldz, int ldx);
+int fc_dw32_splitk(int M, int N, int64_t K);
+void fc_dw32(const FcDw32Params& p, hipStream_t s);
+
 // Weight gradient: dW[co][k] = sum_m dz[m][co] in(m, k), db[co] = sum_m dz[m][co],
 // split-K over m into fp32 slabs [splitk][kf+1][Cout], then reduced into the
 // canonical gw[Cout][C][KS][KS], gb[Cout] (grad = beta*grad + sum).

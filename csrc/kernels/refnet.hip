@@ -77,9 +77,6 @@ constexpr int kSlabW2 = 2 * 10 * 4 * 64;  // 5120
 constexpr int kSlab = kSlabW2 + 4 * 64;   // 5376
 constexpr int kBwdGrid = 256 * 4;         // one wave per SIMD (~320 registers)
 
-__device__ __forceinline__ uint32_t bf16_bits(float v) {
-  return (uint32_t)__builtin_bit_cast(unsigned short, (bf16)v);
-}
 __device__ __forceinline__ void u8x4_ints(uint32_t w, uint32_t& lo, uint32_t& hi) {
   const uint32_t f0 = __builtin_bit_cast(uint32_t, (float)(w & 0xffu));
   const uint32_t f1 = __builtin_bit_cast(uint32_t, (float)((w >> 8) & 0xffu));

@@ -31,6 +31,7 @@
 // reduced in a fixed order (deterministic).
 #include "kernels.h"
 #include "mfma.h"
+#include "mcc/ab.h"
 
 #include <algorithm>
 
@@ -70,9 +71,11 @@ __device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
 __device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 __device__ __forceinline__ f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
 __device__ __forceinline__ void st4(float* p, const f32x4& v) { *reinterpret_cast<f32x4*>(p) = v; }
-__device__ __forceinline__ f32x4 relu4(const f32x4& v) {
-  return f32x4{fmaxf(v[0], 0.f), fmaxf(v[1], 0.f), fmaxf(v[2], 0.f), fmaxf(v[3], 0.f)};
-}
+// ReLU on the bit pattern (v_max_i32: no NaN canonicalisation, -0 -> +0)
+__device__ __forceinline__ float relu(float v) { return __builtin_bit_cast(float, max(__builtin_bit_cast(int, v), 0)); }
+__device__ __forceinline__ f32x4 relu4(const f32x4& v) { return f32x4{relu(v[0]), relu(v[1]), relu(v[2]), relu(v[3])}; }
+__device__ __forceinline__ void wg_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+__device__ __forceinline__ void lds_fence() { asm volatile("" ::: "memory"); }
 
 struct WaveIdx {
   int v = 0;
@@ -370,6 +373,189 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1, 1)))
   slab[kSlabB2 + lane] = db2;
 }
 
+// ---- two-wave backward ----
+// ref32_bwd_kernel holds the dW2 accumulators and the dX weights in one wave
+// (one wave per SIMD), so its 610 MFMAs per image run with every LDS and
+// dependency latency exposed (2.7 ms for a 1.3 ms MFMA floor). Here a
+// workgroup of two waves shares one image, the roles split by register set:
+//   wave 0: stages image k's X (global loads one image ahead), recomputes
+//           conv1 -> Y1, then conv2 dW / db (39 + 234 MFMAs);
+//   wave 1: stages image k's dZ2 = dY2 * (Y2 > 0) (its 56 prefetch registers
+//           fit beside the dX weights, not beside the dW2 accumulators), then
+//           conv2 dX -> dZ1 (compact, wave-private; the ReLU mask read from
+//           Y1) and conv1 dW (288 + 49 MFMAs).
+// Two barriers per image (A: image staged, B: both done with it); the other
+// workgroup's waves on the SIMD fill the barrier waits. 2 waves per SIMD.
+constexpr int kB2Z1 = kZ2 + kZ2F;               // dZ1 [196 pixels][16 ci] (wave 1)
+constexpr int kB2Floats = kB2Z1 + 196 * 16;     // 9712
+constexpr int kBwd2Lds = kB2Floats * 4;         // 38,848 B
+static_assert(4 * kBwd2Lds <= 163840, "ref32_bwd2: four workgroups per CU");
+
+__global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2, 2))) ref32_bwd2_kernel(RefBwdParams p) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int r = lane & 15, g = lane >> 4;
+  const int grid = (int)gridDim.x;
+  for (int i = (int)threadIdx.x * 4; i < kB2Floats; i += 128 * 4) st4(smem + i, f32x4{0.f, 0.f, 0.f, 0.f});
+  wg_barrier();
+  float* slab = p.slab + (size_t)blockIdx.x * kSlab;
+
+  if (wv == 0) {
+    Conv1 c1;
+    c1.init(p.w1, p.b1, r, g);
+    f32x4 acc2[2][9];
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int t = 0; t < 9; ++t) acc2[mt][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float db2 = 0.f;
+    uint32_t xw[4];
+    WaveIdx widx;
+    widx.load(p.idx, blockIdx.x, grid, p.B, 0);
+    auto load_img = [&](int k) {
+      if ((k & 63) == 0 && k > 0) widx.load(p.idx, blockIdx.x, grid, p.B, k);
+      load_x(xw, p.x + (size_t)widx.get(k) * kImgPix, lane);
+    };
+    if ((int)blockIdx.x < p.B) load_img(0);
+    for (int img = blockIdx.x, k = 0; img < p.B; img += grid, ++k) {
+      stage_x(smem, xw, lane);
+      if (img + grid < p.B) load_img(k + 1);
+      lds_fence();
+      c1.run(smem, r, g);
+      wg_barrier();  // A: X, dZ2, Y1 of image k ready
+      // conv2 dW: acc2[mt][t] += dZ2^T (co) . Y1 patches (ci), K = output pixels
+#pragma unroll 2
+      for (int s = 0; s < 13; ++s) {  // (2 steps per iteration: the next step's reads overlap these MFMAs)
+        const int q = 4 * s + g;
+        const bool ok = q < 49;
+        const int oy = (q * 9363) >> 16, ox = q - 7 * oy;
+        const float* zb = smem + kZ2 + (ok ? oy * 8 + ox : 63) * 32 + r;  // (7, 7): zero
+        const float* yb = smem + kY1 + (ok ? (2 * oy * 15 + 2 * ox) * 16 : 0) + r;
+        const float a0 = zb[0], a1 = zb[16];
+        float b[9];
+#pragma unroll
+        for (int t = 0; t < 9; ++t) b[t] = yb[((t / 3) * 15 + t % 3) * 16];
+#pragma unroll
+        for (int t = 0; t < 9; ++t) {
+          acc2[0][t] = mfma4(a0, b[t], acc2[0][t]);
+          acc2[1][t] = mfma4(a1, b[t], acc2[1][t]);
+        }
+      }
+      // db2 (VALU): lane -> co = lane & 31, pixels of parity lane >> 5
+#pragma unroll 5
+      for (int q = lane >> 5; q < 49; q += 2) {
+        const int oy = (q * 9363) >> 16, ox = q - 7 * oy;
+        db2 += smem[kZ2 + (oy * 8 + ox) * 32 + (lane & 31)];
+      }
+      wg_barrier();  // B: image k consumed
+    }
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+      for (int t = 0; t < 9; ++t)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) slab[((mt * 9 + t) * 4 + i) * 64 + lane] = acc2[mt][t][i];
+    slab[kSlabB2 + lane] = db2;
+  } else {
+    // conv2 dX A operand per tap: W2[co = 8 g + s][ci = r][t]
+    float wdx[9][8];
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+      for (int s = 0; s < 8; ++s) wdx[t][s] = p.w2[((8 * g + s) * 16 + r) * 9 + t];
+    f32x4 acc1 = {0.f, 0.f, 0.f, 0.f};
+    // conv1 dW B operand: tap r of the lane's pixel (r = 9: ones for db1)
+    const int x1off = r < 9 ? (r / 3) * kXP + r % 3 : 0;
+    const float x1one = r == 9 ? 1.f : 0.f;
+    // dZ2 staging (this wave has the free registers for the one-image-ahead loads)
+    f32x4 dyv[7], y2v[7];
+    const float* y2all = static_cast<const float*>(p.y2);
+    const float* dyall = static_cast<const float*>(p.dy2);
+    auto load_img = [&](int img) {
+#pragma unroll
+      for (int it = 0; it < 7; ++it) {
+        const int e4 = min(lane + 64 * it, 391);
+        dyv[it] = ld4(dyall + (size_t)img * kY2 + 4 * e4);
+        y2v[it] = ld4(y2all + (size_t)img * kY2 + 4 * e4);
+      }
+    };
+    if ((int)blockIdx.x < p.B) load_img(blockIdx.x);
+    for (int img = blockIdx.x; img < p.B; img += grid) {
+      // dZ2 = dY2 * (Y2 > 0) into the 8 x 8 grid
+#pragma unroll
+      for (int it = 0; it < 7; ++it) {
+        const int e4 = lane + 64 * it;
+        if (e4 < 392) {
+          const int q = e4 >> 3, c4 = 4 * (e4 & 7);
+          const int oy = (q * 9363) >> 16, ox = q - 7 * oy;
+          f32x4 z;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) z[e] = y2v[it][e] > 0.f ? dyv[it][e] : 0.f;
+          st4(smem + kZ2 + (oy * 8 + ox) * 32 + c4, z);
+        }
+      }
+      if (img + grid < p.B) load_img(img + grid);
+      wg_barrier();  // A
+      // conv2 dX by phase: dY1^T = W2 . dZ2 patches; dZ1 = dY1 * (Y1 > 0). The
+      // phase's 4 tiles run together: 4 independent accumulator chains, and a
+      // tap's 8 fragment reads are issued a tap ahead of its MFMAs.
+#pragma unroll
+      for (int ph = 0; ph < 4; ++ph) {
+        const int py = ph >> 1, pxx = ph & 1;
+        constexpr int kTaps[4] = {1, 2, 2, 4};
+        f32x4 acc[4];
+#pragma unroll
+        for (int T = 0; T < 4; ++T) acc[T] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int u = 0; u < kTaps[ph]; ++u) {
+          // tap u of the phase: (a, b) = (u >> 1, u & 1) for phase 3, else the single varying index
+          const int a = py == 0 ? 0 : (pxx == 0 ? u : u >> 1);
+          const int b = pxx == 0 ? 0 : (py == 0 ? u : u & 1);
+          const int kh = py == 0 ? 1 : (a == 0 ? 0 : 2), di = py == 1 && a == 0 ? 1 : 0;
+          const int kw = pxx == 0 ? 1 : (b == 0 ? 0 : 2), dj = pxx == 1 && b == 0 ? 1 : 0;
+          f32x4 z[4][2];
+#pragma unroll
+          for (int T = 0; T < 4; ++T) {
+            const int i = 2 * T + (r >> 3), j = r & 7;
+            const float* zb = smem + kZ2 + (min(i, 6) * 8 + min(j, 6)) * 32 + 8 * g + (di * 8 + dj) * 32;
+            z[T][0] = ld4(zb);
+            z[T][1] = ld4(zb + 4);
+          }
+#pragma unroll
+          for (int s2 = 0; s2 < 8; ++s2)
+#pragma unroll
+            for (int T = 0; T < 4; ++T) acc[T] = mfma4(wdx[kh * 3 + kw][s2], z[T][s2 >> 2][s2 & 3], acc[T]);
+        }
+#pragma unroll
+        for (int T = 0; T < 4; ++T) {
+          const int i = 2 * T + (r >> 3), j = r & 7;
+          if (i < 7 && j < 7) {
+            const int y = 2 * i + py, x = 2 * j + pxx;
+            const f32x4 y1 = ld4(smem + kY1 + ((y + 1) * 15 + x + 1) * 16 + 4 * g);
+            f32x4 dz;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) dz[e] = y1[e] > 0.f ? acc[T][e] : 0.f;
+            st4(smem + kB2Z1 + (y * 14 + x) * 16 + 4 * g, dz);
+          }
+        }
+      }
+      lds_fence();
+      // conv1 dW: acc1 += dZ1^T (rows ci) . X patches (columns taps; 9 = ones), K = 196 pixels
+#pragma unroll 7
+      for (int s = 0; s < 49; ++s) {
+        const int px = 4 * s + g;
+        const int y = (px * 2341) >> 15, x = px - 14 * y;
+        const float a = smem[kB2Z1 + px * 16 + r];
+        const float bx = smem[2 * y * kXP + 2 * x + x1off];
+        acc1 = mfma4(a, r < 9 ? bx : x1one, acc1);
+      }
+      wg_barrier();  // B
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) slab[kSlabW1 + i * 64 + lane] = acc1[i];
+  }
+}
+
 // Fixed-order sum of the per-wave slabs -> canonical gradients.
 constexpr int kRedWaves = 16;
 __global__ void __launch_bounds__(64 * kRedWaves) ref32_bwd_reduce_kernel(RefBwdParams p, int nslabs) {
@@ -413,7 +599,8 @@ void ref32_forward(const RefFwdParams& p, hipStream_t s) {
 
 void ref32_backward(const RefBwdParams& p, hipStream_t s) {
   if (p.B <= 0) return;
-  hipLaunchKernelGGL(ref32_bwd_kernel, dim3(kBwdGrid), dim3(64), kBwdLds, s, p);
+  if (ab_flag("ref_bwd1")) hipLaunchKernelGGL(ref32_bwd_kernel, dim3(kBwdGrid), dim3(64), kBwdLds, s, p);
+  else hipLaunchKernelGGL(ref32_bwd2_kernel, dim3(kBwdGrid), dim3(128), kBwd2Lds, s, p);
   hipLaunchKernelGGL(ref32_bwd_reduce_kernel, dim3(kSlab / 64), dim3(64 * kRedWaves), 0, s, p, kBwdGrid);
 }
 
