@@ -311,12 +311,19 @@ def test_bench_batch_step_matches_small_batches(cuda):
         ref_logits[i : i + nb] = small.get_logits(nb)
         ref_grads += small.get_grads()
     assert _relerr(logits, ref_logits) < 1e-2
+    report = []
     for L in spec.layers():
         if L["nweights"] == 0:
             continue
         for off, n, what in ((L["w_off"], L["nweights"], "W"), (L["b_off"], L["nbiases"], "b")):
             err = _relerr(grads[off : off + n], ref_grads[off : off + n])
             assert err < 2e-2, f"layer {L['kind']} {what} grad rel err {err:.3e}"
+            # per output channel: one wrong channel of 16 could hide under the layer norm
+            e, c = _per_channel_err(grads[off : off + n], ref_grads[off : off + n], L["C"],
+                                    floor_frac=0.3 if what == "b" else 1e-2)
+            report.append(f"{L['kind']} C={L['C']} {what}: layer {err:.2e}, max per-channel {e:.2e} (channel {c})")
+            assert e < BENCH_BATCH_CHANNEL_TOL[what], "\n".join(report)
+    print("\n".join(report))
 
 
 @pytest.mark.gpu
@@ -366,12 +373,19 @@ def test_fc_igemm_bench_batch_matches_small_batches(cuda, model, B, b, fc_plan, 
         ref_grads += small.get_grads()
     tl, tg = (1e-5, 1e-4) if dtype == "fp32" else (1e-2, 2e-2)
     assert _relerr(logits, ref_logits) < tl
+    report = []
     for L in spec.layers():
         if L["nweights"] == 0:
             continue
         for off, n, what in ((L["w_off"], L["nweights"], "W"), (L["b_off"], L["nbiases"], "b")):
             err = _relerr(grads[off : off + n], ref_grads[off : off + n])
             assert err < tg, f"layer {L['kind']} C={L['C']} {what} grad rel err {err:.3e}"
+            e, c = _per_channel_err(grads[off : off + n], ref_grads[off : off + n], L["C"],
+                                    floor_frac=0.3 if what == "b" else 1e-2)
+            report.append(f"{L['kind']} C={L['C']} {what}: layer {err:.2e}, max per-channel {e:.2e} (channel {c})")
+            bound = 10 * tg if dtype == "fp32" else BENCH_BATCH_CHANNEL_TOL[what]
+            assert e < bound, "\n".join(report)
+    print("\n".join(report))
 
 
 @pytest.mark.gpu
@@ -526,13 +540,22 @@ def _per_channel_err(g, r, C, floor_frac=1e-2):
 # channel is O(1) (test_per_channel_check_flags_one_bad_channel).
 PER_CHANNEL_TOL = {"W": 6e-2, "b": 8e-2, "logit": 1e-2}
 # vgg224 (224^2 images, 28^2..224^2-pixel sums per channel): a few channels
-# per layer sit at 0.1-0.25 while the median is 1e-3..1e-2 (measured on
-# MI355X, tools/probes/perchannel_diag.py; the fp32 engine on the same spec is
-# <= 6e-6 per channel except conv1 W 3e-3) -- a handful of pooling / ReLU
-# decisions taken on the other side of a bf16 rounding.  Bounded by the
-# distribution: median and 99th percentile tight, the max loose but below
-# the O(1) error of a wrong channel.
-PER_CHANNEL_DIST_TOL = {"vgg224": dict(median=2.5e-2, p99=1.2e-1, W=0.3, b=0.4)}
+# per layer sit well above the median -- pooling / ReLU decisions taken on
+# the other side of a bf16 rounding (the fp32 engine on the same spec is
+# <= 6e-6 per channel except conv1 W 3e-3).  Bounded by the distribution.
+# Measured on MI355X (round 5, profiles/pytest_gpu_r5b.txt), max / p99 / median:
+#   conv C=64   W 4.9e-2 / 4.2e-2 / 7.0e-3   b 6.8e-2 / 5.7e-2 / 5.0e-3
+#   conv C=128  W 6.0e-2 / 3.7e-2 / 5.9e-3   b 9.0e-2 / 4.9e-2 / 4.3e-3
+#   conv C=256  W 5.9e-2 / 2.8e-2 / 3.6e-3   b 3.9e-2 / 3.1e-2 / 2.7e-3
+#   conv C=512  W 2.5e-2 / 1.9e-2 / 2.2e-3   b 2.6e-2 / 1.8e-2 / 1.7e-3
+#   fc   C=64   W 1.2e-2 / 8.9e-3 / 1.6e-4   b 1.9e-2 / 1.3e-2 / 0
+#   fc   C=10   W 2.6e-3 / 2.5e-3 / 9.6e-4   b 2.6e-3 / 2.5e-3 / 6.2e-4
+# (bounds ~2x the worst layer; a wrong channel is O(1))
+PER_CHANNEL_DIST_TOL = {"vgg224": dict(median=2e-2, p99=1e-1, W=0.12, b=0.18)}
+# full bench batch vs the sum of small-batch chunks (both bf16 engines: the
+# difference is fp32 summation order plus bf16 rounding of chunk-dependent
+# intermediates); per output channel, same scale as PER_CHANNEL_TOL
+BENCH_BATCH_CHANNEL_TOL = {"W": 6e-2, "b": 8e-2}
 
 
 def test_per_channel_check_flags_one_bad_channel():
