@@ -392,7 +392,7 @@ void GpuNet::build() {
       st.fc_tall_dx = (pv->kind == Stage::CONV || pv->act == gpu::ACT_NONE) &&
                       gpu::fc_tall_supported(max_batch_, st.Kin, st.Nout);
     }
-    st.head = st.kind == Stage::FC && st.last && s > 0 && dtype_ == DType::BF16 &&
+    st.head = st.kind == Stage::FC && st.last && s > 0 && !(dtype_ == DType::F32 && ab_flag("no_head32")) &&
               gpu::xent_head_supported(st.Nout, st.Kin, st.in_ld);
     // FC weight gradient on the implicit-GEMM dW kernel (a 1x1 "conv" over the
     // batch, C = in_ld with the pad columns dropped by the reduce)
@@ -1072,7 +1072,7 @@ void GpuNet::loss(const uint8_t* labels, const int32_t* idx, float grad_scale, b
     h.act = pv.kind == Stage::FC ? pv.act : gpu::ACT_NONE;  // conv masks are applied by its staging
     h.dh = pv.grad_buf;
     h.slab = scratch_; h.ldp = last.ldp;
-    gpu::xent_head(h, s);
+    gpu::xent_head(dtype_, h, s);
     gpu::DwReduceParams r;
     r.S = gpu::xent_head_slabs(B_); r.Nout = last.Nout; r.kfeat = last.Kin; r.ldp = last.ldp; r.part = scratch_;
     r.partial_stride = (int64_t)last.Nout * last.ldp;

@@ -486,15 +486,15 @@ struct XentParams {
 // Needs N <= 16, Kin < 128, ldh % 8 == 0.
 struct XentHeadParams {
   XentParams x;
-  const void* h = nullptr; int ldh = 0;     // last FC input activations, bf16 [M][ldh]
+  const void* h = nullptr; int ldh = 0;     // last FC input activations, T [M][ldh]
   const float* w = nullptr;                // last FC weights, fp32 [N][Kin]
   int Kin = 0, act = 0;                    // act of h's producer (ACT_*)
-  void* dh = nullptr;                      // bf16 [M][ldh]
+  void* dh = nullptr;                      // T [M][ldh]
   float* slab = nullptr; int ldp = 0;      // [nwg][N][ldp]
 };
 bool xent_head_supported(int N, int Kin, int ldh);
 int xent_head_slabs(int M);
-void xent_head(const XentHeadParams& p, hipStream_t s);
+void xent_head(DType t, const XentHeadParams& p, hipStream_t s);  // T = bf16 or fp32
 
 // Explicit im2col for the large-image path: out[(n*OH+oy)*OW+ox][k], k =
 // (kh*KS+kw)*SC + c (zero for k >= KS*KS*SC), source through `s` (tile

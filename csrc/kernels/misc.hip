@@ -110,32 +110,42 @@ __global__ void __launch_bounds__(256) softmax_xent_kernel(XentParams p) {
 // round trip) for small heads (LeNet-5: 84 -> 10; the reference model: 200 -> 10).
 constexpr int kHeadRows = 128;
 constexpr int kHeadThreads = 512;
-constexpr int kHeadLd = kHeadRows + 8;  // bf16 row stride of the transposed images (16-byte aligned)
+// row stride of the transposed E / H images (16-byte aligned rows)
+template <typename T>
+__host__ __device__ constexpr int head_ld() { return kHeadRows + (sizeof(T) == 2 ? 8 : 4); }
 // LDS sized by the input width (16 * NT columns, NT = ceil((Kin + 1) / 16)):
 // LeNet-5's 84 -> 10 head needs 36.6 KB, four workgroups per CU, so the
 // 1024 workgroups of a 131072-row batch run in one round (a fixed 128-column
 // layout took 47.6 KB: three per CU, two rounds; 33.2 -> 31.5 us,
 // profiles/xent_head_lds_ab_r2.txt)
 __host__ __device__ constexpr int head_nt(int Kin) { return (Kin + 1 + 15) >> 4; }
+template <typename T>
 __host__ __device__ constexpr int head_lds(int Kin) {
-  return 16 * (16 * head_nt(Kin)) * 4 + 16 * kHeadLd * 2 + 16 * head_nt(Kin) * kHeadLd * 2;
+  return 16 * (16 * head_nt(Kin)) * 4 + (16 + 16 * head_nt(Kin)) * head_ld<T>() * (int)sizeof(T);
 }
 
+// T = bf16: the bf16 engine's rounding points (weights, dlogits, H through
+// bf16); T = float: the fp32 engine, no rounding, the dW tile on f32 MFMA.
+template <typename T>
 __global__ void __launch_bounds__(kHeadThreads) xent_head_kernel(XentHeadParams hp) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  typedef typename Vec8<T>::type V8;
+  constexpr bool kB = sizeof(T) == 2;
+  constexpr int kHeadLd = head_ld<T>();
   __shared__ float red[3][kHeadThreads / 64];
   const XentParams& p = hp.x;
   const int N = p.N, Kin = hp.Kin;
   const int NT = head_nt(Kin), kw = 16 * NT;  // Ws row stride (floats) = HT rows
   float* Ws = reinterpret_cast<float*>(smem);
-  bf16* E = reinterpret_cast<bf16*>(smem + 16 * kw * 4);
-  bf16* HT = E + 16 * kHeadLd;
+  T* E = reinterpret_cast<T*>(smem + 16 * kw * 4);
+  T* HT = E + 16 * kHeadLd;
   const int tid = threadIdx.x;
   const int r = tid >> 2, q = tid & 3;
   // weights rounded through bf16, as the packed compute copy of the FC path
   for (int i = tid; i < 16 * kw; i += kHeadThreads) {
     const int n = i / kw, k = i - n * kw;
-    Ws[i] = (n < N && k < Kin) ? (float)(bf16)hp.w[(size_t)n * Kin + k] : 0.f;
+    const float wv = (n < N && k < Kin) ? hp.w[(size_t)n * Kin + k] : 0.f;
+    Ws[i] = kB ? (float)(bf16)wv : wv;
   }
   const int row = blockIdx.x * kHeadRows + r;
   const bool live = row < p.M;
@@ -177,7 +187,7 @@ __global__ void __launch_bounds__(kHeadThreads) xent_head_kernel(XentHeadParams 
         const float pj = __expf(v[j] - m) * inv;
         const float d = pj - (j == label ? 1.f : 0.f);
         mse += d * d;
-        e[j] = (float)(bf16)(d * p.scale);  // the bf16 dlogits of the unfused path
+        e[j] = kB ? (float)(bf16)(d * p.scale) : d * p.scale;  // the dlogits of the unfused path
         if (p.probs && q == 0) p.probs[(size_t)row * N + j] = pj;
       }
     }
@@ -192,21 +202,21 @@ __global__ void __launch_bounds__(kHeadThreads) xent_head_kernel(XentHeadParams 
   }
   if (q == 0) {
 #pragma unroll
-    for (int j = 0; j < 16; ++j) E[j * kHeadLd + r] = (bf16)e[j];
+    for (int j = 0; j < 16; ++j) E[j * kHeadLd + r] = (T)e[j];
   }
   __syncthreads();  // Ws
 
   // data gradient of the head input + the H^T image (row Kin = ones: bias);
   // thread q of a sample owns the 8-feature chunks q, q+4, ...
-  const bf16* hrow = static_cast<const bf16*>(hp.h) + (size_t)row * hp.ldh;
-  bf16* drow = static_cast<bf16*>(hp.dh) + (size_t)row * hp.ldh;
+  const T* hrow = static_cast<const T*>(hp.h) + (size_t)row * hp.ldh;
+  T* drow = static_cast<T*>(hp.dh) + (size_t)row * hp.ldh;
   const int K8 = (Kin + 7) & ~7;
   for (int k0 = 8 * q; k0 < K8; k0 += 32) {
-    bf16x8 hv;
+    V8 hv;
     if (live) hv = load8(hrow + k0);
     else {
 #pragma unroll
-      for (int i = 0; i < 8; ++i) hv[i] = (bf16)0.f;
+      for (int i = 0; i < 8; ++i) hv[i] = (T)0.f;
     }
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -220,18 +230,18 @@ __global__ void __launch_bounds__(kHeadThreads) xent_head_kernel(XentHeadParams 
         acc[4 + i] += e[n] * w1[i];
       }
     }
-    bf16x8 o;
+    V8 o;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const int k = k0 + i;
       const float y = (float)hv[i];
-      o[i] = k < Kin ? (bf16)(acc[i] * act_grad_y(hp.act, y)) : (bf16)0.f;
-      HT[k * kHeadLd + r] = (k < Kin && live) ? hv[i] : (bf16)((k == Kin && live) ? 1.f : 0.f);
+      o[i] = k < Kin ? (T)(acc[i] * act_grad_y(hp.act, y)) : (T)0.f;
+      HT[k * kHeadLd + r] = (k < Kin && live) ? hv[i] : (T)((k == Kin && live) ? 1.f : 0.f);
     }
     if (live) store8(drow + k0, o);
   }
   if (q == 0)
-    for (int k = K8; k < 16 * NT; ++k) HT[k * kHeadLd + r] = (bf16)((k == Kin && live) ? 1.f : 0.f);
+    for (int k = K8; k < 16 * NT; ++k) HT[k * kHeadLd + r] = (T)((k == Kin && live) ? 1.f : 0.f);
   __syncthreads();
 
   // weight + bias gradient of the workgroup's rows: wave w computes the
@@ -611,14 +621,19 @@ bool xent_head_supported(int N, int Kin, int ldh) {
 
 int xent_head_slabs(int M) { return cdiv(M, kHeadRows); }
 
-void xent_head(const XentHeadParams& p, hipStream_t s) {
+void xent_head(DType t, const XentHeadParams& p, hipStream_t s) {
   MCC_CHECK(p.x.M > 0 && xent_head_supported(p.x.N, p.Kin, p.ldh), "xent_head: needs N <= 16, Kin < 256, ldh % 8 == 0");
   MCC_CHECK(p.x.ldl % 4 == 0 && (reinterpret_cast<uintptr_t>(p.x.logits) & 15) == 0 && p.x.ldl >= ((p.x.N + 3) & ~3),
             "xent_head: logits rows must be 16-byte aligned");
   MCC_CHECK(p.h && p.dh && p.w && p.slab && p.ldp >= p.Kin + 1 && (reinterpret_cast<uintptr_t>(p.h) & 15) == 0 &&
                 (reinterpret_cast<uintptr_t>(p.dh) & 15) == 0,
             "xent_head: bad buffers");
-  hipLaunchKernelGGL(xent_head_kernel, dim3((unsigned)xent_head_slabs(p.x.M)), dim3(kHeadThreads), head_lds(p.Kin), s, p);
+  if (t == DType::BF16)
+    hipLaunchKernelGGL(xent_head_kernel<bf16>, dim3((unsigned)xent_head_slabs(p.x.M)), dim3(kHeadThreads),
+                       head_lds<bf16>(p.Kin), s, p);
+  else
+    hipLaunchKernelGGL(xent_head_kernel<float>, dim3((unsigned)xent_head_slabs(p.x.M)), dim3(kHeadThreads),
+                       head_lds<float>(p.Kin), s, p);
 }
 
 void softmax_xent(DType t, const XentParams& p, hipStream_t s) {
