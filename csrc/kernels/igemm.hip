@@ -95,6 +95,29 @@ __device__ __forceinline__ float qswap2(float v) {
 __device__ __forceinline__ int qswap1i(int v) { return __builtin_amdgcn_mov_dpp(v, 0xB1, 0xf, 0xf, false); }
 __device__ __forceinline__ int qswap2i(int v) { return __builtin_amdgcn_mov_dpp(v, 0x4E, 0xf, 0xf, false); }
 
+// POOL epilogue (round 5): the pooling kernels run the MFMA in the C
+// orientation (A = pixels, B = weights), so lane (r16, g) of a fragment holds
+// rows 4g..4g+3 -- the four positions of ONE pooling window -- of channel
+// r16: the pool and its first-max-wins argmax are three in-lane compares.
+// (The C^T layout spread a window over a DPP quad: two exchanges of value
+// and index per channel, ~15 VALU per pooled value, which cost VGG-11's
+// forward 1.2 ms of 12.3, tools/probes/lenet_phase_probe.py MCC_IG_ABL=1.)
+// One bf16 + one argmax byte per lane; 16 lanes = 16 consecutive channels.
+__device__ __forceinline__ void pool_window_store(const IgemmParams& p, const f32x4& acc, int mwin, int ch, float bias,
+                                                  bool bias_act) {
+  float mx = acc[0];
+  uint32_t a = 0;
+  if (acc[1] > mx) { mx = acc[1]; a = 1; }
+  if (acc[2] > mx) { mx = acc[2]; a = 2; }
+  if (acc[3] > mx) { mx = acc[3]; a = 3; }
+  float v = mx + bias;
+  if (bias_act) v = act_apply(p.act, v);
+  const bf16 o = (bf16)v;
+  if (bias_act && p.act == ACT_RELU && !((float)o > 0.f)) a = 4;  // ReLU-inactive window: argmax byte 4
+  static_cast<bf16*>(p.out)[(size_t)mwin * p.ldo + ch] = o;
+  p.out_arg[(size_t)mwin * p.N + ch] = (uint8_t)a;
+}
+
 // POOL: fused 2x2/2 max-pool epilogue.  The GEMM rows enumerate (b, py, px,
 // pos) so each pooling window is four consecutive rows = four lanes of one
 // DPP quad (the C^T fragment holds pixel r16 in lane r16); the max and its
@@ -103,6 +126,12 @@ __device__ __forceinline__ int qswap2i(int v) { return __builtin_amdgcn_mov_dpp(
 // U8: the input is the u8 image set (optional sample-index gather, /255 as
 // cnn.c:457) with few channels (the first layer): the pixel tile is gathered
 // through registers (bytes -> bf16) into the same swizzled LDS image.
+// epilogue ablations (timing studies only; tools/build_variant.sh): 1 = no
+// pool exchange, 2 = no bias / activation / argmax codes
+#ifndef MCC_IG_ABL
+#define MCC_IG_ABL 0
+#endif
+
 template <int BN, bool BIAS_ACT, bool POOL, bool U8>
 __global__ void __launch_bounds__(kIgT, 2) igemm_conv_kernel(IgemmParams p) {
   constexpr int BM = kIgBM;
@@ -362,11 +391,25 @@ __global__ void __launch_bounds__(kIgT, 2) igemm_conv_kernel(IgemmParams p) {
 #pragma unroll
       for (int i = 0; i < FN; ++i)
 #pragma unroll
-        for (int j = 0; j < FM; ++j) acc[i][j] = mma(acc[i][j], wb[i], xa[j]);
+        for (int j = 0; j < FM; ++j) acc[i][j] = POOL ? mma(acc[i][j], xa[j], wb[i]) : mma(acc[i][j], wb[i], xa[j]);
     }
     __syncthreads();
   }
 
+  if constexpr (POOL) {  // lane: channel r16, window rows 4g..4g+3 (see pool_window_store)
+#pragma unroll
+    for (int i = 0; i < FN; ++i) {
+      const int ch = n0 + wn * (BN / 2) + i * 16 + r16;
+      if (ch >= p.N) continue;
+      const float bv = BIAS_ACT && p.bias ? p.bias[ch] : 0.f;
+#pragma unroll
+      for (int j = 0; j < FM; ++j) {
+        const int m = m0 + wm * 64 + j * 16 + 4 * g;
+        if (m < p.M) pool_window_store(p, acc[i][j], m >> 2, ch, bv, BIAS_ACT);
+      }
+    }
+    return;
+  }
   // ---- epilogue: lane holds channels 4g..4g+3 of pixel r16 per fragment ----
   bf16* out = static_cast<bf16*>(p.out);
 #pragma unroll
@@ -385,7 +428,7 @@ __global__ void __launch_bounds__(kIgT, 2) igemm_conv_kernel(IgemmParams p) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) v[e] = acc[i][j][e];
       uint32_t arg = 0;
-      if constexpr (POOL) {  // every lane of the quad takes part in the exchange
+      if constexpr (POOL && !(MCC_IG_ABL & 1)) {  // every lane of the quad takes part in the exchange
         const int pos = r16 & 3;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
@@ -403,6 +446,7 @@ __global__ void __launch_bounds__(kIgT, 2) igemm_conv_kernel(IgemmParams p) {
       if (POOL && (r16 & 3) != 0) continue;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
+        if (MCC_IG_ABL & 2) break;
         v[e] += bv[e];
         if (BIAS_ACT) v[e] = act_apply(p.act, v[e]);
       }
@@ -413,7 +457,7 @@ __global__ void __launch_bounds__(kIgT, 2) igemm_conv_kernel(IgemmParams p) {
       }
       const bf16x4 o = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
       const int orow = POOL ? (m >> 2) : m;
-      if (POOL && BIAS_ACT && p.act == ACT_RELU) {  // ReLU-inactive window: argmax byte 4
+      if (POOL && BIAS_ACT && !(MCC_IG_ABL & 2) && p.act == ACT_RELU) {  // ReLU-inactive window: argmax byte 4
 #pragma unroll
         for (int e = 0; e < 4; ++e)
           if (!((float)o[e] > 0.f)) arg = (arg & ~(0xffu << (8 * e))) | (4u << (8 * e));
@@ -617,7 +661,8 @@ __global__ void __launch_bounds__(kBigT, 1) igemm_big_kernel(IgemmParams p) {
 #pragma unroll
       for (int f = 0; f < FA; ++f)
 #pragma unroll
-        for (int e = 0; e < 2; ++e) acc[ha][f][hb][e] = mma(acc[ha][f][hb][e], fa[f][ks], fb[e][ks]);
+        for (int e = 0; e < 2; ++e)
+          acc[ha][f][hb][e] = POOL ? mma(acc[ha][f][hb][e], fb[e][ks], fa[f][ks]) : mma(acc[ha][f][hb][e], fa[f][ks], fb[e][ks]);
   };
 
   const int nk = p.K / BK;  // host: K % 64 == 0
@@ -642,6 +687,24 @@ __global__ void __launch_bounds__(kBigT, 1) igemm_big_kernel(IgemmParams p) {
         else mfma_q(1, 0, fb0);
       });
 
+  if constexpr (POOL) {  // lane: channel r16, window rows 4g..4g+3 (see pool_window_store)
+#pragma unroll
+    for (int ha = 0; ha < 2; ++ha)
+#pragma unroll
+      for (int f = 0; f < FA; ++f) {
+        const int ch = n0 + ha * HA + wr * (HA / 2) + f * 16 + r16;
+        if (ch >= p.N) continue;
+        const float bv = BIAS_ACT && p.bias ? p.bias[ch] : 0.f;
+#pragma unroll
+        for (int hb = 0; hb < 2; ++hb)
+#pragma unroll
+          for (int e2 = 0; e2 < 2; ++e2) {
+            const int m = m0 + hb * HB + wc * 32 + e2 * 16 + 4 * g;
+            if (m < p.M) pool_window_store(p, acc[ha][f][hb][e2], m >> 2, ch, bv, BIAS_ACT);
+          }
+      }
+    return;
+  }
   // ---- epilogue: lane holds channels 4g..4g+3 of pixel r16 per fragment ----
   bf16* out = static_cast<bf16*>(p.out);
 #pragma unroll
@@ -664,7 +727,7 @@ __global__ void __launch_bounds__(kBigT, 1) igemm_big_kernel(IgemmParams p) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) v[e] = acc[ha][f][hb][e2][e];
           uint32_t arg = 0;
-          if constexpr (POOL) {  // every lane of the quad takes part in the exchange
+          if constexpr (POOL && !(MCC_IG_ABL & 1)) {  // every lane of the quad takes part in the exchange
             const int pos = r16 & 3;
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
@@ -682,6 +745,7 @@ __global__ void __launch_bounds__(kBigT, 1) igemm_big_kernel(IgemmParams p) {
           if (POOL && (r16 & 3) != 0) continue;
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
+            if (MCC_IG_ABL & 2) break;
             v[e] += bv[e];
             if (BIAS_ACT) v[e] = act_apply(p.act, v[e]);
           }
@@ -692,7 +756,7 @@ __global__ void __launch_bounds__(kBigT, 1) igemm_big_kernel(IgemmParams p) {
           }
           const bf16x4 o = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
           const int orow = POOL ? (m >> 2) : m;
-          if (POOL && BIAS_ACT && p.act == ACT_RELU) {  // ReLU-inactive window: argmax byte 4
+          if (POOL && BIAS_ACT && !(MCC_IG_ABL & 2) && p.act == ACT_RELU) {  // ReLU-inactive window: argmax byte 4
 #pragma unroll
             for (int e = 0; e < 4; ++e)
               if (!((float)o[e] > 0.f)) arg = (arg & ~(0xffu << (8 * e))) | (4u << (8 * e));

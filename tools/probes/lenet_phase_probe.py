@@ -24,10 +24,12 @@ def run_one(path):
     assert os.path.dirname(mcc.__file__).startswith(os.path.abspath(path)), mcc.__file__
     B = int(os.environ.get("PROBE_B", "163840"))
     spec = mcc.make_model(os.environ.get("PROBE_MODEL", "lenet5"))
-    imgs, labels = mcc.synth_dataset(65536, 1, 28, 28, 10, seed=1)
+    C, H, W = spec.input_shape()
+    ndata = min(65536, max(B, 1024))
+    imgs, labels = mcc.synth_dataset(ndata, C, H, W, spec.num_classes(), seed=1)
     dev = torch.device("cuda", 0)
     d_img, d_lab = torch.from_numpy(imgs).to(dev), torch.from_numpy(labels).to(dev)
-    idx = torch.randint(0, 65536, (B,), dtype=torch.int32, device=dev)
+    idx = torch.randint(0, ndata, (B,), dtype=torch.int32, device=dev)
     net = mcc.GpuNet(spec, "bf16", B)
     net.set_params(mcc.init_params(spec, seed=0, mode="fast").astype(np.float32))
     s = torch.cuda.current_stream().cuda_stream
