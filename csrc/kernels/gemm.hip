@@ -363,6 +363,14 @@ void gemm(DType t, const GemmParams& p, hipStream_t s) {
 }
 
 int gemm_fwd_splitk(int M, int N, int K) {
+  // long-K bf16 layers with M, N >= 256 (VGG-11 FC1: 640 x 4096 x 25088):
+  // split K so that 128x128 tiles fill the chip (launch_gemm then picks them)
+  // -- 64x64 tiles over the whole K ran at ~310 TFLOP/s
+  if (M >= 256 && N >= 256 && K >= 8192) {
+    const int64_t t128 = (int64_t)cdiv(M, 128) * cdiv(N, 128);
+    int sk = (int)std::min<int64_t>(8, std::max<int64_t>(1, (1024 + t128 - 1) / t128));
+    return std::max(1, std::min(sk, K / 1024));
+  }
   const int64_t tiles = (int64_t)cdiv(M, 64) * cdiv(N, 64);
   if (tiles >= 512 || K < 1024) return 1;
   int sk = (int)std::min<int64_t>(16, 1024 / std::max<int64_t>(1, tiles));

@@ -335,6 +335,20 @@ __global__ void __launch_bounds__(kIgT, 2) igemm_conv_kernel(IgemmParams p) {
         store8(A + (j * kIgT + tid) * 8, v);
       }
     }
+    } else if (p.c_shift >= 6) {
+      // C = 2^s >= 64: the 64-deep K-step is one tap, no channel wrap, K % 64
+      // == 0; the tap comes from a shift (no runtime division per step) and
+      // a piece is 2 adds + 2 bounds tests + its address
+      const int tap = k0 >> p.c_shift;
+      const int c0 = k0 - (tap << p.c_shift);
+      const int ky = p.KS == 3 ? tap / 3 : tap / p.KS, kx = tap - ky * p.KS;
+      const int toff = ((ky * p.W + kx) << p.c_shift) + c0;
+#pragma unroll
+      for (int j = 0; j < AJ; ++j) {
+        const int iy = a_iy[j] + ky, ix = a_ix[j] + kx;
+        const bool ok = (unsigned)iy < (unsigned)p.H && (unsigned)ix < (unsigned)p.W;
+        glds16(ok ? in + (a_base[j] + a_seg[j] + toff) : zero, A + (j * kIgT + wave * 64) * 8);
+      }
     } else {
       // C % 32 == 0: a 64-deep K-step spans at most two taps (the second from
       // the piece's channel wrap; C = 32: slots 4..7), both wave-uniform
@@ -356,7 +370,7 @@ __global__ void __launch_bounds__(kIgT, 2) igemm_conv_kernel(IgemmParams p) {
     }
 #pragma unroll
     for (int j = 0; j < BJ; ++j) {
-      const bf16* src = (b_ptr[j] && k0 + b_k[j] < p.K) ? b_ptr[j] + k0 : zero;
+      const bf16* src = (b_ptr[j] && (p.c_shift >= 6 || k0 + b_k[j] < p.K)) ? b_ptr[j] + k0 : zero;
       glds16(src, Bw + (j * kIgT + wave * 64) * 8);
     }
   };
@@ -614,9 +628,10 @@ __global__ void __launch_bounds__(kBigT, 1) igemm_big_kernel(IgemmParams p) {
   auto stage_b = [&](int kt, int h) {
     bf16* dst = smem + (kt & 1) * BUF + 2 * QA + h * QB;
     const int k0 = kt * BK;
-    const int tap = k0 / p.C;  // uniform; C % 64 == 0
+    // uniform; C % 64 == 0 (a shift when C is a power of two: no runtime division per step)
+    const int tap = p.c_shift >= 0 ? k0 >> p.c_shift : k0 / p.C;
     const int c0 = k0 - tap * p.C;
-    const int ky = tap / p.KS, kx = tap - ky * p.KS;
+    const int ky = p.KS == 3 ? tap / 3 : tap / p.KS, kx = tap - ky * p.KS;
     const int toff = (ky * p.W + kx) * p.C + c0;
 #pragma unroll
     for (int j = 0; j < GB; ++j) {
@@ -830,8 +845,10 @@ __global__ void __launch_bounds__(kIgT, 2) igemm_dw_kernel(IgemmDwParams p) {
     d_col[j] = co0 + ((s % SD) ^ swz128(row)) * 8;
     dm_[j] = ks0 * BK + row;
   }
-  int m_[JX], b_[JX], oy_[JX], ox_[JX];
-  int x_ky[JX], x_kx[JX], x_c[JX], x_kind[JX];  // kind: 0 tap, 1 ones, 2 zero
+  // (round 5) the pixel's input corner (iy0, ix0) and element offset pb are
+  // carried with (oy, ox): no per-step multiplies (see igemm_dwbig_kernel)
+  int m_[JX], oy_[JX], ox_[JX], iy0_[JX], ix0_[JX], pb_[JX];
+  int x_ky[JX], x_kx[JX], x_off[JX], x_kind[JX];  // kind: 0 tap, 1 ones, 2 zero
 #pragma unroll
   for (int j = 0; j < JX; ++j) {
     const int s = j * kIgT + tid;
@@ -840,21 +857,28 @@ __global__ void __launch_bounds__(kIgT, 2) igemm_dw_kernel(IgemmDwParams p) {
     const int k = k0 + ls * 8;
     if (k < p.kf) {
       const int tap = k / p.C;
-      x_c[j] = k - tap * p.C;
+      const int c = k - tap * p.C;
       x_ky[j] = tap / p.KS;
       x_kx[j] = tap - x_ky[j] * p.KS;
+      x_off[j] = (x_ky[j] * p.W + x_kx[j]) * p.C + c;
       x_kind[j] = 0;
     } else {
-      x_c[j] = 0; x_ky[j] = 0; x_kx[j] = 0;
+      x_off[j] = 0; x_ky[j] = 0; x_kx[j] = 0;
       x_kind[j] = k == p.kf ? 1 : 2;
     }
     const int m = ks0 * BK + row;
     m_[j] = m;
-    b_[j] = mdiv(p.div_ohw, m);
-    const int rem = m - b_[j] * p.OH * p.OW;
+    const int b = mdiv(p.div_ohw, m);
+    const int rem = m - b * p.OH * p.OW;
     oy_[j] = mdiv(p.div_ow, rem);
     ox_[j] = rem - oy_[j] * p.OW;
+    iy0_[j] = oy_[j] * p.stride - p.pad;
+    ix0_[j] = ox_[j] * p.stride - p.pad;
+    pb_[j] = ((b * p.H + iy0_[j]) * p.W + ix0_[j]) * p.C;
   }
+  const int sW = p.stride * p.W, sC = p.stride * p.C;
+  const int inc_x = p.adv_x * sC, inc_c1 = (sW - p.OW * p.stride) * p.C, inc_y = p.adv_y * sW * p.C;
+  const int inc_c2 = (p.H - p.OH * p.stride) * p.W * p.C, inc_b = p.adv_b * p.H * p.W * p.C;
   const uint64_t zero_u = reinterpret_cast<uint64_t>(zero), ones_u = reinterpret_cast<uint64_t>(ones);
 
   auto stage = [&](int buf) {  // the next K-step of this split
@@ -871,21 +895,33 @@ __global__ void __launch_bounds__(kIgT, 2) igemm_dw_kernel(IgemmDwParams p) {
 #pragma unroll
     for (int j = 0; j < JX; ++j) {
       const bool mok = m_[j] < p.M;
-      const int iy = oy_[j] * p.stride - p.pad + x_ky[j], ix = ox_[j] * p.stride - p.pad + x_kx[j];
+      const int iy = iy0_[j] + x_ky[j], ix = ix0_[j] + x_kx[j];
       const bool tap_ok = mok && x_kind[j] == 0 && (unsigned)iy < (unsigned)p.H && (unsigned)ix < (unsigned)p.W;
-      const int off = ((b_[j] * p.H + iy) * p.W + ix) * p.C + x_c[j];  // < 2^31 (host check); unused if !tap_ok
+      const int off = pb_[j] + x_off[j];  // < 2^31 (host check); unused if !tap_ok
       const uint64_t x_u = reinterpret_cast<uint64_t>(in) + 2 * (uint64_t)(uint32_t)off;
       const uint64_t xs = tap_ok ? x_u : ((mok && x_kind[j] == 1) ? ones_u : zero_u);
       glds16(reinterpret_cast<const bf16*>(xs), X + (j * kIgT + wave * 64) * 8);
       // advance this row by BK pixels
       m_[j] += BK;
       ox_[j] += p.adv_x;
-      const int c1 = ox_[j] >= p.OW ? 1 : 0;
-      ox_[j] -= c1 * p.OW;
-      oy_[j] += p.adv_y + c1;
-      const int c2 = oy_[j] >= p.OH ? 1 : 0;
-      oy_[j] -= c2 * p.OH;
-      b_[j] += p.adv_b + c2;
+      ix0_[j] += p.adv_x * p.stride;
+      pb_[j] += inc_x;
+      if (ox_[j] >= p.OW) {
+        ox_[j] -= p.OW;
+        ix0_[j] -= p.OW * p.stride;
+        oy_[j] += 1;
+        iy0_[j] += p.stride;
+        pb_[j] += inc_c1;
+      }
+      oy_[j] += p.adv_y;
+      iy0_[j] += p.adv_y * p.stride;
+      pb_[j] += inc_y;
+      if (oy_[j] >= p.OH) {
+        oy_[j] -= p.OH;
+        iy0_[j] -= p.OH * p.stride;
+        pb_[j] += inc_c2;
+      }
+      pb_[j] += inc_b;
     }
   };
 
@@ -1095,30 +1131,42 @@ __global__ void __launch_bounds__(kBigT, 1) igemm_dwbig_kernel(IgemmDwParams p) 
   }
   // X pieces: pixel row j (decoded once, advanced per K-step with carries),
   // tap/channel per (half, j) packed as c << 8 | ky << 4 | kx (-1: k >= kf)
-  int m_[GB], b_[GB], oy_[GB], ox_[GB];
-  int x_tap[2][GB];
+  // (round 5) the pixel's input corner (iy0, ix0) and its element offset pb
+  // are carried along with (oy, ox) -- no per-step multiplies: a piece was
+  // 5 quarter-rate v_mul_lo_u32 (stride, H, W, C) per K-step
+  int m_[GB], oy_[GB], ox_[GB], iy0_[GB], ix0_[GB], pb_[GB];
+  int x_tap[2][GB], x_off[2][GB];
 #pragma unroll
   for (int j = 0; j < GB; ++j) {
     const int s = j * kBigT + tid;
     const int row = s >> 4;
     const int m = ks0 * BK + row;
     m_[j] = m;
-    b_[j] = mdiv(p.div_ohw, m);
-    const int rem = m - b_[j] * p.OH * p.OW;
+    const int b = mdiv(p.div_ohw, m);
+    const int rem = m - b * p.OH * p.OW;
     oy_[j] = mdiv(p.div_ow, rem);
     ox_[j] = rem - oy_[j] * p.OW;
+    iy0_[j] = oy_[j] * p.stride - p.pad;
+    ix0_[j] = ox_[j] * p.stride - p.pad;
+    pb_[j] = ((b * p.H + iy0_[j]) * p.W + ix0_[j]) * p.C;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int k = k0 + h * CB + ((s & 15) ^ swz128(row)) * 8;
       if (k < p.kf) {
         const int tap = k / p.C, c = k - tap * p.C;
         const int ky = tap / p.KS, kx = tap - ky * p.KS;
-        x_tap[h][j] = (c << 8) | (ky << 4) | kx;
+        x_tap[h][j] = (ky << 4) | kx;
+        x_off[h][j] = (ky * p.W + kx) * p.C + c;
       } else {
         x_tap[h][j] = -1;
+        x_off[h][j] = 0;
       }
     }
   }
+  // uniform carry increments of (iy0, ix0, pb)
+  const int sW = p.stride * p.W, sC = p.stride * p.C;
+  const int inc_x = p.adv_x * sC, inc_c1 = (sW - p.OW * p.stride) * p.C, inc_y = p.adv_y * sW * p.C;
+  const int inc_c2 = (p.H - p.OH * p.stride) * p.W * p.C, inc_b = p.adv_b * p.H * p.W * p.C;
 
   auto stage_a = [&](int ks, int h) {
     bf16* dst = smem + ((ks - ks0) & 1) * BUF + h * QA;
@@ -1135,9 +1183,9 @@ __global__ void __launch_bounds__(kBigT, 1) igemm_dwbig_kernel(IgemmDwParams p) 
 #pragma unroll
     for (int j = 0; j < GB; ++j) {
       const int t = x_tap[h][j];
-      const int iy = oy_[j] * p.stride - p.pad + ((t >> 4) & 15), ix = ox_[j] * p.stride - p.pad + (t & 15);
+      const int iy = iy0_[j] + ((t >> 4) & 15), ix = ix0_[j] + (t & 15);
       const bool ok = t >= 0 && m_[j] < p.M && (unsigned)iy < (unsigned)p.H && (unsigned)ix < (unsigned)p.W;
-      const int off = ((b_[j] * p.H + iy) * p.W + ix) * p.C + (t >> 8);  // < 2^31 (host check); unused if !ok
+      const int off = pb_[j] + x_off[h][j];  // < 2^31 (host check); unused if !ok
       const uint64_t src = reinterpret_cast<uint64_t>(in) + 2 * (uint64_t)(uint32_t)off;
       glds16(reinterpret_cast<const bf16*>(ok ? src : zero_u), dst + (j * kBigT + wave * 64) * 8);
     }
@@ -1147,12 +1195,24 @@ __global__ void __launch_bounds__(kBigT, 1) igemm_dwbig_kernel(IgemmDwParams p) 
     for (int j = 0; j < GB; ++j) {
       m_[j] += BK;
       ox_[j] += p.adv_x;
-      const int c1 = ox_[j] >= p.OW ? 1 : 0;
-      ox_[j] -= c1 * p.OW;
-      oy_[j] += p.adv_y + c1;
-      const int c2 = oy_[j] >= p.OH ? 1 : 0;
-      oy_[j] -= c2 * p.OH;
-      b_[j] += p.adv_b + c2;
+      ix0_[j] += p.adv_x * p.stride;
+      pb_[j] += inc_x;
+      if (ox_[j] >= p.OW) {  // (compiles to selects)
+        ox_[j] -= p.OW;
+        ix0_[j] -= p.OW * p.stride;
+        oy_[j] += 1;
+        iy0_[j] += p.stride;
+        pb_[j] += inc_c1;
+      }
+      oy_[j] += p.adv_y;
+      iy0_[j] += p.adv_y * p.stride;
+      pb_[j] += inc_y;
+      if (oy_[j] >= p.OH) {
+        oy_[j] -= p.OH;
+        iy0_[j] -= p.OH * p.stride;
+        pb_[j] += inc_c2;
+      }
+      pb_[j] += inc_b;
     }
   };
 
@@ -1340,6 +1400,9 @@ void igemm_conv(const IgemmParams& p0, hipStream_t s) {
     MCC_CHECK(igemm_conv_supported(p.C, p.N, p.KS), "igemm_conv: needs C % 32 == 0 (1x1: C % 8) and N % 8 == 0");
   }
   MCC_CHECK(p.K == p.KS * p.KS * p.C, "igemm_conv: K must be KS*KS*C");
+  p.c_shift = -1;
+  for (int sh = 0; sh < 31; ++sh)
+    if (p.C == (1 << sh)) p.c_shift = sh;
   MCC_CHECK(p.M == p.B * p.OH * p.OW && p.M > 0, "igemm_conv: M must be B*OH*OW");
   MCC_CHECK(p.ldw >= p.K && p.ldw % 8 == 0 && p.ldo >= p.N && p.ldo % 4 == 0, "igemm_conv: bad leading dims");
   MCC_CHECK(!p.relu_mask || (!p.epi_bias_act && !p.pool), "igemm_conv: relu_mask is a data-gradient epilogue");
@@ -1370,6 +1433,9 @@ void igemm_conv(const IgemmParams& p0, hipStream_t s) {
   }
   // 256-pixel tiles for the wide layers (p.tile = 0: 128x128 kernel only;
   // 128: 256x128 tiles only; -1 = auto, as 1)
+  // (round 5: 256x128 tiles for the pooled 128-channel conv2 measured 18.66 k
+  // vs 18.70 k img/s with the in-lane pool epilogue; all 128-channel layers
+  // on them 16.7 k)
   const int big_mode = p.tile >= 0 ? p.tile : 1;
   // auto: 256x256 tiles where N % 256 == 0 (the 128-channel variant measured
   // slower than the 128x128 kernel on VGG conv2 / conv3-dX: profiles/igemm256_ab_r2.txt)

@@ -543,6 +543,7 @@ struct IgemmParams {
   int tile = -1;                     // -1 auto, 0: 128x128 kernel,
                                      // 128 / 256: 256-pixel x 128 / 256-channel kernel where legal
   DivMagic div_ohw, div_ow;
+  int c_shift = -1;                  // set at launch: log2(C) when C is a power of two (K-step tap by shift)
 };
 bool igemm_conv_supported(int C, int N, int KS);
 void igemm_conv(const IgemmParams& p, hipStream_t s);
