@@ -746,6 +746,8 @@ void conv_direct_forward(const Conv1DirectParams& p, hipStream_t s) {
   if (p.Cin == 1)
     hipLaunchKernelGGL((conv_direct_fwd_kernel<5, 1, 6>), grid, block, fwd_lds(p), s, p, p.wt, p.bias, p.out,
                        p.out_arg);
+  else if (p.H == 14 && p.W == 14 && p.pad == 0 && ab_flag("f32_mfma_fwd2"))
+    lenet32_conv2_fwd(p, s);  // f32 MFMA (lenet_f32.hip; measured slower, opt-in)
   else
     hipLaunchKernelGGL((conv_direct_fwd_kernel<5, 6, 16>), grid, block, fwd_lds(p), s, p, p.wt, p.bias, p.out,
                        p.out_arg);

@@ -256,6 +256,7 @@ int lenet32_dw1_grid(int N);
 int lenet32_dw2_grid(int N);
 void lenet32_dw1(const Conv1DirectParams& p, hipStream_t s);
 void lenet32_dw2(const Conv1DirectParams& p, hipStream_t s);
+void lenet32_conv2_fwd(const Conv1DirectParams& p, hipStream_t s);  // LeNet-5 conv2 forward on f32 MFMA
 
 // Forward of the u8 RGB first conv (C = 3, 3x3, stride 1, pad 1, bias + ReLU
 // + 2x2/2 max-pool fused), bf16 MFMA, output pooled NHWC [N][H/2][W/2][Cout]

@@ -354,6 +354,91 @@ __global__ void __launch_bounds__(kD1T) lenet32_dw1_kernel(Conv1DirectParams p) 
 
 }  // namespace
 
+// ---------------------------------------------------------------------------
+// conv2 forward on exact f32 MFMA (round 5): 6 -> 16, 5x5 valid (14x14 ->
+// 10x10), ReLU, 2x2 max-pool with argmax.  One wave per image; the GEMM is
+// C[pixel][co] = sum_k patch[pixel][k] W[k][co], K = 25 taps x 6 channels =
+// 150 (38 steps of v_mfma_f32_16x16x4_f32, 152: zero weights past 150), the
+// 100 pixels window-major in 7 tiles of 16 rows (row 4w + i = position i of
+// pooling window w), so lane (co, g) of tile T holds the four positions of
+// window 4T + g: the pool, its first-max argmax, bias and ReLU are in-lane.
+// Operands: the image's Y1 (HWC, 6 floats per pixel, as stored) in LDS, A
+// read per lane at a per-lane base + a per-step offset register; weights in
+// 38 registers.  MEASURED, NOT THE DEFAULT (MCC_AB=f32_mfma_fwd2 selects it):
+// 1,073 us vs 1,051 us for the packed-FMA kernel conv_direct_fwd<5, 6, 16>
+// at B = 163,840 (two interleaved accumulator chains: 1,155 us) -- the f32
+// matrix rate equals the packed-FMA vector rate on gfx950, and the MFMA
+// form's 266 instructions per image (16 / 16 useful rows, K 152 / 150) run
+// as one dependent chain per tile against one LDS operand read each.
+constexpr int kC2Steps = 38;
+constexpr int kC2Img = 14 * 14 * 6;  // floats
+__global__ void __launch_bounds__(64) lenet32_conv2_fwd_kernel(Conv1DirectParams p, const float* __restrict__ wt,
+                                                               const float* __restrict__ bias, float* __restrict__ out,
+                                                               uint8_t* __restrict__ out_arg) {
+  __shared__ __attribute__((aligned(16))) float ys[kC2Img + 4];
+  const int lane = threadIdx.x, r = lane & 15, g = lane >> 4;
+  // B operand: W[k = 4s + g][co = r], k = tap * 6 + ci (tap-major packed copy: wt[ci][tap][co])
+  float wb[kC2Steps];
+  int koff[kC2Steps];
+#pragma unroll
+  for (int st = 0; st < kC2Steps; ++st) {
+    const int k = 4 * st + g;
+    const int tap = k / 6, ci = k - 6 * tap;
+    wb[st] = k < 150 ? wt[(ci * 25 + tap) * 16 + r] : 0.f;
+    koff[st] = k < 150 ? ((tap / 5) * 14 + tap % 5) * 6 + ci : 0;
+  }
+  const float bv = bias[r];
+  const int pos = r & 3, pofs = ((pos >> 1) * 14 + (pos & 1)) * 6;
+  const int grid = (int)gridDim.x;
+  for (int img = blockIdx.x; img < p.N; img += grid) {
+    // (no register prefetch: 16 waves per CU hide the load; 20 more VGPRs
+    // would cost a wave per SIMD)
+    const float4* src = reinterpret_cast<const float4*>(p.xf + (size_t)img * kC2Img);
+    float4 v4[5];
+#pragma unroll
+    for (int i = 0; i < 5; ++i) v4[i] = src[min(lane + 64 * i, kC2Img / 4 - 1)];
+    __syncthreads();  // (one wave: orders the previous image's reads before the overwrite)
+#pragma unroll
+    for (int i = 0; i < 5; ++i)
+      if (lane + 64 * i < kC2Img / 4) reinterpret_cast<float4*>(ys)[lane + 64 * i] = v4[i];
+    __syncthreads();
+    float* o = out + (size_t)img * 25 * 16;
+    uint8_t* oa = out_arg + (size_t)img * 25 * 16;
+#pragma unroll 1
+    for (int T = 0; T < 7; ++T) {
+      // A operand rows: row r -> window 4T + (r >> 2) (25..27: padding), position r & 3
+      const int wr = min(4 * T + (r >> 2), 24);
+      const int py = (wr * 13) >> 6, px = wr - 5 * py;  // wr / 5 for wr < 25
+      const float* yb = ys + (2 * py * 14 + 2 * px) * 6 + pofs;
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int st = 0; st < kC2Steps; ++st)
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(yb[koff[st]], wb[st], acc, 0, 0, 0);
+      // lane: window 4T + g, positions 0..3 (first max wins), channel r
+      float best = acc[0];
+      uint32_t a = 0;
+      if (acc[1] > best) { best = acc[1]; a = 1; }
+      if (acc[2] > best) { best = acc[2]; a = 2; }
+      if (acc[3] > best) { best = acc[3]; a = 3; }
+      const float y = fmaxf(best + bv, 0.f);
+      const int w = 4 * T + g;
+      if (w < 25) {
+        o[w * 16 + r] = y;
+        oa[w * 16 + r] = (uint8_t)(y > 0.f ? a : 4u);
+      }
+    }
+  }
+}
+
+int lenet32_conv2_fwd_grid(int N) { return std::max(1, std::min(N, 256 * 16)); }  // 16 waves per CU (<= 128 VGPRs)
+void lenet32_conv2_fwd(const Conv1DirectParams& p, hipStream_t s) {
+  MCC_CHECK(p.Cin == 6 && p.C == 16 && p.KS == 5 && p.pad == 0 && p.H == 14 && p.W == 14 && p.PH == 5 && p.PW == 5 &&
+                p.xf && p.wt && p.bias && p.out && p.out_arg,
+            "lenet32_conv2_fwd: LeNet-5 conv2 shape only");
+  hipLaunchKernelGGL(lenet32_conv2_fwd_kernel, dim3((unsigned)lenet32_conv2_fwd_grid(p.N)), dim3(64), 0, s, p, p.wt,
+                     p.bias, p.out, p.out_arg);
+}
+
 int lenet32_dw2_grid(int N) { return std::max(1, std::min((N + kD2Imgs - 1) / kD2Imgs, 256 * 2)); }  // 2 per CU (VGPRs)
 int lenet32_dw1_grid(int N) { return std::max(1, std::min((N + kD1Imgs - 1) / kD1Imgs, 256 * 4)); }
 

@@ -833,3 +833,37 @@ def test_fp32_lenet_sparse_dw_matches_dense(cuda, monkeypatch):
         for off, n, what in ((L["w_off"], L["nweights"], "W"), (L["b_off"], L["nbiases"], "b")):
             e, c = _per_channel_err(g_sparse[off : off + n], g_dense[off : off + n], L["C"], floor_frac=1e-3)
             assert e < 1e-5, f"conv C={L['C']} {what}: channel {c} rel err {e:.3e}"
+
+
+@pytest.mark.gpu
+def test_fp32_lenet_mfma_conv2_fwd_matches_direct(cuda, monkeypatch):
+    """The opt-in f32-MFMA LeNet-5 conv2 forward (lenet32_conv2_fwd_kernel,
+    MCC_AB=f32_mfma_fwd2) vs the default packed-FMA direct kernel: logits and
+    every weight gradient (a different summation order: fp32 rounding; a
+    flipped near-tie argmax would show as an O(1) channel error)."""
+    spec = mcc.make_model("lenet5")
+    B = 3001
+    imgs, labels = mcc.synth_dataset(B, 1, 28, 28, 10, seed=22)
+    params = mcc.init_params(spec, seed=5, mode="fast").astype(np.float32)
+    d_img = torch.from_numpy(imgs).to(cuda)
+    d_lab = torch.from_numpy(labels).to(cuda)
+
+    def run(ab):
+        monkeypatch.setenv("MCC_AB", ab)
+        net = mcc.GpuNet(spec, "fp32", B)
+        net.set_params(params)
+        s = torch.cuda.current_stream().cuda_stream
+        net.forward(d_img.data_ptr(), 0, B, s)
+        net.loss(d_lab.data_ptr(), 0, 1.0 / B, True, s)
+        net.backward_all(s)
+        torch.cuda.synchronize()
+        return net.get_logits(B), net.get_grads()
+
+    (l_mfma, g_mfma), (l_dir, g_dir) = run("f32_mfma_fwd2"), run("")
+    assert _relerr(l_mfma, l_dir) < 1e-5
+    for L in spec.layers():
+        if L["nweights"] == 0:
+            continue
+        for off, n, what in ((L["w_off"], L["nweights"], "W"), (L["b_off"], L["nbiases"], "b")):
+            e, c = _per_channel_err(g_mfma[off : off + n], g_dir[off : off + n], L["C"], floor_frac=1e-3)
+            assert e < 1e-4, f"{L['kind']} C={L['C']} {what}: channel {c} rel err {e:.3e}"
