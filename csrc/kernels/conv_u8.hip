@@ -71,39 +71,50 @@ __global__ void __launch_bounds__(kU8T) u8conv_fwd_kernel(U8ConvParams p) {
   const int srow = dy + (g < 3 ? g : 2);  // staged row (0 = input row y0 - 1)
   const int ntiles = PW / 4;
 
-  const int64_t nunits = (int64_t)p.N * PH;
-  const int64_t wave_id = (int64_t)blockIdx.x * (kU8T / 64) + wave, nwaves = (int64_t)gridDim.x * (kU8T / 64);
+  // units (image b, pooled row wy) advance by nwaves: (b, wy) carried, no
+  // per-unit division (round 5: the 64-bit u / PH and the per-dword i / RDW
+  // divisions were ~40 % of this kernel's VALU on CIFAR-3conv)
+  const int nunits = p.N * PH;  // host: < 2^31
+  const int wave_id = blockIdx.x * (kU8T / 64) + wave, nwaves = gridDim.x * (kU8T / 64);
+  const int adv_b = nwaves / PH, adv_y = nwaves - adv_b * PH;
 
-  // register prefetch of a unit's 4 rows: dword i of the 4 rows = lane + 64 * q
+  // register prefetch of a unit's 4 rows: dword i of the 4 rows = lane + 64 * q;
+  // per q: source offset within the first row's image position, LDS offset | staged row (2 bits)
+  int qsrc[RD], qlds[RD];
+#pragma unroll
+  for (int q = 0; q < RD; ++q) {
+    const int i = lane + 64 * q;
+    const int rr = i / RDW, dw = i - rr * RDW;
+    qsrc[q] = rr * p.W * 3 + 4 * dw;
+    qlds[q] = i < 4 * RDW ? ((rr * RP + 4 + 4 * dw) | rr) : -1;
+  }
   uint32_t pre[RD];
-  auto fetch = [&](int64_t u) {
-    const int b = (int)(u / PH), wy = (int)(u - (int64_t)b * PH);
+  auto fetch = [&](int b, int wy) {
     const int img = p.idx ? p.idx[b] : b;
-    const uint8_t* src = p.x + (size_t)img * p.H * p.W * 3;
+    const uint8_t* src = p.x + (size_t)img * p.H * p.W * 3 + (ptrdiff_t)(2 * wy - 1) * p.W * 3;
 #pragma unroll
     for (int q = 0; q < RD; ++q) {
-      const int i = lane + 64 * q;
-      const int rr = i / RDW, dw = i - rr * RDW;
-      const int y = 2 * wy - 1 + rr;
-      const bool ok = i < 4 * RDW && (unsigned)y < (unsigned)p.H;
-      pre[q] = ok ? *reinterpret_cast<const uint32_t*>(src + (size_t)y * p.W * 3 + 4 * dw) : 0u;
+      const int y = 2 * wy - 1 + (qlds[q] & 3);
+      const bool ok = qlds[q] >= 0 && (unsigned)y < (unsigned)p.H;
+      pre[q] = ok ? *reinterpret_cast<const uint32_t*>(src + qsrc[q]) : 0u;
     }
   };
   auto stash = [&]() {
 #pragma unroll
-    for (int q = 0; q < RD; ++q) {
-      const int i = lane + 64 * q;
-      const int rr = i / RDW, dw = i - rr * RDW;
-      if (i < 4 * RDW) *reinterpret_cast<uint32_t*>(rows + rr * RP + 4 + 4 * dw) = pre[q];
-    }
+    for (int q = 0; q < RD; ++q)
+      if (qlds[q] >= 0) *reinterpret_cast<uint32_t*>(rows + (qlds[q] & ~3)) = pre[q];
   };
 
-  int64_t u = wave_id;
-  if (u < nunits) fetch(u);
+  int u = wave_id;
+  int b = u / PH, wy = u - (u / PH) * PH;
+  if (u < nunits) fetch(b, wy);
   for (; u < nunits; u += nwaves) {
     stash();  // (wave-private region: the wave's own earlier reads are ordered before these writes)
-    const int b = (int)(u / PH), wy = (int)(u - (int64_t)b * PH);
-    if (u + nwaves < nunits) fetch(u + nwaves);
+    const int bc = b, wyc = wy;
+    wy += adv_y;
+    b += adv_b;
+    if (wy >= PH) { wy -= PH; ++b; }
+    if (u + nwaves < nunits) fetch(b, wy);
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the LDS writes landed (single wave: no barrier)
     __builtin_amdgcn_wave_barrier();
     for (int t = 0; t < ntiles; ++t) {
@@ -114,18 +125,19 @@ __global__ void __launch_bounds__(kU8T) u8conv_fwd_kernel(U8ConvParams p) {
       const uint32_t lo = __builtin_amdgcn_alignbyte(d.y, d.x, off & 3);
       const uint32_t hi = __builtin_amdgcn_alignbyte(d.z, d.y, off & 3);
       const uint32_t b8 = (uint32_t)(((uint64_t)d.z << 32 | d.y) >> (sh + 32)) & 0xffu;  // byte 8
-      bf16x8 a0, a1;
-      a0[0] = (bf16)(float)(lo & 0xffu);
-      a0[1] = (bf16)(float)((lo >> 8) & 0xffu);
-      a0[2] = (bf16)(float)((lo >> 16) & 0xffu);
-      a0[3] = (bf16)(float)(lo >> 24);
-      a0[4] = (bf16)(float)(hi & 0xffu);
-      a0[5] = (bf16)(float)((hi >> 8) & 0xffu);
-      a0[6] = (bf16)(float)((hi >> 16) & 0xffu);
-      a0[7] = (bf16)(float)(hi >> 24);
-      a1 = bf16x8{(bf16)(float)b8, (bf16)0.f, (bf16)0.f, (bf16)0.f, (bf16)0.f, (bf16)0.f, (bf16)0.f, (bf16)0.f};
+      // bytes -> bf16: an integer < 256 is exact in fp32 with a zero low half,
+      // so its bf16 is the float's high half (v_cvt_f32_ubyteN + one v_perm per pair)
+      auto ip2 = [](uint32_t w, int k) {  // bytes k, k+1 of w
+        const uint32_t f0 = __builtin_bit_cast(uint32_t, (float)((w >> (8 * k)) & 0xffu));
+        const uint32_t f1 = __builtin_bit_cast(uint32_t, (float)((w >> (8 * k + 8)) & 0xffu));
+        return __builtin_amdgcn_perm(f1, f0, 0x07060302u);
+      };
+      typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
+      const bf16x8 a0 = __builtin_bit_cast(bf16x8, (u32x4v{ip2(lo, 0), ip2(lo, 2), ip2(hi, 0), ip2(hi, 2)}));
+      const uint32_t f8 = __builtin_bit_cast(uint32_t, (float)b8) >> 16;
+      const bf16x8 a1 = __builtin_bit_cast(bf16x8, (u32x4v{f8, 0u, 0u, 0u}));
       const int wx = 4 * t + g;  // the window this lane's accumulators hold
-      const size_t o = (((size_t)b * PH + wy) * PW + wx) * p.Cout + r;
+      const size_t o = (((size_t)bc * PH + wyc) * PW + wx) * p.Cout + r;
 #pragma unroll
       for (int j = 0; j < NT; ++j) {
         f32x4 acc = {0.f, 0.f, 0.f, 0.f};
@@ -136,7 +148,8 @@ __global__ void __launch_bounds__(kU8T) u8conv_fwd_kernel(U8ConvParams p) {
         if (acc[1] > best) { best = acc[1]; a = 1; }
         if (acc[2] > best) { best = acc[2]; a = 2; }
         if (acc[3] > best) { best = acc[3]; a = 3; }
-        const float y = fmaxf(best * (1.0f / 255.0f) + bias[j], 0.f);
+        // ReLU on the bit pattern (v_max_i32: no NaN canonicalisation)
+        const float y = __builtin_bit_cast(float, max(__builtin_bit_cast(int, fmaf(best, 1.0f / 255.0f, bias[j])), 0));
         reinterpret_cast<bf16*>(p.out)[o + 16 * j] = (bf16)y;
         p.out_arg[o + 16 * j] = (uint8_t)(y > 0.f ? a : 4);
       }
@@ -148,7 +161,8 @@ __global__ void __launch_bounds__(kU8T) u8conv_fwd_kernel(U8ConvParams p) {
 
 bool u8conv_fwd_supported(const U8ConvParams& p) {
   return p.N >= 1 && p.H % 2 == 0 && p.W % 8 == 0 && (p.Cout == 32 || p.Cout == 64) &&
-         (3 * p.W) % 4 == 0 && 4 * u8_row_dwords(p.W) <= 64 * 12 && (int64_t)p.N * p.H * p.W * 3 < (1ll << 40);
+         (3 * p.W) % 4 == 0 && 4 * u8_row_dwords(p.W) <= 64 * 12 && (int64_t)p.N * p.H * p.W * 3 < (1ll << 40) &&
+         (int64_t)p.N * (p.H / 2) < (1ll << 31);
 }
 
 void u8conv_forward(const U8ConvParams& p, hipStream_t s) {
