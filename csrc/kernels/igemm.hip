@@ -85,16 +85,6 @@ __device__ __forceinline__ int swz128(int row) { return 2 * (row & 3) + 8 * ((ro
 // ---------------------------------------------------------------------------
 // forward / data gradient
 // ---------------------------------------------------------------------------
-// DPP quad permutations (lanes 4q..4q+3): xor 1, xor 2
-__device__ __forceinline__ float qswap1(float v) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0xB1, 0xf, 0xf, false));
-}
-__device__ __forceinline__ float qswap2(float v) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x4E, 0xf, 0xf, false));
-}
-__device__ __forceinline__ int qswap1i(int v) { return __builtin_amdgcn_mov_dpp(v, 0xB1, 0xf, 0xf, false); }
-__device__ __forceinline__ int qswap2i(int v) { return __builtin_amdgcn_mov_dpp(v, 0x4E, 0xf, 0xf, false); }
-
 // POOL epilogue (round 5): the pooling kernels run the MFMA in the C
 // orientation (A = pixels, B = weights), so lane (r16, g) of a fragment holds
 // rows 4g..4g+3 -- the four positions of ONE pooling window -- of channel
@@ -103,31 +93,29 @@ __device__ __forceinline__ int qswap2i(int v) { return __builtin_amdgcn_mov_dpp(
 // and index per channel, ~15 VALU per pooled value, which cost VGG-11's
 // forward 1.2 ms of 12.3, tools/probes/lenet_phase_probe.py MCC_IG_ABL=1.)
 // One bf16 + one argmax byte per lane; 16 lanes = 16 consecutive channels.
-__device__ __forceinline__ void pool_window_store(const IgemmParams& p, const f32x4& acc, int mwin, int ch, float bias,
-                                                  bool bias_act) {
+template <int A>  // activation kind (with_act); 0 also when there is no bias / activation
+__device__ __forceinline__ void pool_window_store(bf16* out, int ldo, uint8_t* out_arg, int N, const f32x4& acc, int mwin,
+                                                  int ch, float bias) {
   float mx = acc[0];
   uint32_t a = 0;
   if (acc[1] > mx) { mx = acc[1]; a = 1; }
   if (acc[2] > mx) { mx = acc[2]; a = 2; }
   if (acc[3] > mx) { mx = acc[3]; a = 3; }
-  float v = mx + bias;
-  if (bias_act) v = act_apply(p.act, v);
-  const bf16 o = (bf16)v;
-  if (bias_act && p.act == ACT_RELU && !((float)o > 0.f)) a = 4;  // ReLU-inactive window: argmax byte 4
-  static_cast<bf16*>(p.out)[(size_t)mwin * p.ldo + ch] = o;
-  p.out_arg[(size_t)mwin * p.N + ch] = (uint8_t)a;
+  const bf16 o = (bf16)act_c<A>(mx + bias);
+  if (A == ACT_RELU && !((float)o > 0.f)) a = 4;  // ReLU-inactive window: argmax byte 4
+  out[(size_t)mwin * ldo + ch] = o;
+  out_arg[(size_t)mwin * N + ch] = (uint8_t)a;
 }
 
 // POOL: fused 2x2/2 max-pool epilogue.  The GEMM rows enumerate (b, py, px,
-// pos) so each pooling window is four consecutive rows = four lanes of one
-// DPP quad (the C^T fragment holds pixel r16 in lane r16); the max and its
-// first-max-wins argmax (PyTorch order) come out of two quad exchanges, and
+// pos) so each pooling window is four consecutive rows (pool_window_store);
 // the pre-pool conv output is never written.
 // U8: the input is the u8 image set (optional sample-index gather, /255 as
 // cnn.c:457) with few channels (the first layer): the pixel tile is gathered
 // through registers (bytes -> bf16) into the same swizzled LDS image.
-// epilogue ablations (timing studies only; tools/build_variant.sh): 1 = no
-// pool exchange, 2 = no bias / activation / argmax codes
+// Epilogues branch once on the activation kind (with_act, mfma.h).
+// epilogue ablation (timing studies only; tools/build_variant.sh): 2 = no
+// bias / activation
 #ifndef MCC_IG_ABL
 #define MCC_IG_ABL 0
 #endif
@@ -411,75 +399,58 @@ __global__ void __launch_bounds__(kIgT, 2) igemm_conv_kernel(IgemmParams p) {
   }
 
   if constexpr (POOL) {  // lane: channel r16, window rows 4g..4g+3 (see pool_window_store)
+    bf16* const out = static_cast<bf16*>(p.out);
+    uint8_t* const oarg = p.out_arg;
+    const int ldo = p.ldo, Mx = p.M, Nx = p.N;
+    auto epi = [&](auto ak) {
 #pragma unroll
-    for (int i = 0; i < FN; ++i) {
-      const int ch = n0 + wn * (BN / 2) + i * 16 + r16;
-      if (ch >= p.N) continue;
-      const float bv = BIAS_ACT && p.bias ? p.bias[ch] : 0.f;
+      for (int i = 0; i < FN; ++i) {
+        const int ch = n0 + wn * (BN / 2) + i * 16 + r16;
+        if (ch >= p.N) continue;
+        const float bv = BIAS_ACT && p.bias ? p.bias[ch] : 0.f;
 #pragma unroll
-      for (int j = 0; j < FM; ++j) {
-        const int m = m0 + wm * 64 + j * 16 + 4 * g;
-        if (m < p.M) pool_window_store(p, acc[i][j], m >> 2, ch, bv, BIAS_ACT);
+        for (int j = 0; j < FM; ++j) {
+          const int m = m0 + wm * 64 + j * 16 + 4 * g;
+          if (m < Mx) pool_window_store<decltype(ak)::v>(out, ldo, oarg, Nx, acc[i][j], m >> 2, ch, bv);
+        }
       }
-    }
+    };
+    if (BIAS_ACT) with_act(p.act, epi); else epi(ActK<0>{});
     return;
   }
   // ---- epilogue: lane holds channels 4g..4g+3 of pixel r16 per fragment ----
   bf16* out = static_cast<bf16*>(p.out);
+  const int ldo = p.ldo, Mx = p.M, Nx = p.N;  // registers: the stores below would re-read the kernarg copy
+  const bf16* rmask = static_cast<const bf16*>(p.relu_mask);
+  auto epi = [&](auto ak) {
+    constexpr int A = decltype(ak)::v;
 #pragma unroll
-  for (int i = 0; i < FN; ++i) {
-    const int ch = n0 + wn * (BN / 2) + i * 16 + 4 * g;
-    const bool chok = ch < p.N;
-    float bv[4] = {0.f, 0.f, 0.f, 0.f};
-    if (BIAS_ACT && p.bias && chok) {
+    for (int i = 0; i < FN; ++i) {
+      const int ch = n0 + wn * (BN / 2) + i * 16 + 4 * g;
+      const bool chok = ch < Nx;
+      float bv[4] = {0.f, 0.f, 0.f, 0.f};
+      if (BIAS_ACT && p.bias && chok) {
 #pragma unroll
-      for (int e = 0; e < 4; ++e) bv[e] = p.bias[ch + e];
-    }
+        for (int e = 0; e < 4; ++e) bv[e] = p.bias[ch + e];
+      }
 #pragma unroll
-    for (int j = 0; j < FM; ++j) {
-      const int m = m0 + wm * 64 + j * 16 + r16;
-      float v[4];
+      for (int j = 0; j < FM; ++j) {
+        const int m = m0 + wm * 64 + j * 16 + r16;
+        if (!chok || m >= Mx) continue;
+        float v[4];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] = acc[i][j][e];
-      uint32_t arg = 0;
-      if constexpr (POOL && !(MCC_IG_ABL & 1)) {  // every lane of the quad takes part in the exchange
-        const int pos = r16 & 3;
+        for (int e = 0; e < 4; ++e) v[e] = (MCC_IG_ABL & 2) ? acc[i][j][e] : act_c<A>(acc[i][j][e] + bv[e]);
+        if (!BIAS_ACT && rmask) {  // data gradient straight to dZ of a ReLU layer: dX * (y > 0)
+          const bf16x4 y = *reinterpret_cast<const bf16x4*>(rmask + (size_t)m * ldo + ch);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          int a = pos;
-          float o = qswap1(v[e]);
-          int oa = qswap1i(a);
-          if (o > v[e] || (o == v[e] && oa < a)) { v[e] = o; a = oa; }
-          o = qswap2(v[e]);
-          oa = qswap2i(a);
-          if (o > v[e] || (o == v[e] && oa < a)) { v[e] = o; a = oa; }
-          arg |= (uint32_t)a << (8 * e);
+          for (int e = 0; e < 4; ++e) v[e] = (float)y[e] > 0.f ? v[e] : 0.f;
         }
+        *reinterpret_cast<bf16x4*>(out + (size_t)m * ldo + ch) = cvt4(v[0], v[1], v[2], v[3]);
       }
-      if (!chok || m >= p.M) continue;
-      if (POOL && (r16 & 3) != 0) continue;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        if (MCC_IG_ABL & 2) break;
-        v[e] += bv[e];
-        if (BIAS_ACT) v[e] = act_apply(p.act, v[e]);
-      }
-      if (!BIAS_ACT && p.relu_mask) {  // data gradient straight to dZ of a ReLU layer: dX * (y > 0)
-        const bf16x4 y = *reinterpret_cast<const bf16x4*>(static_cast<const bf16*>(p.relu_mask) + (size_t)m * p.ldo + ch);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = (float)y[e] > 0.f ? v[e] : 0.f;
-      }
-      const bf16x4 o = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
-      const int orow = POOL ? (m >> 2) : m;
-      if (POOL && BIAS_ACT && !(MCC_IG_ABL & 2) && p.act == ACT_RELU) {  // ReLU-inactive window: argmax byte 4
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-          if (!((float)o[e] > 0.f)) arg = (arg & ~(0xffu << (8 * e))) | (4u << (8 * e));
-      }
-      *reinterpret_cast<bf16x4*>(out + (size_t)orow * p.ldo + ch) = o;
-      if (POOL) *reinterpret_cast<uint32_t*>(p.out_arg + (size_t)orow * p.N + ch) = arg;
     }
-  }
+  };
+  if constexpr (BIAS_ACT) with_act(p.act, epi);
+  else epi(ActK<0>{});
 }
 
 // ---------------------------------------------------------------------------
@@ -526,8 +497,17 @@ constexpr int kBigBP = 256;
 // ping-pong variant, wave group 1 one barrier behind with s_setprio around the
 // MFMA clusters, measured slower on VGG-11: 18.41 vs 17.66 ms/step, and was
 // removed in round 3.)
+#ifndef MCC_IG_PIPE
+#define MCC_IG_PIPE 2  // 1: s_setprio around the MFMA clusters (measured slower); 2: stage after them
+#endif
 template <int GA, int GB, class RD, class ST, class MM>
 __device__ __forceinline__ void pipe_loop(int nk, RD&& rd, ST&& st, MM&& mm) {
+  constexpr bool kLate = MCC_IG_PIPE & 2;  // stage after the MFMA cluster
+  auto mmp = [&](int q) {
+    if (MCC_IG_PIPE & 1) __builtin_amdgcn_s_setprio(1);
+    mm(q);
+    if (MCC_IG_PIPE & 1) __builtin_amdgcn_s_setprio(0);
+  };
   st(0, 0); st(0, 1); st(0, 2); st(0, 3);
   {
     for (int kt = 0; kt < nk; ++kt) {
@@ -535,20 +515,23 @@ __device__ __forceinline__ void pipe_loop(int nk, RD&& rd, ST&& st, MM&& mm) {
       vm_wait<GA + GB>();  // A0, B0 landed (B1, A1 in flight)
       raw_barrier();
       rd(kt, 0);
-      if (nx) st(kt + 1, 0);
-      mm(0);
+      if (!kLate && nx) st(kt + 1, 0);
+      mmp(0);
+      if (kLate && nx) st(kt + 1, 0);
       if (nx) vm_wait<2 * GA>(); else vm_wait<GA>();  // B1 (A1, A0' in flight)
       raw_barrier();
       rd(kt, 1);
-      if (nx) st(kt + 1, 1);
-      mm(1);
+      if (!kLate && nx) st(kt + 1, 1);
+      mmp(1);
+      if (kLate && nx) st(kt + 1, 1);
       if (nx) vm_wait<GA + GB>(); else vm_wait<0>();  // A1 (A0', B0' in flight)
       raw_barrier();
       rd(kt, 2);
-      if (nx) st(kt + 1, 2);
-      mm(2);
+      if (!kLate && nx) st(kt + 1, 2);
+      mmp(2);
+      if (kLate && nx) st(kt + 1, 2);  // issue order B1', A1' kept (the counted waits)
       if (nx) st(kt + 1, 3);
-      mm(3);
+      mmp(3);
     }
   }
 }
@@ -703,83 +686,67 @@ __global__ void __launch_bounds__(kBigT, 1) igemm_big_kernel(IgemmParams p) {
       });
 
   if constexpr (POOL) {  // lane: channel r16, window rows 4g..4g+3 (see pool_window_store)
+    bf16* const out = static_cast<bf16*>(p.out);
+    uint8_t* const oarg = p.out_arg;
+    const int ldo = p.ldo, Mx = p.M, Nx = p.N;
+    auto epi = [&](auto ak) {
 #pragma unroll
-    for (int ha = 0; ha < 2; ++ha)
+      for (int ha = 0; ha < 2; ++ha)
 #pragma unroll
-      for (int f = 0; f < FA; ++f) {
-        const int ch = n0 + ha * HA + wr * (HA / 2) + f * 16 + r16;
-        if (ch >= p.N) continue;
-        const float bv = BIAS_ACT && p.bias ? p.bias[ch] : 0.f;
+        for (int f = 0; f < FA; ++f) {
+          const int ch = n0 + ha * HA + wr * (HA / 2) + f * 16 + r16;
+          if (ch >= p.N) continue;
+          const float bv = BIAS_ACT && p.bias ? p.bias[ch] : 0.f;
 #pragma unroll
-        for (int hb = 0; hb < 2; ++hb)
+          for (int hb = 0; hb < 2; ++hb)
 #pragma unroll
-          for (int e2 = 0; e2 < 2; ++e2) {
-            const int m = m0 + hb * HB + wc * 32 + e2 * 16 + 4 * g;
-            if (m < p.M) pool_window_store(p, acc[ha][f][hb][e2], m >> 2, ch, bv, BIAS_ACT);
-          }
-      }
+            for (int e2 = 0; e2 < 2; ++e2) {
+              const int m = m0 + hb * HB + wc * 32 + e2 * 16 + 4 * g;
+              if (m < Mx) pool_window_store<decltype(ak)::v>(out, ldo, oarg, Nx, acc[ha][f][hb][e2], m >> 2, ch, bv);
+            }
+        }
+    };
+    if (BIAS_ACT) with_act(p.act, epi); else epi(ActK<0>{});
     return;
   }
   // ---- epilogue: lane holds channels 4g..4g+3 of pixel r16 per fragment ----
   bf16* out = static_cast<bf16*>(p.out);
+  const int ldo = p.ldo, Mx = p.M, Nx = p.N;  // registers: the stores below would re-read the kernarg copy
+  const bf16* rmask = static_cast<const bf16*>(p.relu_mask);
+  auto epi = [&](auto ak) {
+    constexpr int A = decltype(ak)::v;
 #pragma unroll
-  for (int ha = 0; ha < 2; ++ha)
+    for (int ha = 0; ha < 2; ++ha)
 #pragma unroll
-    for (int f = 0; f < FA; ++f) {
-      const int ch = n0 + ha * HA + wr * (HA / 2) + f * 16 + 4 * g;
-      const bool chok = ch < p.N;
-      float bv[4] = {0.f, 0.f, 0.f, 0.f};
-      if (BIAS_ACT && p.bias && chok) {
+      for (int f = 0; f < FA; ++f) {
+        const int ch = n0 + ha * HA + wr * (HA / 2) + f * 16 + 4 * g;
+        const bool chok = ch < Nx;
+        float bv[4] = {0.f, 0.f, 0.f, 0.f};
+        if (BIAS_ACT && p.bias && chok) {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) bv[e] = p.bias[ch + e];
-      }
+          for (int e = 0; e < 4; ++e) bv[e] = p.bias[ch + e];
+        }
 #pragma unroll
-      for (int hb = 0; hb < 2; ++hb)
+        for (int hb = 0; hb < 2; ++hb)
 #pragma unroll
-        for (int e2 = 0; e2 < 2; ++e2) {
-          const int m = m0 + hb * HB + wc * 32 + e2 * 16 + r16;
-          float v[4];
-#pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = acc[ha][f][hb][e2][e];
-          uint32_t arg = 0;
-          if constexpr (POOL && !(MCC_IG_ABL & 1)) {  // every lane of the quad takes part in the exchange
-            const int pos = r16 & 3;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              int a = pos;
-              float o = qswap1(v[e]);
-              int oa = qswap1i(a);
-              if (o > v[e] || (o == v[e] && oa < a)) { v[e] = o; a = oa; }
-              o = qswap2(v[e]);
-              oa = qswap2i(a);
-              if (o > v[e] || (o == v[e] && oa < a)) { v[e] = o; a = oa; }
-              arg |= (uint32_t)a << (8 * e);
-            }
-          }
-          if (!chok || m >= p.M) continue;
-          if (POOL && (r16 & 3) != 0) continue;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            if (MCC_IG_ABL & 2) break;
-            v[e] += bv[e];
-            if (BIAS_ACT) v[e] = act_apply(p.act, v[e]);
-          }
-          if (!BIAS_ACT && p.relu_mask) {  // data gradient straight to dZ of a ReLU layer
-            const bf16x4 y = *reinterpret_cast<const bf16x4*>(static_cast<const bf16*>(p.relu_mask) + (size_t)m * p.ldo + ch);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] = (float)y[e] > 0.f ? v[e] : 0.f;
-          }
-          const bf16x4 o = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
-          const int orow = POOL ? (m >> 2) : m;
-          if (POOL && BIAS_ACT && !(MCC_IG_ABL & 2) && p.act == ACT_RELU) {  // ReLU-inactive window: argmax byte 4
+          for (int e2 = 0; e2 < 2; ++e2) {
+            const int m = m0 + hb * HB + wc * 32 + e2 * 16 + r16;
+            if (!chok || m >= Mx) continue;
+            float v[4];
 #pragma unroll
             for (int e = 0; e < 4; ++e)
-              if (!((float)o[e] > 0.f)) arg = (arg & ~(0xffu << (8 * e))) | (4u << (8 * e));
+              v[e] = (MCC_IG_ABL & 2) ? acc[ha][f][hb][e2][e] : act_c<A>(acc[ha][f][hb][e2][e] + bv[e]);
+            if (!BIAS_ACT && rmask) {  // data gradient straight to dZ of a ReLU layer
+              const bf16x4 y = *reinterpret_cast<const bf16x4*>(rmask + (size_t)m * ldo + ch);
+#pragma unroll
+              for (int e = 0; e < 4; ++e) v[e] = (float)y[e] > 0.f ? v[e] : 0.f;
+            }
+            *reinterpret_cast<bf16x4*>(out + (size_t)m * ldo + ch) = cvt4(v[0], v[1], v[2], v[3]);
           }
-          *reinterpret_cast<bf16x4*>(out + (size_t)orow * p.ldo + ch) = o;
-          if (POOL) *reinterpret_cast<uint32_t*>(p.out_arg + (size_t)orow * p.N + ch) = arg;
-        }
-    }
+      }
+  };
+  if constexpr (BIAS_ACT) with_act(p.act, epi);
+  else epi(ActK<0>{});
 }
 
 // ---------------------------------------------------------------------------

@@ -59,6 +59,27 @@ __device__ __forceinline__ float act_apply(int act, float v) {
   if (act == 2) return tanhf(v);
   return v;
 }
+// compile-time activation: with_act(p.act, [&](auto a) { ... act_c<a.v>(x) ... })
+// branches once on the uniform kind instead of once per element (an unrolled
+// 128-value epilogue otherwise carries a tanh path and two scalar branches per
+// value)
+template <int A> struct ActK { static constexpr int v = A; };
+template <int A> __device__ __forceinline__ float act_c(float v) {
+  if constexpr (A == 1) return __builtin_bit_cast(float, max(__builtin_bit_cast(int, v), 0));  // ReLU (-0 -> +0)
+  else if constexpr (A == 2) return tanhf(v);
+  else return v;
+}
+template <class F> __device__ __forceinline__ void with_act(int act, F&& f) {
+  if (act == 1) f(ActK<1>{});
+  else if (act == 2) f(ActK<2>{});
+  else f(ActK<0>{});
+}
+__device__ __forceinline__ bf16x4 cvt4(float a, float b, float c, float d) {
+  using f2 = float __attribute__((ext_vector_type(2)));
+  using h2 = bf16 __attribute__((ext_vector_type(2)));
+  const h2 lo = __builtin_convertvector(f2{a, b}, h2), hi = __builtin_convertvector(f2{c, d}, h2);
+  return bf16x4{lo[0], lo[1], hi[0], hi[1]};
+}
 // derivative expressed in the activation output y
 __device__ __forceinline__ float act_grad_y(int act, float y) {
   if (act == 1) return y > 0.f ? 1.f : 0.f;
