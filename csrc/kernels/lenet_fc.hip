@@ -105,6 +105,37 @@ __device__ __forceinline__ u32x2 pack4(float a, float b, float c, float d) {
   return u32x2{bf16_bits(a) | (bf16_bits(b) << 16), bf16_bits(c) | (bf16_bits(d) << 16)};
 }
 
+// Reductions over the four lanes r, r + 16, r + 32, r + 48 of one image (the
+// MFMA C layout of P3) on v_permlane16/32_swap (VALU) instead of __shfl_xor's
+// ds_bpermute (an LDS round trip per step on the softmax's critical path).
+// With both operands = x, the swap leaves {x of this lane's 16-row pair
+// partner, own x} in the two results (in a lane-dependent order), so a
+// commutative combine gives both lanes the same value, bit for bit what the
+// xor-16 / xor-32 shuffle pair gave.
+__device__ __forceinline__ float ubits(uint32_t u) { return __builtin_bit_cast(float, u); }
+__device__ __forceinline__ uint32_t fbits(float f) { return __builtin_bit_cast(uint32_t, f); }
+__device__ __forceinline__ float sum4lanes(float x) {
+  const auto a = __builtin_amdgcn_permlane16_swap(fbits(x), fbits(x), false, false);
+  x = ubits(a[0]) + ubits(a[1]);
+  const auto b = __builtin_amdgcn_permlane32_swap(fbits(x), fbits(x), false, false);
+  return ubits(b[0]) + ubits(b[1]);
+}
+// first max wins (cnn.c:508-513): the larger value, on ties the lower class
+__device__ __forceinline__ void argmax4lanes(float& mx, int& am) {
+#pragma unroll
+  for (int step = 0; step < 2; ++step) {
+    const auto v = step ? __builtin_amdgcn_permlane32_swap(fbits(mx), fbits(mx), false, false)
+                        : __builtin_amdgcn_permlane16_swap(fbits(mx), fbits(mx), false, false);
+    const auto i = step ? __builtin_amdgcn_permlane32_swap((uint32_t)am, (uint32_t)am, false, false)
+                        : __builtin_amdgcn_permlane16_swap((uint32_t)am, (uint32_t)am, false, false);
+    const float va = ubits(v[0]), vb = ubits(v[1]);
+    const int ia = (int)i[0], ib = (int)i[1];
+    const bool b_wins = vb > va || (vb == va && ib < ia);
+    mx = b_wins ? vb : va;
+    am = b_wins ? ib : ia;
+  }
+}
+
 __global__ void __launch_bounds__(kThreads, 1) lenet_fc_kernel(LenetFcParams P) {
   __shared__ __attribute__((aligned(16))) char smem[kLds];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -308,18 +339,12 @@ __global__ void __launch_bounds__(kThreads, 1) lenet_fc_kernel(LenetFcParams P) 
 #pragma unroll
       for (int i = 1; i < 4; ++i)
         if (v[i] > mx) { mx = v[i]; am = 4 * g + i; }
-#pragma unroll
-      for (int o = 16; o <= 32; o <<= 1) {  // first max wins (cnn.c:508-513)
-        const float m2 = __shfl_xor(mx, o);
-        const int a2 = __shfl_xor(am, o);
-        if (m2 > mx || (m2 == mx && a2 < am)) { mx = m2; am = a2; }
-      }
+      argmax4lanes(mx, am);
       float sum = 0.f;
 #pragma unroll
       for (int i = 0; i < 4; ++i)
         if (4 * g + i < N3) sum += __expf(v[i] - mx);
-      sum += __shfl_xor(sum, 16);
-      sum += __shfl_xor(sum, 32);
+      sum = sum4lanes(sum);
       const float inv = 1.f / sum;
       float e[4], mse = 0.f, vl = 0.f;
 #pragma unroll
@@ -333,10 +358,8 @@ __global__ void __launch_bounds__(kThreads, 1) lenet_fc_kernel(LenetFcParams P) 
           if (j == label) vl = v[i];
         }
       }
-      mse += __shfl_xor(mse, 16);
-      mse += __shfl_xor(mse, 32);
-      vl += __shfl_xor(vl, 16);
-      vl += __shfl_xor(vl, 32);
+      mse = sum4lanes(mse);
+      vl = sum4lanes(vl);
       *reinterpret_cast<u32x2*>(smem + OE + (w ? rm1 : rm0) * SE + 8 * g) = pack4(e[0], e[1], e[2], e[3]);
       if (valid) {
         const int row = row0 + m;
