@@ -465,32 +465,54 @@ __global__ void __launch_bounds__(kThreads, 1) lenet_fc_kernel(LenetFcParams P) 
         wrow[2 * c + 1] = OW1 + pw1(32 * c + 8 * g + 4 + q) * SW1;
       }
       char* dyb = static_cast<char*>(P.dy);
+      const bool st0 = r < nvalid, st1 = 16 + r < nvalid;
+      char* drow0 = dyb + (size_t)(row0 + (st0 ? r : 0)) * P.ldd * 2 + 8 * g;
+      char* drow1 = dyb + (size_t)(row0 + (st1 ? 16 + r : 0)) * P.ldd * 2 + 8 * g;
+      const char* hrow0 = smem + OH1 + rm0 * SH1 + 16 * g;
+      const char* hrow1 = smem + OH1 + rm1 * SH1 + 16 * g;
+      // k-tiles b = w, w + 8, w + 16 for BOTH image tiles: one W1 fragment
+      // read feeds two independent MFMA chains
 #pragma unroll
-      for (int mt = 0; mt < 2; ++mt) {
-        const int m = 16 * mt + r;
-        const bool store = m < nvalid;
-        char* drow = dyb + (size_t)(row0 + (store ? m : 0)) * P.ldd * 2 + 8 * g;
+      for (int k = 0; k < 3; ++k) {
+        const int b = w + 8 * k;
+        bf16x8 fw[2], f0[2], f1[2];
+        fw[0] = tr8(smem + wrow[0] + (16 * b + 4 * p) * 2, smem + wrow[1] + (16 * b + 4 * p) * 2);
+        f0[0] = ld128(hrow0);
+        f1[0] = ld128(hrow1);
+        f32x4 acc0 = z4, acc1 = z4;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          if (k == 3 && w != mt) break;
-          const int b = k < 3 ? w + 8 * k : 24;
-          const char* hrow = smem + OH1 + (mt ? rm1 : rm0) * SH1 + 16 * g;
-          bf16x8 fw[2], fh[2];
-          fw[0] = tr8(smem + wrow[0] + (16 * b + 4 * p) * 2, smem + wrow[1] + (16 * b + 4 * p) * 2);
-          fh[0] = ld128(hrow);
-          f32x4 acc = z4;
-#pragma unroll
-          for (int c = 0; c < 4; ++c) {
-            if (c + 1 < 4) {
-              fw[(c + 1) & 1] = tr8(smem + wrow[2 * c + 2] + (16 * b + 4 * p) * 2, smem + wrow[2 * c + 3] + (16 * b + 4 * p) * 2);
-              fh[(c + 1) & 1] = ld128(hrow + 64 * (c + 1));
-            }
-            __builtin_amdgcn_sched_barrier(0);
-            acc = mma(acc, fw[c & 1], fh[c & 1]);
-            __builtin_amdgcn_sched_barrier(0);
+        for (int c = 0; c < 4; ++c) {
+          if (c + 1 < 4) {
+            fw[(c + 1) & 1] = tr8(smem + wrow[2 * c + 2] + (16 * b + 4 * p) * 2, smem + wrow[2 * c + 3] + (16 * b + 4 * p) * 2);
+            f0[(c + 1) & 1] = ld128(hrow0 + 64 * (c + 1));
+            f1[(c + 1) & 1] = ld128(hrow1 + 64 * (c + 1));
           }
-          if (store) *reinterpret_cast<u32x2*>(drow + 32 * b) = pack4(acc[0], acc[1], acc[2], acc[3]);
+          __builtin_amdgcn_sched_barrier(0);
+          acc0 = mma(acc0, fw[c & 1], f0[c & 1]);
+          acc1 = mma(acc1, fw[c & 1], f1[c & 1]);
+          __builtin_amdgcn_sched_barrier(0);
         }
+        if (st0) *reinterpret_cast<u32x2*>(drow0 + 32 * b) = pack4(acc0[0], acc0[1], acc0[2], acc0[3]);
+        if (st1) *reinterpret_cast<u32x2*>(drow1 + 32 * b) = pack4(acc1[0], acc1[1], acc1[2], acc1[3]);
+      }
+      if (w < 2) {  // k-tile 24 of image tile w
+        const int b = 24;
+        const char* hrow = w ? hrow1 : hrow0;
+        bf16x8 fw[2], fh[2];
+        fw[0] = tr8(smem + wrow[0] + (16 * b + 4 * p) * 2, smem + wrow[1] + (16 * b + 4 * p) * 2);
+        fh[0] = ld128(hrow);
+        f32x4 acc = z4;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          if (c + 1 < 4) {
+            fw[(c + 1) & 1] = tr8(smem + wrow[2 * c + 2] + (16 * b + 4 * p) * 2, smem + wrow[2 * c + 3] + (16 * b + 4 * p) * 2);
+            fh[(c + 1) & 1] = ld128(hrow + 64 * (c + 1));
+          }
+          __builtin_amdgcn_sched_barrier(0);
+          acc = mma(acc, fw[c & 1], fh[c & 1]);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        if (w ? st1 : st0) *reinterpret_cast<u32x2*>((w ? drow1 : drow0) + 32 * b) = pack4(acc[0], acc[1], acc[2], acc[3]);
       }
     }
   }
