@@ -60,8 +60,17 @@ constexpr int kXPitch = 64;
 constexpr int kXCopy = 30 * kXPitch;  // 1920
 // forward
 constexpr int kFX0 = 0, kFX2 = kXCopy;
-constexpr int kFY1 = 2 * kXCopy;       // 3840: Y1 HWC, 15 x 15 pixels (pad row / column 0) x 32 B
-constexpr int kFLds = kFY1 + 225 * 32;  // 11040
+// Y1 of the padded 15 x 15 grid (pad row / column 0) as 4 parity planes
+// (yy & 1, xx & 1) x 2 channel halves x 8 x 8 pixels x 16 B: conv2 (stride 2)
+// reads one plane per tap, so the 16 lanes of a b128 read take consecutive
+// 16-byte slots (2-way only where a 7-pixel output row wraps) instead of 4
+// slots of a 32-byte-pitch HWC image (4-way: 57 % of the kernel's LDS cycles
+// were bank conflicts, profiles/lenet5_ref_pmc_r5.txt)
+constexpr int kFY1 = 2 * kXCopy;        // 3840
+constexpr int kFLds = kFY1 + 8 * 1024;  // 12032
+__host__ __device__ constexpr int y1p_off(int yy, int xx, int half) {
+  return (((((yy & 1) * 2 + (xx & 1)) * 2 + half) * 64 + (yy >> 1) * 8 + (xx >> 1)) * 16);
+}
 // backward
 constexpr int kBX0 = 0, kBX2 = kXCopy;
 constexpr int kBXc = 2 * kXCopy;          // 3840: X column-parity planes E / O / Os, 30 rows x 32 B
@@ -213,7 +222,11 @@ __host__ __device__ constexpr int y1tap(int t) { return ((t / 3) * 15 + t % 3) *
 // ============================================================================
 // Forward
 // ============================================================================
-__global__ void __launch_bounds__(64) ref_fwd_kernel(RefFwdParams p) {
+#ifndef MCC_REF_FWD_W4
+#define MCC_REF_FWD_W4 0  // 1: cap at 128 VGPRs (4 waves per SIMD; spills 3 registers)
+#endif
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MCC_REF_FWD_W4 ? 4 : 1, MCC_REF_FWD_W4 ? 4 : 8)))
+ref_fwd_kernel(RefFwdParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x;
   const int n16 = lane & 15, g = lane >> 4;
@@ -235,8 +248,8 @@ __global__ void __launch_bounds__(64) ref_fwd_kernel(RefFwdParams p) {
   int koff[5];
 #pragma unroll
   for (int c = 0; c < 5; ++c) {
-    const int t = 2 * c + (g >> 1);
-    koff[c] = (t < 9 ? y1tap(t) : 0) + 16 * (g & 1);
+    const int t = 2 * c + (g >> 1);  // taps >= 9: tap 0 (zero weights)
+    koff[c] = t < 9 ? y1p_off(t / 3, t % 3, g & 1) : y1p_off(0, 0, g & 1);
   }
 
   zero_lds(smem, kFLds, lane);
@@ -268,7 +281,7 @@ __global__ void __launch_bounds__(64) ref_fwd_kernel(RefFwdParams p) {
       // lane (pixel, g): channels 4g .. 4g+3
       const u32x2 v = pack4(relu(acc[0]) * (1.f / 255.f), relu(acc[1]) * (1.f / 255.f),
                             relu(acc[2]) * (1.f / 255.f), relu(acc[3]) * (1.f / 255.f));
-      if (16 * T + n16 < 196) *reinterpret_cast<u32x2*>(smem + kFY1 + ((y + 1) * 15 + x + 1) * 32 + 8 * g) = v;
+      if (16 * T + n16 < 196) *reinterpret_cast<u32x2*>(smem + kFY1 + y1p_off(y + 1, x + 1, g >> 1) + 8 * (g & 1)) = v;
     }
     wave_lds_sync();
 
@@ -278,7 +291,7 @@ __global__ void __launch_bounds__(64) ref_fwd_kernel(RefFwdParams p) {
     for (int T = 0; T < 4; ++T) {
       const int q = min(16 * T + n16, 48);
       const int oy = (q * 37) >> 8, ox = q - 7 * oy;  // q / 7 for q < 49
-      const char* pb = smem + kFY1 + (2 * oy * 15 + 2 * ox) * 32;
+      const char* pb = smem + kFY1 + (oy * 8 + ox) * 16;  // + the tap's plane / offset (koff)
       bf16x8 bf[5];
 #pragma unroll
       for (int c = 0; c < 5; ++c) bf[c] = *reinterpret_cast<const bf16x8*>(pb + koff[c]);
@@ -807,7 +820,19 @@ size_t ref_slab_bytes(bool f32) { return f32 ? ref32_slab_bytes() : (size_t)kBwd
 void ref_forward(const RefFwdParams& p, hipStream_t s) {
   if (p.f32) return ref32_forward(p, s);
   if (p.B <= 0) return;
-  const int grid = std::min(p.B, 256 * 14);
+  // persistent grid = what the device holds at once (132 VGPRs: 3 waves per
+  // SIMD, 12 per CU): a grid past residency (it was 14 per CU) runs its
+  // last workgroups as a second, mostly idle round
+  static int resident = 0;
+  if (resident == 0) {
+    int per_cu = 0, dev = 0, cus = 0;
+    MCC_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, ref_fwd_kernel, 64, kFLds) == hipSuccess &&
+                  hipGetDevice(&dev) == hipSuccess &&
+                  hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess,
+              "ref_forward: occupancy query failed");
+    resident = std::max(1, per_cu) * std::max(1, cus);
+  }
+  const int grid = std::min(p.B, resident);
   hipLaunchKernelGGL(ref_fwd_kernel, dim3(grid), dim3(64), kFLds, s, p);
 }
 
