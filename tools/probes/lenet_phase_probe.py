@@ -2,7 +2,8 @@
 """Time the LeNet-5 step's three parts (forward() = lenet_fwd, loss() = the
 fused FC chain, backward_all() = lenet_bwd) with HIP events, for the
 in-tree module or ablation builds (tools/build_variant.sh); PROBE_MODEL picks
-another model (e.g. ref: fwd = ref_fwd, bwd = FC backward + ref_bwd):
+another model (e.g. ref: fwd = ref_fwd, bwd = FC backward + ref_bwd), PROBE_DTYPE
+the compute dtype (bf16 default, fp32):
 
     python tools/probes/lenet_phase_probe.py [variant_dir ...]
 
@@ -30,7 +31,7 @@ def run_one(path):
     dev = torch.device("cuda", 0)
     d_img, d_lab = torch.from_numpy(imgs).to(dev), torch.from_numpy(labels).to(dev)
     idx = torch.randint(0, ndata, (B,), dtype=torch.int32, device=dev)
-    net = mcc.GpuNet(spec, "bf16", B)
+    net = mcc.GpuNet(spec, os.environ.get("PROBE_DTYPE", "bf16"), B)
     net.set_params(mcc.init_params(spec, seed=0, mode="fast").astype(np.float32))
     s = torch.cuda.current_stream().cuda_stream
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
