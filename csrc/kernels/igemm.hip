@@ -491,8 +491,10 @@ constexpr int kBigBP = 256;
 
 // K loop of the 256-tile kernels.  Quadrant order (A0,B0) (A0,B1) (A1,B1)
 // (A1,B0); phase q reads its new register subtile (rd q: 0 = A0+B0, 1 = B1,
-// 2 = A1), stages quarter q of the next K-tile (st q: A0', B0', B1', A1') and
-// runs its MFMAs (mm q).  GA / GB = glds per thread per A / B quarter.
+// 2 = A1), runs its MFMAs (mm q) and then stages quarter q of the next K-tile
+// (st q: A0', B0', B1', A1'; issued after the MFMA cluster so the staging
+// address VALU overlaps the MFMAs in flight -- same issue order, same counted
+// waits; round 5: +2-5 %).  GA / GB = glds per thread per A / B quarter.
 // One barrier per phase, all waves in step (reads, then MFMAs).  (A staggered
 // ping-pong variant, wave group 1 one barrier behind with s_setprio around the
 // MFMA clusters, measured slower on VGG-11: 18.41 vs 17.66 ms/step, and was
