@@ -1206,23 +1206,27 @@ __global__ void __launch_bounds__(kBigT, 1) igemm_dwbig_kernel(IgemmDwParams p) 
   // put an s_waitcnt vmcnt(0) in front of every quarter's reads, draining the
   // quarter pipeline's DMA lookahead (measured: the ISA showed vmcnt(4),
   // s_barrier, vmcnt(0) per quarter)
-  auto tr = [&](const bf16* img, int ncols, int kr, int col0) {
-    const int row = kr + q;
+  // Address of the 4-row block at rows 8g + q (ks 0, low half); the other
+  // three blocks of a fragment pair (rows + 4, + 32, + 36) have the same
+  // swizzle (it depends on row & 3 and row bit 3 only), so they are constant
+  // byte offsets in the instruction (tr4_async_at): no v_add per read.
+  auto tr_addr = [&](const bf16* img, int ncols, int col0) {
+    const int row = 8 * g + q;
     const int col = col0 + 4 * pp;
     const int sw = ncols == 128 ? swz128(row) : swz_tr64(row);
-    return tr4_async(img + row * ncols + (((col >> 3) ^ sw) << 3) + (col & 7));
+    return img + row * ncols + (((col >> 3) ^ sw) << 3) + (col & 7);
   };
   bf16x8 fa[FA][2], fb0[2][2], fb1[2][2];
   auto read_a = [&](const bf16* img, int h) {
     bf16x4 lo[FA][2], hi[FA][2];
 #pragma unroll
-    for (int f = 0; f < FA; ++f)
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        const int kr = 32 * ks + 8 * g, c0 = wr * (CA / 2) + f * 16;
-        lo[f][ks] = tr(img + h * QA, CA, kr, c0);
-        hi[f][ks] = tr(img + h * QA, CA, kr + 4, c0);
-      }
+    for (int f = 0; f < FA; ++f) {
+      const bf16* a0 = tr_addr(img + h * QA, CA, wr * (CA / 2) + f * 16);
+      lo[f][0] = tr4_async_at<0>(a0);
+      hi[f][0] = tr4_async_at<8 * CA>(a0);
+      lo[f][1] = tr4_async_at<64 * CA>(a0);
+      hi[f][1] = tr4_async_at<72 * CA>(a0);
+    }
     lds_wait();
 #pragma unroll
     for (int f = 0; f < FA; ++f)
@@ -1236,14 +1240,13 @@ __global__ void __launch_bounds__(kBigT, 1) igemm_dwbig_kernel(IgemmDwParams p) 
   auto read_b = [&](const bf16* img, int h, bf16x8 (&fb)[2][2]) {
     bf16x4 lo[2][2], hi[2][2];
 #pragma unroll
-    for (int e = 0; e < 2; ++e)
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        const int kr = 32 * ks + 8 * g, c0 = wc * 32 + e * 16;
-        const bf16* base = img + 2 * QA + h * QB;
-        lo[e][ks] = tr(base, CB, kr, c0);
-        hi[e][ks] = tr(base, CB, kr + 4, c0);
-      }
+    for (int e = 0; e < 2; ++e) {
+      const bf16* b0 = tr_addr(img + 2 * QA + h * QB, CB, wc * 32 + e * 16);
+      lo[e][0] = tr4_async_at<0>(b0);
+      hi[e][0] = tr4_async_at<8 * CB>(b0);
+      lo[e][1] = tr4_async_at<64 * CB>(b0);
+      hi[e][1] = tr4_async_at<72 * CB>(b0);
+    }
     lds_wait();
 #pragma unroll
     for (int e = 0; e < 2; ++e)

@@ -147,6 +147,15 @@ __device__ __forceinline__ bf16x4 tr4_async(const bf16* p) {
   asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(a));
   return __builtin_bit_cast(bf16x4, r);
 }
+// ... with a constant byte offset in the instruction (no v_add per read)
+template <int OFF>
+__device__ __forceinline__ bf16x4 tr4_async_at(const bf16* p) {
+  static_assert(OFF >= 0 && OFF < 65536, "ds offset field");
+  v4s r;
+  const uint32_t a = (uint32_t)(uintptr_t)((const __attribute__((address_space(3))) bf16*)(p));
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(r) : "v"(a), "n"(OFF));
+  return __builtin_bit_cast(bf16x4, r);
+}
 // wait for every outstanding LDS read and pin the given fragments after it
 template <typename F>
 __device__ __forceinline__ void lds_pin(F& f) { asm volatile("" : "+v"(f)); }
