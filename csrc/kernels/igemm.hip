@@ -902,10 +902,12 @@ __global__ void __launch_bounds__(kIgT, 2) igemm_dw_kernel(IgemmDwParams p) {
 
   // transpose-read of a [BK][ncols] image: 4 consecutive K rows (pixels) of
   // 16 columns; lane 4q+p of a 16-lane group addresses row kr+q, columns 4p..
+  // (address of rows kr + q; rows kr + 4 + q have the same swizzle, so the
+  // second read of a fragment takes its offset in the instruction)
   auto tra = [&](const bf16* img, int ncols, int kr, int col0) {  // (inline asm: see tr4_async)
     const int row = kr + q;
     const int col = col0 + 4 * pp;
-    return tr4_async(img + row * ncols + (((col >> 3) ^ swz128(row)) << 3) + (col & 7));
+    return img + row * ncols + (((col >> 3) ^ swz128(row)) << 3) + (col & 7);
   };
 
   if (ks0 < ks1) {
@@ -924,13 +926,15 @@ __global__ void __launch_bounds__(kIgT, 2) igemm_dw_kernel(IgemmDwParams p) {
         bf16x4 al[FM], ah[FM], bl[4], bh[4];
 #pragma unroll
         for (int f = 0; f < FM; ++f) {
-          al[f] = tra(D, BM, kr, wm * (BM / 2) + f * 16);
-          ah[f] = tra(D, BM, kr + 4, wm * (BM / 2) + f * 16);
+          const bf16* pa = tra(D, BM, kr, wm * (BM / 2) + f * 16);
+          al[f] = tr4_async_at<0>(pa);
+          ah[f] = tr4_async_at<8 * BM>(pa);  // + 4 rows
         }
 #pragma unroll
         for (int f = 0; f < 4; ++f) {
-          bl[f] = tra(X, BN, kr, wn * 64 + f * 16);
-          bh[f] = tra(X, BN, kr + 4, wn * 64 + f * 16);
+          const bf16* pb = tra(X, BN, kr, wn * 64 + f * 16);
+          bl[f] = tr4_async_at<0>(pb);
+          bh[f] = tr4_async_at<8 * BN>(pb);
         }
         lds_wait();
         bf16x8 a[FM], b[4];
