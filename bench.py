@@ -59,7 +59,7 @@ def metric_for(model):
     return METRIC if model == "lenet5" else f"images/sec (whole node), {model}, at 1/2/4/8 MI355X"
 
 
-def timed_run(args, spec, dtype, B, d_img, d_lab, dev, dev_idx, rank, world, multi):
+def timed_run(args, spec, dtype, B, d_img, d_lab, dev, dev_idx, rank, world, multi, eager_anchor=False):
     """Build a trainer, warm up, time exactly args.steps steps between
     barrier + device synchronize on both sides (max over ranks), free it."""
     import torch
@@ -120,41 +120,66 @@ def timed_run(args, spec, dtype, B, d_img, d_lab, dev, dev_idx, rank, world, mul
             if args.graph == "on":
                 raise RuntimeError(f"--graph on: capture failed: {why}")
             graph_note = f"off (capture failed: {why})"
-    for _ in range(max(0, args.warmup - 1)):
-        step()
-    torch.cuda.synchronize()
-    if multi:
-        dist.barrier()
-    torch.cuda.synchronize()
-    tr.zero_stats()
-    issued0 = tr.sync.issued
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    if multi:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    coll_per_step = (tr.sync.issued - issued0) / max(1, args.steps) if coll_graph is None else coll_graph
-    if multi:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    def timed(fn, warmup, counted):
+        """`warmup` untimed calls, then exactly args.steps timed ones bracketed
+        by barrier + device synchronize on both sides; returns (seconds, MAX
+        over ranks; collectives issued per timed step, from the host counter
+        when `counted`)"""
+        for _ in range(max(0, warmup)):
+            fn()
+        torch.cuda.synchronize()
+        if multi:
+            dist.barrier()
+        torch.cuda.synchronize()
+        tr.zero_stats()
+        issued0 = tr.sync.issued
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            fn()
+        torch.cuda.synchronize()
+        if multi:
+            dist.barrier()
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        per = (tr.sync.issued - issued0) / max(1, args.steps) if counted else None
+        if multi:
+            t = torch.tensor([el], device=dev, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t.item())
+        return el, per
+
+    # (the eager first step above is warmup step 1 of the headline region)
+    elapsed, per = timed(step, args.warmup - 1, coll_graph is None)
+    coll_per_step = per if coll_graph is None else coll_graph
     st = tr.net.get_stats()
+    # Same-path anchor for the N > 1 points, which run per-kernel launches: at
+    # N = 1 the same trainer is timed again with eager launches, same K / W,
+    # AFTER the headline region (whose warmup is therefore unchanged)
+    eager = None
+    if eager_anchor and step is not step_launch:
+        e_el, _ = timed(step_launch, args.warmup, True)
+        eager = {"value": round(B * world * args.steps / e_el, 1), "ms_per_step": round(1000.0 * e_el / args.steps, 4),
+                 "steps": args.steps, "warmup": args.warmup,
+                 "train_loss_mean": round(tr.net.get_stats()["loss_sum"] / (B * args.steps), 4),
+                 "launch": "per-kernel launches (the N > 1 launch mode, --graph off semantics), same trainer, "
+                           "timed after the graph region"}
     nb = len(tr.sync.buckets)
     res = {
         "elapsed": elapsed,
+        "eager": eager,
+        "loss_key": "train_loss_mean",  # mean over the K timed steps
         "loss": round(st["loss_sum"] / (B * args.steps), 4),
         "launch": graph_note,
         "optimizer": ("sgd lr={} (plain SGD, the reference's Layer_update, cnn.c:303-314)".format(args.lr)
                       if args.momentum == 0 else f"sgd lr={args.lr} momentum={args.momentum}"),
         "allreduce": (f"{'rccl' if args.dist_backend == 'nccl' else 'gloo (rehearsal)'}: {coll_per_step:g} "
                       f"all-reduce(s)/step over {nb} bucket(s) <= {args.bucket_mb} MiB, async on RCCL's stream, "
-                      "joined before SGD"
+                      "joined before its SGD"
                       + ("; at one rank RCCL elides the in-place SUM: no reduction kernel runs"
                          " (--force-reduce runs one)" if tr.sync.elided else "")
                       + ("; forced one-rank reduction kernel (AVG)" if args.force_reduce and world == 1 else "")
+                      + ("; SGD split per bucket: each bucket's update joins only its own all-reduce"
+                         if tr.split_sgd and nb > 1 else "")
                       if coll_per_step else "none (--no-dist)"),
     }
     del step, g, tr
@@ -197,6 +222,7 @@ def timed_run64(args, spec, B, d_img, d_lab, dev):
     del net
     return {
         "elapsed": elapsed,
+        "loss_key": "train_loss_last",  # the last timed step's mean loss (read once: no per-step host sync)
         "loss": round(loss, 4),
         "launch": "per-kernel launches on GpuNet64's stream (fp64 GEMMs on v_mfma_f64_16x16x4_f64)",
         "optimizer": f"sgd lr={args.lr} (plain SGD, the reference's Layer_update, cnn.c:303-314)",
@@ -237,6 +263,9 @@ def main():
     ap.add_argument("--fp32-extra", choices=["auto", "on", "off"], default="auto",
                     help="also time LeNet-5 fp32 (BASELINE config 2) in the same run and report it under "
                          "\"fp32\" in the JSON line; auto = on at N=1 for a bf16 LeNet-5 run")
+    ap.add_argument("--eager-anchor", choices=["auto", "on", "off"], default="auto",
+                    help="also time the headline trainer with per-kernel launches (the launch mode of the N > 1 "
+                         "points) after the graph region and report it under \"eager\"; auto = on at N=1")
     ap.add_argument("--no-dist", action="store_true",
                     help="N=1 only: no process group, no collectives (A/B against the RCCL path)")
     ap.add_argument("--graph", choices=["auto", "on", "off"], default="auto",
@@ -304,12 +333,15 @@ def main():
     multi = dist.is_initialized() and world > 1
 
     if args.dtype == "fp64":
+        if args.momentum != 0:
+            raise SystemExit("bench: --dtype fp64 runs the reference's plain SGD (GpuNet64.sgd): --momentum 0 only")
         if world > 1:
             raise SystemExit("bench: --dtype fp64 (the reference precision, GpuNet64) runs on one GPU")
         head = timed_run64(args, spec, B, d_img, d_lab, dev)
         args.fp32_extra = "off"
     else:
-        head = timed_run(args, spec, args.dtype, B, d_img, d_lab, dev, dev_idx, rank, world, multi)
+        head = timed_run(args, spec, args.dtype, B, d_img, d_lab, dev, dev_idx, rank, world, multi,
+                         eager_anchor=args.eager_anchor == "on" or (args.eager_anchor == "auto" and world == 1))
     # BASELINE config 2 ("LeNet-5 fp32 on one MI355X") in the same run: a
     # second trainer after the first is freed, same graph replay, same K / W
     extra = None
@@ -341,10 +373,12 @@ def main():
                 "input_shape": f"{C}x{H}x{W}",
                 "optimizer": head["optimizer"],
                 "allreduce": head["allreduce"],
-                "train_loss_last": head["loss"],
+                head["loss_key"]: head["loss"],
                 "launch": head["launch"],
             },
         }
+        if head.get("eager"):
+            out["eager"] = head["eager"]
         if extra is not None:
             v32 = B * world * args.steps / extra["elapsed"]
             out["fp32"] = {
@@ -356,7 +390,7 @@ def main():
                 "steps": args.steps,
                 "warmup": args.warmup,
                 "vs_baseline": round(v32 / BASELINE_IMG_S, 2) if args.model == "lenet5" else None,
-                "train_loss_last": extra["loss"],
+                extra["loss_key"]: extra["loss"],
                 "launch": extra["launch"],
             }
         sys.stdout.flush()

@@ -39,6 +39,7 @@ struct CliArgs {
   double bucket_mb = 4.0;   // DP gradient bucket size (MiB)
   bool profile = false;     // per-phase timers
   bool no_graph = false;    // run the step eagerly instead of replaying a hipGraph
+  int split_sgd = -1;       // per-bucket SGD after each bucket's all-reduce: -1 auto (world > 1), 0 off, 1 on
   bool quiet = false;
   int64_t synthetic = 0;    // --synthetic N: generated data instead of IDX files
   std::string comm = "rccl";  // cnn_dist: rccl | host (several ranks on one GPU) | local (world 1)
@@ -54,7 +55,7 @@ inline void usage(const char* prog) {
                "  [--model ref|lenet5|cifar3|vgg11] [--epochs N] [--batch B] [--lr X]\n"
                "  [--momentum X] [--weight-decay X] [--seed S] [--dtype bf16|fp32|fp64]\n"
                "  [--ref-compat] [--fp32] [--save W] [--load W] [--max-train N]\n"
-               "  [--bucket-mb MB] [--log-every N] [--profile] [--no-graph] [--json PATH|-]\n"
+               "  [--bucket-mb MB] [--log-every N] [--profile] [--no-graph] [--split-sgd auto|on|off] [--json PATH|-]\n"
                "  [--comm rccl|host|local]   (cnn_dist: RCCL; host shared memory for several ranks\n"
                "  [--sampler random|seq]     (GPU: rand() %% N per rank shard, or sequential global batches)\n"
                "                             on one GPU; no collectives at world 1)\n"
@@ -91,6 +92,11 @@ inline int parse_cli(int argc, char** argv, CliArgs& a) {
     else if (s == "--fp32") a.fp32 = true;
     else if (s == "--profile") a.profile = true;
     else if (s == "--no-graph") a.no_graph = true;
+    else if (s == "--split-sgd") {
+      const std::string v = next();
+      a.split_sgd = v == "on" ? 1 : v == "off" ? 0 : v == "auto" ? -1 : -2;
+      if (a.split_sgd == -2) { usage(argv[0]); std::exit(100); }
+    }
     else if (s == "--quiet") a.quiet = true;
     else if (s == "--comm") a.comm = next();
     else if (s == "--sampler") a.sampler = next();

@@ -218,6 +218,12 @@ int run_gpu_training(const CliArgs& a, Comm& comm, const char* program) {
   std::vector<hipEvent_t> ev_b(buckets.size());
   hipEvent_t ev_join;
   for (auto& e : ev_b) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  // per-bucket SGD (default at world > 1): bucket k's parameters are updated
+  // as soon as ITS all-reduce has landed, so the FC update of LeNet-5 / the
+  // reference model overlaps the conv block's (last, small) collective
+  const bool split_sgd = coll && buckets.size() > 1 && (a.split_sgd == 1 || (a.split_sgd < 0 && world > 1));
+  std::vector<hipEvent_t> ev_done(buckets.size());
+  for (auto& e : ev_done) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   HIPCHK(hipEventCreateWithFlags(&ev_join, hipEventDisableTiming));
   // The loss is scaled by 1/(b*world) and the bucket all-reduce sums over
   // ranks, so the update uses the global-batch mean.  (ncclAvg is a
@@ -244,15 +250,25 @@ int run_gpu_training(const CliArgs& a, Comm& comm, const char* program) {
         HIPCHK(hipEventRecord(ev_b[k], S));
         HIPCHK(hipStreamWaitEvent(C, ev_b[k], 0));
         comm.allreduce_sum_f32(net.grads() + buckets[k].off, buckets[k].count, C);
+        if (split_sgd) HIPCHK(hipEventRecord(ev_done[k], C));
       }
     }
     if (timed) timer.mark(2, S);
-    if (coll) {  // join before the update
-      HIPCHK(hipEventRecord(ev_join, C));
-      HIPCHK(hipStreamWaitEvent(S, ev_join, 0));
+    if (split_sgd) {
+      // join bucket by bucket (the comm stream runs them in issue order)
+      for (size_t k = 0; k < buckets.size(); ++k) {
+        HIPCHK(hipStreamWaitEvent(S, ev_done[k], 0));
+        if (timed && k == 0) timer.mark(3, S);
+        net.sgd_range((float)a.lr, (float)a.momentum, (float)a.weight_decay, buckets[k].off, buckets[k].count, S);
+      }
+    } else {
+      if (coll) {  // join before the update
+        HIPCHK(hipEventRecord(ev_join, C));
+        HIPCHK(hipStreamWaitEvent(S, ev_join, 0));
+      }
+      if (timed) timer.mark(3, S);
+      net.sgd((float)a.lr, (float)a.momentum, (float)a.weight_decay, S);
     }
-    if (timed) timer.mark(3, S);
-    net.sgd((float)a.lr, (float)a.momentum, (float)a.weight_decay, S);
     gpu::advance_counter(d_step.as<uint64_t>(), S);
     if (timed) timer.mark(4, S);
   };
@@ -449,6 +465,7 @@ int run_gpu_training(const CliArgs& a, Comm& comm, const char* program) {
   }
   comm.barrier();
   for (auto& e : ev_b) (void)hipEventDestroy(e);
+  for (auto& e : ev_done) (void)hipEventDestroy(e);
   (void)hipEventDestroy(ev_join);
   (void)hipEventDestroy(ev_sync);
   (void)hipStreamDestroy(S);

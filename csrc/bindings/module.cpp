@@ -410,6 +410,12 @@ PYBIND11_MODULE(_C, m) {
       .def("sgd",
            [](GpuNet& n, float lr, float mu, float wd, uintptr_t s) { n.sgd(lr, mu, wd, stream_of(s)); },
            py::arg("lr"), py::arg("momentum") = 0.f, py::arg("weight_decay") = 0.f, py::arg("stream") = 0)
+      .def("sgd_range",
+           [](GpuNet& n, float lr, float mu, float wd, int64_t off, int64_t cnt, uintptr_t s) {
+             n.sgd_range(lr, mu, wd, off, cnt, stream_of(s));
+           },
+           py::arg("lr"), py::arg("momentum"), py::arg("weight_decay"), py::arg("off"), py::arg("count"),
+           py::arg("stream") = 0)
       .def("pack", [](GpuNet& n, uintptr_t s) { n.pack(stream_of(s)); }, py::arg("stream") = 0)
       .def("stage_param_range",
            [](const GpuNet& n, int s) {
@@ -444,6 +450,26 @@ PYBIND11_MODULE(_C, m) {
         py::arg("act") = 0, py::arg("bias") = 0, py::arg("aux") = 0, py::arg("ldaux") = 0, py::arg("C") = 0,
         py::arg("ldc") = 0, py::arg("Cf") = 0, py::arg("splitk") = 1, py::arg("pstride") = 0,
         py::arg("stream") = 0);
+  // the engine's FC forward for long-K layers (VGG-11 FC1): split-K partials
+  // into `scratch` + the finishing bias / activation pass; splitk < 1 = the
+  // engine's own rule (gemm_fwd_splitk)
+  k.def("gemm_fwd_splitk", &gpu::gemm_fwd_splitk, py::arg("M"), py::arg("N"), py::arg("K"));
+  k.def("gemm_splitk_fwd",
+        [](const std::string& dt, int M, int N, int K, uintptr_t A, int lda, uintptr_t W, int ldw, int act,
+           uintptr_t bias, uintptr_t C, int ldc, uintptr_t scratch, int splitk, uintptr_t s) {
+          gpu::GemmParams p;
+          p.M = M; p.N = N; p.K = K;
+          p.A = ptr<void>(A); p.lda = lda;
+          p.B = ptr<void>(W); p.ldb = ldw;
+          p.bias = ptr<float>(bias);
+          p.epi = gpu::EPI_BIAS_ACT; p.act = act; p.C = ptr<void>(C); p.ldc = ldc;
+          const int sk = splitk >= 1 ? splitk : gpu::gemm_fwd_splitk(M, N, K);
+          gpu::gemm_splitk_fwd(parse_dtype(dt), p, ptr<float>(scratch), sk, stream_of(s));
+          return sk;
+        },
+        py::arg("dtype"), py::arg("M"), py::arg("N"), py::arg("K"), py::arg("A"), py::arg("lda"), py::arg("W"),
+        py::arg("ldw"), py::arg("act"), py::arg("bias"), py::arg("C"), py::arg("ldc"), py::arg("scratch"),
+        py::arg("splitk") = 0, py::arg("stream") = 0);
   k.def("fc",
         [](int M, int N, int K, uintptr_t A, int lda, uintptr_t W, int ldw, int epi, int act, uintptr_t bias,
            uintptr_t aux, int ldaux, uintptr_t C, int ldc, uintptr_t Cf, uintptr_t dbg, uintptr_t s) {

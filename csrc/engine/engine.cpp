@@ -305,8 +305,9 @@ void GpuNet::build() {
       // 128x128 / 256-tile MFMA kernels (the whole-image LDS kernels
       // measured slower there).  CIFAR-3conv conv3 (64 -> 128): 3.91 -> 4.32 M img/s; conv2
       // (32 -> 64) measured slower on igemm (3.83 M), so C % 64 only.
+      const int ig_cmod = ab_flag("ig32") ? 32 : 64;
       if (!st.big && s > 0 && dtype_ == DType::BF16 && !no_igemm_ && st.stride == 1 &&
-          st.inC % 64 == 0 && st.C % 64 == 0 &&
+          st.inC % ig_cmod == 0 && st.C % 64 == 0 &&
           gpu::igemm_conv_supported(st.inC, st.C, st.KS) && gpu::igemm_conv_supported(st.C, st.inC, st.KS))
         st.big = true;
       st.kgem = r8(KK * st.inC);
@@ -685,7 +686,13 @@ void GpuNet::build() {
     const Stage& st = *sp;
     if (st.kind != Stage::FC) continue;
     const int ld = st.last ? r8(spec_.num_classes()) : st.out_ld;
-    scratch = std::max(scratch, (size_t)gpu::gemm_fwd_splitk(Bm, st.Nout, st.Kin) * Bm * ld * 4);
+    // the split count is not monotonic in the batch (VGG-11 FC1 at max batch
+    // 1024: sk 4 x 1024 rows, at 768: sk 6 x 768 rows): size for every batch
+    // forward() can see
+    size_t need = 0;
+    for (int b = 1; b <= Bm; ++b)
+      need = std::max(need, (size_t)gpu::gemm_fwd_splitk(b, st.Nout, st.Kin) * b * ld * 4);
+    scratch = std::max(scratch, need);
   }
   if (lenet_) scratch = std::max(scratch, gpu::lenet_slab_bytes());
   if (fcchain_) scratch = std::max(scratch, gpu::lenet_fc_slab_bytes(Bm));
@@ -767,7 +774,7 @@ std::string GpuNet::plan() const {
          << (st.permC ? " nhwc-flatten" : "")
          << (st.fc_tall ? (st.fc_tall_dx ? " tall[fwd dx]" : " tall[fwd]")
                         : st.fc_ig ? (st.fc_igdx ? " igemm[fwd dx]" : " igemm[fwd]") : "")
-         << "\n";
+         << (st.head ? " head[softmax-CE fused]" : "") << "\n";
     }
   }
   return os.str();
@@ -1013,8 +1020,10 @@ void GpuNet::forward_stages(size_t first, bool defer_fc, hipStream_t s) {
       p.bias = params_ + st.b_off;
       if (st.last) { p.epi = gpu::EPI_LOGITS; p.Cf = logits_; p.ldc = logits_ld_; }
       else { p.epi = gpu::EPI_BIAS_ACT; p.act = st.act; p.C = st.act_buf; p.ldc = st.out_ld; }
-      const int sk = gpu::gemm_fwd_splitk(B, st.Nout, st.Kin);
-      MCC_CHECK((size_t)sk * B * p.ldc * 4 <= scratch_bytes_ || sk == 1, "fc forward split-K scratch too small");
+      int sk = gpu::gemm_fwd_splitk(B, st.Nout, st.Kin);
+      // (build() sizes the scratch for every B <= max_batch; the clamp only
+      // guards a future change of the split rule)
+      while (sk > 1 && (size_t)sk * B * p.ldc * 4 > scratch_bytes_) --sk;
       gpu::gemm_splitk_fwd(dtype_, p, scratch_, sk, s);
     }
   }
@@ -1477,6 +1486,34 @@ void GpuNet::sgd(float lr, float momentum, float weight_decay, hipStream_t s) {
   }
   gpu::sgd_update(params_, grads_, momentum != 0.f ? mom_ : nullptr, spec_.nparams, lr, momentum, weight_decay, s);
   pack(s);
+}
+
+void GpuNet::sgd_range(float lr, float momentum, float weight_decay, int64_t off, int64_t count, hipStream_t s) {
+  MCC_CHECK(off >= 0 && count > 0 && off + count <= spec_.nparams, "sgd_range: bad parameter range");
+  bool lo_ok = false, hi_ok = false;  // whole stages only: [w_off of one, end of another]
+  for (const Stage* st : stages_) {
+    if (st->nw + st->nb == 0) continue;
+    lo_ok = lo_ok || st->w_off == off;
+    hi_ok = hi_ok || st->w_off + st->nw + st->nb == off + count;
+  }
+  MCC_CHECK(lo_ok && hi_ok, "sgd_range: range must start and end at stage boundaries");
+  if (momentum != 0.f) ensure_momentum();
+  if (fused_pack_) {
+    gpu::SgdPackParams p = pack_;
+    p.nstages = 0;  // the weight stages inside the range (sorted by w_off, as pack_)
+    for (int i = 0; i < pack_.nstages; ++i)
+      if (pack_.st[i].w_off >= off && pack_.st[i].w_off < off + count) p.st[p.nstages++] = pack_.st[i];
+    p.lo = off;
+    p.n = off + count;
+    p.update = true;
+    p.mom = momentum != 0.f ? mom_ : nullptr;
+    p.lr = lr; p.mu = momentum; p.wd = weight_decay;
+    gpu::sgd_pack(dtype_, p, s);
+    return;
+  }
+  gpu::sgd_update(params_ + off, grads_ + off, momentum != 0.f ? mom_ + off : nullptr, count, lr, momentum,
+                  weight_decay, s);
+  pack(s);  // (the table path refreshes every copy: idempotent)
 }
 
 void GpuNet::stage_param_range(int stage, int64_t& off, int64_t& count) const {

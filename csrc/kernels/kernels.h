@@ -656,6 +656,7 @@ struct SgdPackParams {
   const float* grads = nullptr;
   float* mom = nullptr;
   int64_t n = 0;
+  int64_t lo = 0;      // parameters [lo, n) only (a stage boundary: sgd_range); 0 = all
   float lr = 0.f, mu = 0.f, wd = 0.f;
   bool update = true;  // false: refresh the packed copies only
   void* packed = nullptr;

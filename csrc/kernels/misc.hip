@@ -483,12 +483,14 @@ __global__ void __launch_bounds__(256) sgd_pack_kernel(SgdPackParams p) {
   };
   const int64_t stride = (int64_t)(gridDim.x - p.ntiles) * blockDim.x * 4;
   int s = 0;  // monotone per thread: i only grows
-  for (int64_t i0 = ((int64_t)(blockIdx.x - p.ntiles) * blockDim.x + threadIdx.x) * 4; i0 < p.n; i0 += stride) {
+  const int64_t lo4 = p.lo & ~int64_t(3);  // the groups stay 16-byte aligned
+  for (int64_t i0 = lo4 + ((int64_t)(blockIdx.x - p.ntiles) * blockDim.x + threadIdx.x) * 4; i0 < p.n; i0 += stride) {
     int s3 = s;
     const int r0 = region(i0, s), r3 = region(min(i0 + 3, p.n - 1), s3);
-    if (r0 == r3 && (r0 & 1) && p.st[s].tile0 >= 0) continue;  // done by the tiles
-    if (r0 != r3 || i0 + 3 >= p.n) {
+    if (r0 == r3 && (r0 & 1) && p.st[s].tile0 >= 0 && i0 >= p.lo) continue;  // done by the tiles
+    if (r0 != r3 || i0 + 3 >= p.n || i0 < p.lo) {
       for (int e = 0; e < 4 && i0 + e < p.n; ++e) {
+        if (i0 + e < p.lo) continue;  // the group straddles the range start
         int se = s;
         const int re = region(i0 + e, se);
         if ((re & 1) && p.st[se].tile0 >= 0) continue;
@@ -703,7 +705,8 @@ void sgd_pack(DType t, const SgdPackParams& pin, hipStream_t s) {
       p.ntiles += cdiv(N, kPackTN) * cdiv(st.inC, kPackTC);
     }
   }
-  const dim3 grid((unsigned)(p.ntiles + (int)grid_for(p.n, 4))), block(256);
+  MCC_CHECK(p.lo >= 0 && p.lo < p.n, "sgd_pack: empty parameter range");
+  const dim3 grid((unsigned)(p.ntiles + (int)grid_for(p.n - (p.lo & ~int64_t(3)), 4))), block(256);
   if (t == DType::BF16) {
     if (p.update) hipLaunchKernelGGL((sgd_pack_kernel<bf16, true>), grid, block, 0, s, p);
     else hipLaunchKernelGGL((sgd_pack_kernel<bf16, false>), grid, block, 0, s, p);

@@ -126,6 +126,27 @@ class BucketedAllReduce:
         for w in works:
             w.wait()
 
+    def backward_update(self, stream_handle: int, update):
+        """backward() with the update split per bucket: every bucket's
+        all-reduce is issued as in backward(), then, in issue order, the
+        compute stream joins bucket k's collective and calls
+        ``update(off, count)`` for its parameter range (GpuNet.sgd_range).
+        The update of the early buckets (LeNet-5: the FC stages, 96 % of the
+        bytes) runs while the last bucket's collective -- the one issued after
+        the fused conv-block backward -- is still in flight, so only the
+        small conv-parameter update waits for it.  Bit-identical to
+        backward() + a whole-buffer SGD (the update is elementwise)."""
+        works = []
+        for hi, lo, off, cnt in self.buckets:
+            self.net.backward(hi, lo, stream_handle)
+            works.append(dist.all_reduce(self.grads[off : off + cnt], op=self.op, group=self.group, async_op=True)
+                         if self.active else None)
+        self.issued += sum(w is not None for w in works)
+        for (hi, lo, off, cnt), w in zip(self.buckets, works):
+            if w is not None:
+                w.wait()
+            update(off, cnt)
+
 
 def broadcast_params(params: torch.Tensor, src: int = 0, group=None):
     if dist.is_initialized():

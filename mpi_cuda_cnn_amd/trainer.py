@@ -37,6 +37,7 @@ class GpuTrainer:
         group=None,
         bucket_bytes: int = 4 << 20,
         force_reduce: bool = False,
+        split_sgd: bool | None = None,
     ):
         self.spec = _C.make_model(model) if isinstance(model, str) else model
         self.device = torch.cuda.current_device() if device is None else device
@@ -57,6 +58,9 @@ class GpuTrainer:
             broadcast_params(self.params, 0, group)
             self.net.pack(self.stream)
         self.sync = BucketedAllReduce(self.net, self.grads, group, bucket_bytes, force_reduce)
+        # per-bucket SGD (BucketedAllReduce.backward_update): default where a
+        # collective can be in flight after the backward, i.e. world > 1
+        self.split_sgd = (self.world > 1) if split_sgd is None else bool(split_sgd)
 
     @property
     def stream(self) -> int:
@@ -69,8 +73,12 @@ class GpuTrainer:
         idx_ptr = 0 if idx is None else idx.data_ptr()
         self.net.forward(images.data_ptr(), idx_ptr, B, s)
         self.net.loss(labels.data_ptr(), idx_ptr, self.sync.loss_scale(B), True, s)
-        self.sync.backward(s)
-        self.net.sgd(self.lr, self.momentum, self.weight_decay, s)
+        if self.split_sgd and len(self.sync.buckets) > 1:
+            self.sync.backward_update(
+                s, lambda off, cnt: self.net.sgd_range(self.lr, self.momentum, self.weight_decay, off, cnt, s))
+        else:
+            self.sync.backward(s)
+            self.net.sgd(self.lr, self.momentum, self.weight_decay, s)
 
     def zero_stats(self):
         self.net.zero_stats(self.stream)

@@ -151,3 +151,42 @@ def test_cnn_dist_host_comm_rank_death_exits_111(idx_files, tmp_path):
     assert rcs[0] == 111 and rcs[2] == 111, (rcs, outs[0][1][-1500:], outs[2][1][-1500:])
     assert "aborting" in outs[0][1] + outs[2][1]
     assert dt < 120
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 4])
+def test_cnn_dist_split_sgd_equals_joined(idx_files, tmp_path, world):
+    """Per-bucket SGD (the default at world > 1: bucket k's parameters are
+    updated as soon as ITS all-reduce landed, so the FC update overlaps the
+    conv block's collective) ends bit-identical to the joined update (one
+    whole-buffer SGD after every bucket's all-reduce), inside the captured
+    hipGraph, with momentum and several buckets (--bucket-mb 0.01)."""
+    r1, _ = _launch(world, idx_files, str(tmp_path / "s{rank}.bin"), ["--split-sgd", "on"])
+    r2, _ = _launch(world, idx_files, str(tmp_path / "j{rank}.bin"), ["--split-sgd", "off"])
+    assert r1.returncode == 0 and r2.returncode == 0, (r1.stderr[-2000:], r2.stderr[-2000:])
+    js = json.loads([ln for ln in r1.stdout.splitlines() if ln.startswith("{")][-1])
+    assert js["buckets"] > 1 and js["hipgraph"] is True
+    for k in range(world):
+        s = mcc.load_weights(str(tmp_path / f"s{k}.bin"))[1]
+        j = mcc.load_weights(str(tmp_path / f"j{k}.bin"))[1]
+        np.testing.assert_array_equal(s, j, err_msg=f"rank {k}")
+
+
+@pytest.mark.gpu
+def test_cnn_dist_rccl_world1_split_sgd_equals_joined(idx_files, tmp_path):
+    """The same equivalence on the real RCCL communicator at world 1 (the only
+    RCCL world one GPU allows): split vs joined update, bit-identical."""
+    def run(w, mode):
+        env = dict(os.environ, RANK="0", WORLD_SIZE="1", LOCAL_RANK="0", MCC_COMM_TIMEOUT="60",
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(29500 + os.getpid() % 1000))
+        env.pop("MCC_AB", None)
+        r = subprocess.run([CNN_DIST] + idx_files + [
+            "--comm", "rccl", "--model", "lenet5", "--batch", "512", "--epochs", "1", "--lr", "0.05",
+            "--momentum", "0.9", "--bucket-mb", "0.01", "--split-sgd", mode, "--json", "-", "--save", w],
+            capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
+        assert r.returncode == 0, r.stderr[-3000:]
+        return mcc.load_weights(w)[1]
+
+    s = run(str(tmp_path / "s.bin"), "on")
+    j = run(str(tmp_path / "j.bin"), "off")
+    np.testing.assert_array_equal(s, j)

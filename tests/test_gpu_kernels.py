@@ -209,3 +209,30 @@ def test_fc_tall_kernel(cuda, M, N, K, act, dtype):
     err = float((out.double() - ref).norm() / ref.norm())
     assert err < (1e-5 if dtype == "fp32" else 1e-2), err
     assert float((out.double() - ref).abs().max()) < (1e-4 if dtype == "fp32" else 0.05) * float(ref.abs().max())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M", [640, 768, 896, 2])
+def test_fc1_splitk_forward_vgg_shape(cuda, M):
+    """VGG-11 FC1 (25,088 -> 4,096, bias + ReLU) on the engine's long-K
+    forward: split-K 128x128 partials + the finishing bias/ReLU pass, at the
+    bench batch (640) and the batches whose split count differs (768 -> 6,
+    896 -> 5; 2 -> no split), against torch's fp32 matmul of the same bf16
+    operands, per output channel (reference semantics: cnn.c:113-152)."""
+    N, K = 4096, 25088
+    g = torch.Generator(device=cuda).manual_seed(7)
+    A = (torch.rand(M, K, device=cuda, generator=g) * 0.1).to(torch.bfloat16)  # ReLU'd activations
+    W = (torch.randn(N, K, device=cuda, generator=g) * 0.01).to(torch.bfloat16)
+    bias = torch.randn(N, device=cuda, generator=g) * 0.05
+    C = torch.zeros(M, N, device=cuda, dtype=torch.bfloat16)
+    sk = K_.gemm_fwd_splitk(M, N, K)
+    scratch = torch.empty(max(1, sk) * M * N, device=cuda, dtype=torch.float32)
+    used = K_.gemm_splitk_fwd("bf16", M, N, K, A.data_ptr(), K, W.data_ptr(), K, K_.ACT_RELU, bias.data_ptr(),
+                              C.data_ptr(), N, scratch.data_ptr(), splitk=0, stream=_s())
+    torch.cuda.synchronize()
+    assert used == sk >= 1, (M, sk)
+    ref = torch.relu(A.float() @ W.float().t() + bias)
+    err = (C.float() - ref).norm(dim=0) / ref.norm(dim=0).clamp_min(1e-3 * ref.norm() / N ** 0.5)
+    # bf16 output rounding (2^-9 relative) dominates; a dropped split or K
+    # slice would be O(1) on every channel
+    assert err.max().item() < 1e-2, (err.max().item(), int(err.argmax()))

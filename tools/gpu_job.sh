@@ -36,7 +36,7 @@ if [ -n "$BENCH" ]; then
     envs=(); args=()
     for w in $a; do if [ ${#args[@]} -eq 0 ] && [[ "$w" == *=* ]]; then envs+=("$w"); else args+=("$w"); fi; done
     (for e in "${envs[@]}"; do export "$e"; done; timeout -k 10 200 python bench.py "${args[@]}") > $O/bench_$i.json 2> $O/bench_$i.err || { echo "bench '$a' failed"; tail -20 $O/bench_$i.err; exit 1; }
-    echo "[$a] $(grep -h '^{' $O/bench_$i.json | python3 -c "import json,sys;d=json.loads(sys.stdin.read());print(d['value'], d['ms_per_step'], d['config'].get('train_loss_last'))")"
+    echo "[$a] $(grep -h '^{' $O/bench_$i.json | python3 -c "import json,sys;d=json.loads(sys.stdin.read());print(d['value'], d['ms_per_step'], d['config'].get('train_loss_mean', d['config'].get('train_loss_last')), d.get('eager',{}).get('ms_per_step'))")"
   done
 fi
 if [ -n "$PROF" ]; then
