@@ -95,6 +95,7 @@ struct GpuNet::Stage {
   gpu::Conv1DirectParams pd1;
   // u8 RGB first layer (3x3 pad 1, ReLU, 2x2 pool), bf16: row-worker forward (conv_u8.hip)
   bool u8fwd = false;
+  bool c2k = false;  // CIFAR-3conv conv2 kernels (cifar_c2.hip)
 };
 
 static inline int r8(int x) { return (x + 7) & ~7; }
@@ -332,6 +333,13 @@ void GpuNet::build() {
       }
       st.ig_pool = st.ig_fwd && st.pooled && st.pk == 2 && st.ps == 2 && st.OH % 2 == 0 && st.OW % 2 == 0;
       if (!st.big && dtype_ == DType::BF16) plan_pipe(st, s == 0);
+      // CIFAR-3conv conv2 (32 -> 64 at 16x16, pooled ReLU): dedicated kernels
+      // (cifar_c2.hip) over the pipelined small-image ones; same packed
+      // weights ([r16(C)][kpad], k = tap * 32 + c) and output layouts
+      st.c2k = !st.big && dtype_ == DType::BF16 && s > 0 && !ab_flag("no_c2k") && st.cvec && st.CL == 32 &&
+               st.kpad == 288 && st.pk == 2 && st.ps == 2 &&
+               gpu::cifar_c2_supported(st.inC, st.inH, st.inW, st.C, st.KS, st.stride, st.pad, st.act == gpu::ACT_RELU,
+                                       st.pooled);
       if (!st.big && dtype_ == DType::F32 && st.pooled && st.stride == 1 &&
           (s == 0 || st.inC > 1)) {
         gpu::Conv1DirectParams& d = st.pd1;
@@ -768,6 +776,7 @@ std::string GpuNet::plan() const {
         os << " direct-f32[" << (st.direct_fwd ? "fwd" : "") << (st.direct1 || st.direct_dw ? " dw" : "")
            << (st.direct_dx ? " dx" : "") << "]";
       if (st.u8fwd) os << " u8fwd" << (st.c0dw && !st.big ? " dw:pooled-direct" : "");
+      if (st.c2k) os << " c2k[fwd]";
       os << "\n";
     } else {
       os << "  [" << s << "] fc " << st.Kin << " -> " << st.Nout << (st.last ? " (logits)" : "")
@@ -956,6 +965,14 @@ void GpuNet::forward_stages(size_t first, bool defer_fc, hipStream_t s) {
       p.wt = reinterpret_cast<const float*>(packed_) + st.pk_fwd; p.bias = params_ + st.b_off;
       p.out = static_cast<float*>(st.act_buf); p.out_arg = st.arg_buf;
       gpu::conv_direct_forward(p, s);
+    } else if (st.kind == Stage::CONV && st.c2k) {
+      gpu::CifarC2Params c;
+      c.B = B;
+      c.x = stages_[si - 1]->act_buf;
+      c.w = static_cast<const char*>(packed_) + es * st.pk_fwd; c.ldw = st.kpad;
+      c.bias = params_ + st.b_off;
+      c.y = st.act_buf; c.arg = st.arg_buf;
+      gpu::cifar_c2_forward(c, s);
     } else if (st.kind == Stage::CONV && st.pipe_fwd) {
       gpu::ConvPipeParams p = st.pf;
       p.N = B;

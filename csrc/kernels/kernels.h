@@ -727,5 +727,23 @@ void sgd64(double* w, double* g, double lr, int64_t n, hipStream_t s);
 void u8_batch64(const uint8_t* data, const uint8_t* lab, const int32_t* idx, double* x, int32_t* labels, int B,
                 int npix, hipStream_t s);
 
+// CIFAR-3conv conv2 (cifar_c2.hip): conv 32 -> 64, 3x3, stride 1, pad 1 on
+// 16x16 NHWC bf16, ReLU + 2x2/2 max-pool, one persistent workgroup image at a
+// time with the input tile swizzled in LDS and the weights in registers.
+// Layouts are the ones the small-image path uses: x [B][16][16][32], packed
+// weights [64][ldw] with k = tap*32 + c, y / arg [B][8][8][64] (argmax
+// position 0..3 = TL TR BL BR, 4 = ReLU-inactive window).
+struct CifarC2Params {
+  int B = 0;
+  const void* x = nullptr;
+  const void* w = nullptr;
+  int ldw = 0;
+  const float* bias = nullptr;
+  void* y = nullptr;
+  uint8_t* arg = nullptr;
+};
+bool cifar_c2_supported(int inC, int H, int W, int C, int KS, int stride, int pad, int act_relu, int pooled);
+void cifar_c2_forward(const CifarC2Params& p, hipStream_t s);
+
 }  // namespace gpu
 }  // namespace mcc
