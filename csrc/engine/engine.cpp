@@ -96,6 +96,7 @@ struct GpuNet::Stage {
   // u8 RGB first layer (3x3 pad 1, ReLU, 2x2 pool), bf16: row-worker forward (conv_u8.hip)
   bool u8fwd = false;
   bool c2k = false;  // CIFAR-3conv conv2 kernels (cifar_c2.hip)
+  bool c2bwd = false;  // ... and their backward (dX / dW from the pooled dY + argmax)
 };
 
 static inline int r8(int x) { return (x + 7) & ~7; }
@@ -340,6 +341,7 @@ void GpuNet::build() {
                st.kpad == 288 && st.pk == 2 && st.ps == 2 &&
                gpu::cifar_c2_supported(st.inC, st.inH, st.inW, st.C, st.KS, st.stride, st.pad, st.act == gpu::ACT_RELU,
                                        st.pooled);
+      st.c2bwd = st.c2k && st.CLd == 64 && st.kpad_d == 576 && !ab_flag("no_c2bwd");
       if (!st.big && dtype_ == DType::F32 && st.pooled && st.stride == 1 &&
           (s == 0 || st.inC > 1)) {
         gpu::Conv1DirectParams& d = st.pd1;
@@ -676,6 +678,7 @@ void GpuNet::build() {
       if (st.direct1) scratch = std::max(scratch, gpu::conv1_direct_slab_bytes(st.pd1));
       if (st.direct_dw) scratch = std::max(scratch, gpu::conv_direct_dw_slab_bytes(st.pd1));
       if (st.c0dw) scratch = std::max(scratch, gpu::conv0_dw_slab_bytes(st.pc0));
+      if (st.c2bwd) scratch = std::max(scratch, gpu::cifar_c2_dw_scratch_bytes());
       if (st.pipe_dw) {
         const size_t nv = (size_t)st.pdw.cout_pad * st.pdw.ncols_pad;
         scratch = std::max(scratch, (st.pdw.grid + ceil_div(st.pdw.grid, 16)) * nv * 4);
@@ -776,7 +779,7 @@ std::string GpuNet::plan() const {
         os << " direct-f32[" << (st.direct_fwd ? "fwd" : "") << (st.direct1 || st.direct_dw ? " dw" : "")
            << (st.direct_dx ? " dx" : "") << "]";
       if (st.u8fwd) os << " u8fwd" << (st.c0dw && !st.big ? " dw:pooled-direct" : "");
-      if (st.c2k) os << " c2k[fwd]";
+      if (st.c2k) os << (st.c2bwd ? " c2k[fwd dx dw]" : " c2k[fwd]");
       os << "\n";
     } else {
       os << "  [" << s << "] fc " << st.Kin << " -> " << st.Nout << (st.last ? " (logits)" : "")
@@ -1318,6 +1321,11 @@ void GpuNet::backward(int hi, int lo, hipStream_t s) {
         w.dy = st.grad_buf; w.aux_y = st.act_buf; w.aux_arg = st.arg_buf;
         w.slab = scratch_;
         gpu::conv_dw_rows(w, grads_ + st.w_off, grads_ + st.b_off, ws);
+      } else if (st.c2bwd) {
+        gpu::CifarC2BwdParams c;
+        c.B = B; c.dy = st.grad_buf; c.arg = st.arg_buf; c.x = stages_[si - 1]->act_buf;
+        c.slab = scratch_;
+        gpu::cifar_c2_dw(c, grads_ + st.w_off, grads_ + st.b_off, ws);
       } else if (st.pipe_dw) {
         gpu::ConvDwPipeParams w = st.pdw;
         w.N = B;
@@ -1328,7 +1336,13 @@ void GpuNet::backward(int hi, int lo, hipStream_t s) {
         gpu::conv_dw_pipe(w, ws);
         gpu::conv_dw_pipe_reduce(w, grads_ + st.w_off, grads_ + st.b_off, ws);
       }
-      if (st.pipe_dx && si > 0) {
+      if (st.c2bwd) {
+        gpu::CifarC2BwdParams c;
+        c.B = B; c.dy = st.grad_buf; c.arg = st.arg_buf;
+        c.wd = static_cast<const char*>(packed_) + es * st.pk_dx; c.ldw = st.kpad_d;
+        c.dx = stages_[si - 1]->grad_buf;
+        gpu::cifar_c2_dx(c, s);
+      } else       if (st.pipe_dx && si > 0) {
         gpu::ConvPipeParams p = st.pdx;
         p.N = B;
         p.in.src = st.grad_buf; p.in.aux_y = st.act_buf; p.in.aux_arg = st.arg_buf;
@@ -1336,8 +1350,8 @@ void GpuNet::backward(int hi, int lo, hipStream_t s) {
         p.out = stages_[si - 1]->grad_buf;
         gpu::conv_pipe_forward(p, s);
       }
-      const bool dw_done = st.pipe_dw || st.rows_dw || st.direct1 || st.direct_dw || st.c0dw;
-      if (dw_done && (st.pipe_dx || si == 0)) continue;
+      const bool dw_done = st.pipe_dw || st.rows_dw || st.direct1 || st.direct_dw || st.c0dw || st.c2bwd;
+      if (dw_done && (st.pipe_dx || st.c2bwd || si == 0)) continue;
       // weight gradient
       if (!dw_done) {
       gpu::ConvDwParams w;

@@ -744,6 +744,24 @@ struct CifarC2Params {
 };
 bool cifar_c2_supported(int inC, int H, int W, int C, int KS, int stride, int pad, int act_relu, int pooled);
 void cifar_c2_forward(const CifarC2Params& p, hipStream_t s);
+// Backward of the same layer from the pooled output gradient dy [B][8][8][64]
+// and the forward's argmax codes: data gradient dx [B][16][16][32] (plain
+// store; flipped packed weights wd [32][ldw], k = tap*64 + co) and the weight
+// / bias gradient (per-workgroup partials in slab, then dw_slab_reduce into the
+// canonical OIHW gw and gb).
+struct CifarC2BwdParams {
+  int B = 0;
+  const void* dy = nullptr;
+  const uint8_t* arg = nullptr;
+  const void* x = nullptr;   // dW: the layer input [B][16][16][32]
+  const void* wd = nullptr;  // dX
+  int ldw = 0;
+  void* dx = nullptr;
+  float* slab = nullptr;     // dW: cifar_c2_dw_scratch_bytes()
+};
+void cifar_c2_dx(const CifarC2BwdParams& p, hipStream_t s);
+size_t cifar_c2_dw_scratch_bytes();
+void cifar_c2_dw(const CifarC2BwdParams& p, float* gw, float* gb, hipStream_t s);
 
 }  // namespace gpu
 }  // namespace mcc

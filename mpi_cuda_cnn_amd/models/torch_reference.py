@@ -104,9 +104,19 @@ class TorchReference(nn.Module):
             parts.append(m.bias.detach().reshape(-1))
         return torch.cat(parts)
 
-    def forward(self, x):
-        """x: NCHW float in [0,1]. Returns logits (pre-softmax)."""
+    def forward(self, x, forced=None):
+        """x: NCHW float in [0,1]. Returns logits (pre-softmax).
+
+        ``forced`` (mimic_bf16 only): per fused stage (a conv with its max-pool,
+        or an fc), None or the VALUE the engine stored for that stage's output
+        (NCHW / [B, N]).  The oracle then continues from the engine's own
+        activations (straight-through: the value is replaced, the gradient
+        flows through the oracle's graph), so each layer's gradient is checked
+        on the engine's forward state: in a deep bf16 net, one-ulp differences
+        otherwise grow through the layers until ReLU / pool decisions near 0
+        flip between engine and oracle."""
         n = len(self.mods)
+        stage = 0
         for i, (L, m) in enumerate(zip(self.layer_info[1:], self.mods)):
             if L["kind"] == "fc" and x.dim() > 2:
                 x = x.reshape(x.shape[0], -1)
@@ -135,6 +145,10 @@ class TorchReference(nn.Module):
             nxt = self.layer_info[i + 2] if i + 2 < len(self.layer_info) else None
             if self.mimic_bf16 and not (nxt is not None and nxt["kind"] == "maxpool"):
                 x = _RoundBF16.apply(x)
+                if forced is not None and stage < len(forced) and forced[stage] is not None:
+                    f = forced[stage].to(x.dtype).reshape(x.shape)
+                    x = x + (f - x).detach()
+                stage += 1
         return x
 
 

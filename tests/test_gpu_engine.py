@@ -497,6 +497,49 @@ def test_rows_dw_matches_pipe_dw(cuda, B, monkeypatch):
     np.testing.assert_array_equal(g_rows[rest], g_pipe[rest])
 
 
+def _model_step(cuda, model, B, seed=7):
+    spec = mcc.make_model(model)
+    C, H, W = spec.input_shape()
+    imgs, labels = mcc.synth_dataset(B, C, H, W, spec.num_classes(), seed=seed)
+    params = mcc.init_params(spec, seed=seed).astype(np.float32)
+    net = mcc.GpuNet(spec, "bf16", B)
+    net.set_params(params)
+    d_img = torch.from_numpy(imgs).to(cuda)
+    d_lab = torch.from_numpy(labels).to(cuda)
+    s = torch.cuda.current_stream().cuda_stream
+    net.forward(d_img.data_ptr(), 0, B, s)
+    net.loss(d_lab.data_ptr(), 0, 1.0 / B, True, s)
+    net.backward_all(s)
+    torch.cuda.synchronize()
+    return spec, net.plan(), net.get_logits(B), net.get_grads()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B", [96, 2900])
+def test_cifar_c2_kernels_match_pipe(cuda, B, monkeypatch):
+    """CIFAR-3conv conv2 on its dedicated kernels (cifar_c2.hip: forward, data
+    gradient and weight gradient from the pooled dY + argmax) vs the generic
+    pipelined small-image kernels (MCC_AB=no_c2k).  B = 2900 gives every
+    persistent workgroup several images and a ragged tail.  Same bf16 rounding
+    points, different fp32 summation orders: logits and every layer's W / b
+    agree per output channel to a few 1e-3 (a wrong tap / channel / window is
+    O(1)); conv1's gradient checks the data gradient."""
+    monkeypatch.setenv("MCC_AB", "")
+    spec, plan, lg, g = _model_step(cuda, "cifar3", B)
+    assert "c2k[fwd dx dw]" in plan, plan
+    monkeypatch.setenv("MCC_AB", "no_c2k")
+    _, plan0, lg0, g0 = _model_step(cuda, "cifar3", B)
+    assert "c2k" not in plan0, plan0
+    assert _relerr(lg, lg0) < 2e-3
+    for L in spec.layers():
+        if L["nweights"] == 0:
+            continue
+        for off, n, what in ((L["w_off"], L["nweights"], "W"), (L["b_off"], L["nbiases"], "b")):
+            e, c = _per_channel_err(g[off : off + n], g0[off : off + n], L["C"],
+                                    floor_frac=0.3 if what == "b" else 1e-2)
+            assert e < 1e-2, (L["kind"], L["C"], what, c, e)
+
+
 _BIG_SPECS = {
     "big96": "input 3 96 96; conv 16 k3 s1 p1 relu; pool 2; conv 32 k3 s2 p1 relu; "
              "conv 32 k3 s1 p1 relu; pool 2; fc 64 relu; fc 10 softmax",
@@ -509,19 +552,42 @@ _BIG_SPECS = {
 }
 
 
-def _oracle_bf16(spec, params, imgs, labels, round_input, u8_fp32_first=False):
+def _oracle_bf16(spec, params, imgs, labels, round_input, u8_fp32_first=False, forced=None):
     """fp64 oracle fed the engine's bf16 rounding points (TorchReference
     mimic_bf16); round_input: the first layer reads bf16(x/255) (the exact-
     integer u8 paths read x/255 unrounded); u8_fp32_first: the first layer's
-    value as the u8 RGB kernel forms it (integer sum, fp32 scale + bias)."""
+    value as the u8 RGB kernel forms it (integer sum, fp32 scale + bias);
+    forced: the engine's stored stage outputs (_stage_values), which the
+    oracle continues from (TorchReference.forward)."""
     ref = TorchReference(spec, dtype=torch.float64, mimic_bf16=True, u8_fp32_first=u8_fp32_first)
     ref.load_flat(torch.from_numpy(params.astype(np.float64)))
     x = images_to_nchw(imgs, torch.float64)
     if round_input:
         x = x.to(torch.bfloat16).to(torch.float64)
-    logits = ref(x)
+    logits = ref(x, forced=forced)
     F.cross_entropy(logits, torch.from_numpy(labels.astype(np.int64))).backward()
     return logits.detach().numpy(), ref.flat_grads().numpy()
+
+
+def _stage_values(net, spec, B):
+    """The engine's stored output of every fused stage but the last (conv
+    stages NHWC -> NCHW, fc stages [B, N]) as fp64 torch tensors."""
+    L = spec.layers()[1:]
+    shapes = []
+    i = 0
+    while i < len(L):
+        l = L[i]
+        if l["kind"] == "conv" and i + 1 < len(L) and L[i + 1]["kind"] == "maxpool":
+            i += 1
+            l = L[i]
+        shapes.append((l["kind"], l["C"], l["H"], l["W"]))
+        i += 1
+    out = []
+    for si, (kind, C, H, W) in enumerate(shapes[:-1]):
+        y, _ = net.stage_output(si, B)
+        y = torch.from_numpy(np.asarray(y, dtype=np.float64))
+        out.append(y.reshape(B, C) if kind == "fc" else y.reshape(B, H, W, C).permute(0, 3, 1, 2))
+    return out
 
 
 def _per_channel_errs(g, r, C, floor_frac=1e-2):
@@ -606,31 +672,44 @@ def test_bf16_grads_per_channel_vs_rounded_oracle(cuda, model):
     s = torch.cuda.current_stream().cuda_stream
     net.zero_stats(s)
     net.forward(d_img.data_ptr(), 0, B, s)
+    # the real VGG-11 (8 bf16 convs + 3 FCs): the oracle continues from the
+    # engine's stored stage outputs, so one-ulp differences cannot compound
+    # into flipped ReLU / pool decisions (TorchReference.forward)
+    forced = _stage_values(net, spec, B) if model == "vgg11" else None
     net.loss(d_lab.data_ptr(), 0, 1.0 / B, True, s)
     net.backward_all(s)
     torch.cuda.synchronize()
     # exact-integer first layer: the single-channel pipelined conv (plan "fwd:s1")
     # or the u8 RGB row-worker forward (plan "u8fwd", with the row-staged dW)
     round_input = "fwd:s1" not in plan and "u8fwd" not in plan
-    ref_logits, ref_grads = _oracle_bf16(spec, params, imgs, labels, round_input, u8_fp32_first="u8fwd" in plan)
+    ref_logits, ref_grads = _oracle_bf16(spec, params, imgs, labels, round_input, u8_fp32_first="u8fwd" in plan,
+                                         forced=forced)
     grads = net.get_grads()
     lerr = _relerr(net.get_logits(B), ref_logits)
     report = [f"{model}: logits {lerr:.2e} (round_input={round_input})"]
     bad = []
+    # B = 2 (vgg11): an FC weight row is dZ[0,c] X[0] + dZ[1,c] X[1]; where the
+    # two nearly cancel (measured: one FC1 row of 4096), a one-ulp bf16
+    # difference in dZ is a large fraction of the row: rows are measured
+    # against 10 % of the RMS row norm at least, as the fp32 test does
+    wfloor = 0.1 if model == "vgg11" else 1e-2
     for L in spec.layers():
         if L["nweights"] == 0:
             continue
         for off, n, what in ((L["w_off"], L["nweights"], "W"), (L["b_off"], L["nbiases"], "b")):
             e, c = _per_channel_err(grads[off : off + n], ref_grads[off : off + n], L["C"],
-                                    floor_frac=0.3 if what == "b" else 1e-2)
-            report.append(f"  {L['kind']} C={L['C']} {what}: max per-channel {e:.2e} (channel {c})")
+                                    floor_frac=0.3 if what == "b" else wfloor)
+            r = ref_grads[off : off + n].reshape(L["C"], -1).astype(np.float64)
+            rel_norm = np.linalg.norm(r[c]) / max(np.linalg.norm(r) / np.sqrt(L["C"]), 1e-30)
+            report.append(f"  {L['kind']} C={L['C']} {what}: max per-channel {e:.2e} (channel {c}, "
+                          f"norm {rel_norm:.2e} x RMS)")
             dist = PER_CHANNEL_DIST_TOL.get(model)
             if dist is None:
                 if e > PER_CHANNEL_TOL[what]:
                     bad.append(report[-1])
                 continue
             es = _per_channel_errs(grads[off : off + n], ref_grads[off : off + n], L["C"],
-                                   floor_frac=0.3 if what == "b" else 1e-2)
+                                   floor_frac=0.3 if what == "b" else wfloor)
             med, p99 = np.quantile(es, [0.5, 0.99])
             report[-1] += f", p99 {p99:.2e}, median {med:.2e}"
             if e > dist[what] or p99 > dist["p99"] or med > dist["median"]:
