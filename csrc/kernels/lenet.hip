@@ -1035,16 +1035,26 @@ constexpr int kQLds = kQDz1 + 2 * kQDz1buf;
 static_assert(kQOne1 % 256 == kBOne1 % 256 && kQDz1 % 256 == kBDz1 % 256, "bank-model offsets");
 static_assert(kQXs % 256 == kBXs % 256, "bank-model offsets");
 static_assert(2 * kQLds <= 163840, "lenet_bwd4: two workgroups per CU");
+// One-barrier schedule (round 6): dZ2 / Y1 (+ the dW2 ones pixel) double-
+// buffered -- region 1 after the two-barrier layout, at a multiple of 256 B so
+// it keeps region 0's bank mapping -- so image k+1's dZ2 / Y1 are staged right
+// after a wave's compute(k), and X0 of image k is staged after barrier A(k)
+// (its buffer's last reader, conv1 dW of image k-2, ran in compute(k-1)).
+constexpr int kQR1 = (kQLds + 255) / 256 * 256;      // 63232
+constexpr int kQLds1 = kQR1 + kQXs;                   // + dZ2 / Y1 / ones: 77952
+static_assert(kQXs >= kBOne2 + 16, "region 0 = [0, kQXs)");
+static_assert(2 * kQLds1 <= 163840, "lenet_bwd4 one-barrier: two workgroups per CU");
 constexpr int kXw0 = MCC_BWD4_XW0;  // X0 row groups (of 8 rows) staged by w0; the rest by w3
 static_assert(kXw0 >= 1 && kXw0 <= 3, "X0 staging split");
 
 template <int T0, int T1>
 __device__ __forceinline__ void lenet_dx2_tiles(char* smem, const bf16x8 (&wdx)[15], const uint32_t* a1w, int hxa,
-                                                int hxb, int n16, int g, int dxci, int dxj, int dz1) {
+                                                int hxb, int n16, int g, int dxci, int dxj, int dz1, int roff = 0) {
   bf16x8 fr[15], nx[5];
+  const char* rs = smem + roff;  // dZ2 region of this image
 #pragma unroll
   for (int c = 0; c < 15; ++c)
-    fr[c] = *reinterpret_cast<const bf16x8*>(smem + (dxwrap(c) ? hxb : hxa) + dxoff(c) + T0 * 1280);
+    fr[c] = *reinterpret_cast<const bf16x8*>(rs + (dxwrap(c) ? hxb : hxa) + dxoff(c) + T0 * 1280);
   f32x4 accp = {0.f, 0.f, 0.f, 0.f};
   auto epilogue = [&](int T, const f32x4& acc) {
     uint32_t top[4], bot[4];
@@ -1067,7 +1077,7 @@ __device__ __forceinline__ void lenet_dx2_tiles(char* smem, const bf16x8 (&wdx)[
     if (T + 1 < T1) {
 #pragma unroll
       for (int c = 10; c < 15; ++c)
-        nx[c - 10] = *reinterpret_cast<const bf16x8*>(smem + (dxwrap(c) ? hxb : hxa) + dxoff(c) + (T + 1) * 1280);
+        nx[c - 10] = *reinterpret_cast<const bf16x8*>(rs + (dxwrap(c) ? hxb : hxa) + dxoff(c) + (T + 1) * 1280);
     }
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -1113,13 +1123,17 @@ __device__ __forceinline__ void lenet_dx2_tiles(char* smem, const bf16x8 (&wdx)[
 // One role's per-image loop: every wave runs the same barrier sequence, but
 // each role is its own inlined loop, so its registers (w0's 52 dW2
 // accumulators, w1..w3's 60 dX2 weight registers) are not live in the others.
-template <typename Load, typename Begin, typename Compute, typename Stage>
+// pre(k): staging of image k that must follow barrier A(k) in the
+// one-barrier schedule (X0); post(k): staging of image k's dZ2 / Y1 into
+// region k & 1.  Two-barrier schedule (kOne = false): both after barrier B.
+template <bool kOne, typename Load, typename Begin, typename Compute, typename Pre, typename Post>
 __device__ __forceinline__ int lenet_bwd4_loop(const LenetBwdParams& p, Load&& load, Begin&& begin, Compute&& compute,
-                                               Stage&& stage) {
+                                               Pre&& pre, Post&& post) {
   const int grid = (int)gridDim.x;
   if ((int)blockIdx.x < p.B) {
     load(0);
-    stage(0);
+    if constexpr (!kOne) pre(0);
+    post(0);
   }
   int k = 0;
 #if MCC_LENET_STAMP
@@ -1137,18 +1151,24 @@ __device__ __forceinline__ int lenet_bwd4_loop(const LenetBwdParams& p, Load&& l
 #endif
   for (int img = blockIdx.x; img < p.B; img += grid, ++k) {
     stamp(k, 0);
-    wg_barrier();  // A: image k staged (dZ2, Y1, X0[k & 1])
+    wg_barrier();  // A: image k staged (dZ2, Y1; two-barrier: X0[k & 1] too)
     stamp(k, 1);
     begin();
+    if constexpr (kOne) pre(k);
     const bool more = img + grid < p.B;
     if (more && !(MCC_LENET_ABL & 256)) load(k + 1);
     compute(k);
     stamp(k, 2);
-    wg_barrier();  // B: dZ2 / Y1 / X0[(k - 1) & 1] / dZ1[(k - 1) & 1] free
+    if constexpr (!kOne) wg_barrier();  // B: dZ2 / Y1 / X0[(k - 1) & 1] / dZ1[(k - 1) & 1] free
     stamp(k, 3);
-    if (more) stage((k + 1) & 1);
+    if (more) {
+      if constexpr (!kOne) pre(k + 1);
+      post(k + 1);
+    }
     stamp(k, 4);
   }
+  // one-barrier: the last image's dZ1 / X0 complete before w3's trailing conv1 dW
+  if constexpr (kOne) wg_barrier();
 #if MCC_LENET_STAMP
   if ((threadIdx.x & 63) == 0) {
     unsigned long long* st = reinterpret_cast<unsigned long long*>(p.slab + (size_t)512 * kSlab) +
@@ -1160,8 +1180,11 @@ __device__ __forceinline__ int lenet_bwd4_loop(const LenetBwdParams& p, Load&& l
   return k;
 }
 
+template <bool kOne>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) lenet_bwd4_kernel(LenetBwdParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int kLds = kOne ? kQLds1 : kQLds;
+  auto roff = [](int k) { return kOne ? (k & 1) * kQR1 : 0; };  // dZ2 / Y1 region of image k
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int n16 = lane & 15, g = lane >> 4;
   const int sk = lane & 7, srow = lane >> 3;
@@ -1169,12 +1192,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
 
   {
     const u32x4 z = {0u, 0u, 0u, 0u};
-    for (int i = threadIdx.x * 16; i < kQLds; i += 256 * 16) *reinterpret_cast<u32x4*>(smem + i) = z;
+    for (int i = threadIdx.x * 16; i < kLds; i += 256 * 16) *reinterpret_cast<u32x4*>(smem + i) = z;
   }
   wg_barrier();
-  if (wv == 0) {  // bf16 ones: the dW2 bias pixel and the dW1 bias rows
+  if (wv == 0) {  // bf16 ones: the dW2 bias pixel (each region) and the dW1 bias rows
     const uint32_t one2 = 0x3f803f80u;
     if (lane < 4) *reinterpret_cast<uint32_t*>(smem + kBOne2 + 4 * lane) = one2;
+    if (kOne && lane < 4) *reinterpret_cast<uint32_t*>(smem + kQR1 + kBOne2 + 4 * lane) = one2;
     for (int i = lane; i < 30 * 16; i += 64)
       *reinterpret_cast<uint32_t*>(smem + kQOne1 + (i >> 4) * 80 + (i & 15) * 4) = one2;
   }
@@ -1207,17 +1231,18 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
     WaveIdx widx;
     widx.load(p.idx, blockIdx.x, grid, p.B, 0);
     auto load = [&](int k) { LENET_LOAD_X(0, kXw0) };
-    auto stage = [&](int buf) { LENET_STAGE_X(0, kXw0) };
-    auto compute = [&](int) {
+    auto pre = [&](int k) { const int buf = k & 1; LENET_STAGE_X(0, kXw0) };
+    auto compute = [&](int k) {
       if constexpr (!(MCC_LENET_ABL & 1)) {
         bf16x8 af[2], bfr[2][13];
+        char* rs = smem + roff(k);
         auto load_chunk = [&](int c, int buf) {
-          af[buf] = tr8(smem + aw2[c][0], smem + aw2[c][1]);
+          af[buf] = tr8(rs + aw2[c][0], rs + aw2[c][1]);
 #pragma unroll
           for (int t = 0; t < 13; ++t) {
             const int o = tapoff2(2 * t);
             const int* base = t == 12 ? bw2c[c] : ((2 * t) % 5 == 4 ? bw2b[c] : bw2a[c]);
-            bfr[buf][t] = tr8(smem + base[0] + o, smem + base[1] + o);
+            bfr[buf][t] = tr8(rs + base[0] + o, rs + base[1] + o);
           }
         };
         load_chunk(0, 0);
@@ -1231,7 +1256,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
         }
       }
     };
-    lenet_bwd4_loop(p, load, nothing, compute, stage);
+    lenet_bwd4_loop<kOne>(p, load, nothing, compute, pre, [](int) {});
 #pragma unroll
     for (int t = 0; t < 13; ++t)
 #pragma unroll
@@ -1289,19 +1314,20 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
       cw = *reinterpret_cast<const u32x2*>(p.a2 + (size_t)img * kY2Elems + zq * 16 + 8 * zh);
     }
   };
-  auto stage_dz2 = [&] {
+  auto stage_dz2 = [&](int k) {
+    char* smem_r = smem + roff(k);
     if (lane < 50 && !(MCC_LENET_ABL & 8)) {
       const u32x4 z = {0u, 0u, 0u, 0u};
-      *reinterpret_cast<u32x4*>(smem + zbase) = z;
-      *reinterpret_cast<u32x4*>(smem + zbase + 32) = z;
-      *reinterpret_cast<u32x4*>(smem + zbase + 640) = z;
-      *reinterpret_cast<u32x4*>(smem + zbase + 672) = z;
+      *reinterpret_cast<u32x4*>(smem_r + zbase) = z;
+      *reinterpret_cast<u32x4*>(smem_r + zbase + 32) = z;
+      *reinterpret_cast<u32x4*>(smem_r + zbase + 640) = z;
+      *reinterpret_cast<u32x4*>(smem_r + zbase + 672) = z;
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         const uint32_t code = (cw[i >> 2] >> (8 * (i & 3))) & 0xffu;
         const uint32_t v = (dy[i >> 1] >> (16 * (i & 1))) & 0xffffu;
         const int off = ((code & 2u) ? 640 : 0) + ((code & 1u) ? 32 : 0);  // code 4: value 0 at TL
-        *reinterpret_cast<unsigned short*>(smem + zbase + off + 2 * i) = (unsigned short)(code < 4u ? v : 0u);
+        *reinterpret_cast<unsigned short*>(smem_r + zbase + off + 2 * i) = (unsigned short)(code < 4u ? v : 0u);
       }
     }
   };
@@ -1312,12 +1338,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
 #pragma unroll
     for (int r = 0; r < 4; ++r) yv[r] = *reinterpret_cast<const u32x4*>(y1g + min(lane + 64 * r, 195) * 8);
   };
-  auto stage_y1 = [&] {
+  auto stage_y1 = [&](int k) {
     if constexpr (!(MCC_LENET_ABL & 64)) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int px = lane + 64 * r;
-        if (px < 196) *reinterpret_cast<u32x4*>(smem + kBY1 + px * 16) = yv[r];
+        if (px < 196) *reinterpret_cast<u32x4*>(smem + roff(k) + kBY1 + px * 16) = yv[r];
       }
     }
   };
@@ -1328,26 +1354,28 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
       if constexpr (MCC_BWD4_STAGE) load_y1(k); else load_dz2(k);
       load_codes(k, kT1);
     };
-    auto stage = [&](int) {
-      if constexpr (MCC_BWD4_STAGE) stage_y1(); else stage_dz2();
+    auto post = [&](int k) {
+      if constexpr (MCC_BWD4_STAGE) stage_y1(k); else stage_dz2(k);
     };
     auto compute = [&](int k) {
-      if constexpr (!(MCC_LENET_ABL & 2)) lenet_dx2_tiles<0, kT1>(smem, wdx, a1w, hxa, hxb, n16, g, dxci, dxj, dz1_of(k));
+      if constexpr (!(MCC_LENET_ABL & 2))
+        lenet_dx2_tiles<0, kT1>(smem, wdx, a1w, hxa, hxb, n16, g, dxci, dxj, dz1_of(k), roff(k));
     };
-    lenet_bwd4_loop(p, load, begin, compute, stage);
+    lenet_bwd4_loop<kOne>(p, load, begin, compute, [](int) {}, post);
   } else if (wv == 2) {
     // ---- w2: dX tiles [kT1, kT2); stages Y1 (or dZ2) ----
     auto load = [&](int k) {
       if constexpr (MCC_BWD4_STAGE) load_dz2(k); else load_y1(k);
       load_codes(k, kT2 - kT1);
     };
-    auto stage = [&](int) {
-      if constexpr (MCC_BWD4_STAGE) stage_dz2(); else stage_y1();
+    auto post = [&](int k) {
+      if constexpr (MCC_BWD4_STAGE) stage_dz2(k); else stage_y1(k);
     };
     auto compute = [&](int k) {
-      if constexpr (!(MCC_LENET_ABL & 2)) lenet_dx2_tiles<kT1, kT2>(smem, wdx, a1w, hxa, hxb, n16, g, dxci, dxj, dz1_of(k));
+      if constexpr (!(MCC_LENET_ABL & 2))
+        lenet_dx2_tiles<kT1, kT2>(smem, wdx, a1w, hxa, hxb, n16, g, dxci, dxj, dz1_of(k), roff(k));
     };
-    lenet_bwd4_loop(p, load, begin, compute, stage);
+    lenet_bwd4_loop<kOne>(p, load, begin, compute, [](int) {}, post);
   } else {
     // ---- w3: conv1 dW of the previous image + dX tile 6; X0 rows 16..27 ----
     int a1b[2], b1b;
@@ -1394,13 +1422,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
       LENET_LOAD_X(kXw0, 4 - kXw0)
       if constexpr (kT2 < 7) load_codes(k, 7 - kT2);
     };
-    auto stage = [&](int buf) { LENET_STAGE_X(kXw0, 4 - kXw0) };
+    auto pre = [&](int k) { const int buf = k & 1; LENET_STAGE_X(kXw0, 4 - kXw0) };
     auto compute = [&](int k) {
       if (k > 0) dw1((k - 1) & 1);
       if constexpr (!(MCC_LENET_ABL & 2) && kT2 < 7)
-        lenet_dx2_tiles<kT2, 7>(smem, wdx, a1w, hxa, hxb, n16, g, dxci, dxj, dz1_of(k));
+        lenet_dx2_tiles<kT2, 7>(smem, wdx, a1w, hxa, hxb, n16, g, dxci, dxj, dz1_of(k), roff(k));
     };
-    const int n = lenet_bwd4_loop(p, load, begin, compute, stage);
+    const int n = lenet_bwd4_loop<kOne>(p, load, begin, compute, pre, [](int) {});
     if (n > 0) dw1((n - 1) & 1);  // the last image's conv1 dW
 #pragma unroll
     for (int i = 0; i < 4; ++i) slab[kSlabW2 + i * 64 + lane] = acc1[i];
@@ -1470,7 +1498,8 @@ void lenet_backward(const LenetBwdParams& p, hipStream_t s) {
   if (p.B <= 0) return;
   const int grid = lenet_bwd_grid();
   if (ab_flag("lenet_bwd2")) hipLaunchKernelGGL(lenet_bwd_kernel, dim3(grid), dim3(128), kBLds, s, p);
-  else hipLaunchKernelGGL(lenet_bwd4_kernel, dim3(grid), dim3(256), kQLds, s, p);
+  else if (ab_flag("bwd4_twobar")) hipLaunchKernelGGL(lenet_bwd4_kernel<false>, dim3(grid), dim3(256), kQLds, s, p);
+  else hipLaunchKernelGGL(lenet_bwd4_kernel<true>, dim3(grid), dim3(256), kQLds1, s, p);
   hipLaunchKernelGGL(lenet_bwd_reduce_kernel, dim3(kSlab / 64), dim3(64 * kRedWaves), 0, s, p, grid);
 }
 

@@ -56,10 +56,15 @@ def init_process_group(backend: str, device: torch.device | None = None):
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("RANK", "0")
     os.environ.setdefault("WORLD_SIZE", "1")
-    if "MASTER_PORT" not in os.environ:
+    own_port = "MASTER_PORT" not in os.environ
+
+    def pick_port():
         with socket.socket() as s:
             s.bind(("127.0.0.1", 0))
             os.environ["MASTER_PORT"] = str(s.getsockname()[1])
+
+    if own_port:
+        pick_port()
     kw = {"timeout": comm_timeout()}
     if backend == "nccl":
         # No recycled HIP events between collectives: with the cache on, the
@@ -78,7 +83,18 @@ def init_process_group(backend: str, device: torch.device | None = None):
         opts = dist.ProcessGroupNCCL.Options()
         opts.is_high_priority_stream = True
         kw["pg_options"] = opts
-    dist.init_process_group(backend, **kw)
+    # A port we picked ourselves is free when probed but can be taken before
+    # the store binds it (seen once on a GPU box: EADDRINUSE between two
+    # back-to-back bench runs): pick another and retry.  A launcher-given
+    # port is shared with the other ranks and is never changed here.
+    for attempt in range(5 if own_port else 1):
+        try:
+            dist.init_process_group(backend, **kw)
+            return
+        except dist.DistNetworkError as e:
+            if not own_port or "EADDRINUSE" not in str(e) or attempt == 4:
+                raise
+            pick_port()
 
 
 class BucketedAllReduce:

@@ -59,11 +59,13 @@ def _pool_codes(z):
     return v, pos, gap
 
 
-@pytest.fixture(params=["", "lenet_fwd1,lenet_bwd2"], ids=["round5", "round4"])
+@pytest.fixture(params=["", "bwd4_twobar", "lenet_fwd1,lenet_bwd2"], ids=["round6", "round5", "round4"])
 def kernel_gen(request, monkeypatch):
     """The default kernels (window-in-lane forward lenet_fwd2, four-wave
-    backward lenet_bwd4) and, under MCC_AB=lenet_fwd1,lenet_bwd2, the round-4
-    pair they replaced: both against the same oracle."""
+    backward lenet_bwd4 on the one-barrier schedule), the round-5 two-barrier
+    schedule of lenet_bwd4 (MCC_AB=bwd4_twobar) and, under
+    MCC_AB=lenet_fwd1,lenet_bwd2, the round-4 pair: all against the same
+    oracle."""
     monkeypatch.setenv("MCC_AB", request.param)
     return request.param
 
