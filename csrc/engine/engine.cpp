@@ -97,6 +97,7 @@ struct GpuNet::Stage {
   bool u8fwd = false;
   bool c2k = false;  // CIFAR-3conv conv2 kernels (cifar_c2.hip)
   bool c2bwd = false;  // ... and their backward (dX / dW from the pooled dY + argmax)
+  bool c3k = false;  // CIFAR-3conv conv3 kernels (cifar_c3.hip): forward, dX, dW (no grad_xform)
 };
 
 static inline int r8(int x) { return (x + 7) & ~7; }
@@ -333,6 +334,13 @@ void GpuNet::build() {
         st.ig_dx = st.stride == 1 && gpu::igemm_conv_supported(st.C, st.inC, st.KS);
       }
       st.ig_pool = st.ig_fwd && st.pooled && st.pk == 2 && st.ps == 2 && st.OH % 2 == 0 && st.OW % 2 == 0;
+      // CIFAR-3conv conv3 (64 -> 128 at 8x8, pooled ReLU): dedicated kernels
+      // over the implicit GEMM, same packed weights ([C][kgem] / [inC][kgem_d],
+      // k = tap * channels + c) and output layouts
+      st.c3k = st.big && dtype_ == DType::BF16 && s > 0 && !no_igemm_ && !ab_flag("no_c3k") && st.pooled &&
+               st.pk == 2 && st.ps == 2 && st.kgem == 576 && st.kgem_d == 1152 &&
+               gpu::cifar_c3_supported(st.inC, st.inH, st.inW, st.C, st.KS, st.stride, st.pad,
+                                       st.act == gpu::ACT_RELU, st.pooled);
       if (!st.big && dtype_ == DType::BF16) plan_pipe(st, s == 0);
       // CIFAR-3conv conv2 (32 -> 64 at 16x16, pooled ReLU): dedicated kernels
       // (cifar_c2.hip) over the pipelined small-image ones; same packed
@@ -661,6 +669,7 @@ void GpuNet::build() {
       if (st.c0dw) scratch = std::max(scratch, gpu::conv0_dw_slab_bytes(st.pc0));
       if (sp != stages_[0] && !st.ig_dx)
         col_bytes_ = std::max(col_bytes_, es * (size_t)Bm * st.inH * st.inW * st.kgem_d);
+      if (st.c3k) scratch = std::max(scratch, gpu::cifar_c3_dw_scratch_bytes());
       if (st.ig_dw0) {
         const int sk = gpu::igemm_dw_splitk((int)rows, st.C, st.kgem);
         scratch = std::max(scratch, gpu::igemm_dw_slab_bytes(st.C, st.kgem, sk));
@@ -762,7 +771,8 @@ std::string GpuNet::plan() const {
     if (st.kind == Stage::CONV) {
       os << "  [" << s << "] conv " << st.inC << "x" << st.inH << "x" << st.inW << " -> " << st.C << "x" << st.OH << "x"
          << st.OW << (st.pooled ? " +maxpool" : "") << " k" << st.KS << "s" << st.stride << "p" << st.pad
-         << (st.big ? (st.ig_fwd ? " igemm" : " im2col+gemm") : (st.cvec ? " lds-cvec" : " lds-scalar"))
+         << (st.big ? (st.c3k ? " c3k[fwd dx dw]" : st.ig_fwd ? " igemm" : " im2col+gemm")
+                    : (st.cvec ? " lds-cvec" : " lds-scalar"))
          << (st.c0dw ? " dw:pooled-direct" : "") << (st.dz_fused ? " dz<-next-dx" : "")
          << (st.generic ? " generic" : "") << " chunks=" << st.nchunks
          << " imgs=" << st.imgs_fwd << "/"
@@ -927,6 +937,16 @@ void GpuNet::forward_stages(size_t first, bool defer_fc, hipStream_t s) {
       u.w = params_ + st.w_off; u.bias = params_ + st.b_off;
       u.out = static_cast<uint16_t*>(st.act_buf); u.out_arg = st.arg_buf;
       gpu::u8conv_forward(u, s);
+      continue;
+    }
+    if (st.kind == Stage::CONV && st.c3k) {
+      gpu::CifarC3Params c;
+      c.B = B;
+      c.x = stages_[si - 1]->act_buf;
+      c.w = static_cast<const char*>(packed_) + es * st.pk_fwd; c.ldw = st.kgem;
+      c.bias = params_ + st.b_off;
+      c.y = st.act_buf; c.arg = st.arg_buf;
+      gpu::cifar_c3_forward(c, s);
       continue;
     }
     if (st.kind == Stage::CONV && st.big && st.ig_fwd) {
@@ -1198,6 +1218,17 @@ void GpuNet::backward(int hi, int lo, hipStream_t s) {
           c.dy = static_cast<const uint16_t*>(st.grad_buf); c.arg = st.arg_buf;
           c.slab = scratch_;
           gpu::conv0_dw(c, grads_ + st.w_off, grads_ + st.b_off, ws);
+          continue;
+        }
+        if (st.c3k) {  // dX / dW straight from the pooled dY and argmax (no dZ pass)
+          fork();
+          gpu::CifarC3BwdParams c;
+          c.B = B; c.dy = st.grad_buf; c.arg = st.arg_buf; c.x = stages_[si - 1]->act_buf;
+          c.slab = scratch_;
+          gpu::cifar_c3_dw(c, grads_ + st.w_off, grads_ + st.b_off, ws);
+          c.wd = static_cast<const char*>(packed_) + es * st.pk_dx; c.ldw = st.kgem_d;
+          c.dx = stages_[si - 1]->grad_buf;
+          gpu::cifar_c3_dx(c, s);
           continue;
         }
         // dZ = relu'/unpool(dY) at conv-output size

@@ -762,6 +762,18 @@ struct CifarC2BwdParams {
 void cifar_c2_dx(const CifarC2BwdParams& p, hipStream_t s);
 size_t cifar_c2_dw_scratch_bytes();
 void cifar_c2_dw(const CifarC2BwdParams& p, float* gw, float* gb, hipStream_t s);
+// CIFAR-3conv conv3 (cifar_c3.hip): conv 64 -> 128, 3x3, pad 1 on 8x8 NHWC
+// bf16, ReLU + 2x2/2 max-pool; same parameter blocks.  x [B][8][8][64],
+// weights [128][ldw] with k = tap*64 + c (the implicit-GEMM packing), y / arg
+// [B][4][4][128]; wd [64][ldw] with k = tap*128 + co (flipped taps), dx
+// [B][8][8][64]; slab cifar_c3_dw_scratch_bytes().
+using CifarC3Params = CifarC2Params;
+using CifarC3BwdParams = CifarC2BwdParams;
+bool cifar_c3_supported(int inC, int H, int W, int C, int KS, int stride, int pad, int act_relu, int pooled);
+void cifar_c3_forward(const CifarC3Params& p, hipStream_t s);
+void cifar_c3_dx(const CifarC3BwdParams& p, hipStream_t s);
+size_t cifar_c3_dw_scratch_bytes();
+void cifar_c3_dw(const CifarC3BwdParams& p, float* gw, float* gb, hipStream_t s);
 
 }  // namespace gpu
 }  // namespace mcc

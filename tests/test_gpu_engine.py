@@ -516,20 +516,23 @@ def _model_step(cuda, model, B, seed=7):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("B", [96, 2900])
-def test_cifar_c2_kernels_match_pipe(cuda, B, monkeypatch):
-    """CIFAR-3conv conv2 on its dedicated kernels (cifar_c2.hip: forward, data
-    gradient and weight gradient from the pooled dY + argmax) vs the generic
-    pipelined small-image kernels (MCC_AB=no_c2k).  B = 2900 gives every
-    persistent workgroup several images and a ragged tail.  Same bf16 rounding
-    points, different fp32 summation orders: logits and every layer's W / b
-    agree per output channel to a few 1e-3 (a wrong tap / channel / window is
-    O(1)); conv1's gradient checks the data gradient."""
+@pytest.mark.parametrize("flag,marker", [("no_c2k", "c2k[fwd dx dw]"), ("no_c3k", "c3k[fwd dx dw]")])
+def test_cifar_dedicated_kernels_match_generic(cuda, B, flag, marker, monkeypatch):
+    """CIFAR-3conv conv2 / conv3 on their dedicated kernels (cifar_c2.hip /
+    cifar_c3.hip: forward, data gradient and weight gradient from the pooled
+    dY + argmax) vs the generic kernels of the same layer (MCC_AB=no_c2k: the
+    pipelined small-image kernels; no_c3k: the implicit GEMM + grad_xform).
+    B = 2900 gives every persistent workgroup several images and a ragged
+    tail.  Same bf16 rounding points, different fp32 summation orders: logits
+    and every layer's W / b agree per output channel to a few 1e-3 (a wrong
+    tap / channel / window is O(1)); the layers below check the data
+    gradient."""
     monkeypatch.setenv("MCC_AB", "")
     spec, plan, lg, g = _model_step(cuda, "cifar3", B)
-    assert "c2k[fwd dx dw]" in plan, plan
-    monkeypatch.setenv("MCC_AB", "no_c2k")
+    assert marker in plan, plan
+    monkeypatch.setenv("MCC_AB", flag)
     _, plan0, lg0, g0 = _model_step(cuda, "cifar3", B)
-    assert "c2k" not in plan0, plan0
+    assert marker not in plan0, plan0
     assert _relerr(lg, lg0) < 2e-3
     for L in spec.layers():
         if L["nweights"] == 0:
