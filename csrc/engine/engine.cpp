@@ -334,8 +334,9 @@ void GpuNet::build() {
         st.ig_dx = st.stride == 1 && gpu::igemm_conv_supported(st.C, st.inC, st.KS);
       }
       st.ig_pool = st.ig_fwd && st.pooled && st.pk == 2 && st.ps == 2 && st.OH % 2 == 0 && st.OW % 2 == 0;
-      // CIFAR-3conv conv3 (64 -> 128 at 8x8, pooled ReLU): dedicated kernels
-      // over the implicit GEMM, same packed weights ([C][kgem] / [inC][kgem_d],
+      // 64 -> 128 3x3 pooled ReLU convs on 8 x 8 output tiles (CIFAR-3conv
+      // conv3 at 8x8, VGG-11 conv2 at 112x112): dedicated kernels over the
+      // implicit GEMM, same packed weights ([C][kgem] / [inC][kgem_d],
       // k = tap * channels + c) and output layouts
       st.c3k = st.big && dtype_ == DType::BF16 && s > 0 && !no_igemm_ && !ab_flag("no_c3k") && st.pooled &&
                st.pk == 2 && st.ps == 2 && st.kgem == 576 && st.kgem_d == 1152 &&
@@ -485,7 +486,9 @@ void GpuNet::build() {
       Stage& cur = *stages_[s];
       Stage& pv = *stages_[s - 1];
       // (not for a conv0_dw first layer: its weight gradient reads the pooled dY itself)
-      pv.dz_fused = cur.kind == Stage::CONV && cur.big && cur.ig_dx && pv.kind == Stage::CONV && pv.big && !pv.c0dw &&
+      // (not when cur runs the cifar_c3 kernels: their dX is a plain store of dY)
+      pv.dz_fused = cur.kind == Stage::CONV && cur.big && cur.ig_dx && !cur.c3k && pv.kind == Stage::CONV && pv.big &&
+                    !pv.c0dw &&
                     !pv.pooled && pv.act == gpu::ACT_RELU && dtype_ == DType::BF16 &&
                     pv.C == cur.inC;
     }
@@ -946,6 +949,7 @@ void GpuNet::forward_stages(size_t first, bool defer_fc, hipStream_t s) {
       c.w = static_cast<const char*>(packed_) + es * st.pk_fwd; c.ldw = st.kgem;
       c.bias = params_ + st.b_off;
       c.y = st.act_buf; c.arg = st.arg_buf;
+      c.H = st.inH; c.W = st.inW;
       gpu::cifar_c3_forward(c, s);
       continue;
     }
@@ -1225,6 +1229,7 @@ void GpuNet::backward(int hi, int lo, hipStream_t s) {
           gpu::CifarC3BwdParams c;
           c.B = B; c.dy = st.grad_buf; c.arg = st.arg_buf; c.x = stages_[si - 1]->act_buf;
           c.slab = scratch_;
+          c.H = st.inH; c.W = st.inW;
           gpu::cifar_c3_dw(c, grads_ + st.w_off, grads_ + st.b_off, ws);
           c.wd = static_cast<const char*>(packed_) + es * st.pk_dx; c.ldw = st.kgem_d;
           c.dx = stages_[si - 1]->grad_buf;

@@ -48,8 +48,6 @@ namespace {
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int kImgIn = 8 * 8 * 64;    // input elements per image (NHWC)
-constexpr int kImgOut = 4 * 4 * 128;  // pooled output elements per image
 
 // [10 x 12 px][32 B] planes (forward X, data-gradient dZ); stride 32 mod 128 B
 // so the 8 lanes of a ds_write_b128 group (8 chunks of one pixel) hit 8
@@ -74,12 +72,27 @@ __device__ __forceinline__ u32x4 unpool_pos3(const u32x4& d, uint32_t a0, uint32
 // ------------------------------------------------------------------ forward
 constexpr int kFBuf = 4 * kPS;  // 15,488 B
 
+// tile t of the batch -> (image, tile row, tile column); TY x TX tiles per image
+struct Tile3 {
+  int img, ty, tx;
+};
+__device__ __forceinline__ Tile3 tile_of(int t, int TY, int TX) {
+  Tile3 r;
+  r.img = t / (TY * TX);
+  const int q = t - r.img * TY * TX;
+  r.ty = q / TX;
+  r.tx = q - r.ty * TX;
+  return r;
+}
+
 __global__ void __launch_bounds__(256, 2) cifar_c3_fwd_kernel(CifarC3Params p) {
   __shared__ __attribute__((aligned(16))) char smem[2 * kFBuf];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);  // output channels 32 wv .. 32 wv + 31
   const int r16 = lane & 15, g = lane >> 4;
   const int grid = (int)gridDim.x;
+  const int H = p.H, W = p.W, TY = H >> 3, TX = W >> 3, PH = H >> 1, PW = W >> 1;
+  const int ntiles = p.B * TY * TX;
 
   for (int i = tid * 16; i < 2 * kFBuf; i += 256 * 16) *reinterpret_cast<u32x4*>(smem + i) = u32x4{0u, 0u, 0u, 0u};
 
@@ -92,43 +105,55 @@ __global__ void __launch_bounds__(256, 2) cifar_c3_fwd_kernel(CifarC3Params p) {
     for (int ks = 0; ks < 18; ++ks) wb[nt][ks] = load8(w + (size_t)(32 * wv + 16 * nt + r16) * p.ldw + 32 * ks + 8 * g);
   const float bv0 = p.bias[32 * wv + r16], bv1 = p.bias[32 * wv + 16 + r16];
 
-  // A fragments: row tile T = window row T; lane row r16 = window slot r16 >> 2
-  // (window column), position r16 & 3 = (dy, dx); chunk g of the K step's 32
-  // channels -> plane 2 (ks & 1) + (g >> 1), half g & 1
+  // A fragments: row tile T = window row T of the 8 x 8 output tile; lane row
+  // r16 = window slot r16 >> 2 (window column), position r16 & 3 = (dy, dx);
+  // chunk g of the K step's 32 channels -> plane 2 (ks & 1) + (g >> 1), half g & 1
   const int la = (g >> 1) * kPS + poff((r16 >> 1) & 1, 2 * (r16 >> 2) + (r16 & 1)) + 16 * (g & 1);
 
-  // staging: 16-byte chunk j = tid + 256 i = pixel j >> 3, channel chunk j & 7
-  int soff[2];
+  // staging: the tile's 10 x 10 input halo (zero outside the image) as 800
+  // 16-byte items j = tid + 256 i: halo pixel j >> 3, channel chunk j & 7
+  int soff[4], goff[4], shy[4], shx[4];
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
+  for (int i = 0; i < 4; ++i) {
     const int j = tid + 256 * i, px = j >> 3, c = j & 7;
-    soff[i] = (c >> 1) * kPS + poff((px >> 3) + 1, (px & 7) + 1) + 16 * (c & 1);
+    shy[i] = j < 800 ? px / 10 : -100;  // (-100: no item)
+    shx[i] = px % 10;
+    soff[i] = (c >> 1) * kPS + poff(px / 10, px % 10) + 16 * (c & 1);
+    goff[i] = ((px / 10) * W + px % 10) * 64 + 8 * c;
   }
-  const char* xg = static_cast<const char*>(p.x);
-  u32x4 st[2];
-  auto load = [&](int img) {
-    const u32x4* src = reinterpret_cast<const u32x4*>(xg + (size_t)img * (kImgIn * 2));
+  const bf16* xg = static_cast<const bf16*>(p.x);
+  u32x4 st[4];
+  auto load = [&](int t) {
+    const Tile3 q = tile_of(t, TY, TX);
+    const int y0 = q.ty * 8 - 1, x0 = q.tx * 8 - 1;
+    const bf16* base = xg + ((size_t)q.img * H * W + (int64_t)y0 * W + x0) * 64;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) st[i] = src[tid + 256 * i];
+    for (int i = 0; i < 4; ++i) {
+      const int y = y0 + shy[i], x = x0 + shx[i];
+      const bool in = shy[i] >= 0 && y >= 0 && y < H && x >= 0 && x < W;
+      st[i] = in ? *reinterpret_cast<const u32x4*>(base + goff[i]) : u32x4{0u, 0u, 0u, 0u};
+    }
   };
-  __syncthreads();  // zero fill before the first interior write
-  int img = blockIdx.x;
-  if (img < p.B) load(img);
-  for (int k = 0; img < p.B; img += grid, ++k) {
+  __syncthreads();  // zero fill before the first write
+  int t = blockIdx.x;
+  if (t < ntiles) load(t);
+  for (int k = 0; t < ntiles; t += grid, ++k) {
     char* tb = smem + (k & 1) * kFBuf;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) *reinterpret_cast<u32x4*>(tb + soff[i]) = st[i];
-    __syncthreads();  // image k staged; every wave is past image k - 1's reads of this buffer (k - 2)
-    if (img + grid < p.B) load(img + grid);
+    for (int i = 0; i < 4; ++i)
+      if (shy[i] >= 0) *reinterpret_cast<u32x4*>(tb + soff[i]) = st[i];
+    __syncthreads();  // tile k staged; every wave is past tile k - 1's reads of this buffer (k - 2)
+    const Tile3 q = tile_of(t, TY, TX);
+    if (t + grid < ntiles) load(t + grid);
 
     f32x4 acc[4][2];
 #pragma unroll
-    for (int t = 0; t < 4; ++t) acc[t][0] = acc[t][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int r = 0; r < 4; ++r) acc[r][0] = acc[r][1] = f32x4{0.f, 0.f, 0.f, 0.f};
     const char* rb = tb + la;
     auto read_a = [&](int ks, bf16x8 (&a)[4]) {
       const int tap = ks >> 1, off = (ks & 1) * 2 * kPS + poff(tap / 3, tap % 3);
 #pragma unroll
-      for (int t = 0; t < 4; ++t) a[t] = *reinterpret_cast<const bf16x8*>(rb + off + poff(2 * t, 0));
+      for (int r = 0; r < 4; ++r) a[r] = *reinterpret_cast<const bf16x8*>(rb + off + poff(2 * r, 0));
     };
     bf16x8 a[2][4];
     read_a(0, a[0]);
@@ -137,22 +162,21 @@ __global__ void __launch_bounds__(256, 2) cifar_c3_fwd_kernel(CifarC3Params p) {
       if (ks + 1 < 18) read_a(ks + 1, a[(ks + 1) & 1]);
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        acc[t][0] = mma(acc[t][0], a[ks & 1][t], wb[0][ks]);
-        acc[t][1] = mma(acc[t][1], a[ks & 1][t], wb[1][ks]);
+      for (int r = 0; r < 4; ++r) {
+        acc[r][0] = mma(acc[r][0], a[ks & 1][r], wb[0][ks]);
+        acc[r][1] = mma(acc[r][1], a[ks & 1][r], wb[1][ks]);
       }
       __builtin_amdgcn_sched_barrier(0);
     }
 
-    // pool + bias + ReLU: lane (channel r16 of tile nt, window g of window row t)
-    bf16* yo = static_cast<bf16*>(p.y) + (size_t)img * kImgOut;
-    uint8_t* ao = p.arg + (size_t)img * kImgOut;
+    // pool + bias + ReLU: lane (channel r16 of tile nt, window g of window row r)
+    const size_t obase = ((size_t)q.img * PH + q.ty * 4) * PW + q.tx * 4;
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const int win = 4 * t + g;
+    for (int r = 0; r < 4; ++r) {
+      const size_t o0 = (obase + (size_t)r * PW + g) * 128;
 #pragma unroll
       for (int nt = 0; nt < 2; ++nt) {
-        const f32x4 v = acc[t][nt];
+        const f32x4 v = acc[r][nt];
         float best = v[0];
         int arg = 0;
 #pragma unroll
@@ -162,9 +186,9 @@ __global__ void __launch_bounds__(256, 2) cifar_c3_fwd_kernel(CifarC3Params p) {
           arg = gt ? i : arg;
         }
         const bf16 yb = (bf16)fmaxf(best + (nt ? bv1 : bv0), 0.f);
-        const int o = win * 128 + 32 * wv + 16 * nt + r16;
-        yo[o] = yb;
-        ao[o] = (uint8_t)((float)yb > 0.f ? arg : 4);  // 4: ReLU-inactive window
+        const size_t o = o0 + 32 * wv + 16 * nt + r16;
+        static_cast<bf16*>(p.y)[o] = yb;
+        p.arg[o] = (uint8_t)((float)yb > 0.f ? arg : 4);  // 4: ReLU-inactive window
       }
     }
   }
@@ -180,6 +204,8 @@ cifar_c3_dx_kernel(CifarC3BwdParams p) {
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);  // input channels 32 wv .. 32 wv + 31
   const int r16 = lane & 15, g = lane >> 4;
   const int grid = (int)gridDim.x;
+  const int H = p.H, W = p.W, TY = H >> 3, TX = W >> 3, PH = H >> 1, PW = W >> 1;
+  const int ntiles = p.B * TY * TX;
 
   for (int i = tid * 16; i < 2 * kXBuf; i += 128 * 16) *reinterpret_cast<u32x4*>(smem + i) = u32x4{0u, 0u, 0u, 0u};
 
@@ -192,43 +218,65 @@ cifar_c3_dx_kernel(CifarC3BwdParams p) {
 #pragma unroll
     for (int ks = 0; ks < 36; ++ks) wa[ct][ks] = load8(wd + (size_t)(32 * wv + 16 * ct + r16) * p.ldw + 32 * ks + 8 * g);
 
-  // B fragments: pixel tile pt = image rows 2 pt, 2 pt + 1; lane column r16 ->
+  // B fragments: pixel tile pt = tile rows 2 pt, 2 pt + 1; lane column r16 ->
   // pixel (2 pt + (r16 >> 3), (r16 & 7) ^ 4 (r16 >> 3)), chunk 4 (ks & 3) + g
   const int py = r16 >> 3, px = (r16 & 7) ^ (4 * py);
   const int lb = (g >> 1) * kPS + poff(py, px) + 16 * (g & 1);
 
-  // staging: thread (window w, channel chunk c) for two (w, c) items
+  // staging: the 10 x 10 dZ halo of the tile = the positions of 6 x 6 pooled
+  // windows (tile windows -1 .. 4); item (window a, b; channel chunk c) for
+  // j = tid + 128 i < 576, its in-halo positions as a 4-bit mask
   const char* dyg = static_cast<const char*>(p.dy);
-  int sbase[2];
+  int sbase[5], sgoff[5], swa[5], swb[5];
+  uint32_t smask[5];
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int t = tid + 128 * i, w = t >> 4, c = t & 15;
-    sbase[i] = (c >> 1) * kPS + poff(2 * (w >> 2) + 1, 2 * (w & 3) + 1) + 16 * (c & 1);
+  for (int i = 0; i < 5; ++i) {
+    const int j = tid + 128 * i, wi = j >> 4, c = j & 15;
+    const int wa_ = wi / 6, wb_ = wi % 6;
+    uint32_t m = 0;
+#pragma unroll
+    for (int pos = 0; pos < 4; ++pos) {
+      const int hy = 2 * wa_ + (pos >> 1) - 1, hx = 2 * wb_ + (pos & 1) - 1;
+      if (j < 576 && hy >= 0 && hy < 10 && hx >= 0 && hx < 10) m |= 1u << pos;
+    }
+    smask[i] = m;
+    swa[i] = wa_;
+    swb[i] = wb_;
+    sbase[i] = (c >> 1) * kPS + (((2 * wa_ - 1) * kPit) + 2 * wb_ - 1) * 32 + 16 * (c & 1);  // (may be < 0: masked)
+    sgoff[i] = ((wa_ - 1) * PW + (wb_ - 1)) * 128 + 8 * c;
   }
-  u32x4 sd[2];
-  uint32_t sa[2][2];
-  auto load = [&](int img) {
+  u32x4 sd[5];
+  uint32_t sa[5][2];
+  auto load = [&](int t) {
+    const Tile3 q = tile_of(t, TY, TX);
+    const int wy0 = q.ty * 4, wx0 = q.tx * 4;
+    const size_t base = ((size_t)q.img * PH + wy0) * PW + wx0;  // pooled pixel of tile window (0, 0)
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const size_t e = (size_t)img * kImgOut + (size_t)(tid + 128 * i) * 8;  // (w, c) = element 128 w + 8 c
-      sd[i] = *reinterpret_cast<const u32x4*>(dyg + 2 * e);
-      const uint2 a = *reinterpret_cast<const uint2*>(p.arg + e);
-      sa[i][0] = a.x; sa[i][1] = a.y;
+    for (int i = 0; i < 5; ++i) {
+      const int wy = wy0 + swa[i] - 1, wx = wx0 + swb[i] - 1;
+      const bool in = smask[i] && wy >= 0 && wy < PH && wx >= 0 && wx < PW;
+      const int64_t e = (int64_t)base * 128 + sgoff[i];
+      sd[i] = in ? *reinterpret_cast<const u32x4*>(dyg + 2 * e) : u32x4{0u, 0u, 0u, 0u};
+      uint2 av = {0u, 0u};
+      if (in) av = *reinterpret_cast<const uint2*>(p.arg + e);
+      sa[i][0] = av.x; sa[i][1] = av.y;
     }
   };
   bf16* dxo = static_cast<bf16*>(p.dx);
-  __syncthreads();  // zero fill before the first interior write
-  int img = blockIdx.x;
-  if (img < p.B) load(img);
-  for (int k = 0; img < p.B; img += grid, ++k) {
+  __syncthreads();  // zero fill before the first write
+  int t = blockIdx.x;
+  if (t < ntiles) load(t);
+  for (int k = 0; t < ntiles; t += grid, ++k) {
     char* tb = smem + (k & 1) * kXBuf;
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < 5; ++i)
 #pragma unroll
       for (int pos = 0; pos < 4; ++pos)
-        *reinterpret_cast<u32x4*>(tb + sbase[i] + poff(pos >> 1, pos & 1)) = unpool_pos3(sd[i], sa[i][0], sa[i][1], pos);
-    __syncthreads();  // image k staged; buffer k & 1's previous readers (image k - 2) are done
-    if (img + grid < p.B) load(img + grid);
+        if (smask[i] & (1u << pos))
+          *reinterpret_cast<u32x4*>(tb + sbase[i] + poff(pos >> 1, pos & 1)) = unpool_pos3(sd[i], sa[i][0], sa[i][1], pos);
+    __syncthreads();  // tile k staged; buffer k & 1's previous readers (tile k - 2) are done
+    const Tile3 q = tile_of(t, TY, TX);
+    if (t + grid < ntiles) load(t + grid);
 
     f32x4 acc[2][4];
 #pragma unroll
@@ -254,14 +302,14 @@ cifar_c3_dx_kernel(CifarC3BwdParams p) {
       __builtin_amdgcn_sched_barrier(0);
     }
 
-    // lane: channels 32 wv + 16 ct + 4 g .. + 3 of its pixel in tile pt
-    bf16* o = dxo + (size_t)img * kImgIn;
+    // lane: channels 32 wv + 16 ct + 4 g .. + 3 of its pixel in tile row pair pt
+    const size_t obase = ((size_t)q.img * H + q.ty * 8) * W + q.tx * 8;
 #pragma unroll
     for (int pt = 0; pt < 4; ++pt)
 #pragma unroll
       for (int ct = 0; ct < 2; ++ct) {
         const f32x4 v = acc[ct][pt];
-        *reinterpret_cast<bf16x4*>(o + ((2 * pt + py) * 8 + px) * 64 + 32 * wv + 16 * ct + 4 * g) =
+        *reinterpret_cast<bf16x4*>(dxo + (obase + (size_t)(2 * pt + py) * W + px) * 64 + 32 * wv + 16 * ct + 4 * g) =
             cvt4(v[0], v[1], v[2], v[3]);
       }
   }
@@ -283,6 +331,8 @@ __global__ void __launch_bounds__(512, 1) cifar_c3_dw_kernel(CifarC3BwdParams p)
   const int wc = wv & 1, wn = wv >> 1;  // output channels 64 wc .., input channels 16 wn .. (all 9 taps)
   const int r16 = lane & 15, g = lane >> 4;
   const int grid = (int)gridDim.x;
+  const int H = p.H, W = p.W, TY = H >> 3, TX = W >> 3, PH = H >> 1, PW = W >> 1;
+  const int ntiles = p.B * TY * TX;
 
   for (int i = tid * 16; i < 2 * kWBuf; i += 512 * 16) *reinterpret_cast<u32x4*>(smem + i) = u32x4{0u, 0u, 0u, 0u};
 
@@ -297,33 +347,43 @@ __global__ void __launch_bounds__(512, 1) cifar_c3_dw_kernel(CifarC3BwdParams p)
   const int q4 = r16 >> 2, p4 = r16 & 3;
   const int xb = kWZT + wn * kWXPS + ((2 * (g >> 1) + (q4 >> 1)) * 10 + 4 * (g & 1) + (q4 & 1)) * 32 + 8 * p4;
 
-  // staging: threads 0..255 rebuild dZ^T (window w, chunk c: 8 channels x 4
-  // positions) and sum the bias; threads 256..511 stage X (two chunks each)
+  // staging: threads 0..255 rebuild dZ^T from the tile's 4 x 4 pooled windows
+  // (window w, chunk c: 8 channels x 4 positions) and sum the bias; threads
+  // 256..511 stage the 10 x 10 X halo (zero outside the image), 800 items
   const bool zthr = tid < 256;
   const int w = tid & 15, c = (tid >> 4) & 15;
   int zo[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) zo[j] = zt3(8 * c + j, 4 * w);
-  int xo[2];
+  int xo[4], xgo[4], xhy[4], xhx[4];
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
+  for (int i = 0; i < 4; ++i) {
     const int j = (tid & 255) + 256 * i, px = j >> 3, cc = j & 7;
-    xo[i] = kWZT + (cc >> 1) * kWXPS + (((px >> 3) + 1) * 10 + (px & 7) + 1) * 32 + 16 * (cc & 1);
+    xhy[i] = j < 800 ? px / 10 : -100;
+    xhx[i] = px % 10;
+    xo[i] = kWZT + (cc >> 1) * kWXPS + px * 32 + 16 * (cc & 1);
+    xgo[i] = ((px / 10) * W + px % 10) * 64 + 8 * cc;
   }
   const char* dyg = static_cast<const char*>(p.dy);
-  const char* xg = static_cast<const char*>(p.x);
-  u32x4 sv[2];
+  const bf16* xg = static_cast<const bf16*>(p.x);
+  u32x4 sv[4];
   uint32_t sa0 = 0u, sa1 = 0u;
-  auto load = [&](int img) {
+  auto load = [&](int t) {
+    const Tile3 q = tile_of(t, TY, TX);
     if (zthr) {
-      const size_t e = (size_t)img * kImgOut + w * 128 + 8 * c;
+      const size_t e = (((size_t)q.img * PH + q.ty * 4 + (w >> 2)) * PW + q.tx * 4 + (w & 3)) * 128 + 8 * c;
       sv[0] = *reinterpret_cast<const u32x4*>(dyg + 2 * e);
       const uint2 a = *reinterpret_cast<const uint2*>(p.arg + e);
       sa0 = a.x; sa1 = a.y;
     } else {
-      const u32x4* src = reinterpret_cast<const u32x4*>(xg + (size_t)img * (kImgIn * 2));
+      const int y0 = q.ty * 8 - 1, x0 = q.tx * 8 - 1;
+      const bf16* base = xg + ((size_t)q.img * H * W + (int64_t)y0 * W + x0) * 64;
 #pragma unroll
-      for (int i = 0; i < 2; ++i) sv[i] = src[(tid & 255) + 256 * i];
+      for (int i = 0; i < 4; ++i) {
+        const int y = y0 + xhy[i], x = x0 + xhx[i];
+        const bool in = xhy[i] >= 0 && y >= 0 && y < H && x >= 0 && x < W;
+        sv[i] = in ? *reinterpret_cast<const u32x4*>(base + xgo[i]) : u32x4{0u, 0u, 0u, 0u};
+      }
     }
   };
   float bsum[8];
@@ -336,10 +396,10 @@ __global__ void __launch_bounds__(512, 1) cifar_c3_dw_kernel(CifarC3BwdParams p)
 #pragma unroll
     for (int t = 0; t < 9; ++t) acc[ct][t] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  __syncthreads();  // zero fill before the first interior write
-  int img = blockIdx.x;
-  if (img < p.B) load(img);
-  for (int k = 0; img < p.B; img += grid, ++k) {
+  __syncthreads();  // zero fill before the first write
+  int t = blockIdx.x;
+  if (t < ntiles) load(t);
+  for (int k = 0; t < ntiles; t += grid, ++k) {
     char* tb = smem + (k & 1) * kWBuf;
     if (zthr) {
 #pragma unroll
@@ -354,10 +414,11 @@ __global__ void __launch_bounds__(512, 1) cifar_c3_dw_kernel(CifarC3BwdParams p)
       }
     } else {
 #pragma unroll
-      for (int i = 0; i < 2; ++i) *reinterpret_cast<u32x4*>(tb + xo[i]) = sv[i];
+      for (int i = 0; i < 4; ++i)
+        if (xhy[i] >= 0) *reinterpret_cast<u32x4*>(tb + xo[i]) = sv[i];
     }
-    __syncthreads();  // image k staged; buffer k & 1's previous readers (image k - 2) are done
-    if (img + grid < p.B) load(img + grid);
+    __syncthreads();  // tile k staged; buffer k & 1's previous readers (tile k - 2) are done
+    if (t + grid < ntiles) load(t + grid);
 
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
@@ -366,12 +427,12 @@ __global__ void __launch_bounds__(512, 1) cifar_c3_dw_kernel(CifarC3BwdParams p)
       for (int ct = 0; ct < 4; ++ct) a[ct] = *reinterpret_cast<const bf16x8*>(tb + za[ks][ct]);
       const bf16* xr = reinterpret_cast<const bf16*>(tb + xb);
 #pragma unroll
-      for (int t = 0; t < 9; ++t) {
-        const int off = ((4 * ks + t / 3) * 10 + t % 3) * 16;  // bf16 elements (32 B per pixel)
+      for (int tp = 0; tp < 9; ++tp) {
+        const int off = ((4 * ks + tp / 3) * 10 + tp % 3) * 16;  // bf16 elements (32 B per pixel)
         const bf16x4 lo = tr4(xr + off), hi = tr4(xr + off + 2 * 16);  // s = 0, 1: +2 px
         const bf16x8 bfr = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
 #pragma unroll
-        for (int ct = 0; ct < 4; ++ct) acc[ct][t] = mma(acc[ct][t], a[ct], bfr);
+        for (int ct = 0; ct < 4; ++ct) acc[ct][tp] = mma(acc[ct][tp], a[ct], bfr);
       }
     }
   }
@@ -380,10 +441,10 @@ __global__ void __launch_bounds__(512, 1) cifar_c3_dw_kernel(CifarC3BwdParams p)
 #pragma unroll
   for (int ct = 0; ct < 4; ++ct)
 #pragma unroll
-    for (int t = 0; t < 9; ++t)
+    for (int tp = 0; tp < 9; ++tp)
 #pragma unroll
       for (int i = 0; i < 4; ++i)
-        slab[(64 * wc + 16 * ct + 4 * g + i) * kDw3Cols + 64 * t + 16 * wn + r16] = acc[ct][t][i];
+        slab[(64 * wc + 16 * ct + 4 * g + i) * kDw3Cols + 64 * tp + 16 * wn + r16] = acc[ct][tp][i];
   // bias: the 16 lanes (windows) of a 16-lane group share channel chunk c
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
@@ -401,21 +462,28 @@ __global__ void __launch_bounds__(512, 1) cifar_c3_dw_kernel(CifarC3BwdParams p)
 }  // namespace
 
 bool cifar_c3_supported(int inC, int H, int W, int C, int KS, int stride, int pad, int act_relu, int pooled) {
-  return inC == 64 && H == 8 && W == 8 && C == 128 && KS == 3 && stride == 1 && pad == 1 && act_relu && pooled;
+  return inC == 64 && H % 8 == 0 && W % 8 == 0 && H > 0 && W > 0 && C == 128 && KS == 3 && stride == 1 && pad == 1 &&
+         act_relu && pooled;
+}
+static int c3_tiles(int B, int H, int W) {
+  MCC_CHECK(H > 0 && W > 0 && H % 8 == 0 && W % 8 == 0, "cifar_c3: H, W must be multiples of 8");
+  MCC_CHECK((int64_t)B * H * W * 128 < (1ll << 40) && (int64_t)B * (H / 8) * (W / 8) < (1ll << 31),
+            "cifar_c3: batch too large");
+  return B * (H / 8) * (W / 8);
 }
 
 void cifar_c3_forward(const CifarC3Params& p, hipStream_t s) {
   if (p.B <= 0) return;
   MCC_CHECK(p.x && p.w && p.bias && p.y && p.arg && p.ldw >= 576 && p.ldw % 8 == 0, "cifar_c3_forward: bad params");
-  MCC_CHECK((int64_t)p.B * kImgIn < (1ll << 31), "cifar_c3_forward: batch exceeds 32-bit offsets");
-  hipLaunchKernelGGL(cifar_c3_fwd_kernel, dim3(std::min(p.B, 2 * 256)), dim3(256), 0, s, p);
+  const int nt = c3_tiles(p.B, p.H, p.W);
+  hipLaunchKernelGGL(cifar_c3_fwd_kernel, dim3(std::min(nt, 2 * 256)), dim3(256), 0, s, p);
 }
 
 void cifar_c3_dx(const CifarC3BwdParams& p, hipStream_t s) {
   if (p.B <= 0) return;
   MCC_CHECK(p.dy && p.arg && p.wd && p.dx && p.ldw >= 1152 && p.ldw % 8 == 0, "cifar_c3_dx: bad params");
-  MCC_CHECK((int64_t)p.B * kImgIn < (1ll << 31), "cifar_c3_dx: batch exceeds 32-bit offsets");
-  hipLaunchKernelGGL(cifar_c3_dx_kernel, dim3(std::min(p.B, 2 * 256)), dim3(128), 0, s, p);
+  const int nt = c3_tiles(p.B, p.H, p.W);
+  hipLaunchKernelGGL(cifar_c3_dx_kernel, dim3(std::min(nt, 2 * 256)), dim3(128), 0, s, p);
 }
 
 size_t cifar_c3_dw_scratch_bytes() {
@@ -426,8 +494,7 @@ size_t cifar_c3_dw_scratch_bytes() {
 void cifar_c3_dw(const CifarC3BwdParams& p, float* gw, float* gb, hipStream_t s) {
   if (p.B <= 0) return;
   MCC_CHECK(p.dy && p.arg && p.x && p.slab && gw && gb, "cifar_c3_dw: bad params");
-  MCC_CHECK((int64_t)p.B * kImgIn < (1ll << 31), "cifar_c3_dw: batch exceeds 32-bit offsets");
-  const int grid = std::min(p.B, kDw3Grid);
+  const int grid = std::min(c3_tiles(p.B, p.H, p.W), kDw3Grid);
   hipLaunchKernelGGL(cifar_c3_dw_kernel, dim3(grid), dim3(512), 0, s, p);
   dw_slab_reduce(p.slab, grid, 128, kDw3Cols, p.slab + (size_t)kDw3Grid * 128 * kDw3Cols, 128, 64, 3, XL_C8, 64, 576,
                  gw, gb, s);

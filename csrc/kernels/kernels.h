@@ -741,6 +741,7 @@ struct CifarC2Params {
   const float* bias = nullptr;
   void* y = nullptr;
   uint8_t* arg = nullptr;
+  int H = 8, W = 8;  // cifar_c3: conv grid (multiples of 8; 8 x 8 output tiles)
 };
 bool cifar_c2_supported(int inC, int H, int W, int C, int KS, int stride, int pad, int act_relu, int pooled);
 void cifar_c2_forward(const CifarC2Params& p, hipStream_t s);
@@ -758,15 +759,17 @@ struct CifarC2BwdParams {
   int ldw = 0;
   void* dx = nullptr;
   float* slab = nullptr;     // dW: cifar_c2_dw_scratch_bytes()
+  int H = 8, W = 8;          // cifar_c3: conv grid (multiples of 8)
 };
 void cifar_c2_dx(const CifarC2BwdParams& p, hipStream_t s);
 size_t cifar_c2_dw_scratch_bytes();
 void cifar_c2_dw(const CifarC2BwdParams& p, float* gw, float* gb, hipStream_t s);
-// CIFAR-3conv conv3 (cifar_c3.hip): conv 64 -> 128, 3x3, pad 1 on 8x8 NHWC
-// bf16, ReLU + 2x2/2 max-pool; same parameter blocks.  x [B][8][8][64],
-// weights [128][ldw] with k = tap*64 + c (the implicit-GEMM packing), y / arg
-// [B][4][4][128]; wd [64][ldw] with k = tap*128 + co (flipped taps), dx
-// [B][8][8][64]; slab cifar_c3_dw_scratch_bytes().
+// conv 64 -> 128, 3x3, pad 1, ReLU + 2x2/2 max-pool on an H x W NHWC bf16 grid
+// (H, W multiples of 8: CIFAR-3conv conv3 at 8 x 8, VGG-11 conv2 at 112 x 112)
+// in 8 x 8 output tiles (cifar_c3.hip); same parameter blocks.  x
+// [B][H][W][64], weights [128][ldw] with k = tap*64 + c (the implicit-GEMM
+// packing), y / arg [B][H/2][W/2][128]; wd [64][ldw] with k = tap*128 + co
+// (flipped taps), dx [B][H][W][64]; slab cifar_c3_dw_scratch_bytes().
 using CifarC3Params = CifarC2Params;
 using CifarC3BwdParams = CifarC2BwdParams;
 bool cifar_c3_supported(int inC, int H, int W, int C, int KS, int stride, int pad, int act_relu, int pooled);

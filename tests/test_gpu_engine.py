@@ -543,6 +543,47 @@ def test_cifar_dedicated_kernels_match_generic(cuda, B, flag, marker, monkeypatc
             assert e < 1e-2, (L["kind"], L["C"], what, c, e)
 
 
+def _spec_step(cuda, spec, B, seed=7):
+    C, H, W = spec.input_shape()
+    imgs, labels = mcc.synth_dataset(B, C, H, W, spec.num_classes(), seed=seed)
+    params = mcc.init_params(spec, seed=seed).astype(np.float32)
+    net = mcc.GpuNet(spec, "bf16", B)
+    net.set_params(params)
+    d_img = torch.from_numpy(imgs).to(cuda)
+    d_lab = torch.from_numpy(labels).to(cuda)
+    s = torch.cuda.current_stream().cuda_stream
+    net.forward(d_img.data_ptr(), 0, B, s)
+    net.loss(d_lab.data_ptr(), 0, 1.0 / B, True, s)
+    net.backward_all(s)
+    torch.cuda.synchronize()
+    return net.plan(), net.get_logits(B), net.get_grads()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("hw,B", [(16, 37), (16, 600), (24, 50), (112, 2)])
+def test_c3k_tiled_grid_matches_igemm(cuda, hw, B, monkeypatch):
+    """The 64 -> 128 pooled conv kernels (cifar_c3.hip) on grids of several 8 x
+    8 output tiles -- halo staging across tile edges, zero halo at the image
+    border, tiles per image 4 / 9 / 196 (VGG-11 conv2's 112 x 112) -- vs the
+    implicit GEMM + grad_xform (MCC_AB=no_c3k), per output channel."""
+    spec = mcc.parse_model_spec(f"input 3 {2 * hw} {2 * hw}; conv 64 k3 s1 p1 relu; pool 2; "
+                                f"conv 128 k3 s1 p1 relu; pool 2; fc 10 softmax", f"tiles{hw}")
+    monkeypatch.setenv("MCC_AB", "")
+    plan, lg, g = _spec_step(cuda, spec, B)
+    assert "c3k[fwd dx dw]" in plan, plan
+    monkeypatch.setenv("MCC_AB", "no_c3k")
+    plan0, lg0, g0 = _spec_step(cuda, spec, B)
+    assert "c3k" not in plan0, plan0
+    assert _relerr(lg, lg0) < 2e-3
+    for L in spec.layers():
+        if L["nweights"] == 0:
+            continue
+        for off, n, what in ((L["w_off"], L["nweights"], "W"), (L["b_off"], L["nbiases"], "b")):
+            e, c = _per_channel_err(g[off : off + n], g0[off : off + n], L["C"],
+                                    floor_frac=0.3 if what == "b" else 1e-2)
+            assert e < 1e-2, (L["kind"], L["C"], what, c, e)
+
+
 _BIG_SPECS = {
     "big96": "input 3 96 96; conv 16 k3 s1 p1 relu; pool 2; conv 32 k3 s2 p1 relu; "
              "conv 32 k3 s1 p1 relu; pool 2; fc 64 relu; fc 10 softmax",
