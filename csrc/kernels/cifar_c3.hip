@@ -85,6 +85,9 @@ __device__ __forceinline__ Tile3 tile_of(int t, int TY, int TX) {
   return r;
 }
 
+// TILED = false: one 8 x 8 tile per image (CIFAR-3conv): the halo is the zero
+// padding, written once by the initial fill; only the 64 interior pixels are staged
+template <bool TILED>
 __global__ void __launch_bounds__(256, 2) cifar_c3_fwd_kernel(CifarC3Params p) {
   __shared__ __attribute__((aligned(16))) char smem[2 * kFBuf];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -112,25 +115,27 @@ __global__ void __launch_bounds__(256, 2) cifar_c3_fwd_kernel(CifarC3Params p) {
 
   // staging: the tile's 10 x 10 input halo (zero outside the image) as 800
   // 16-byte items j = tid + 256 i: halo pixel j >> 3, channel chunk j & 7
-  int soff[4], goff[4], shy[4], shx[4];
+  constexpr int NS = TILED ? 4 : 2;
+  int soff[NS], goff[NS], shy[NS], shx[NS];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int j = tid + 256 * i, px = j >> 3, c = j & 7;
-    shy[i] = j < 800 ? px / 10 : -100;  // (-100: no item)
-    shx[i] = px % 10;
-    soff[i] = (c >> 1) * kPS + poff(px / 10, px % 10) + 16 * (c & 1);
-    goff[i] = ((px / 10) * W + px % 10) * 64 + 8 * c;
+  for (int i = 0; i < NS; ++i) {
+    const int j = tid + 256 * i, c = j & 7;
+    const int px = j >> 3, hy = TILED ? px / 10 : (px >> 3) + 1, hx = TILED ? px % 10 : (px & 7) + 1;
+    shy[i] = !TILED || j < 800 ? hy : -100;  // (-100: no item)
+    shx[i] = hx;
+    soff[i] = (c >> 1) * kPS + poff(hy, hx) + 16 * (c & 1);
+    goff[i] = (hy * W + hx) * 64 + 8 * c;
   }
   const bf16* xg = static_cast<const bf16*>(p.x);
-  u32x4 st[4];
+  u32x4 st[NS];
   auto load = [&](int t) {
     const Tile3 q = tile_of(t, TY, TX);
     const int y0 = q.ty * 8 - 1, x0 = q.tx * 8 - 1;
     const bf16* base = xg + ((size_t)q.img * H * W + (int64_t)y0 * W + x0) * 64;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < NS; ++i) {
       const int y = y0 + shy[i], x = x0 + shx[i];
-      const bool in = shy[i] >= 0 && y >= 0 && y < H && x >= 0 && x < W;
+      const bool in = !TILED || (shy[i] >= 0 && y >= 0 && y < H && x >= 0 && x < W);
       st[i] = in ? *reinterpret_cast<const u32x4*>(base + goff[i]) : u32x4{0u, 0u, 0u, 0u};
     }
   };
@@ -140,7 +145,7 @@ __global__ void __launch_bounds__(256, 2) cifar_c3_fwd_kernel(CifarC3Params p) {
   for (int k = 0; t < ntiles; t += grid, ++k) {
     char* tb = smem + (k & 1) * kFBuf;
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < NS; ++i)
       if (shy[i] >= 0) *reinterpret_cast<u32x4*>(tb + soff[i]) = st[i];
     __syncthreads();  // tile k staged; every wave is past tile k - 1's reads of this buffer (k - 2)
     const Tile3 q = tile_of(t, TY, TX);
@@ -197,6 +202,7 @@ __global__ void __launch_bounds__(256, 2) cifar_c3_fwd_kernel(CifarC3Params p) {
 // ------------------------------------------------------------ data gradient
 constexpr int kXBuf = 8 * kPS;  // 30,976 B: dZ, eight 16-channel planes
 
+template <bool TILED>
 __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(1, 1)))
 cifar_c3_dx_kernel(CifarC3BwdParams p) {
   __shared__ __attribute__((aligned(16))) char smem[2 * kXBuf];
@@ -227,17 +233,20 @@ cifar_c3_dx_kernel(CifarC3BwdParams p) {
   // windows (tile windows -1 .. 4); item (window a, b; channel chunk c) for
   // j = tid + 128 i < 576, its in-halo positions as a 4-bit mask
   const char* dyg = static_cast<const char*>(p.dy);
-  int sbase[5], sgoff[5], swa[5], swb[5];
-  uint32_t smask[5];
+  // (TILED = false: the tile's 16 windows only, all four positions; the halo
+  // ring is the zero padding of the initial fill)
+  constexpr int NS = TILED ? 5 : 2;
+  int sbase[NS], sgoff[NS], swa[NS], swb[NS];
+  uint32_t smask[NS];
 #pragma unroll
-  for (int i = 0; i < 5; ++i) {
+  for (int i = 0; i < NS; ++i) {
     const int j = tid + 128 * i, wi = j >> 4, c = j & 15;
-    const int wa_ = wi / 6, wb_ = wi % 6;
+    const int wa_ = TILED ? wi / 6 : (wi >> 2) + 1, wb_ = TILED ? wi % 6 : (wi & 3) + 1;
     uint32_t m = 0;
 #pragma unroll
     for (int pos = 0; pos < 4; ++pos) {
       const int hy = 2 * wa_ + (pos >> 1) - 1, hx = 2 * wb_ + (pos & 1) - 1;
-      if (j < 576 && hy >= 0 && hy < 10 && hx >= 0 && hx < 10) m |= 1u << pos;
+      if ((!TILED || j < 576) && hy >= 0 && hy < 10 && hx >= 0 && hx < 10) m |= 1u << pos;
     }
     smask[i] = m;
     swa[i] = wa_;
@@ -245,16 +254,16 @@ cifar_c3_dx_kernel(CifarC3BwdParams p) {
     sbase[i] = (c >> 1) * kPS + (((2 * wa_ - 1) * kPit) + 2 * wb_ - 1) * 32 + 16 * (c & 1);  // (may be < 0: masked)
     sgoff[i] = ((wa_ - 1) * PW + (wb_ - 1)) * 128 + 8 * c;
   }
-  u32x4 sd[5];
-  uint32_t sa[5][2];
+  u32x4 sd[NS];
+  uint32_t sa[NS][2];
   auto load = [&](int t) {
     const Tile3 q = tile_of(t, TY, TX);
     const int wy0 = q.ty * 4, wx0 = q.tx * 4;
     const size_t base = ((size_t)q.img * PH + wy0) * PW + wx0;  // pooled pixel of tile window (0, 0)
 #pragma unroll
-    for (int i = 0; i < 5; ++i) {
+    for (int i = 0; i < NS; ++i) {
       const int wy = wy0 + swa[i] - 1, wx = wx0 + swb[i] - 1;
-      const bool in = smask[i] && wy >= 0 && wy < PH && wx >= 0 && wx < PW;
+      const bool in = !TILED || (smask[i] && wy >= 0 && wy < PH && wx >= 0 && wx < PW);
       const int64_t e = (int64_t)base * 128 + sgoff[i];
       sd[i] = in ? *reinterpret_cast<const u32x4*>(dyg + 2 * e) : u32x4{0u, 0u, 0u, 0u};
       uint2 av = {0u, 0u};
@@ -269,10 +278,10 @@ cifar_c3_dx_kernel(CifarC3BwdParams p) {
   for (int k = 0; t < ntiles; t += grid, ++k) {
     char* tb = smem + (k & 1) * kXBuf;
 #pragma unroll
-    for (int i = 0; i < 5; ++i)
+    for (int i = 0; i < NS; ++i)
 #pragma unroll
       for (int pos = 0; pos < 4; ++pos)
-        if (smask[i] & (1u << pos))
+        if (!TILED || (smask[i] & (1u << pos)))
           *reinterpret_cast<u32x4*>(tb + sbase[i] + poff(pos >> 1, pos & 1)) = unpool_pos3(sd[i], sa[i][0], sa[i][1], pos);
     __syncthreads();  // tile k staged; buffer k & 1's previous readers (tile k - 2) are done
     const Tile3 q = tile_of(t, TY, TX);
@@ -324,6 +333,7 @@ constexpr int kDw3Grid = 256;
 
 __device__ __forceinline__ int zt3(int co, int k) { return co * 128 + 16 * ((k >> 3) ^ ((co >> 1) & 7)) + 2 * (k & 7); }
 
+template <bool TILED>
 __global__ void __launch_bounds__(512, 1) cifar_c3_dw_kernel(CifarC3BwdParams p) {
   __shared__ __attribute__((aligned(16))) char smem[2 * kWBuf];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -355,18 +365,20 @@ __global__ void __launch_bounds__(512, 1) cifar_c3_dw_kernel(CifarC3BwdParams p)
   int zo[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) zo[j] = zt3(8 * c + j, 4 * w);
-  int xo[4], xgo[4], xhy[4], xhx[4];
+  constexpr int NX = TILED ? 4 : 2;  // (TILED = false: the 64 interior pixels; the halo is the zero fill)
+  int xo[NX], xgo[NX], xhy[NX], xhx[NX];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < NX; ++i) {
     const int j = (tid & 255) + 256 * i, px = j >> 3, cc = j & 7;
-    xhy[i] = j < 800 ? px / 10 : -100;
-    xhx[i] = px % 10;
-    xo[i] = kWZT + (cc >> 1) * kWXPS + px * 32 + 16 * (cc & 1);
-    xgo[i] = ((px / 10) * W + px % 10) * 64 + 8 * cc;
+    const int hy = TILED ? px / 10 : (px >> 3) + 1, hx = TILED ? px % 10 : (px & 7) + 1;
+    xhy[i] = !TILED || j < 800 ? hy : -100;
+    xhx[i] = hx;
+    xo[i] = kWZT + (cc >> 1) * kWXPS + (hy * 10 + hx) * 32 + 16 * (cc & 1);
+    xgo[i] = (hy * W + hx) * 64 + 8 * cc;
   }
   const char* dyg = static_cast<const char*>(p.dy);
   const bf16* xg = static_cast<const bf16*>(p.x);
-  u32x4 sv[4];
+  u32x4 sv[NX];
   uint32_t sa0 = 0u, sa1 = 0u;
   auto load = [&](int t) {
     const Tile3 q = tile_of(t, TY, TX);
@@ -379,9 +391,9 @@ __global__ void __launch_bounds__(512, 1) cifar_c3_dw_kernel(CifarC3BwdParams p)
       const int y0 = q.ty * 8 - 1, x0 = q.tx * 8 - 1;
       const bf16* base = xg + ((size_t)q.img * H * W + (int64_t)y0 * W + x0) * 64;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
+      for (int i = 0; i < NX; ++i) {
         const int y = y0 + xhy[i], x = x0 + xhx[i];
-        const bool in = xhy[i] >= 0 && y >= 0 && y < H && x >= 0 && x < W;
+        const bool in = !TILED || (xhy[i] >= 0 && y >= 0 && y < H && x >= 0 && x < W);
         sv[i] = in ? *reinterpret_cast<const u32x4*>(base + xgo[i]) : u32x4{0u, 0u, 0u, 0u};
       }
     }
@@ -414,7 +426,7 @@ __global__ void __launch_bounds__(512, 1) cifar_c3_dw_kernel(CifarC3BwdParams p)
       }
     } else {
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < NX; ++i)
         if (xhy[i] >= 0) *reinterpret_cast<u32x4*>(tb + xo[i]) = sv[i];
     }
     __syncthreads();  // tile k staged; buffer k & 1's previous readers (tile k - 2) are done
@@ -476,14 +488,16 @@ void cifar_c3_forward(const CifarC3Params& p, hipStream_t s) {
   if (p.B <= 0) return;
   MCC_CHECK(p.x && p.w && p.bias && p.y && p.arg && p.ldw >= 576 && p.ldw % 8 == 0, "cifar_c3_forward: bad params");
   const int nt = c3_tiles(p.B, p.H, p.W);
-  hipLaunchKernelGGL(cifar_c3_fwd_kernel, dim3(std::min(nt, 2 * 256)), dim3(256), 0, s, p);
+  if (p.H == 8 && p.W == 8) hipLaunchKernelGGL(cifar_c3_fwd_kernel<false>, dim3(std::min(nt, 2 * 256)), dim3(256), 0, s, p);
+  else hipLaunchKernelGGL(cifar_c3_fwd_kernel<true>, dim3(std::min(nt, 2 * 256)), dim3(256), 0, s, p);
 }
 
 void cifar_c3_dx(const CifarC3BwdParams& p, hipStream_t s) {
   if (p.B <= 0) return;
   MCC_CHECK(p.dy && p.arg && p.wd && p.dx && p.ldw >= 1152 && p.ldw % 8 == 0, "cifar_c3_dx: bad params");
   const int nt = c3_tiles(p.B, p.H, p.W);
-  hipLaunchKernelGGL(cifar_c3_dx_kernel, dim3(std::min(nt, 2 * 256)), dim3(128), 0, s, p);
+  if (p.H == 8 && p.W == 8) hipLaunchKernelGGL(cifar_c3_dx_kernel<false>, dim3(std::min(nt, 2 * 256)), dim3(128), 0, s, p);
+  else hipLaunchKernelGGL(cifar_c3_dx_kernel<true>, dim3(std::min(nt, 2 * 256)), dim3(128), 0, s, p);
 }
 
 size_t cifar_c3_dw_scratch_bytes() {
@@ -495,7 +509,8 @@ void cifar_c3_dw(const CifarC3BwdParams& p, float* gw, float* gb, hipStream_t s)
   if (p.B <= 0) return;
   MCC_CHECK(p.dy && p.arg && p.x && p.slab && gw && gb, "cifar_c3_dw: bad params");
   const int grid = std::min(c3_tiles(p.B, p.H, p.W), kDw3Grid);
-  hipLaunchKernelGGL(cifar_c3_dw_kernel, dim3(grid), dim3(512), 0, s, p);
+  if (p.H == 8 && p.W == 8) hipLaunchKernelGGL(cifar_c3_dw_kernel<false>, dim3(grid), dim3(512), 0, s, p);
+  else hipLaunchKernelGGL(cifar_c3_dw_kernel<true>, dim3(grid), dim3(512), 0, s, p);
   dw_slab_reduce(p.slab, grid, 128, kDw3Cols, p.slab + (size_t)kDw3Grid * 128 * kDw3Cols, 128, 64, 3, XL_C8, 64, 576,
                  gw, gb, s);
 }
