@@ -150,22 +150,25 @@ __device__ __forceinline__ void d_patch(const float* img, int TW, int py, int px
 // are then provably unclobbered by the output stores and become scalar loads;
 // waves_per_eu(4): four waves per SIMD)
 // wt: tap-major weights [Cin][KS*KS][COUT] (the engine's packed copy)
-template <int KS, int CIN, int COUT>
+// NIMG: images per staged group.  conv1 (196 windows per image) keeps 8; conv2
+// (25 windows per image) takes 10: 250 items for the 256 threads instead of
+// 200 (22 % of the lanes idle at 8), at 3 instead of 4 workgroups per CU (LDS).
+template <int KS, int CIN, int COUT, int NIMG = kDImgs>
 __global__ void __launch_bounds__(kDT) __attribute__((amdgpu_waves_per_eu(4))) conv_direct_fwd_kernel(Conv1DirectParams p, const float* __restrict__ wt,
                                                             const float* __restrict__ bias, float* __restrict__ out,
                                                             uint8_t* __restrict__ out_arg) {
   static_assert(COUT % 2 == 0, "channel pairs");
   constexpr int CP = COUT / 2;
   extern __shared__ __attribute__((aligned(16))) float xs[];
-  __shared__ int sidx[kDImgs];
+  __shared__ int sidx[NIMG];
   const Tile t = d_tile(p);
-  for (int i = threadIdx.x; i < kDImgs * t.IMG; i += kDT) xs[i] = 0.f;
+  for (int i = threadIdx.x; i < NIMG * t.IMG; i += kDT) xs[i] = 0.f;
   Stager sg;
   if constexpr (CIN == 1) sg.init(p, t);
   const int PHW = p.PH * p.PW;
-  const int ngroups = (p.N + kDImgs - 1) / kDImgs;
+  const int ngroups = (p.N + NIMG - 1) / NIMG;
   for (int grp = blockIdx.x; grp < ngroups; grp += gridDim.x) {
-    const int img0 = grp * kDImgs, nimg = min(kDImgs, p.N - img0);
+    const int img0 = grp * NIMG, nimg = min(NIMG, p.N - img0);
     d_index(p, sidx, img0, nimg);
     __syncthreads();  // previous group's reads done (and the zero fill, first time)
     if constexpr (CIN == 1) {
@@ -684,7 +687,10 @@ __global__ void __launch_bounds__(256) conv1_direct_dw_reduce_kernel(Conv1Direct
   }
 }
 
+constexpr int kDImgs2 = 10;  // conv2 forward (Cin > 1): images per group
+int fwd_imgs(const Conv1DirectParams& p) { return p.Cin == 1 ? kDImgs : kDImgs2; }
 size_t fwd_lds(const Conv1DirectParams& p) { return (size_t)kDImgs * d_tile(p).IMG * 4; }
+size_t fwd_lds_n(const Conv1DirectParams& p) { return (size_t)fwd_imgs(p) * d_tile(p).IMG * 4; }
 size_t dw_lds(const Conv1DirectParams& p) {
   return fwd_lds(p) + (size_t)kDImgs * p.PH * p.PW * p.C * 5;  // + dY floats + argmax bytes
 }
@@ -696,7 +702,7 @@ bool conv_direct_fwd_supported(const Conv1DirectParams& p) {
   const Tile t = d_tile(p);
   const bool stage_ok = p.Cin == 1 ? stager_fits(p, t) : (p.pad == 0 && t.TW == p.W && t.IMG % 4 == 0);
   return shape && stage_ok && p.OH % 2 == 0 && p.OW % 2 == 0 && p.OH == p.H + 2 * p.pad - p.KS + 1 &&
-         p.OW == p.W + 2 * p.pad - p.KS + 1 && p.PH == p.OH / 2 && p.PW == p.OW / 2 && fwd_lds(p) <= 64 * 1024;
+         p.OW == p.W + 2 * p.pad - p.KS + 1 && p.PH == p.OH / 2 && p.PW == p.OW / 2 && fwd_lds_n(p) <= 64 * 1024;
 }
 
 // dX geometry: p.H x p.W = the forward input (dX) grid, p.PH x p.PW = pooled dY
@@ -748,9 +754,14 @@ void conv_direct_forward(const Conv1DirectParams& p, hipStream_t s) {
                        p.out_arg);
   else if (p.H == 14 && p.W == 14 && p.pad == 0 && ab_flag("f32_mfma_fwd2"))
     lenet32_conv2_fwd(p, s);  // f32 MFMA (lenet_f32.hip; measured slower, opt-in)
-  else
+  else if (ab_flag("f32_fwd2_g8"))
     hipLaunchKernelGGL((conv_direct_fwd_kernel<5, 6, 16>), grid, block, fwd_lds(p), s, p, p.wt, p.bias, p.out,
                        p.out_arg);
+  else {
+    const int ng = (p.N + kDImgs2 - 1) / kDImgs2;
+    hipLaunchKernelGGL((conv_direct_fwd_kernel<5, 6, 16, kDImgs2>), dim3((unsigned)std::max(1, std::min(ng, 256 * 3))),
+                       block, fwd_lds_n(p), s, p, p.wt, p.bias, p.out, p.out_arg);
+  }
 }
 
 static void dw_reduce(const Conv1DirectParams& p, int grid, float* gw, float* gb, hipStream_t s) {
