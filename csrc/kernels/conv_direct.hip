@@ -150,9 +150,10 @@ __device__ __forceinline__ void d_patch(const float* img, int TW, int py, int px
 // are then provably unclobbered by the output stores and become scalar loads;
 // waves_per_eu(4): four waves per SIMD)
 // wt: tap-major weights [Cin][KS*KS][COUT] (the engine's packed copy)
-// NIMG: images per staged group.  conv1 (196 windows per image) keeps 8; conv2
-// (25 windows per image) takes 10: 250 items for the 256 threads instead of
-// 200 (22 % of the lanes idle at 8), at 3 instead of 4 workgroups per CU (LDS).
+// NIMG: images per staged group, chosen so the group's (image, window) items
+// fill the 256 threads' last round: conv2 (25 windows per image) 10 -> 250
+// items (at 8: 200, 22 % of the lanes idle; 3 instead of 4 workgroups per CU
+// for the LDS); conv1 (196 per image) 9 -> 1,764 = 6.9 rounds (at 8: 6.1).
 template <int KS, int CIN, int COUT, int NIMG = kDImgs>
 __global__ void __launch_bounds__(kDT) __attribute__((amdgpu_waves_per_eu(4))) conv_direct_fwd_kernel(Conv1DirectParams p, const float* __restrict__ wt,
                                                             const float* __restrict__ bias, float* __restrict__ out,
@@ -163,7 +164,7 @@ __global__ void __launch_bounds__(kDT) __attribute__((amdgpu_waves_per_eu(4))) c
   __shared__ int sidx[NIMG];
   const Tile t = d_tile(p);
   for (int i = threadIdx.x; i < NIMG * t.IMG; i += kDT) xs[i] = 0.f;
-  Stager sg;
+  StagerT<kDT, NIMG> sg;
   if constexpr (CIN == 1) sg.init(p, t);
   const int PHW = p.PH * p.PW;
   const int ngroups = (p.N + NIMG - 1) / NIMG;
@@ -688,7 +689,8 @@ __global__ void __launch_bounds__(256) conv1_direct_dw_reduce_kernel(Conv1Direct
 }
 
 constexpr int kDImgs2 = 10;  // conv2 forward (Cin > 1): images per group
-int fwd_imgs(const Conv1DirectParams& p) { return p.Cin == 1 ? kDImgs : kDImgs2; }
+constexpr int kDImgs1 = 9;   // conv1 forward (Cin == 1)
+int fwd_imgs(const Conv1DirectParams& p) { return p.Cin == 1 ? kDImgs1 : kDImgs2; }
 size_t fwd_lds(const Conv1DirectParams& p) { return (size_t)kDImgs * d_tile(p).IMG * 4; }
 size_t fwd_lds_n(const Conv1DirectParams& p) { return (size_t)fwd_imgs(p) * d_tile(p).IMG * 4; }
 size_t dw_lds(const Conv1DirectParams& p) {
@@ -749,9 +751,16 @@ void conv_direct_forward(const Conv1DirectParams& p, hipStream_t s) {
   MCC_CHECK(conv_direct_fwd_supported(p) && (p.x || p.xf) && p.wt && p.bias && p.out && p.out_arg,
             "conv_direct_forward: bad params");
   const dim3 grid((unsigned)direct_grid(p)), block(kDT);
-  if (p.Cin == 1)
+  if (p.Cin == 1 && ab_flag("f32_fwd1_g8"))
     hipLaunchKernelGGL((conv_direct_fwd_kernel<5, 1, 6>), grid, block, fwd_lds(p), s, p, p.wt, p.bias, p.out,
                        p.out_arg);
+  else if (p.Cin == 1) {
+    const Tile t = d_tile(p);  // the stager's packed item fields with 9 images
+    MCC_CHECK(kDImgs1 * t.IMG <= 16384 && kDImgs1 * p.H * (p.W / 4) <= kDU8Items * kDT, "conv_direct_forward: tile");
+    const int ng = (p.N + kDImgs1 - 1) / kDImgs1;
+    hipLaunchKernelGGL((conv_direct_fwd_kernel<5, 1, 6, kDImgs1>), dim3((unsigned)std::max(1, std::min(ng, 256 * 4))),
+                       block, fwd_lds_n(p), s, p, p.wt, p.bias, p.out, p.out_arg);
+  }
   else if (p.H == 14 && p.W == 14 && p.pad == 0 && ab_flag("f32_mfma_fwd2"))
     lenet32_conv2_fwd(p, s);  // f32 MFMA (lenet_f32.hip; measured slower, opt-in)
   else if (ab_flag("f32_fwd2_g8"))
