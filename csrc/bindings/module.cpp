@@ -623,6 +623,23 @@ PYBIND11_MODULE(_C, m) {
       py::arg("M"), py::arg("N"), py::arg("K"), py::arg("A"), py::arg("lda"), py::arg("W"), py::arg("ldw"),
       py::arg("bias"), py::arg("act"), py::arg("out"), py::arg("ldo"), py::arg("stream") = 0, py::arg("f32") = false);
   k.def(
+      "fc_wres",
+      [](int M, int N, int K, uintptr_t A, int lda, uintptr_t W, int ldw, int act, uintptr_t aux, int ldaux,
+         uintptr_t out, int ldo, uintptr_t s, bool f32) {
+        gpu::FcTallParams p;
+        p.M = M; p.N = N; p.K = K; p.f32 = f32;
+        p.A = reinterpret_cast<const void*>(A); p.lda = lda;
+        p.W = reinterpret_cast<const void*>(W); p.ldw = ldw;
+        p.act = act;
+        p.out = reinterpret_cast<void*>(out); p.ldo = ldo;
+        gpu::fc_wres(p, reinterpret_cast<const void*>(aux), ldaux, stream_of(s));
+      },
+      py::arg("M"), py::arg("N"), py::arg("K"), py::arg("A"), py::arg("lda"), py::arg("W"), py::arg("ldw"),
+      py::arg("act"), py::arg("aux"), py::arg("ldaux"), py::arg("out"), py::arg("ldo"), py::arg("stream") = 0,
+      py::arg("f32") = false);
+  k.def("fc_wres_supported", &gpu::fc_wres_supported, py::arg("f32"), py::arg("M"), py::arg("N"), py::arg("K"),
+        py::arg("act"));
+  k.def(
       "cu_hold", [](int nwg, int lds_bytes, double usec, uintptr_t s) { gpu::cu_hold(nwg, lds_bytes, usec, stream_of(s)); },
       py::arg("nwg"), py::arg("lds_bytes"), py::arg("usec"), py::arg("stream") = 0);
   k.attr("EPI_BIAS_ACT") = (int)gpu::EPI_BIAS_ACT;

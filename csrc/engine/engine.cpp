@@ -78,6 +78,10 @@ struct GpuNet::Stage {
   // ... narrow enough (Nout <= 224) for one tile row of the tall-skinny FC
   // kernel (fc_tall.hip: ref FC1 1568 -> 200), forward / data gradient
   bool fc_tall = false, fc_tall_dx = false;
+  // ... short reduction (K <= 224): the data gradient on the W-resident
+  // kernel (fc_wres.hip), x act' of an FC predecessor (wres_act)
+  bool fc_wres = false;
+  int wres_act = 0;
   void* conv_buf = nullptr;      // pre-pool conv output (big + pooled)
   void* dz_buf = nullptr;        // pre-activation gradient at conv-output size (big)
   // persistent pipelined kernels (bf16 small-image layers; geometry planned
@@ -411,6 +415,14 @@ void GpuNet::build() {
       st.fc_tall = true;
       st.fc_tall_dx = (pv->kind == Stage::CONV || pv->act == gpu::ACT_NONE) &&
                       gpu::fc_tall_supported(max_batch_, st.Kin, st.Nout);
+    }
+    // FC data gradient with W resident in LDS (ref FC1 / FC2, LeNet-5 fp32 FC1 /
+    // FC2): the W^T copy [Kin][out_ld] as a per-workgroup column slab
+    if (st.kind == Stage::FC && s > 0 && !st.fc_big && max_batch_ >= 8192 && !ab_flag("no_wres") &&
+        (dtype_ == DType::F32 || dtype_ == DType::BF16) && st.out_ld % 8 == 0 && st.in_ld % 8 == 0) {
+      const Stage* pv = stages_[s - 1];
+      st.wres_act = pv->kind == Stage::FC ? pv->act : gpu::ACT_NONE;
+      st.fc_wres = gpu::fc_wres_supported(dtype_ == DType::F32, max_batch_, st.Kin, st.Nout, st.wres_act);
     }
     st.head = st.kind == Stage::FC && st.last && s > 0 && !(dtype_ == DType::F32 && ab_flag("no_head32")) &&
               gpu::xent_head_supported(st.Nout, st.Kin, st.in_ld);
@@ -797,9 +809,9 @@ std::string GpuNet::plan() const {
     } else {
       os << "  [" << s << "] fc " << st.Kin << " -> " << st.Nout << (st.last ? " (logits)" : "")
          << (st.permC ? " nhwc-flatten" : "")
-         << (st.fc_tall ? (st.fc_tall_dx ? " tall[fwd dx]" : " tall[fwd]")
+         << (st.fc_tall ? (st.fc_tall_dx && !st.fc_wres ? " tall[fwd dx]" : " tall[fwd]")
                         : st.fc_ig ? (st.fc_igdx ? " igemm[fwd dx]" : " igemm[fwd]") : "")
-         << (st.head ? " head[softmax-CE fused]" : "") << "\n";
+         << (st.fc_wres ? " wres[dx]" : "") << (st.head ? " head[softmax-CE fused]" : "") << "\n";
     }
   }
   return os.str();
@@ -1483,7 +1495,15 @@ void GpuNet::backward(int hi, int lo, hipStream_t s) {
       gpu::dw_reduce(r, ws);
       }
       // data gradient
-      if (si > 0 && st.fc_tall_dx) {
+      if (si > 0 && st.fc_wres) {
+        gpu::FcTallParams t;
+        t.M = B; t.N = st.Kin; t.K = st.Nout; t.f32 = dtype_ == DType::F32;
+        t.A = st.grad_buf; t.lda = st.out_ld;
+        t.W = static_cast<const char*>(packed_) + es * st.pk_dx; t.ldw = st.out_ld;  // W^T [Kin][out_ld]
+        t.act = st.wres_act;  // x act'(pv output); a conv predecessor's staging applies its own mask
+        t.out = pv.grad_buf; t.ldo = st.in_ld;
+        gpu::fc_wres(t, pv.act_buf, st.in_ld, s);
+      } else if (si > 0 && st.fc_tall_dx) {
         gpu::FcTallParams t;
         t.M = B; t.N = st.Kin; t.K = st.Nout; t.f32 = dtype_ == DType::F32;
         t.A = st.grad_buf; t.lda = st.out_ld;

@@ -566,6 +566,11 @@ struct FcTallParams {
 };
 bool fc_tall_supported(int M, int N, int K);
 void fc_tall(const FcTallParams& p, hipStream_t s);
+// FC data gradient with W resident in LDS (fc_wres.hip): out = (A W^T) x act'(aux)
+// for a short reduction (K <= 224 bf16 / 208 fp32); p.bias unused, p.act = the
+// previous layer's activation whose gradient multiplies the result (aux = its output)
+bool fc_wres_supported(bool f32, int M, int N, int K, int act);
+void fc_wres(const FcTallParams& p, const void* aux, int ldaux, hipStream_t s);
 
 // fp32 FC weight gradient for skinny outputs (fc_dw32.hip): split-K partials
 // part[s][m][ldp] of dW[m][n] = sum_k dz[k][m] x[k][n] (m < M <= 208, n < N)

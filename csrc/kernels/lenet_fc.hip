@@ -455,7 +455,9 @@ __global__ void __launch_bounds__(kThreads, 1) lenet_fc_kernel(LenetFcParams P) 
     // every wave is done with the input tile: the next one streams into LDS
     // while the data gradient below runs
     __syncthreads();
+#ifndef MCC_FC_ABL_NOLOAD  // timing ablation (tools/build_variant.sh): reuse the first tile's input
     if (t + (int)gridDim.x < ntiles) load_tile(t + gridDim.x);
+#endif
     {      // data gradient: unit (k-tile b, image tile mt); wave w takes b = w,
       // w + 8, w + 16 of both image tiles and b = 24 of image tile w (w < 2)
       int wrow[8];  // W1 LDS rows of this lane's transposed reads, chunk c, half h

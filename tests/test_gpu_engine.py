@@ -329,13 +329,14 @@ def test_bench_batch_step_matches_small_batches(cuda):
 @pytest.mark.gpu
 @pytest.mark.parametrize(
     "model,B,b,fc_plan,dtype",
-    [("cifar3", 65024 + 37, 1024, "igemm[fwd dx]", "bf16"), ("ref", 163840 + 37, 2048, "tall[fwd dx]", "bf16"),
-     ("ref", 163840 + 37, 4096, "tall[fwd dx]", "fp32"), ("lenet5", 163840 + 37, 4096, "tall[fwd dx]", "fp32")],
+    [("cifar3", 65024 + 37, 1024, "igemm[fwd dx]", "bf16"), ("ref", 163840 + 37, 2048, "tall[fwd] wres[dx]", "bf16"),
+     ("ref", 163840 + 37, 4096, "tall[fwd] wres[dx]", "fp32"), ("lenet5", 163840 + 37, 4096, "tall[fwd] wres[dx]", "fp32")],
 )
 def test_fc_igemm_bench_batch_matches_small_batches(cuda, model, B, b, fc_plan, dtype):
     """CIFAR-3conv, the reference model and fp32 LeNet-5 at bench.py's per-GPU
     batches (+ a ragged tail): the wide FC1 (2048 -> 256: 1x1 implicit GEMM;
-    1568 -> 200 and fp32 400 -> 120: the tall-skinny FC kernel) runs on those
+    1568 -> 200 and fp32 400 -> 120: the tall-skinny FC kernel; their data
+    gradients and the FC2 ones on the W-resident kernel) runs on those
     paths there (batch >= 8192) and on the tiled GEMM in small chunks, and the
     fused conv blocks' persistent loops run at full size; logits and every
     layer's summed gradient must agree (the chunked path is pinned to PyTorch
@@ -358,7 +359,7 @@ def test_fc_igemm_bench_batch_matches_small_batches(cuda, model, B, b, fc_plan, 
     logits, grads = big.get_logits(B), big.get_grads()
     del big
     small = mcc.GpuNet(spec, dtype, b)
-    assert "igemm[fwd" not in small.plan() and "tall[fwd" not in small.plan()
+    assert "igemm[fwd" not in small.plan() and "tall[fwd" not in small.plan() and "wres" not in small.plan()
     small.set_params(params)
     ref_logits = np.empty_like(logits)
     ref_grads = np.zeros_like(grads, dtype=np.float64)

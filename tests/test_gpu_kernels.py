@@ -212,6 +212,52 @@ def test_fc_tall_kernel(cuda, M, N, K, act, dtype):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("dtype,M,N,K,act", [
+    ("bf16", 4096 + 37, 1568, 200, "none"),   # ref FC1 data gradient (7 column slabs)
+    ("bf16", 1000, 200, 200, "tanh"),         # ref FC2 data gradient x tanh'
+    ("bf16", 3, 1568, 200, "none"),           # fewer rows than one block
+    ("fp32", 2048 + 11, 1568, 200, "none"),   # ref fp32 FC1 (14 slabs of 112)
+    ("fp32", 777, 200, 200, "tanh"),
+    ("fp32", 4096 + 5, 400, 120, "none"),     # LeNet-5 fp32 FC1 data gradient (208 + 192)
+    ("fp32", 1000, 120, 84, "relu"),          # LeNet-5 fp32 FC2 data gradient x ReLU'
+])
+def test_fc_wres_kernel(cuda, dtype, M, N, K, act):
+    """fc_wres.hip (FC data gradient, W resident in LDS): out = (A W^T) x
+    act'(aux) against an fp64 product; ragged rows, K tails inside the last
+    64-byte k-step (K = 200 bf16 / 84 fp32), a partial last column slab, the
+    aux epilogue.  The padding columns of A and W hold NaN: the kernel must
+    never read them (its k tail uses clamped in-row addresses)."""
+    g = torch.Generator().manual_seed(M + N + K)
+    t = TDT[dtype]
+    f32 = dtype == "fp32"
+    code = {"none": K_.ACT_NONE, "relu": K_.ACT_RELU, "tanh": K_.ACT_TANH}[act]
+    assert K_.fc_wres_supported(f32, M, N, K, code)
+    lda, ldw, ldo = K + 8, K + 8, N + 8
+    a = torch.full((M, lda), float("nan"), dtype=t)
+    a[:, :K] = torch.randn(M, K, generator=g).to(t)
+    a = a.to(cuda)
+    w = torch.full((N, ldw), float("nan"), dtype=t)
+    w[:, :K] = (torch.randn(N, K, generator=g) / K**0.5).to(t)
+    w = w.to(cuda)
+    y = torch.randn(M, N, generator=g)
+    y = (torch.relu(y) if act == "relu" else torch.tanh(y)).to(t).to(cuda)
+    out = torch.full((M, ldo), 7.0, dtype=t, device=cuda)
+    K_.fc_wres(M, N, K, a.data_ptr(), lda, w.data_ptr(), ldw, code, y.data_ptr(), N, out.data_ptr(), ldo, _s(), f32=f32)
+    torch.cuda.synchronize()
+    ref = a[:, :K].double() @ w[:, :K].double().t()
+    if act == "relu":
+        ref = ref * (y.double() > 0)
+    elif act == "tanh":
+        ref = ref * (1 - y.double() ** 2)
+    o = out[:, :N].double()
+    assert bool(torch.isfinite(o).all())
+    err = float((o - ref).norm() / ref.norm())
+    assert err < (1e-6 if f32 else 1e-2), err
+    assert float((o - ref).abs().max()) < (1e-5 if f32 else 0.05) * float(ref.abs().max())
+    assert bool((out[:, N:] == 7.0).all())  # nothing written past N
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("M", [640, 768, 896, 2])
 def test_fc1_splitk_forward_vgg_shape(cuda, M):
     """VGG-11 FC1 (25,088 -> 4,096, bias + ReLU) on the engine's long-K
