@@ -45,6 +45,9 @@ typedef __attribute__((address_space(3))) void lvoid;
 
 constexpr int kTT = 512;                 // threads (8 waves)
 constexpr int kTM = 128;                 // batch rows per tile
+#ifndef MCC_TALL_NS
+#define MCC_TALL_NS 4  // ring depth of the bf16 224-column forward (one workgroup per CU)
+#endif
 constexpr int kTNS = 3;                  // ring depth: 2 stages in flight (bf16 forward: 4, see fc_tall)
 constexpr int kTXBytes = kTM * 64;
 // NF fragments per wave column: tile width TN = 32 NF output columns (7: 224
@@ -94,7 +97,11 @@ __global__ void __launch_bounds__(kTT, NS == 3 ? 2 : 1) fc_tall_kernel(FcTallPar
     const int seg = (lane & 3) ^ tswz(row);
     sk[i] = seg * EPS;
     if (i == 0) {
+#ifdef MCC_TALL_BLOCKED  // timing probe: A read as [M/128][K/EPR][128][EPR] blocks (values meaningless)
+      src[i] = static_cast<const T*>(p.A) + (size_t)m0 * p.lda + row * EPR + seg * EPS;
+#else
       src[i] = static_cast<const T*>(p.A) + (size_t)min(m0 + row, p.M - 1) * p.lda + seg * EPS;
+#endif
     } else {
       const int n = n0 + row;
       src[i] = (row < kTN && n < p.N) ? static_cast<const T*>(p.W) + (size_t)n * p.ldw + seg * EPS : nullptr;
@@ -106,7 +113,11 @@ __global__ void __launch_bounds__(kTT, NS == 3 ? 2 : 1) fc_tall_kernel(FcTallPar
     const int k0 = kt * EPR;
 #pragma unroll
     for (int i = 0; i < DM; ++i) {
+#ifdef MCC_TALL_BLOCKED
+      const T* s = (src[i] && k0 + sk[i] < p.K) ? src[i] + (i == 0 ? (size_t)kt * kTM * EPR : (size_t)k0) : zero;
+#else
       const T* s = (src[i] && k0 + sk[i] < p.K) ? src[i] + k0 : zero;
+#endif
       char* d = i == 0 ? dst + wave * 1024 : dst + kTXBytes + (wave + 8 * (i - 1)) * 1024;
       __builtin_amdgcn_global_load_lds((gvoid*)s, (lvoid*)d, 16, 0, 0);
     }
@@ -126,8 +137,10 @@ __global__ void __launch_bounds__(kTT, NS == 3 ? 2 : 1) fc_tall_kernel(FcTallPar
     // s_barrier: __syncthreads() would drain vmcnt) makes every wave's pieces
     // visible and frees the slot read in iteration kt - 1
     constexpr int VM = (NS - 2) * DM;
-    static_assert(VM == 2 || VM == 3 || VM == 6, "the s_waitcnt below");
-    if constexpr (VM == 6) asm volatile("s_waitcnt vmcnt(6)\n\ts_barrier" ::: "memory");
+    static_assert(VM == 2 || VM == 3 || VM == 6 || VM == 9 || VM == 12, "the s_waitcnt below");
+    if constexpr (VM == 12) asm volatile("s_waitcnt vmcnt(12)\n\ts_barrier" ::: "memory");
+    else if constexpr (VM == 9) asm volatile("s_waitcnt vmcnt(9)\n\ts_barrier" ::: "memory");
+    else if constexpr (VM == 6) asm volatile("s_waitcnt vmcnt(6)\n\ts_barrier" ::: "memory");
     else if constexpr (VM == 3) asm volatile("s_waitcnt vmcnt(3)\n\ts_barrier" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(2)\n\ts_barrier" ::: "memory");
     stage(kt + NS - 1);
@@ -221,7 +234,7 @@ void fc_tall(const FcTallParams& p, hipStream_t s) {
     using T = decltype(t);
     constexpr int NF = decltype(nf)::value;
     using Gm = TallGeom<NF>;
-    using G4 = TallGeom<NF, 4>;
+    using G4 = TallGeom<NF, MCC_TALL_NS>;
     constexpr bool kDeep = sizeof(T) == 2 && NF == 7;
     const int tiles = ((p.M + kTM - 1) / kTM) * ((p.N + Gm::TN - 1) / Gm::TN);
     const dim3 grid((unsigned)tiles), block(kTT);
@@ -230,9 +243,9 @@ void fc_tall(const FcTallParams& p, hipStream_t s) {
       return;
     }
     if constexpr (kDeep) {
-      if (p.act == ACT_TANH) hipLaunchKernelGGL((fc_tall_kernel<T, NF, ACT_TANH, true, 4>), grid, block, G4::LDS, s, p);
-      else if (p.act == ACT_RELU) hipLaunchKernelGGL((fc_tall_kernel<T, NF, ACT_RELU, true, 4>), grid, block, G4::LDS, s, p);
-      else hipLaunchKernelGGL((fc_tall_kernel<T, NF, ACT_NONE, true, 4>), grid, block, G4::LDS, s, p);
+      if (p.act == ACT_TANH) hipLaunchKernelGGL((fc_tall_kernel<T, NF, ACT_TANH, true, MCC_TALL_NS>), grid, block, G4::LDS, s, p);
+      else if (p.act == ACT_RELU) hipLaunchKernelGGL((fc_tall_kernel<T, NF, ACT_RELU, true, MCC_TALL_NS>), grid, block, G4::LDS, s, p);
+      else hipLaunchKernelGGL((fc_tall_kernel<T, NF, ACT_NONE, true, MCC_TALL_NS>), grid, block, G4::LDS, s, p);
       return;
     }
     if (p.act == ACT_TANH) hipLaunchKernelGGL((fc_tall_kernel<T, NF, ACT_TANH, true, 3>), grid, block, Gm::LDS, s, p);

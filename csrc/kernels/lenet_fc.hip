@@ -59,16 +59,16 @@ constexpr int SW1 = 800, SW2 = 240, SW3 = 224, SY = 800, SH1 = 288, SH2 = 224, S
 constexpr int OW1 = 0;                   // W1 [120][400]
 constexpr int OW2 = OW1 + N1 * SW1;      // W2 [84][120]
 constexpr int OW3 = OW2 + N2 * SW2;      // W3 [10][96] (cols 84..95 zero)
-constexpr int OY = OW3 + N3 * SW3;       // FC input tile [32][400]
-constexpr int OH1 = OY + TM * SY;        // H1 [32][128] (cols 120..127 zero), later dH1
+constexpr int OH1 = OW3 + N3 * SW3;      // H1 [32][128] (cols 120..127 zero), later dH1 (the FC input tile
+                                         // [32][400]: its own LDS object, ysm)
 constexpr int OH2 = OH1 + TM * SH1;      // H2 [32][96] (cols 84..95 zero), later dH2
 constexpr int OE = OH2 + TM * SH2;       // E = dlogits [32][16] (cols 10..15 zero)
 constexpr int OLAB = OE + TM * SE;       // labels of the tile (int)
 constexpr int ORED = OLAB + TM * 4;      // statistics of the 8 waves
 constexpr int OBIAS = ORED + 3 * 8 * 4;  // fp32 biases b1 [128] b2 [128] b3 [16] (zero padded)
 constexpr int kLds = OBIAS + (128 + 128 + 16) * 4;
-static_assert(kLds <= 163840, "lenet_fc: LDS budget");
-static_assert(OW2 % 16 == 0 && OW3 % 16 == 0 && OY % 16 == 0 && OH1 % 16 == 0 && OH2 % 16 == 0 && OE % 16 == 0,
+static_assert(kLds + TM * SY <= 163840, "lenet_fc: LDS budget");
+static_assert(OW2 % 16 == 0 && OW3 % 16 == 0 && OH1 % 16 == 0 && OH2 % 16 == 0 && OE % 16 == 0,
               "16-byte aligned LDS buffers");
 
 // canonical slab layout = the flat parameter range of the three FC layers
@@ -86,6 +86,13 @@ __device__ __forceinline__ int pw1(int n) {
   n = n >= N1 ? n - 8 : n;
   return n < 112 ? pa(n) : n;
 }
+
+// workgroup barrier for LDS hand-offs only: __syncthreads() also drains
+// vmcnt (its release fence) -- the logits / prediction stores; the phases
+// exchange nothing through global memory.  (An L2 warm-up DMA of the next
+// input tile issued at P4, one 4-byte load per line, measured neutral:
+// 140.6 / 142.2 vs 144.4 / 140.1 us, and dropped.)
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 __device__ __forceinline__ bf16x8 ld128(const char* p) { return *reinterpret_cast<const bf16x8*>(p); }
 __device__ __forceinline__ bf16x4 ld64(const char* p) { return *reinterpret_cast<const bf16x4*>(p); }
@@ -137,7 +144,11 @@ __device__ __forceinline__ void argmax4lanes(float& mx, int& am) {
 }
 
 __global__ void __launch_bounds__(kThreads, 1) lenet_fc_kernel(LenetFcParams P) {
+  // the input tile is its own LDS object: the compiler then knows the
+  // tile's DMA cannot alias the other buffers and does not drain it
+  // (s_waitcnt vmcnt(0)) in front of the data gradient's LDS reads
   __shared__ __attribute__((aligned(16))) char smem[kLds];
+  __shared__ __attribute__((aligned(16))) char ysm[TM * SY];
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave index in an SGPR: w-derived addresses are scalar
   const int r = lane & 15, g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
@@ -197,18 +208,22 @@ __global__ void __launch_bounds__(kThreads, 1) lenet_fc_kernel(LenetFcParams P) 
   // data gradient runs (P6b); the label of the tile's row tid rides along in
   // a register. ----
   const char* ybase = static_cast<const char*>(P.y);
-  int labpre = 0;
+  // the tile's dataset rows ride along with the DMA; the labels behind them
+  // (a dependent load) are fetched at the top of the tile and land in LDS
+  // after P1: a dependent load here would put an s_waitcnt vmcnt(0) -- the
+  // whole DMA -- right behind the DMA issue
+  int labrow = 0, labpre = 0;
   auto load_tile = [&](int t) {
     const int row0 = t * TM;
     for (int k = tid; k < TM * 50; k += kThreads) {
       const int prow = k / 50, j = k - 50 * (k / 50);
       const char* src = ybase + (size_t)min(row0 + pa(prow), B - 1) * P.ldy * 2 + 16 * j;
       // wave-uniform LDS base of this 64-lane piece; lane l lands at + 16 l
-      __builtin_amdgcn_global_load_lds((gvoid*)src, (lvoid*)(smem + OY + 16 * (k - lane)), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((gvoid*)src, (lvoid*)(ysm + 16 * (k - lane)), 16, 0, 0);
     }
     if (tid < TM) {
       const int gr = min(row0 + tid, B - 1);
-      labpre = P.labels[P.idx ? P.idx[gr] : gr];
+      labrow = P.idx ? P.idx[gr] : gr;
     }
   };
 
@@ -233,7 +248,7 @@ __global__ void __launch_bounds__(kThreads, 1) lenet_fc_kernel(LenetFcParams P) 
     // this wave's input-tile DMAs (and last tile's gradient stores) are done;
     // the barrier makes every wave's pieces visible
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (tid < TM) reinterpret_cast<int*>(smem + OLAB)[tid] = labpre;
+    if (tid < TM) labpre = P.labels[labrow];
     __syncthreads();
 
     // ---- P1: H1^T = relu(W1 Y^T + b1), wave w: features 16w .. 16w+15 ----
@@ -241,8 +256,8 @@ __global__ void __launch_bounds__(kThreads, 1) lenet_fc_kernel(LenetFcParams P) 
     {
       f32x4 acc0 = bias[4 * w + g], acc1 = acc0;
       const char* aw = smem + OW1 + pw1(16 * w + r) * SW1;
-      const char* y0 = smem + OY + rm0 * SY;
-      const char* y1 = smem + OY + rm1 * SY;
+      const char* y0 = ysm + rm0 * SY;
+      const char* y1 = ysm + rm1 * SY;
       // operands of chunk c + 2 are read while chunk c multiplies (a ring of
       // three: the compiler would otherwise hoist all 36 reads -- 144
       // registers on top of the 140 accumulator registers)
@@ -285,7 +300,8 @@ __global__ void __launch_bounds__(kThreads, 1) lenet_fc_kernel(LenetFcParams P) 
             pack4(h[0], h[1], h[2], h[3]);
       }
     }
-    __syncthreads();
+    if (tid < TM) reinterpret_cast<int*>(smem + OLAB)[tid] = labpre;  // read in P3, two barriers on
+    lds_barrier();
 
     // ---- P2: H2^T = relu(W2 H1^T + b2), waves 0..5 ----
     if (w < 6) {
@@ -317,7 +333,7 @@ __global__ void __launch_bounds__(kThreads, 1) lenet_fc_kernel(LenetFcParams P) 
             pack4(h[0], h[1], h[2], h[3]);
       }
     }
-    __syncthreads();
+    lds_barrier();
 
     // ---- P3: logits^T = W3 H2^T + b3 and softmax-CE, wave mt = m-tile ----
     if (w < 2) {
@@ -376,7 +392,7 @@ __global__ void __launch_bounds__(kThreads, 1) lenet_fc_kernel(LenetFcParams P) 
         }
       }
     }
-    __syncthreads();
+    lds_barrier();
 
     // ---- P4: dH2^T = (W3^T E^T) * relu'(H2) (waves 0..5), dW3 += E^T H2, db3 ----
     u32x2 dh2v[2] = {u32x2{0u, 0u}, u32x2{0u, 0u}};
@@ -394,12 +410,12 @@ __global__ void __launch_bounds__(kThreads, 1) lenet_fc_kernel(LenetFcParams P) 
       const bf16x8 bh = tr8(smem + OH2 + tra0 * SH2 + (16 * w + 4 * p) * 2, smem + OH2 + tra1 * SH2 + (16 * w + 4 * p) * 2);
       dw3 = mma(dw3, ae, bh);
     }
-    __syncthreads();  // H2 reads done
+    lds_barrier();  // H2 reads done
     if (w < 6) {
       *reinterpret_cast<u32x2*>(smem + OH2 + rm0 * SH2 + (16 * w + 4 * g) * 2) = dh2v[0];
       *reinterpret_cast<u32x2*>(smem + OH2 + rm1 * SH2 + (16 * w + 4 * g) * 2) = dh2v[1];
     }
-    __syncthreads();
+    lds_barrier();
 
     // ---- P5: dW2 += dH2^T H1, db2; dH1^T = (W2^T dH2^T) * relu'(H1) ----
     u32x2 dh1v[2];
@@ -430,17 +446,17 @@ __global__ void __launch_bounds__(kThreads, 1) lenet_fc_kernel(LenetFcParams P) 
         dh1v[mt] = pack4(d[0], d[1], d[2], d[3]);
       }
     }
-    __syncthreads();  // H1 and dH2 reads done
+    lds_barrier();  // H1 and dH2 reads done
     *reinterpret_cast<u32x2*>(smem + OH1 + rm0 * SH1 + (16 * w + 4 * g) * 2) = dh1v[0];
     *reinterpret_cast<u32x2*>(smem + OH1 + rm1 * SH1 + (16 * w + 4 * g) * 2) = dh1v[1];
-    __syncthreads();
+    lds_barrier();
 
     // ---- P6: dW1 += dH1^T Y, db1; dY^T = W1^T dH1^T -> global ----
     {
       const bf16x8 ad = tr8(smem + OH1 + tra0 * SH1 + (16 * w + 4 * p) * 2, smem + OH1 + tra1 * SH1 + (16 * w + 4 * p) * 2);
       db1 = mma(db1, ad, ones);
-      const char* ya = smem + OY + tra0 * SY + 8 * p;
-      const char* yb = smem + OY + tra1 * SY + 8 * p;
+      const char* ya = ysm + tra0 * SY + 8 * p;
+      const char* yb = ysm + tra1 * SY + 8 * p;
       bf16x8 fy[4];
 #pragma unroll
       for (int b = 0; b < 3; ++b) fy[b] = tr8(ya + 32 * b, yb + 32 * b);
@@ -454,7 +470,7 @@ __global__ void __launch_bounds__(kThreads, 1) lenet_fc_kernel(LenetFcParams P) 
     }
     // every wave is done with the input tile: the next one streams into LDS
     // while the data gradient below runs
-    __syncthreads();
+    lds_barrier();
 #ifndef MCC_FC_ABL_NOLOAD  // timing ablation (tools/build_variant.sh): reuse the first tile's input
     if (t + (int)gridDim.x < ntiles) load_tile(t + gridDim.x);
 #endif
