@@ -175,6 +175,12 @@ __device__ __forceinline__ int swap1(int v) { return __builtin_amdgcn_mov_dpp(v,
 __device__ __forceinline__ uint32_t mid16(uint32_t a, uint32_t b) { return __builtin_amdgcn_alignbit(b, a, 16); }
 
 __device__ __forceinline__ int imax(int a, int b) { return a > b ? a : b; }
+// one v_max3_i32 (the compiler reassociates nested maxes into max + max3 + max)
+__device__ __forceinline__ int max3i(int a, int b, int c) {
+  int r;
+  asm("v_max3_i32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
 // NB: never __builtin_bit_cast an ext_vector element (acc[i]): this clang
 // (ROCm 7.2) lowers it to a bitcast of the whole vector and extracts lane 0,
 // silently reading acc[0] for every i.  __float_as_int on the scalar is fine.
@@ -412,7 +418,7 @@ __global__ void __launch_bounds__(64) lenet_fwd_kernel(LenetFwdParams p) {
       a1s[(e >> 8) + ea1] = (uint8_t)((float)yb > 0.f ? ((best & 3) ^ 3) : 4);
     }
     wave_lds_sync();  // pooled conv1 output and codes complete in LDS
-    {  // bulk copies to HBM: Y1 (196 x 16 B), A1 (84 x 16 B)
+    if constexpr (!(MCC_LENET_ABL & 512)) {  // bulk copies to HBM: Y1 (196 x 16 B), A1 (84 x 16 B)
       u32x4* y1g = reinterpret_cast<u32x4*>(static_cast<bf16*>(p.y1) + (size_t)img * kY1Elems);
       u32x4* a1g = reinterpret_cast<u32x4*>(p.a1 + (size_t)img * kA1Bytes);
 #pragma unroll
@@ -512,7 +518,7 @@ __device__ __forceinline__ bf16x8 lds8v(const char* p) {
   return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
 }
 
-__global__ void __launch_bounds__(64) lenet_fwd2_kernel(LenetFwdParams p) {
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) lenet_fwd2_kernel(LenetFwdParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int lane = threadIdx.x;
   const int n16 = lane & 15, g = lane >> 4;
@@ -611,30 +617,52 @@ __global__ void __launch_bounds__(64) lenet_fwd2_kernel(LenetFwdParams p) {
       auto tile_a = [](int T) { return (2 * (T >> 2)) * 2 * kGxPitch * 2 + 4 * (4 * (T & 3)); };  // py0 = 2 (T/4), px0 = 4 (T%4)
       auto tile_y = [](int T) { return ((2 * (T >> 2)) * 14 + 4 * (T & 3)) * 16; };               // Y1 (py0, px0)
       auto tile_c = [](int T) { return (2 * (T >> 2)) * 16 + 4 * (T & 3); };                      // A1 (py0, px0)
-      bf16x8 fa = lds8v(xf + abase + tile_a(0));
-      bf16x8 fb = lds8v(xf + abase + tile_a(0) + 4 * kGxPitch * 2);
+      // software-pipelined: tile T + 1's MFMAs are issued before tile T's
+      // epilogue (which then needs no wait states for its accumulator), and
+      // tile T + 2's operands are read meanwhile (two operand sets)
+      const f32x4 b4 = {bias1, bias1, bias1, bias1};
+      bf16x8 fa[2], fb[2];
+      fa[0] = lds8v(xf + abase + tile_a(0));
+      fb[0] = lds8v(xf + abase + tile_a(0) + 4 * kGxPitch * 2);
+      fa[1] = lds8v(xf + abase + tile_a(1));
+      fb[1] = lds8v(xf + abase + tile_a(1) + 4 * kGxPitch * 2);
+      f32x4 acc = mma(mma(b4, fa[0], w1[0]), fb[0], w1[1]);
+      float kprev = 0.f;
 #pragma unroll
       for (int T = 0; T < 28; ++T) {
-        f32x4 acc = {bias1, bias1, bias1, bias1};
-        acc = mma(acc, fa, w1[0]);
-        acc = mma(acc, fb, w1[1]);
-        if (T + 1 < 28) {
-          fa = lds8v(xf + abase + tile_a(T + 1));
-          fb = lds8v(xf + abase + tile_a(T + 1) + 4 * kGxPitch * 2);
+        f32x4 accn = acc;
+        if (T + 1 < 28) accn = mma(mma(b4, fa[(T + 1) & 1], w1[0]), fb[(T + 1) & 1], w1[1]);
+        if (T + 2 < 28) {
+          fa[T & 1] = lds8v(xf + abase + tile_a(T + 2));
+          fb[T & 1] = lds8v(xf + abase + tile_a(T + 2) + 4 * kGxPitch * 2);
         }
-        const int k0 = (__float_as_int(acc[0]) & ~3) | 3;
+        __builtin_amdgcn_sched_barrier(0);
+        const int k0 = __float_as_int(acc[0]) | 3;
         const int k1 = (__float_as_int(acc[1]) & ~3) | 2;
         const int k2 = (__float_as_int(acc[2]) & ~3) | 1;
         const int k3 = __float_as_int(acc[3]) & ~3;
-        const int best = imax(imax(imax(k0, k1), imax(k2, k3)), 0);
-        // the two code bits left in the value perturb it by < 2^-21: below the bf16 rounding
-        const bf16 yb = (bf16)(__int_as_float(best) * (1.f / 255.f));
-        if ((T & 3) != 3 || y1last) *reinterpret_cast<bf16*>(y1s + ey1 + tile_y(T)) = yb;
-        a1s[ea1 + tile_c(T)] = (uint8_t)(best > 3 ? (~best & 3) : 4);
+        // ReLU folded into the pool max: the key is >= 0, and > 3 iff the
+        // window's maximum is positive (position code ~key & 3)
+        const int key = max3i(max3i(k0, k1, k2), k3, 0);
+        a1s[ea1 + tile_c(T)] = (uint8_t)(key > 3 ? (~key & 3) : 4);
+        // the two code bits left in the value perturb it by < 2^-21: below the
+        // bf16 rounding.  Scale and convert two tiles at a time (v_pk_mul_f32,
+        // one v_cvt_pk_bf16_f32)
+        if (T & 1) {
+          typedef float f2 __attribute__((ext_vector_type(2)));
+          typedef bf16 b2 __attribute__((ext_vector_type(2)));
+          const f2 v = f2{kprev, __int_as_float(key)} * f2{1.f / 255.f, 1.f / 255.f};
+          const b2 y = __builtin_convertvector(v, b2);
+          *reinterpret_cast<bf16*>(y1s + ey1 + tile_y(T - 1)) = y[0];
+          if ((T & 3) != 3 || y1last) *reinterpret_cast<bf16*>(y1s + ey1 + tile_y(T)) = y[1];
+        } else {
+          kprev = __int_as_float(key);
+        }
+        acc = accn;
       }
     }
     wave_lds_sync();  // pooled conv1 output and codes complete in LDS
-    {  // bulk copies to HBM: Y1 (196 x 16 B), A1 (84 x 16 B)
+    if constexpr (!(MCC_LENET_ABL & 512)) {  // bulk copies to HBM: Y1 (196 x 16 B), A1 (84 x 16 B)
       u32x4* y1g = reinterpret_cast<u32x4*>(static_cast<bf16*>(p.y1) + (size_t)img * kY1Elems);
       u32x4* a1g = reinterpret_cast<u32x4*>(p.a1 + (size_t)img * kA1Bytes);
 #pragma unroll
@@ -672,7 +700,7 @@ __global__ void __launch_bounds__(64) lenet_fwd2_kernel(LenetFwdParams p) {
       }
     }
     wave_lds_sync();
-    {  // Y2: 50 x 16 B, A2: 25 x 16 B
+    if constexpr (!(MCC_LENET_ABL & 1024)) {  // Y2: 50 x 16 B, A2: 25 x 16 B
       u32x4* y2g = reinterpret_cast<u32x4*>(static_cast<bf16*>(p.y2) + (size_t)img * kY2Elems);
       u32x4* a2g = reinterpret_cast<u32x4*>(p.a2 + (size_t)img * kY2Elems);
       // chunks 0..74 = Y2 0..49, A2 0..24 over lanes 0..63, then 64..74
