@@ -440,7 +440,13 @@ __global__ void __launch_bounds__(kDW3T) __attribute__((amdgpu_waves_per_eu(3)))
 // an LDS-atomic scatter of only the nonzero terms (60 K) measured 15x slower
 // (ds_add_f32 retires about one lane per clock), and a v_pk_fma_f32 variant
 // over input-channel pairs (thirds of the plane, one kernel row of weights
-// at a time) 1.8x slower (2,020 vs 1,099 us).
+// at a time) 1.8x slower (2,020 vs 1,099 us).  Round 6, two more packed
+// forms, both slower than this one (1,037 us in the same run): column pairs
+// with even / odd weight layouts (196 registers, 2 waves per SIMD) 1,286 us,
+// and image PAIRS per lane over a quarter plane (every product a splat-weight
+// v_pk_fma_f32: half the FMA issues) 1,104 us at 2 waves per SIMD, 1,234 at 3
+// (spilling); this form spills too (168 registers + 628 in scratch) and is
+// still the fastest: the issue count is not what bounds it.
 // Workgroup = 4 waves = 2 image groups x 2 halves: waves 2k, 2k+1 share group
 // k's staged dY / argmax codes (10 images, lanes 0..59 = image x ci); the
 // weights are staged once per workgroup as [co][ci][28] (16-byte rows).
