@@ -911,7 +911,7 @@ void GpuNet::forward(const uint8_t* images, const int32_t* idx, int B, hipStream
 void GpuNet::flush_forward(hipStream_t s) const {
   if (!fc_pending_) return;
   fc_pending_ = false;
-  const_cast<GpuNet*>(this)->forward_stages(2, false, s);
+  const_cast<GpuNet*>(this)->forward_stages(pending_from_, false, s);
 }
 
 void GpuNet::forward_stages(size_t first, bool defer_fc, hipStream_t s) {
@@ -923,6 +923,16 @@ void GpuNet::forward_stages(size_t first, bool defer_fc, hipStream_t s) {
     Stage& st = *stages_[si];
     if (fcchain_ && defer_fc && si >= 2) {
       fc_pending_ = true;
+      pending_from_ = 2;
+      return;
+    }
+    // the last FC layer of a fused softmax-CE head: its forward runs inside
+    // the head kernel that loss(backward = true) launches (xent_head FWD).
+    // fp32 only: ref 63 + 107 -> 152 us, LeNet-5 36 + 57 -> 88 us; in bf16 the
+    // VALU logits cost more than the MFMA forward they replace (ref 20 + 76 -> 102 us)
+    if (defer_fc && st.head && si + 1 == stages_.size() && dtype_ == DType::F32 && !ab_flag("no_head_fwd")) {
+      fc_pending_ = true;
+      pending_from_ = si;
       return;
     }
     if (lenet_ && si <= 1) {
@@ -1089,7 +1099,7 @@ void GpuNet::loss(const uint8_t* labels, const int32_t* idx, float grad_scale, b
                   int32_t* pred) {
   MCC_CHECK(B_ > 0, "loss: call forward first");
   const Stage& last = *stages_.back();
-  if (fc_pending_ && backward) {
+  if (fcchain_ && fc_pending_ && backward) {
     // forward + softmax-CE + backward of the three FC layers in one kernel;
     // the weight gradients land in grads_ through a fixed-order slab reduce
     const Stage& s1 = *stages_[1];
@@ -1116,7 +1126,8 @@ void GpuNet::loss(const uint8_t* labels, const int32_t* idx, float grad_scale, b
     fc_bwd_done_ = true;
     return;
   }
-  flush_forward(s);
+  const bool head_fwd = backward && last.head && fc_pending_ && pending_from_ + 1 == stages_.size();
+  if (!head_fwd) flush_forward(s);
   gpu::XentParams p;
   p.M = B_; p.N = spec_.num_classes();
   p.logits = logits_; p.ldl = logits_ld_;
@@ -1137,6 +1148,10 @@ void GpuNet::loss(const uint8_t* labels, const int32_t* idx, float grad_scale, b
     h.act = pv.kind == Stage::FC ? pv.act : gpu::ACT_NONE;  // conv masks are applied by its staging
     h.dh = pv.grad_buf;
     h.slab = scratch_; h.ldp = last.ldp;
+    if (head_fwd) {  // the head computes (and writes) the logits itself
+      h.bias = params_ + last.b_off;
+      fc_pending_ = false;
+    }
     gpu::xent_head(dtype_, h, s);
     gpu::DwReduceParams r;
     r.S = gpu::xent_head_slabs(B_); r.Nout = last.Nout; r.kfeat = last.Kin; r.ldp = last.ldp; r.part = scratch_;
@@ -1620,8 +1635,8 @@ const void* GpuNet::stage_output(int stage, int64_t& per_sample, const uint8_t**
   // it ran forward + backward in one kernel (loss() of a training step)
   MCC_CHECK(!(fcchain_ && fc_bwd_done_ && (stage == 2 || stage == 3)),
             "stage_output: FC activations of the fused classifier chain were not written (training step)");
-  MCC_CHECK(!(fcchain_ && fc_pending_ && stage >= 2),
-            "stage_output: the FC forward of the fused classifier chain is still pending (call flush_forward)");
+  MCC_CHECK(!(fc_pending_ && (size_t)stage >= pending_from_),
+            "stage_output: the FC forward is still pending (call flush_forward)");
   per_sample = st.out_elems;
   if (argmax) *argmax = st.pooled ? st.arg_buf : nullptr;
   return st.act_buf;

@@ -492,6 +492,7 @@ struct XentHeadParams {
   int Kin = 0, act = 0;                    // act of h's producer (ACT_*)
   void* dh = nullptr;                      // T [M][ldh]
   float* slab = nullptr; int ldp = 0;      // [nwg][N][ldp]
+  const float* bias = nullptr;             // non-null: the head computes the logits itself (its FC forward)
 };
 bool xent_head_supported(int N, int Kin, int ldh);
 int xent_head_slabs(int M);

@@ -126,8 +126,12 @@ __host__ __device__ constexpr int head_lds(int Kin) {
 
 // T = bf16: the bf16 engine's rounding points (weights, dlogits, H through
 // bf16); T = float: the fp32 engine, no rounding, the dW tile on f32 MFMA.
-template <typename T>
-__global__ void __launch_bounds__(kHeadThreads) xent_head_kernel(XentHeadParams hp) {
+// FWD: the head's forward too (hp.bias != nullptr): the logits from the
+// cached H chunks (each of the 4 threads of a row sums its K chunks, a quad
+// shuffle completes them) -- the last FC layer's separate forward GEMM and its
+// logits round trip disappear; the logits are still written when asked for.
+template <typename T, bool FWD>
+__global__ void __launch_bounds__(kHeadThreads) __attribute__((amdgpu_waves_per_eu(sizeof(T) == 2 ? 4 : 2))) xent_head_kernel(XentHeadParams hp) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   typedef typename Vec8<T>::type V8;
   constexpr bool kB = sizeof(T) == 2;
@@ -149,22 +153,83 @@ __global__ void __launch_bounds__(kHeadThreads) xent_head_kernel(XentHeadParams 
   }
   const int row = blockIdx.x * kHeadRows + r;
   const bool live = row < p.M;
+  const T* hrow = static_cast<const T*>(hp.h) + (size_t)row * hp.ldh;
+  T* drow = static_cast<T*>(hp.dh) + (size_t)row * hp.ldh;
+  const int K8 = (Kin + 7) & ~7;
+  // this thread's 8-feature chunks q, q + 4, ... of the row (<= 8 for Kin < 256)
+  V8 hc[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int k0 = 8 * q + 32 * i;
+    if (live && k0 < K8) {
+      hc[i] = load8(hrow + k0);
+      if (k0 + 8 > Kin) {  // the row's padding columns (never written: may hold NaN)
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (k0 + j >= Kin) hc[i][j] = (T)0.f;
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) hc[i][j] = (T)0.f;
+    }
+  }
+  float lg[16];
+  if constexpr (FWD) {
+    __syncthreads();  // Ws
+#pragma unroll
+    for (int n = 0; n < 16; ++n) lg[n] = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int k0 = 8 * q + 32 * i;
+      if (k0 >= K8) break;
+#pragma unroll
+      for (int n = 0; n < 16; ++n) {
+        if (n >= N) break;
+        const f32x4 w0 = *reinterpret_cast<const f32x4*>(Ws + n * kw + k0);
+        const f32x4 w1 = *reinterpret_cast<const f32x4*>(Ws + n * kw + k0 + 4);
+        float acc = lg[n];  // one sequential f32 fma chain per class
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc = __builtin_fmaf((float)hc[i][j], w0[j], acc);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc = __builtin_fmaf((float)hc[i][4 + j], w1[j], acc);
+        lg[n] = acc;
+      }
+    }
+#pragma unroll
+    for (int n = 0; n < 16; ++n) {
+      if (n >= N) break;
+      lg[n] += __shfl_xor(lg[n], 1);
+      lg[n] += __shfl_xor(lg[n], 2);
+      lg[n] += hp.bias[n];
+    }
+  }
   float loss = 0.f, mse = 0.f, correct = 0.f;
   float e[16];
 #pragma unroll
   for (int j = 0; j < 16; ++j) e[j] = 0.f;
   if (live) {
-    const float* l = p.logits + (size_t)row * p.ldl;
     const int sample = p.labels_idx ? p.labels_idx[row] : row;
     const int label = p.labels[sample];
     float v[16];
+    if constexpr (FWD) {
 #pragma unroll
-    for (int j = 0; j < 16; j += 4) {
-      if (j < N) {
-        const float4 t4 = *reinterpret_cast<const float4*>(l + j);
-        v[j] = t4.x; v[j + 1] = t4.y; v[j + 2] = t4.z; v[j + 3] = t4.w;
-      } else {
-        v[j] = v[j + 1] = v[j + 2] = v[j + 3] = 0.f;
+      for (int j = 0; j < 16; ++j) v[j] = j < N ? lg[j] : 0.f;
+      if (p.logits && q == 0) {
+        float* l = const_cast<float*>(p.logits) + (size_t)row * p.ldl;  // the engine's logits buffer
+#pragma unroll
+        for (int j = 0; j < 16; j += 4)
+          if (j < N) *reinterpret_cast<float4*>(l + j) = make_float4(v[j], v[j + 1], v[j + 2], v[j + 3]);
+      }
+    } else {
+      const float* l = p.logits + (size_t)row * p.ldl;
+#pragma unroll
+      for (int j = 0; j < 16; j += 4) {
+        if (j < N) {
+          const float4 t4 = *reinterpret_cast<const float4*>(l + j);
+          v[j] = t4.x; v[j + 1] = t4.y; v[j + 2] = t4.z; v[j + 3] = t4.w;
+        } else {
+          v[j] = v[j + 1] = v[j + 2] = v[j + 3] = 0.f;
+        }
       }
     }
     float m = v[0];
@@ -204,20 +269,15 @@ __global__ void __launch_bounds__(kHeadThreads) xent_head_kernel(XentHeadParams 
 #pragma unroll
     for (int j = 0; j < 16; ++j) E[j * kHeadLd + r] = (T)e[j];
   }
-  __syncthreads();  // Ws
+  if constexpr (!FWD) __syncthreads();  // Ws
 
   // data gradient of the head input + the H^T image (row Kin = ones: bias);
   // thread q of a sample owns the 8-feature chunks q, q+4, ...
-  const T* hrow = static_cast<const T*>(hp.h) + (size_t)row * hp.ldh;
-  T* drow = static_cast<T*>(hp.dh) + (size_t)row * hp.ldh;
-  const int K8 = (Kin + 7) & ~7;
-  for (int k0 = 8 * q; k0 < K8; k0 += 32) {
-    V8 hv;
-    if (live) hv = load8(hrow + k0);
-    else {
 #pragma unroll
-      for (int i = 0; i < 8; ++i) hv[i] = (T)0.f;
-    }
+  for (int ic = 0; ic < 8; ++ic) {
+    const int k0 = 8 * q + 32 * ic;
+    if (k0 >= K8) break;
+    const V8 hv = hc[ic];
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int n = 0; n < 16; ++n) {
@@ -625,17 +685,20 @@ int xent_head_slabs(int M) { return cdiv(M, kHeadRows); }
 
 void xent_head(DType t, const XentHeadParams& p, hipStream_t s) {
   MCC_CHECK(p.x.M > 0 && xent_head_supported(p.x.N, p.Kin, p.ldh), "xent_head: needs N <= 16, Kin < 256, ldh % 8 == 0");
-  MCC_CHECK(p.x.ldl % 4 == 0 && (reinterpret_cast<uintptr_t>(p.x.logits) & 15) == 0 && p.x.ldl >= ((p.x.N + 3) & ~3),
+  MCC_CHECK((p.bias && !p.x.logits) ||
+                (p.x.ldl % 4 == 0 && (reinterpret_cast<uintptr_t>(p.x.logits) & 15) == 0 && p.x.ldl >= ((p.x.N + 3) & ~3)),
             "xent_head: logits rows must be 16-byte aligned");
   MCC_CHECK(p.h && p.dh && p.w && p.slab && p.ldp >= p.Kin + 1 && (reinterpret_cast<uintptr_t>(p.h) & 15) == 0 &&
                 (reinterpret_cast<uintptr_t>(p.dh) & 15) == 0,
             "xent_head: bad buffers");
-  if (t == DType::BF16)
-    hipLaunchKernelGGL(xent_head_kernel<bf16>, dim3((unsigned)xent_head_slabs(p.x.M)), dim3(kHeadThreads),
-                       head_lds<bf16>(p.Kin), s, p);
-  else
-    hipLaunchKernelGGL(xent_head_kernel<float>, dim3((unsigned)xent_head_slabs(p.x.M)), dim3(kHeadThreads),
-                       head_lds<float>(p.Kin), s, p);
+  const dim3 grid((unsigned)xent_head_slabs(p.x.M)), block(kHeadThreads);
+  if (t == DType::BF16) {
+    if (p.bias) hipLaunchKernelGGL((xent_head_kernel<bf16, true>), grid, block, head_lds<bf16>(p.Kin), s, p);
+    else hipLaunchKernelGGL((xent_head_kernel<bf16, false>), grid, block, head_lds<bf16>(p.Kin), s, p);
+  } else {
+    if (p.bias) hipLaunchKernelGGL((xent_head_kernel<float, true>), grid, block, head_lds<float>(p.Kin), s, p);
+    else hipLaunchKernelGGL((xent_head_kernel<float, false>), grid, block, head_lds<float>(p.Kin), s, p);
+  }
 }
 
 void softmax_xent(DType t, const XentParams& p, hipStream_t s) {
