@@ -928,9 +928,11 @@ void GpuNet::forward_stages(size_t first, bool defer_fc, hipStream_t s) {
     }
     // the last FC layer of a fused softmax-CE head: its forward runs inside
     // the head kernel that loss(backward = true) launches (xent_head FWD).
-    // fp32 only: ref 63 + 107 -> 152 us, LeNet-5 36 + 57 -> 88 us; in bf16 the
-    // VALU logits cost more than the MFMA forward they replace (ref 20 + 76 -> 102 us)
-    if (defer_fc && st.head && si + 1 == stages_.size() && dtype_ == DType::F32 && !ab_flag("no_head_fwd")) {
+    // fp32: ref 63 + 107 -> 152 us, LeNet-5 36 + 57 -> 88 us.  bf16 only with
+    // the MFMA head: the VALU head's logits cost more than the MFMA forward
+    // they replace (ref 20 + 76 -> 102 us)
+    if (defer_fc && st.head && si + 1 == stages_.size() && !ab_flag("no_head_fwd") &&
+        (dtype_ == DType::F32 || !ab_flag("head_valu"))) {
       fc_pending_ = true;
       pending_from_ = si;
       return;
@@ -1148,6 +1150,10 @@ void GpuNet::loss(const uint8_t* labels, const int32_t* idx, float grad_scale, b
     h.act = pv.kind == Stage::FC ? pv.act : gpu::ACT_NONE;  // conv masks are applied by its staging
     h.dh = pv.grad_buf;
     h.slab = scratch_; h.ldp = last.ldp;
+    if (dtype_ == DType::BF16) {  // the MFMA head reads the packed forward copy
+      h.wpk = static_cast<const char*>(packed_) + 2 * last.pk_fwd;
+      h.ldw = r8(last.Kin);
+    }
     if (head_fwd) {  // the head computes (and writes) the logits itself
       h.bias = params_ + last.b_off;
       fc_pending_ = false;

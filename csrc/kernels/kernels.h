@@ -493,6 +493,9 @@ struct XentHeadParams {
   void* dh = nullptr;                      // T [M][ldh]
   float* slab = nullptr; int ldp = 0;      // [nwg][N][ldp]
   const float* bias = nullptr;             // non-null: the head computes the logits itself (its FC forward)
+  // bf16 only, optional: the packed bf16 weights [N][ldw] (ldw % 8 == 0,
+  // 16-byte aligned) select the MFMA head (xent_head_mfma_kernel)
+  const void* wpk = nullptr; int ldw = 0;
 };
 bool xent_head_supported(int N, int Kin, int ldh);
 int xent_head_slabs(int M);

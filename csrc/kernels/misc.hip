@@ -10,8 +10,12 @@
 //  pack_gather  : refresh the packed bf16/fp32 compute copies (MFMA order,
 //                 transposed shadows) from the fp32 master after the update.
 #include "kernels.h"
+#include "mcc/ab.h"
 #include "mfma.h"
 #include "stats.h"
+
+#include <algorithm>
+#include <type_traits>
 
 namespace mcc {
 namespace gpu {
@@ -338,6 +342,245 @@ __global__ void __launch_bounds__(kHeadThreads) __attribute__((amdgpu_waves_per_
     float t = 0.f;
 #pragma unroll
     for (int w = 0; w < kHeadThreads / 64; ++w) t += red[tid][w];
+    stat_add(p.stats, tid, t);
+  }
+}
+
+// The bf16 head on the matrix cores.  The VALU head above spends its time on
+// per-element work that is all GEMM-shaped: the logits (H W^T), the data
+// gradient (E W, 16 FMAs per feature and thread) and the H^T image for dW
+// (Kin ds_write_b16 per row).  Here every product is a 16x16x32 MFMA and the
+// transposes are ds_read_b64_tr_b16 reads of row-major LDS images:
+//   Hs [128][SH]  the workgroup's H rows (16-byte writes; col Kin = 1, the bias)
+//   Ws [16][SH]   W in bf16 (the packed forward copy)
+//   Es [128][16]  e = (softmax - onehot) * scale, bf16
+// Wave w owns rows 16w..16w+15 for the forward, softmax and dgrad:
+//   logits C[row][n] = sum_k Hs[row][k] Ws[n][k]        (NT/2 MFMAs, fp32 + bias)
+//   softmax-CE across the 16 lanes of a C column group (class = lane & 15)
+//   dH^T   C[k][row] = sum_n Ws^T[k][n] Es^T[n][row]    (NT MFMAs, K = 16 of 32 live)
+//          -> act' from Hs, 8-byte stores of 4 consecutive features
+// and after one barrier the workgroup's dW/db slab, C[n][k] = sum_row Es^T Hs
+// (4 MFMAs per 16-column tile, tiles w, w + 8).
+constexpr int kHmWaves = kHeadRows / 16;
+__host__ __device__ constexpr int headm_sh(int Kin) { return 16 * head_nt(Kin) + 8; }  // 16-byte pad: b128 rows spread over banks
+__host__ __device__ constexpr int headm_lds(int Kin) { return (kHeadRows + 16) * headm_sh(Kin) * 2 + kHeadRows * 32; }
+
+__device__ __forceinline__ bf16x8 head_tr8(const bf16* p0, const bf16* p1) {
+  return __builtin_shufflevector(tr4(p0), tr4(p1), 0, 1, 2, 3, 4, 5, 6, 7);
+}
+
+// dead-lane store target: one 64-byte slot per resident wave (a single
+// shared line would take every wave's dead lanes into one L2 channel)
+constexpr int kHeadSinkSlots = 4096;
+__device__ __attribute__((aligned(64))) float kHeadSink[kHeadSinkSlots * 16];
+
+// Persistent: workgroup b takes the 128-row tiles b, b + grid, ... (the slab
+// index stays the tile index).  The next tile's H rows are loaded into
+// registers while this tile computes -- one HBM latency per workgroup instead
+// of one per tile.  Every global load and store is unconditional (clamped
+// rows, dead stores to kHeadSink), so the compiler's vmcnt bookkeeping lets
+// the prefetch stay in flight across the whole tile.
+// KCH = ceil(16 NT / 32): the 32-feature groups of an H row (ref 200 -> 7,
+// LeNet-5 84 -> 3): the prefetch buffer holds exactly those
+template <bool FWD, int KCH>
+__global__ void __launch_bounds__(kHeadThreads) __attribute__((amdgpu_waves_per_eu(4))) xent_head_mfma_kernel(XentHeadParams hp) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  __shared__ float red[3][kHmWaves];
+  const XentParams& p = hp.x;
+  const int N = p.N, Kin = hp.Kin, M = p.M;
+  const int NT = head_nt(Kin), kw = 16 * NT, SH = kw + 8;
+  const int K8 = (Kin + 7) & ~7;
+  const int ntiles = (M + kHeadRows - 1) / kHeadRows;
+  bf16* Hs = reinterpret_cast<bf16*>(smem);
+  bf16* Ws = Hs + kHeadRows * SH;
+  bf16* Es = Ws + 16 * SH;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, r = lane & 15;
+  const int q4 = r >> 2, p4 = lane & 3;  // tr reads: lane 4q + p -> row q, columns 4p..4p+3
+  const bf16x8 z8 = __builtin_bit_cast(bf16x8, f32x4{0.f, 0.f, 0.f, 0.f});
+  float* const sink32 = kHeadSink + ((blockIdx.x * kHmWaves + w) & (kHeadSinkSlots - 1)) * 16;
+  bf16* const sink16 = reinterpret_cast<bf16*>(sink32);
+
+  // H rows of this wave: lane -> row lane >> 2, 8-feature chunks (lane & 3) + 4 it
+  const int hr = lane >> 2, hq = lane & 3;
+  bf16x8 hc[KCH];
+  int sidx[4];  // dataset index of the C-layout rows 4g + i (labels_idx), prefetched with H
+  auto load_h = [&](int tile, int kw, int K8) {
+    const int row = min(tile * kHeadRows + 16 * w + hr, M - 1);
+    const bf16* hrow = static_cast<const bf16*>(hp.h) + (size_t)row * hp.ldh;
+#pragma unroll
+    for (int it = 0; it < KCH; ++it) hc[it] = load8(hrow + min(8 * (hq + 4 * it), K8 - 8));  // no branch
+    if (p.labels_idx) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) sidx[i] = p.labels_idx[min(tile * kHeadRows + 16 * w + 4 * g + i, M - 1)];
+    }
+  };
+  load_h(blockIdx.x, kw, K8);
+  // W (bf16 forward copy), once per workgroup: thread -> class tid >> 5, chunk tid & 31
+  {
+    const int wn = tid >> 5, wc = tid & 31;
+    const bf16x8 wv0 = load8(static_cast<const bf16*>(hp.wpk) + (size_t)min(wn, N - 1) * hp.ldw + min(8 * wc, K8 - 8));
+    if (8 * wc < kw) {
+      bf16x8 wv = wv0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (wn >= N || 8 * wc + j >= Kin) wv[j] = (bf16)0.f;
+      store8(Ws + wn * SH + 8 * wc, wv);
+    }
+  }
+  const float bias = FWD ? hp.bias[min(r, N - 1)] : 0.f;
+  float loss = 0.f, mse = 0.f, correct = 0.f;
+
+  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int row0 = tile * kHeadRows + 16 * w;
+    // re-materialised per tile: hoisted out of the tile loop, the per-lane
+    // masks derived from these (64-bit each, ~300 SGPRs) spill
+    int Kin = hp.Kin, K8 = (hp.Kin + 7) & ~7, N = p.N, NT = head_nt(hp.Kin), kw = 16 * NT, SH = kw + 8;
+    asm volatile("" : "+s"(Kin), "+s"(K8), "+s"(N), "+s"(NT), "+s"(kw), "+s"(SH));
+    int lane = tid & 63;  // (and every lane-derived index: 64 hoisted k0 + j alone took 56 VGPRs)
+    asm volatile("" : "+v"(lane));
+    const int g = lane >> 4, r = lane & 15, q4 = r >> 2, p4 = lane & 3, hr = lane >> 2, hq = lane & 3;
+    // labels (and logits) of the C-layout rows 4g + i, class r
+    int lab[4];
+    float lgv[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      lab[i] = (int)p.labels[p.labels_idx ? sidx[i] : min(row0 + 4 * g + i, M - 1)];
+      if constexpr (!FWD) lgv[i] = p.logits[(size_t)min(row0 + 4 * g + i, M - 1) * p.ldl + min(r, N - 1)];
+    }
+    // this tile's H image (dead rows and padding columns zero, column Kin = 1)
+    const bool hlive = row0 + hr < M;
+#pragma unroll
+    for (int it = 0; it < KCH; ++it) {
+      const int k0 = 8 * (hq + 4 * it);
+      if (k0 < kw) {
+        bf16x8 v = (hlive && k0 < K8) ? hc[it] : z8;
+        if (k0 + 8 > Kin) {  // padding columns (never written upstream: may hold NaN)
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            if (k0 + j >= Kin) v[j] = (bf16)((k0 + j == Kin && hlive) ? 1.f : 0.f);
+        }
+        store8(Hs + (16 * w + hr) * SH + k0, v);
+      }
+    }
+#ifndef MCC_HEAD_NOPF
+    load_h(min(tile + (int)gridDim.x, ntiles - 1), kw, K8);  // next tile (the last tile reloads itself)
+#endif
+    __syncthreads();
+
+    if constexpr (FWD) {
+      f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int c = 0; c < KCH; ++c) {
+        const int kk = 32 * c + 8 * g;
+        bf16x8 a = z8, b = z8;
+        if (kk < kw) {
+          a = load8(Hs + (16 * w + r) * SH + kk);
+          b = load8(Ws + r * SH + kk);
+        }
+        acc = mma(acc, a, b);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        lgv[i] = acc[i] + bias;
+        const int rw = row0 + 4 * g + i;
+        float* dst = (p.logits && rw < M && r < N) ? const_cast<float*>(p.logits) + (size_t)rw * p.ldl + r : sink32;
+        *dst = lgv[i];
+      }
+    }
+
+    __builtin_amdgcn_sched_barrier(0);
+    // softmax-CE of rows 4g + i across the 16 lanes of the group (class r)
+#pragma unroll 1  // (unrolled: four rows' shuffle chains in flight, +30 VGPRs and a spilled prefetch)
+    for (int i = 0; i < 4; ++i) {
+      const int rw = row0 + 4 * g + i;
+      const bool live = rw < M;
+      const float v = r < N ? lgv[i] : -INFINITY;
+      float m = v;
+      int am = r;
+#pragma unroll
+      for (int o = 8; o > 0; o >>= 1) {  // max, smallest class among equal maxima (first max wins, cnn.c:510)
+        const float om = __shfl_xor(m, o);
+        const int oa = __shfl_xor(am, o);
+        if (om > m || (om == m && oa < am)) { m = om; am = oa; }
+      }
+      const float ex = r < N ? __expf(v - m) : 0.f;
+      float s = ex;
+#pragma unroll
+      for (int o = 8; o > 0; o >>= 1) s += __shfl_xor(s, o);
+      const int label = lab[i];
+      const float pj = ex * (1.f / s);
+      const float d = pj - (r == label ? 1.f : 0.f);
+      float d2 = r < N ? d * d : 0.f;
+#pragma unroll
+      for (int o = 8; o > 0; o >>= 1) d2 += __shfl_xor(d2, o);
+      const float vl = __shfl(v, (lane & 48) + (label & 15));
+      const bool first = live && r == 0;
+      loss += first ? __logf(s) - (vl - m) : 0.f;
+      mse += first ? d2 / (float)N : 0.f;
+      correct += (first && am == label) ? 1.f : 0.f;
+      *((first && p.pred) ? p.pred + rw : reinterpret_cast<int32_t*>(sink32)) = am;
+      *((p.probs && live && r < N) ? p.probs + (size_t)rw * N + r : sink32) = pj;  // (eval only)
+      Es[(16 * w + 4 * g + i) * 16 + r] = (live && r < N) ? (bf16)(d * p.scale) : (bf16)0.f;  // the unfused dlogits
+    }
+
+    __builtin_amdgcn_sched_barrier(0);
+    // dH^T tile t: C[16t + 4g + i][row r] (this wave's rows; its Es rows were
+    // written by this wave: LDS keeps one wave's accesses in order)
+    {
+      const bf16x8 eb = g < 2 ? load8(Es + (16 * w + r) * 16 + 8 * g) : z8;  // n >= 16: zero
+      const int wr = (8 * g + q4) & 15;  // g >= 2: any class row (times the zero half of eb)
+      const int drow = row0 + r;
+      const bool dlive = drow < M;
+      bf16* drp = static_cast<bf16*>(hp.dh) + (size_t)drow * hp.ldh;
+#pragma unroll 1
+      for (int t = 0; t < NT; ++t) {
+        const bf16x8 a = head_tr8(Ws + wr * SH + 16 * t + 4 * p4, Ws + (wr ^ 4) * SH + 16 * t + 4 * p4);
+        const f32x4 c = mma(f32x4{0.f, 0.f, 0.f, 0.f}, a, eb);
+        const int kc = 16 * t + 4 * g;
+        const bf16x4 y = *reinterpret_cast<const bf16x4*>(Hs + (16 * w + r) * SH + kc);
+        bf16x4 o;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) o[i] = kc + i < Kin ? (bf16)(c[i] * act_grad_y(hp.act, (float)y[i])) : (bf16)0.f;
+        *reinterpret_cast<bf16x4*>((dlive && kc < K8) ? drp + kc : sink16) = o;
+      }
+    }
+    __syncthreads();
+
+    // dW/db slab of the tile: C[n][k] = sum over its 128 rows of Es^T Hs, tiles t = w, w + 8
+    for (int t = w; t < NT; t += kHmWaves) {
+      f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < kHeadRows / 32; ++ks) {
+        const int rb = 32 * ks + 8 * g + q4;
+        const bf16x8 a = head_tr8(Es + rb * 16 + 4 * p4, Es + (rb + 4) * 16 + 4 * p4);
+        const bf16x8 b = head_tr8(Hs + rb * SH + 16 * t + 4 * p4, Hs + (rb + 4) * SH + 16 * t + 4 * p4);
+        acc = mma(acc, a, b);
+      }
+      float* slab = hp.slab + (size_t)tile * N * hp.ldp;
+      const int k = 16 * t + r;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int n = 4 * g + i;
+        *((n < N && k <= Kin) ? slab + n * hp.ldp + k : sink32) = acc[i];
+      }
+    }
+    __syncthreads();  // Hs / Es free for the next tile
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    loss += __shfl_xor(loss, o);
+    mse += __shfl_xor(mse, o);
+    correct += __shfl_xor(correct, o);
+  }
+  if (lane == 0) {
+    red[0][w] = loss;
+    red[1][w] = mse;
+    red[2][w] = correct;
+  }
+  __syncthreads();
+  if (tid < 3 && p.stats) {
+    float t = 0.f;
+#pragma unroll
+    for (int v = 0; v < kHmWaves; ++v) t += red[tid][v];
     stat_add(p.stats, tid, t);
   }
 }
@@ -692,7 +935,39 @@ void xent_head(DType t, const XentHeadParams& p, hipStream_t s) {
                 (reinterpret_cast<uintptr_t>(p.dh) & 15) == 0,
             "xent_head: bad buffers");
   const dim3 grid((unsigned)xent_head_slabs(p.x.M)), block(kHeadThreads);
-  if (t == DType::BF16) {
+  if (t == DType::BF16 && p.wpk && !ab_flag("head_valu")) {
+    MCC_CHECK(p.ldw % 8 == 0 && p.ldw >= p.Kin && (reinterpret_cast<uintptr_t>(p.wpk) & 15) == 0,
+              "xent_head: packed weights need 16-byte rows");
+    // persistent: as many workgroups as fit at once (A/B: MCC_AB=head_tile1, one tile each)
+    const int lds = headm_lds(p.Kin), kch = (16 * head_nt(p.Kin) + 31) / 32;
+    static int fit_lds = -1, fit = 0;
+    if (fit_lds != lds) {
+      int per_cu = 0, dev = 0, cus = 0;
+      MCC_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, xent_head_mfma_kernel<true, 8>, kHeadThreads, lds) ==
+                        hipSuccess &&
+                    hipGetDevice(&dev) == hipSuccess &&
+                    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess,
+                "xent_head: occupancy query failed");
+      fit = std::max(1, per_cu) * std::max(1, cus);
+      fit_lds = lds;
+    }
+    const dim3 pg(ab_flag("head_tile1") ? grid.x : std::min(grid.x, (unsigned)fit));
+    auto go = [&](auto kc) {
+      constexpr int KC = decltype(kc)::value;
+      if (p.bias) hipLaunchKernelGGL((xent_head_mfma_kernel<true, KC>), pg, block, lds, s, p);
+      else hipLaunchKernelGGL((xent_head_mfma_kernel<false, KC>), pg, block, lds, s, p);
+    };
+    switch (kch) {
+      case 1: go(std::integral_constant<int, 1>{}); break;
+      case 2: go(std::integral_constant<int, 2>{}); break;
+      case 3: go(std::integral_constant<int, 3>{}); break;
+      case 4: go(std::integral_constant<int, 4>{}); break;
+      case 5: go(std::integral_constant<int, 5>{}); break;
+      case 6: go(std::integral_constant<int, 6>{}); break;
+      case 7: go(std::integral_constant<int, 7>{}); break;
+      default: go(std::integral_constant<int, 8>{}); break;
+    }
+  } else if (t == DType::BF16) {
     if (p.bias) hipLaunchKernelGGL((xent_head_kernel<bf16, true>), grid, block, head_lds<bf16>(p.Kin), s, p);
     else hipLaunchKernelGGL((xent_head_kernel<bf16, false>), grid, block, head_lds<bf16>(p.Kin), s, p);
   } else {

@@ -1089,3 +1089,50 @@ def test_fp32_head_and_fc_dw32_match_generic(cuda, monkeypatch, model, ab):
             e, c = _per_channel_err(g1[off : off + n], g0[off : off + n], L["C"],
                                     floor_frac=0.3 if what == "b" else 1e-2)
             assert e < 1e-4, f"{model} {ab} {L['kind']} C={L['C']} {what}: channel {c} rel err {e:.3e}"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B", [16411, 256])
+def test_bf16_mfma_head_matches_valu_head(cuda, monkeypatch, B):
+    """The bf16 MFMA classifier head (xent_head_mfma_kernel: the last FC
+    layer's forward, softmax-CE, dgrad and dW slab on 16x16x32 MFMAs) vs the
+    VALU head it replaced behind the separate FC forward (MCC_AB=head_valu),
+    on the reference model with a ragged last workgroup: logits, loss,
+    accuracy and every layer's W / b per output channel.  Both round e, W and
+    H through bf16 and accumulate in fp32; only the summation order differs."""
+    spec = mcc.make_model("ref")
+    imgs, labels = mcc.synth_dataset(B, 1, 28, 28, 10, seed=29)
+    params = mcc.init_params(spec, seed=4, mode="fast").astype(np.float32)
+    d_img = torch.from_numpy(imgs).to(cuda)
+    d_lab = torch.from_numpy(labels).to(cuda)
+
+    def run(flag):
+        if flag:
+            monkeypatch.setenv("MCC_AB", flag)
+        else:
+            monkeypatch.delenv("MCC_AB", raising=False)
+        net = mcc.GpuNet(spec, "bf16", B)
+        net.set_params(params)
+        s = torch.cuda.current_stream().cuda_stream
+        net.zero_stats(s)
+        net.forward(d_img.data_ptr(), 0, B, s)
+        net.loss(d_lab.data_ptr(), 0, 1.0 / B, True, s)
+        net.backward_all(s)
+        torch.cuda.synchronize()
+        out = net.get_logits(B), net.get_grads(), net.get_stats()
+        del net
+        return out
+
+    l0, g0, s0 = run("")
+    l1, g1, s1 = run("head_valu")
+    assert np.isfinite(l0).all() and np.isfinite(g0).all()
+    assert _relerr(l0, l1) < 1e-5
+    assert abs(s0["loss_sum"] - s1["loss_sum"]) < 1e-4 * abs(s1["loss_sum"])
+    assert abs(s0["correct"] - s1["correct"]) <= max(2, B // 2000)
+    for L in spec.layers():
+        if L["nweights"] == 0:
+            continue
+        for off, n, what in ((L["w_off"], L["nweights"], "W"), (L["b_off"], L["nbiases"], "b")):
+            e, c = _per_channel_err(g0[off : off + n], g1[off : off + n], L["C"],
+                                    floor_frac=0.3 if what == "b" else 1e-2)
+            assert e < 5e-3, f"{L['kind']} C={L['C']} {what}: channel {c} rel err {e:.3e}"
