@@ -1158,9 +1158,9 @@ void GpuNet::loss(const uint8_t* labels, const int32_t* idx, float grad_scale, b
       h.bias = params_ + last.b_off;
       fc_pending_ = false;
     }
-    gpu::xent_head(dtype_, h, s);
+    const int slabs = gpu::xent_head(dtype_, h, s);
     gpu::DwReduceParams r;
-    r.S = gpu::xent_head_slabs(B_); r.Nout = last.Nout; r.kfeat = last.Kin; r.ldp = last.ldp; r.part = scratch_;
+    r.S = slabs; r.Nout = last.Nout; r.kfeat = last.Kin; r.ldp = last.ldp; r.part = scratch_;
     r.partial_stride = (int64_t)last.Nout * last.ldp;
     r.gw = grads_ + last.w_off; r.gb = grads_ + last.b_off;
     r.permC = 0; r.permHW = 0;  // device order (see set_params)

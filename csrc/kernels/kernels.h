@@ -499,7 +499,8 @@ struct XentHeadParams {
 };
 bool xent_head_supported(int N, int Kin, int ldh);
 int xent_head_slabs(int M);
-void xent_head(DType t, const XentHeadParams& p, hipStream_t s);  // T = bf16 or fp32
+// returns the number of slabs written (<= xent_head_slabs(M); dw_reduce's S)
+int xent_head(DType t, const XentHeadParams& p, hipStream_t s);  // T = bf16 or fp32
 
 // Explicit im2col for the large-image path: out[(n*OH+oy)*OW+ox][k], k =
 // (kh*KS+kw)*SC + c (zero for k >= KS*KS*SC), source through `s` (tile

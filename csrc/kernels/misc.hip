@@ -362,49 +362,71 @@ __global__ void __launch_bounds__(kHeadThreads) __attribute__((amdgpu_waves_per_
 // and after one barrier the workgroup's dW/db slab, C[n][k] = sum_row Es^T Hs
 // (4 MFMAs per 16-column tile, tiles w, w + 8).
 constexpr int kHmWaves = kHeadRows / 16;
-__host__ __device__ constexpr int headm_sh(int Kin) { return 16 * head_nt(Kin) + 8; }  // 16-byte pad: b128 rows spread over banks
+// KCH = ceil(16 NT / 32): the 32-feature groups of an H row (ref 200 -> 7,
+// LeNet-5 84 -> 3).  LDS rows hold all KCH groups (zero past column Kin), so
+// the forward's K loop needs no masks; +16 bytes of pad spread b128 rows over
+// the banks.
+__host__ __device__ constexpr int head_kch(int Kin) { return (16 * head_nt(Kin) + 31) / 32; }
+__host__ __device__ constexpr int headm_sh(int Kin) { return 32 * head_kch(Kin) + 8; }
 __host__ __device__ constexpr int headm_lds(int Kin) { return (kHeadRows + 16) * headm_sh(Kin) * 2 + kHeadRows * 32; }
 
 __device__ __forceinline__ bf16x8 head_tr8(const bf16* p0, const bf16* p1) {
   return __builtin_shufflevector(tr4(p0), tr4(p1), 0, 1, 2, 3, 4, 5, 6, 7);
 }
+// row_ror:n within each 16-lane row (DPP, folds into the consuming VALU op):
+// four rotations 8, 4, 2, 1 leave a commutative reduction in every lane
+template <int N>
+__device__ __forceinline__ float ror16(float x) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x120 + N, 0xF, 0xF, false));
+}
+template <int N>
+__device__ __forceinline__ int ror16(int x) { return __builtin_amdgcn_update_dpp(0, x, 0x120 + N, 0xF, 0xF, false); }
+template <int N>
+__device__ __forceinline__ void head_argmax_step(float& m, int& am) {
+  const float om = ror16<N>(m);
+  const int oa = ror16<N>(am);
+  const bool take = (om > m) | ((om == m) & (oa < am));  // (branch-free: no exec-mask blocks)
+  m = take ? om : m;
+  am = take ? oa : am;
+}
+template <int N>
+__device__ __forceinline__ float head_sum_step(float x) { return x + ror16<N>(x); }
 
-// dead-lane store target: one 64-byte slot per resident wave (a single
-// shared line would take every wave's dead lanes into one L2 channel)
+// dead-lane store target: one 512-byte slot per resident wave (a whole dead
+// dH row fits; a single shared line would take every wave's dead lanes into
+// one L2 channel)
 constexpr int kHeadSinkSlots = 4096;
-__device__ __attribute__((aligned(64))) float kHeadSink[kHeadSinkSlots * 16];
+__device__ __attribute__((aligned(64))) float kHeadSink[kHeadSinkSlots * 128];
 
-// Persistent: workgroup b takes the 128-row tiles b, b + grid, ... (the slab
-// index stays the tile index).  The next tile's H rows are loaded into
-// registers while this tile computes -- one HBM latency per workgroup instead
-// of one per tile.  Every global load and store is unconditional (clamped
-// rows, dead stores to kHeadSink), so the compiler's vmcnt bookkeeping lets
-// the prefetch stay in flight across the whole tile.
-// KCH = ceil(16 NT / 32): the 32-feature groups of an H row (ref 200 -> 7,
-// LeNet-5 84 -> 3): the prefetch buffer holds exactly those
+// Persistent: workgroup b takes the 128-row tiles b, b + grid, ... and keeps
+// its dW/db partial in the MFMA accumulators across them (one slab per
+// workgroup).  The next tile's H rows are loaded into registers while this
+// tile computes -- one HBM latency per workgroup instead of one per tile.
+// Every global load and store is unconditional (clamped rows, dead stores to
+// kHeadSink), so the compiler's vmcnt bookkeeping lets the prefetch stay in
+// flight across the whole tile.
 template <bool FWD, int KCH>
 __global__ void __launch_bounds__(kHeadThreads) __attribute__((amdgpu_waves_per_eu(4))) xent_head_mfma_kernel(XentHeadParams hp) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __shared__ float red[3][kHmWaves];
+  constexpr int SH = 32 * KCH + 8;
   const XentParams& p = hp.x;
   const int N = p.N, Kin = hp.Kin, M = p.M;
-  const int NT = head_nt(Kin), kw = 16 * NT, SH = kw + 8;
   const int K8 = (Kin + 7) & ~7;
   const int ntiles = (M + kHeadRows - 1) / kHeadRows;
   bf16* Hs = reinterpret_cast<bf16*>(smem);
   bf16* Ws = Hs + kHeadRows * SH;
   bf16* Es = Ws + 16 * SH;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, r = lane & 15;
-  const int q4 = r >> 2, p4 = lane & 3;  // tr reads: lane 4q + p -> row q, columns 4p..4p+3
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4;
   const bf16x8 z8 = __builtin_bit_cast(bf16x8, f32x4{0.f, 0.f, 0.f, 0.f});
-  float* const sink32 = kHeadSink + ((blockIdx.x * kHmWaves + w) & (kHeadSinkSlots - 1)) * 16;
+  float* const sink32 = kHeadSink + ((blockIdx.x * kHmWaves + w) & (kHeadSinkSlots - 1)) * 128;
   bf16* const sink16 = reinterpret_cast<bf16*>(sink32);
 
   // H rows of this wave: lane -> row lane >> 2, 8-feature chunks (lane & 3) + 4 it
   const int hr = lane >> 2, hq = lane & 3;
   bf16x8 hc[KCH];
   int sidx[4];  // dataset index of the C-layout rows 4g + i (labels_idx), prefetched with H
-  auto load_h = [&](int tile, int kw, int K8) {
+  auto load_h = [&](int tile, int K8) {
     const int row = min(tile * kHeadRows + 16 * w + hr, M - 1);
     const bf16* hrow = static_cast<const bf16*>(hp.h) + (size_t)row * hp.ldh;
 #pragma unroll
@@ -414,12 +436,12 @@ __global__ void __launch_bounds__(kHeadThreads) __attribute__((amdgpu_waves_per_
       for (int i = 0; i < 4; ++i) sidx[i] = p.labels_idx[min(tile * kHeadRows + 16 * w + 4 * g + i, M - 1)];
     }
   };
-  load_h(blockIdx.x, kw, K8);
+  load_h(blockIdx.x, K8);
   // W (bf16 forward copy), once per workgroup: thread -> class tid >> 5, chunk tid & 31
   {
     const int wn = tid >> 5, wc = tid & 31;
     const bf16x8 wv0 = load8(static_cast<const bf16*>(hp.wpk) + (size_t)min(wn, N - 1) * hp.ldw + min(8 * wc, K8 - 8));
-    if (8 * wc < kw) {
+    if (8 * wc < 32 * KCH) {
       bf16x8 wv = wv0;
 #pragma unroll
       for (int j = 0; j < 8; ++j)
@@ -427,15 +449,16 @@ __global__ void __launch_bounds__(kHeadThreads) __attribute__((amdgpu_waves_per_
       store8(Ws + wn * SH + 8 * wc, wv);
     }
   }
-  const float bias = FWD ? hp.bias[min(r, N - 1)] : 0.f;
+  const float bias = FWD ? hp.bias[min(lane & 15, N - 1)] : 0.f;
   float loss = 0.f, mse = 0.f, correct = 0.f;
+  f32x4 dwacc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
 
   for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     const int row0 = tile * kHeadRows + 16 * w;
     // re-materialised per tile: hoisted out of the tile loop, the per-lane
     // masks derived from these (64-bit each, ~300 SGPRs) spill
-    int Kin = hp.Kin, K8 = (hp.Kin + 7) & ~7, N = p.N, NT = head_nt(hp.Kin), kw = 16 * NT, SH = kw + 8;
-    asm volatile("" : "+s"(Kin), "+s"(K8), "+s"(N), "+s"(NT), "+s"(kw), "+s"(SH));
+    int Kin = hp.Kin, K8 = (hp.Kin + 7) & ~7, N = p.N, NT = head_nt(hp.Kin);
+    asm volatile("" : "+s"(Kin), "+s"(K8), "+s"(N), "+s"(NT));
     int lane = tid & 63;  // (and every lane-derived index: 64 hoisted k0 + j alone took 56 VGPRs)
     asm volatile("" : "+v"(lane));
     const int g = lane >> 4, r = lane & 15, q4 = r >> 2, p4 = lane & 3, hr = lane >> 2, hq = lane & 3;
@@ -452,33 +475,22 @@ __global__ void __launch_bounds__(kHeadThreads) __attribute__((amdgpu_waves_per_
 #pragma unroll
     for (int it = 0; it < KCH; ++it) {
       const int k0 = 8 * (hq + 4 * it);
-      if (k0 < kw) {
-        bf16x8 v = (hlive && k0 < K8) ? hc[it] : z8;
-        if (k0 + 8 > Kin) {  // padding columns (never written upstream: may hold NaN)
+      bf16x8 v = (hlive && k0 < K8) ? hc[it] : z8;
+      if (k0 + 8 > Kin) {  // padding columns (never written upstream: may hold NaN)
 #pragma unroll
-          for (int j = 0; j < 8; ++j)
-            if (k0 + j >= Kin) v[j] = (bf16)((k0 + j == Kin && hlive) ? 1.f : 0.f);
-        }
-        store8(Hs + (16 * w + hr) * SH + k0, v);
+        for (int j = 0; j < 8; ++j)
+          if (k0 + j >= Kin) v[j] = (bf16)((k0 + j == Kin && hlive) ? 1.f : 0.f);
       }
+      store8(Hs + (16 * w + hr) * SH + k0, v);
     }
-#ifndef MCC_HEAD_NOPF
-    load_h(min(tile + (int)gridDim.x, ntiles - 1), kw, K8);  // next tile (the last tile reloads itself)
-#endif
+    load_h(min(tile + (int)gridDim.x, ntiles - 1), K8);  // next tile (the last tile reloads itself)
     __syncthreads();
 
     if constexpr (FWD) {
       f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int c = 0; c < KCH; ++c) {
-        const int kk = 32 * c + 8 * g;
-        bf16x8 a = z8, b = z8;
-        if (kk < kw) {
-          a = load8(Hs + (16 * w + r) * SH + kk);
-          b = load8(Ws + r * SH + kk);
-        }
-        acc = mma(acc, a, b);
-      }
+      for (int c = 0; c < KCH; ++c)
+        acc = mma(acc, load8(Hs + (16 * w + r) * SH + 32 * c + 8 * g), load8(Ws + r * SH + 32 * c + 8 * g));
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         lgv[i] = acc[i] + bias;
@@ -489,82 +501,106 @@ __global__ void __launch_bounds__(kHeadThreads) __attribute__((amdgpu_waves_per_
     }
 
     __builtin_amdgcn_sched_barrier(0);
-    // softmax-CE of rows 4g + i across the 16 lanes of the group (class r)
-#pragma unroll 1  // (unrolled: four rows' shuffle chains in flight, +30 VGPRs and a spilled prefetch)
+    const float inv_n = 1.f / (float)N;
+    // softmax-CE of rows 4g + i across the 16 lanes of the group (class r);
+    // the loss term -(v_label - m) is added by the label's lane, log(sum) by
+    // lane 0 (the wave sum at the end adds them up)
+#pragma unroll 1  // (unrolled: four rows' reduction chains in flight, +30 VGPRs and a spilled prefetch)
     for (int i = 0; i < 4; ++i) {
       const int rw = row0 + 4 * g + i;
       const bool live = rw < M;
       const float v = r < N ? lgv[i] : -INFINITY;
       float m = v;
       int am = r;
-#pragma unroll
-      for (int o = 8; o > 0; o >>= 1) {  // max, smallest class among equal maxima (first max wins, cnn.c:510)
-        const float om = __shfl_xor(m, o);
-        const int oa = __shfl_xor(am, o);
-        if (om > m || (om == m && oa < am)) { m = om; am = oa; }
-      }
+      head_argmax_step<8>(m, am);  // max, smallest class among equal maxima (first max wins, cnn.c:510)
+      head_argmax_step<4>(m, am);
+      head_argmax_step<2>(m, am);
+      head_argmax_step<1>(m, am);
       const float ex = r < N ? __expf(v - m) : 0.f;
-      float s = ex;
-#pragma unroll
-      for (int o = 8; o > 0; o >>= 1) s += __shfl_xor(s, o);
+      const float s = head_sum_step<1>(head_sum_step<2>(head_sum_step<4>(head_sum_step<8>(ex))));
       const int label = lab[i];
-      const float pj = ex * (1.f / s);
+      const float pj = ex * __builtin_amdgcn_rcpf(s);
       const float d = pj - (r == label ? 1.f : 0.f);
-      float d2 = r < N ? d * d : 0.f;
-#pragma unroll
-      for (int o = 8; o > 0; o >>= 1) d2 += __shfl_xor(d2, o);
-      const float vl = __shfl(v, (lane & 48) + (label & 15));
+      const float d2 = head_sum_step<1>(head_sum_step<2>(head_sum_step<4>(head_sum_step<8>(r < N ? d * d : 0.f))));
       const bool first = live && r == 0;
-      loss += first ? __logf(s) - (vl - m) : 0.f;
-      mse += first ? d2 / (float)N : 0.f;
+      loss += (first ? __logf(s) : 0.f) - ((live && r == label) ? v - m : 0.f);
+      mse += first ? d2 * inv_n : 0.f;
       correct += (first && am == label) ? 1.f : 0.f;
       *((first && p.pred) ? p.pred + rw : reinterpret_cast<int32_t*>(sink32)) = am;
       *((p.probs && live && r < N) ? p.probs + (size_t)rw * N + r : sink32) = pj;  // (eval only)
       Es[(16 * w + 4 * g + i) * 16 + r] = (live && r < N) ? (bf16)(d * p.scale) : (bf16)0.f;  // the unfused dlogits
     }
 
-    __builtin_amdgcn_sched_barrier(0);
     // dH^T tile t: C[16t + 4g + i][row r] (this wave's rows; its Es rows were
-    // written by this wave: LDS keeps one wave's accesses in order)
+    // written by this wave: LDS keeps one wave's accesses in order).  Tiles
+    // before the last lie below Kin: no masks; a dead row stores to the sink.
     {
       const bf16x8 eb = g < 2 ? load8(Es + (16 * w + r) * 16 + 8 * g) : z8;  // n >= 16: zero
       const int wr = (8 * g + q4) & 15;  // g >= 2: any class row (times the zero half of eb)
-      const int drow = row0 + r;
-      const bool dlive = drow < M;
-      bf16* drp = static_cast<bf16*>(hp.dh) + (size_t)drow * hp.ldh;
-#pragma unroll 1
-      for (int t = 0; t < NT; ++t) {
-        const bf16x8 a = head_tr8(Ws + wr * SH + 16 * t + 4 * p4, Ws + (wr ^ 4) * SH + 16 * t + 4 * p4);
-        const f32x4 c = mma(f32x4{0.f, 0.f, 0.f, 0.f}, a, eb);
-        const int kc = 16 * t + 4 * g;
-        const bf16x4 y = *reinterpret_cast<const bf16x4*>(Hs + (16 * w + r) * SH + kc);
-        bf16x4 o;
+      bf16* drp = row0 + r < M ? static_cast<bf16*>(hp.dh) + (size_t)(row0 + r) * hp.ldh : sink16;
+      const bf16* hrw = Hs + (16 * w + r) * SH + 4 * g;
+      const bf16* wa = Ws + wr * SH + 4 * p4;
+      with_act(hp.act, [&](auto ak) {
+        constexpr int A = decltype(ak)::v;
+        auto tile_dh = [&](int t, auto last) {
+          const bf16x8 a = head_tr8(wa + 16 * t, wa + 4 * SH + 16 * t);  // class rows wr, wr + 4
+          const f32x4 c = mma(f32x4{0.f, 0.f, 0.f, 0.f}, a, eb);
+          const int kc = 16 * t + 4 * g;
+          const bf16x4 y = *reinterpret_cast<const bf16x4*>(hrw + 16 * t);
+          float o[4];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) o[i] = kc + i < Kin ? (bf16)(c[i] * act_grad_y(hp.act, (float)y[i])) : (bf16)0.f;
-        *reinterpret_cast<bf16x4*>((dlive && kc < K8) ? drp + kc : sink16) = o;
-      }
+          for (int i = 0; i < 4; ++i) {
+            const float yv = (float)y[i];
+            o[i] = A == 1 ? (yv > 0.f ? c[i] : 0.f) : A == 2 ? c[i] * (1.f - yv * yv) : c[i];
+            if constexpr (decltype(last)::value) o[i] = kc + i < Kin ? o[i] : 0.f;
+          }
+          bf16* dst = drp + kc;
+          if constexpr (decltype(last)::value) dst = kc < K8 ? dst : sink16;
+          *reinterpret_cast<bf16x4*>(dst) = cvt4(o[0], o[1], o[2], o[3]);
+        };
+#pragma unroll 1
+        for (int t = 0; t < NT - 1; ++t) tile_dh(t, std::false_type{});
+        tile_dh(NT - 1, std::true_type{});
+      });
     }
     __syncthreads();
 
-    // dW/db slab of the tile: C[n][k] = sum over its 128 rows of Es^T Hs, tiles t = w, w + 8
-    for (int t = w; t < NT; t += kHmWaves) {
-      f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+    // dW/db of the tile: C[n][k] += sum over its 128 rows of Es^T Hs, tiles
+    // t = w, w + 8 (NT <= 16), accumulated over the workgroup's tiles
 #pragma unroll
-      for (int ks = 0; ks < kHeadRows / 32; ++ks) {
-        const int rb = 32 * ks + 8 * g + q4;
-        const bf16x8 a = head_tr8(Es + rb * 16 + 4 * p4, Es + (rb + 4) * 16 + 4 * p4);
-        const bf16x8 b = head_tr8(Hs + rb * SH + 16 * t + 4 * p4, Hs + (rb + 4) * SH + 16 * t + 4 * p4);
-        acc = mma(acc, a, b);
-      }
-      float* slab = hp.slab + (size_t)tile * N * hp.ldp;
-      const int k = 16 * t + r;
+    for (int tt = 0; tt < 2; ++tt) {
+      const int t = w + kHmWaves * tt;
+      if (t < NT) {
+        f32x4 acc = dwacc[tt];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int n = 4 * g + i;
-        *((n < N && k <= Kin) ? slab + n * hp.ldp + k : sink32) = acc[i];
+        for (int ks = 0; ks < kHeadRows / 32; ++ks) {
+          const int rb = 32 * ks + 8 * g + q4;
+          const bf16x8 a = head_tr8(Es + rb * 16 + 4 * p4, Es + (rb + 4) * 16 + 4 * p4);
+          const bf16x8 b = head_tr8(Hs + rb * SH + 16 * t + 4 * p4, Hs + (rb + 4) * SH + 16 * t + 4 * p4);
+          acc = mma(acc, a, b);
+        }
+        dwacc[tt] = acc;
       }
     }
     __syncthreads();  // Hs / Es free for the next tile
+  }
+  // one slab per workgroup (dw_reduce sums gridDim.x of them, not one per
+  // tile: 2.5x fewer at the reference model's 1,280 tiles)
+  {
+    const int r = lane & 15;
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt) {
+      const int t = w + kHmWaves * tt;
+      if (t < head_nt(hp.Kin)) {
+        float* slab = hp.slab + (size_t)blockIdx.x * p.N * hp.ldp;
+        const int k = 16 * t + r;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int n = 4 * g + i;
+          if (n < p.N && k <= hp.Kin) slab[n * hp.ldp + k] = dwacc[tt][i];
+        }
+      }
+    }
   }
   for (int o = 32; o > 0; o >>= 1) {
     loss += __shfl_xor(loss, o);
@@ -926,7 +962,7 @@ bool xent_head_supported(int N, int Kin, int ldh) {
 
 int xent_head_slabs(int M) { return cdiv(M, kHeadRows); }
 
-void xent_head(DType t, const XentHeadParams& p, hipStream_t s) {
+int xent_head(DType t, const XentHeadParams& p, hipStream_t s) {
   MCC_CHECK(p.x.M > 0 && xent_head_supported(p.x.N, p.Kin, p.ldh), "xent_head: needs N <= 16, Kin < 256, ldh % 8 == 0");
   MCC_CHECK((p.bias && !p.x.logits) ||
                 (p.x.ldl % 4 == 0 && (reinterpret_cast<uintptr_t>(p.x.logits) & 15) == 0 && p.x.ldl >= ((p.x.N + 3) & ~3)),
@@ -935,11 +971,11 @@ void xent_head(DType t, const XentHeadParams& p, hipStream_t s) {
                 (reinterpret_cast<uintptr_t>(p.dh) & 15) == 0,
             "xent_head: bad buffers");
   const dim3 grid((unsigned)xent_head_slabs(p.x.M)), block(kHeadThreads);
-  if (t == DType::BF16 && p.wpk && !ab_flag("head_valu")) {
+  if (t == DType::BF16 && p.wpk && !ab_flag("head_valu")) {  // (returns from inside)
     MCC_CHECK(p.ldw % 8 == 0 && p.ldw >= p.Kin && (reinterpret_cast<uintptr_t>(p.wpk) & 15) == 0,
               "xent_head: packed weights need 16-byte rows");
     // persistent: as many workgroups as fit at once (A/B: MCC_AB=head_tile1, one tile each)
-    const int lds = headm_lds(p.Kin), kch = (16 * head_nt(p.Kin) + 31) / 32;
+    const int lds = headm_lds(p.Kin), kch = head_kch(p.Kin);
     static int fit_lds = -1, fit = 0;
     if (fit_lds != lds) {
       int per_cu = 0, dev = 0, cus = 0;
@@ -967,13 +1003,16 @@ void xent_head(DType t, const XentHeadParams& p, hipStream_t s) {
       case 7: go(std::integral_constant<int, 7>{}); break;
       default: go(std::integral_constant<int, 8>{}); break;
     }
-  } else if (t == DType::BF16) {
+    return (int)pg.x;
+  }
+  if (t == DType::BF16) {
     if (p.bias) hipLaunchKernelGGL((xent_head_kernel<bf16, true>), grid, block, head_lds<bf16>(p.Kin), s, p);
     else hipLaunchKernelGGL((xent_head_kernel<bf16, false>), grid, block, head_lds<bf16>(p.Kin), s, p);
   } else {
     if (p.bias) hipLaunchKernelGGL((xent_head_kernel<float, true>), grid, block, head_lds<float>(p.Kin), s, p);
     else hipLaunchKernelGGL((xent_head_kernel<float, false>), grid, block, head_lds<float>(p.Kin), s, p);
   }
+  return (int)grid.x;
 }
 
 void softmax_xent(DType t, const XentParams& p, hipStream_t s) {
