@@ -112,36 +112,7 @@ __device__ __forceinline__ u32x2 pack4(float a, float b, float c, float d) {
   return u32x2{bf16_bits(a) | (bf16_bits(b) << 16), bf16_bits(c) | (bf16_bits(d) << 16)};
 }
 
-// Reductions over the four lanes r, r + 16, r + 32, r + 48 of one image (the
-// MFMA C layout of P3) on v_permlane16/32_swap (VALU) instead of __shfl_xor's
-// ds_bpermute (an LDS round trip per step on the softmax's critical path).
-// With both operands = x, the swap leaves {x of this lane's 16-row pair
-// partner, own x} in the two results (in a lane-dependent order), so a
-// commutative combine gives both lanes the same value, bit for bit what the
-// xor-16 / xor-32 shuffle pair gave.
-__device__ __forceinline__ float ubits(uint32_t u) { return __builtin_bit_cast(float, u); }
-__device__ __forceinline__ uint32_t fbits(float f) { return __builtin_bit_cast(uint32_t, f); }
-__device__ __forceinline__ float sum4lanes(float x) {
-  const auto a = __builtin_amdgcn_permlane16_swap(fbits(x), fbits(x), false, false);
-  x = ubits(a[0]) + ubits(a[1]);
-  const auto b = __builtin_amdgcn_permlane32_swap(fbits(x), fbits(x), false, false);
-  return ubits(b[0]) + ubits(b[1]);
-}
-// first max wins (cnn.c:508-513): the larger value, on ties the lower class
-__device__ __forceinline__ void argmax4lanes(float& mx, int& am) {
-#pragma unroll
-  for (int step = 0; step < 2; ++step) {
-    const auto v = step ? __builtin_amdgcn_permlane32_swap(fbits(mx), fbits(mx), false, false)
-                        : __builtin_amdgcn_permlane16_swap(fbits(mx), fbits(mx), false, false);
-    const auto i = step ? __builtin_amdgcn_permlane32_swap((uint32_t)am, (uint32_t)am, false, false)
-                        : __builtin_amdgcn_permlane16_swap((uint32_t)am, (uint32_t)am, false, false);
-    const float va = ubits(v[0]), vb = ubits(v[1]);
-    const int ia = (int)i[0], ib = (int)i[1];
-    const bool b_wins = vb > va || (vb == va && ib < ia);
-    mx = b_wins ? vb : va;
-    am = b_wins ? ib : ia;
-  }
-}
+// (sum4lanes / argmax4lanes: mfma.h)
 
 __global__ void __launch_bounds__(kThreads, 1) lenet_fc_kernel(LenetFcParams P) {
   // the input tile is its own LDS object: the compiler then knows the

@@ -422,19 +422,16 @@ __global__ void __launch_bounds__(kHeadThreads) __attribute__((amdgpu_waves_per_
   float* const sink32 = kHeadSink + ((blockIdx.x * kHmWaves + w) & (kHeadSinkSlots - 1)) * 128;
   bf16* const sink16 = reinterpret_cast<bf16*>(sink32);
 
-  // H rows of this wave: lane -> row lane >> 2, 8-feature chunks (lane & 3) + 4 it
-  const int hr = lane >> 2, hq = lane & 3;
+  // H rows of this wave: lane -> row lane & 15, 8-feature chunks (lane >> 4) + 4 it
+  const int hr = lane & 15, hq = lane >> 4;  // (16 rows per 16-lane group: conflict-free b128 LDS writes)
   bf16x8 hc[KCH];
-  int sidx[4];  // dataset index of the C-layout rows 4g + i (labels_idx), prefetched with H
+  int sidx = 0;  // dataset index of row lane & 15 (labels_idx), prefetched with H
   auto load_h = [&](int tile, int K8) {
     const int row = min(tile * kHeadRows + 16 * w + hr, M - 1);
     const bf16* hrow = static_cast<const bf16*>(hp.h) + (size_t)row * hp.ldh;
 #pragma unroll
     for (int it = 0; it < KCH; ++it) hc[it] = load8(hrow + min(8 * (hq + 4 * it), K8 - 8));  // no branch
-    if (p.labels_idx) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i) sidx[i] = p.labels_idx[min(tile * kHeadRows + 16 * w + 4 * g + i, M - 1)];
-    }
+    if (p.labels_idx) sidx = p.labels_idx[min(tile * kHeadRows + 16 * w + (lane & 15), M - 1)];
   };
   load_h(blockIdx.x, K8);
   // W (bf16 forward copy), once per workgroup: thread -> class tid >> 5, chunk tid & 31
@@ -449,7 +446,9 @@ __global__ void __launch_bounds__(kHeadThreads) __attribute__((amdgpu_waves_per_
       store8(Ws + wn * SH + 8 * wc, wv);
     }
   }
-  const float bias = FWD ? hp.bias[min(lane & 15, N - 1)] : 0.f;
+  float bias[4];  // classes 4g + i (the logits tile is C[class][row])
+#pragma unroll
+  for (int i = 0; i < 4; ++i) bias[i] = FWD ? hp.bias[min(4 * g + i, N - 1)] : 0.f;
   float loss = 0.f, mse = 0.f, correct = 0.f;
   f32x4 dwacc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
 
@@ -461,14 +460,14 @@ __global__ void __launch_bounds__(kHeadThreads) __attribute__((amdgpu_waves_per_
     asm volatile("" : "+s"(Kin), "+s"(K8), "+s"(N), "+s"(NT));
     int lane = tid & 63;  // (and every lane-derived index: 64 hoisted k0 + j alone took 56 VGPRs)
     asm volatile("" : "+v"(lane));
-    const int g = lane >> 4, r = lane & 15, q4 = r >> 2, p4 = lane & 3, hr = lane >> 2, hq = lane & 3;
-    // labels (and logits) of the C-layout rows 4g + i, class r
-    int lab[4];
+    const int g = lane >> 4, r = lane & 15, q4 = r >> 2, p4 = lane & 3, hr = lane & 15, hq = lane >> 4;
+    // label (and logits) of row r; this lane's classes are 4g .. 4g + 3
+    const int label = (int)p.labels[p.labels_idx ? sidx : min(row0 + r, M - 1)];
     float lgv[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      lab[i] = (int)p.labels[p.labels_idx ? sidx[i] : min(row0 + 4 * g + i, M - 1)];
-      if constexpr (!FWD) lgv[i] = p.logits[(size_t)min(row0 + 4 * g + i, M - 1) * p.ldl + min(r, N - 1)];
+    if constexpr (!FWD) {  // (ldl >= N rounded up to 4: host check)
+      const float4 l4 = *reinterpret_cast<const float4*>(p.logits + (size_t)min(row0 + r, M - 1) * p.ldl +
+                                                         min(4 * g, ((N + 3) & ~3) - 4));
+      lgv[0] = l4.x; lgv[1] = l4.y; lgv[2] = l4.z; lgv[3] = l4.w;
     }
     // this tile's H image (dead rows and padding columns zero, column Kin = 1)
     const bool hlive = row0 + hr < M;
@@ -486,49 +485,60 @@ __global__ void __launch_bounds__(kHeadThreads) __attribute__((amdgpu_waves_per_
     load_h(min(tile + (int)gridDim.x, ntiles - 1), K8);  // next tile (the last tile reloads itself)
     __syncthreads();
 
-    if constexpr (FWD) {
+    const int rw = row0 + r;
+    const bool live = rw < M;
+    if constexpr (FWD) {  // logits^T: C[class 4g + i][row r] = sum_k W[class][k] H[row][k]
       f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int c = 0; c < KCH; ++c)
-        acc = mma(acc, load8(Hs + (16 * w + r) * SH + 32 * c + 8 * g), load8(Ws + r * SH + 32 * c + 8 * g));
+        acc = mma(acc, load8(Ws + r * SH + 32 * c + 8 * g), load8(Hs + (16 * w + r) * SH + 32 * c + 8 * g));
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        lgv[i] = acc[i] + bias;
-        const int rw = row0 + 4 * g + i;
-        float* dst = (p.logits && rw < M && r < N) ? const_cast<float*>(p.logits) + (size_t)rw * p.ldl + r : sink32;
-        *dst = lgv[i];
-      }
+      for (int i = 0; i < 4; ++i) lgv[i] = 4 * g + i < N ? acc[i] + bias[i] : 0.f;
+      float* dst = (p.logits && live && 4 * g < N) ? const_cast<float*>(p.logits) + (size_t)rw * p.ldl + 4 * g : sink32;
+      *reinterpret_cast<float4*>(dst) = make_float4(lgv[0], lgv[1], lgv[2], lgv[3]);
     }
 
-    __builtin_amdgcn_sched_barrier(0);
-    const float inv_n = 1.f / (float)N;
-    // softmax-CE of rows 4g + i across the 16 lanes of the group (class r);
-    // the loss term -(v_label - m) is added by the label's lane, log(sum) by
-    // lane 0 (the wave sum at the end adds them up)
-#pragma unroll 1  // (unrolled: four rows' reduction chains in flight, +30 VGPRs and a spilled prefetch)
-    for (int i = 0; i < 4; ++i) {
-      const int rw = row0 + 4 * g + i;
-      const bool live = rw < M;
-      const float v = r < N ? lgv[i] : -INFINITY;
-      float m = v;
-      int am = r;
-      head_argmax_step<8>(m, am);  // max, smallest class among equal maxima (first max wins, cnn.c:510)
-      head_argmax_step<4>(m, am);
-      head_argmax_step<2>(m, am);
-      head_argmax_step<1>(m, am);
-      const float ex = r < N ? __expf(v - m) : 0.f;
-      const float s = head_sum_step<1>(head_sum_step<2>(head_sum_step<4>(head_sum_step<8>(ex))));
-      const int label = lab[i];
-      const float pj = ex * __builtin_amdgcn_rcpf(s);
-      const float d = pj - (r == label ? 1.f : 0.f);
-      const float d2 = head_sum_step<1>(head_sum_step<2>(head_sum_step<4>(head_sum_step<8>(r < N ? d * d : 0.f))));
-      const bool first = live && r == 0;
-      loss += (first ? __logf(s) : 0.f) - ((live && r == label) ? v - m : 0.f);
-      mse += first ? d2 * inv_n : 0.f;
+    // softmax-CE of row r: this lane's four classes, then the four lanes
+    // r, r + 16, r + 32, r + 48 of the row (permlane swaps).  log(sum) is
+    // added by lane g = 0, -(v_label - m) by the lane holding the label (the
+    // wave sum at the end adds them up).
+    {
+      float v[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[i] = 4 * g + i < N ? lgv[i] : -INFINITY;
+      float m = v[0];
+      int am = 4 * g;
+#pragma unroll
+      for (int i = 1; i < 4; ++i) {  // first max wins (cnn.c:510)
+        const bool take = v[i] > m;
+        m = take ? v[i] : m;
+        am = take ? 4 * g + i : am;
+      }
+      argmax4lanes(m, am);
+      float ex[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) ex[i] = 4 * g + i < N ? __expf(v[i] - m) : 0.f;
+      const float s = sum4lanes((ex[0] + ex[1]) + (ex[2] + ex[3]));
+      const float inv = __builtin_amdgcn_rcpf(s);
+      float d[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) d[i] = ex[i] * inv - (4 * g + i == label ? 1.f : 0.f);  // (0 past N)
+      const float d2 = sum4lanes((d[0] * d[0] + d[1] * d[1]) + (d[2] * d[2] + d[3] * d[3]));
+      const int lq = label & 3;
+      const float vl = lq == 0 ? v[0] : lq == 1 ? v[1] : lq == 2 ? v[2] : v[3];
+      const bool first = live && g == 0;
+      loss += (first ? __logf(s) : 0.f) - ((live && (label >> 2) == g) ? vl - m : 0.f);
+      mse += first ? d2 * (1.f / (float)N) : 0.f;
       correct += (first && am == label) ? 1.f : 0.f;
       *((first && p.pred) ? p.pred + rw : reinterpret_cast<int32_t*>(sink32)) = am;
-      *((p.probs && live && r < N) ? p.probs + (size_t)rw * N + r : sink32) = pj;  // (eval only)
-      Es[(16 * w + 4 * g + i) * 16 + r] = (live && r < N) ? (bf16)(d * p.scale) : (bf16)0.f;  // the unfused dlogits
+      if (p.probs) {  // (eval only)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          *((live && 4 * g + i < N) ? p.probs + (size_t)rw * N + 4 * g + i : sink32) = ex[i] * inv;
+      }
+      // the unfused dlogits, bf16: row r, classes 4g .. 4g + 3 (zero past N and for dead rows)
+      const float sc = live ? p.scale : 0.f;
+      *reinterpret_cast<bf16x4*>(Es + (16 * w + r) * 16 + 4 * g) = cvt4(d[0] * sc, d[1] * sc, d[2] * sc, d[3] * sc);
     }
 
     // dH^T tile t: C[16t + 4g + i][row r] (this wave's rows; its Es rows were
