@@ -392,11 +392,11 @@ __device__ __forceinline__ void head_argmax_step(float& m, int& am) {
 template <int N>
 __device__ __forceinline__ float head_sum_step(float x) { return x + ror16<N>(x); }
 
-// dead-lane store target: one 512-byte slot per resident wave (a whole dead
+// dead-lane store target: one 1 KB slot per resident wave (a whole dead fp32
 // dH row fits; a single shared line would take every wave's dead lanes into
 // one L2 channel)
-constexpr int kHeadSinkSlots = 4096;
-__device__ __attribute__((aligned(64))) float kHeadSink[kHeadSinkSlots * 128];
+constexpr int kHeadSinkSlots = 4096, kHeadSinkSlot = 256;  // floats
+__device__ __attribute__((aligned(64))) float kHeadSink[kHeadSinkSlots * kHeadSinkSlot];
 
 // Persistent: workgroup b takes the 128-row tiles b, b + grid, ... and keeps
 // its dW/db partial in the MFMA accumulators across them (one slab per
@@ -419,7 +419,7 @@ __global__ void __launch_bounds__(kHeadThreads) __attribute__((amdgpu_waves_per_
   bf16* Es = Ws + 16 * SH;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4;
   const bf16x8 z8 = __builtin_bit_cast(bf16x8, f32x4{0.f, 0.f, 0.f, 0.f});
-  float* const sink32 = kHeadSink + ((blockIdx.x * kHmWaves + w) & (kHeadSinkSlots - 1)) * 128;
+  float* const sink32 = kHeadSink + ((blockIdx.x * kHmWaves + w) & (kHeadSinkSlots - 1)) * kHeadSinkSlot;
   bf16* const sink16 = reinterpret_cast<bf16*>(sink32);
 
   // H rows of this wave: lane -> row lane & 15, 8-feature chunks (lane >> 4) + 4 it
@@ -596,6 +596,241 @@ __global__ void __launch_bounds__(kHeadThreads) __attribute__((amdgpu_waves_per_
   }
   // one slab per workgroup (dw_reduce sums gridDim.x of them, not one per
   // tile: 2.5x fewer at the reference model's 1,280 tiles)
+  {
+    const int r = lane & 15;
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt) {
+      const int t = w + kHmWaves * tt;
+      if (t < head_nt(hp.Kin)) {
+        float* slab = hp.slab + (size_t)blockIdx.x * p.N * hp.ldp;
+        const int k = 16 * t + r;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int n = 4 * g + i;
+          if (n < p.N && k <= hp.Kin) slab[n * hp.ldp + k] = dwacc[tt][i];
+        }
+      }
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    loss += __shfl_xor(loss, o);
+    mse += __shfl_xor(mse, o);
+    correct += __shfl_xor(correct, o);
+  }
+  if (lane == 0) {
+    red[0][w] = loss;
+    red[1][w] = mse;
+    red[2][w] = correct;
+  }
+  __syncthreads();
+  if (tid < 3 && p.stats) {
+    float t = 0.f;
+#pragma unroll
+    for (int v = 0; v < kHmWaves; ++v) t += red[tid][v];
+    stat_add(p.stats, tid, t);
+  }
+}
+
+// The fp32 head on the f32 matrix cores (xent_head_mfma32_kernel): the same
+// persistent structure as the bf16 kernel above, no rounding points.  fp32 has
+// no transposing LDS read, so the operands that need a transpose use the
+// 16x16x4 instruction's own layout (A[r][g], B[g][r]: one value per lane):
+//   logits^T  C[class][row]  f32x8 fragments of W and H rows (8 MFMAs per 32 k)
+//   dH^T      C[k][row]      A = W^T from a staged [k][16] copy whose columns
+//                            are stored in (g, kk) order, so a lane's four
+//                            K-steps are one 16-byte read; B = E^T, 4 MFMAs
+//   dW, db    C[n][k]        A = E^T, B = H, one ds_read_b32 each per MFMA
+// LDS: H [128][32 KCH + 4] fp32 -- KCH <= 7 (the reference model's 200 -> 10
+// head: 153 KB, one workgroup per CU; LeNet-5's 84 -> 10: 71 KB, two).
+__host__ __device__ constexpr int head32_sh(int Kin) { return 32 * head_kch(Kin) + 4; }
+__host__ __device__ constexpr int head32_lds(int Kin) {
+  return ((kHeadRows + 16) * head32_sh(Kin) + 16 * head_nt(Kin) * 16 + kHeadRows * 16) * 4;
+}
+
+template <bool FWD, int KCH>
+__global__ void __launch_bounds__(kHeadThreads) __attribute__((amdgpu_waves_per_eu(KCH <= 4 ? 4 : 2)))
+xent_head_mfma32_kernel(XentHeadParams hp) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  __shared__ float red[3][kHmWaves];
+  constexpr int SH = 32 * KCH + 4;
+  const XentParams& p = hp.x;
+  const int N = p.N, Kin = hp.Kin, M = p.M, NT0 = head_nt(Kin);
+  const int ntiles = (M + kHeadRows - 1) / kHeadRows;
+  float* Hs = reinterpret_cast<float*>(smem);
+  float* Ws = Hs + kHeadRows * SH;  // [16][SH]  W rows
+  float* WT = Ws + 16 * SH;         // [16 NT][16] W^T, column (g, kk) = class 4kk + g
+  float* Es = WT + 16 * NT0 * 16;   // [128][16]
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4;
+  const f32x4 z4 = f32x4{0.f, 0.f, 0.f, 0.f};
+  float* const sink32 = kHeadSink + ((blockIdx.x * kHmWaves + w) & (kHeadSinkSlots - 1)) * kHeadSinkSlot;
+
+  // H rows of this wave: lane -> row lane & 15, 8-feature chunks (lane >> 4) + 4 it
+  const int hr = lane & 15, hq = lane >> 4;
+  const int K8 = (Kin + 7) & ~7;
+  f32x4 hc[KCH][2];
+  int sidx = 0;
+  auto load_h = [&](int tile, int K8) {
+    const int row = min(tile * kHeadRows + 16 * w + hr, M - 1);
+    const float* hrow = static_cast<const float*>(hp.h) + (size_t)row * hp.ldh;
+#pragma unroll
+    for (int it = 0; it < KCH; ++it) {
+      const float* q = hrow + min(8 * (hq + 4 * it), K8 - 8);
+      hc[it][0] = *reinterpret_cast<const f32x4*>(q);
+      hc[it][1] = *reinterpret_cast<const f32x4*>(q + 4);
+    }
+    if (p.labels_idx) sidx = p.labels_idx[min(tile * kHeadRows + 16 * w + (lane & 15), M - 1)];
+  };
+  load_h(blockIdx.x, K8);
+  // W (fp32 master [N][Kin]) once per workgroup: rows into Ws, the permuted
+  // transpose into WT (zero past N / Kin)
+  for (int i = tid; i < 16 * 32 * KCH; i += kHeadThreads) {
+    const int n = i / (32 * KCH), k = i - n * (32 * KCH);
+    const float v = (n < N && k < Kin) ? hp.w[(size_t)n * Kin + k] : 0.f;
+    Ws[n * SH + k] = v;
+    if (k < 16 * NT0) WT[k * 16 + (n & 3) * 4 + (n >> 2)] = v;
+  }
+  float bias[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) bias[i] = FWD ? hp.bias[min(4 * g + i, N - 1)] : 0.f;
+  float loss = 0.f, mse = 0.f, correct = 0.f;
+  f32x4 dwacc[2] = {z4, z4};
+
+  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int row0 = tile * kHeadRows + 16 * w;
+    int Kin = hp.Kin, K8 = (hp.Kin + 7) & ~7, N = p.N, NT = head_nt(hp.Kin);
+    asm volatile("" : "+s"(Kin), "+s"(K8), "+s"(N), "+s"(NT));  // (see xent_head_mfma_kernel)
+    int lane = tid & 63;
+    asm volatile("" : "+v"(lane));
+    const int g = lane >> 4, r = lane & 15, hr = lane & 15, hq = lane >> 4;
+    const int label = (int)p.labels[p.labels_idx ? sidx : min(row0 + r, M - 1)];
+    float lgv[4];
+    if constexpr (!FWD) {
+      const float4 l4 = *reinterpret_cast<const float4*>(p.logits + (size_t)min(row0 + r, M - 1) * p.ldl +
+                                                         min(4 * g, ((N + 3) & ~3) - 4));
+      lgv[0] = l4.x; lgv[1] = l4.y; lgv[2] = l4.z; lgv[3] = l4.w;
+    }
+    // this tile's H image (dead rows and padding columns zero, column Kin = 1)
+    const bool hlive = row0 + hr < M;
+#pragma unroll
+    for (int it = 0; it < KCH; ++it) {
+      const int k0 = 8 * (hq + 4 * it);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        f32x4 v = (hlive && k0 < K8) ? hc[it][h] : z4;
+        const int kb = k0 + 4 * h;
+        if (kb + 4 > Kin) {  // padding columns (never written upstream: may hold NaN)
+          v.x = kb + 0 < Kin ? v.x : (kb + 0 == Kin && hlive ? 1.f : 0.f);
+          v.y = kb + 1 < Kin ? v.y : (kb + 1 == Kin && hlive ? 1.f : 0.f);
+          v.z = kb + 2 < Kin ? v.z : (kb + 2 == Kin && hlive ? 1.f : 0.f);
+          v.w = kb + 3 < Kin ? v.w : (kb + 3 == Kin && hlive ? 1.f : 0.f);
+        }
+        *reinterpret_cast<f32x4*>(Hs + (16 * w + hr) * SH + kb) = v;
+      }
+    }
+    load_h(min(tile + (int)gridDim.x, ntiles - 1), K8);  // next tile (the last tile reloads itself)
+    __syncthreads();
+
+    const int rw = row0 + r;
+    const bool live = rw < M;
+    if constexpr (FWD) {  // logits^T: C[class 4g + i][row r]
+      f32x4 acc = z4;
+#pragma unroll
+      for (int c = 0; c < KCH; ++c)
+        acc = mma(acc, load8(Ws + r * SH + 32 * c + 8 * g), load8(Hs + (16 * w + r) * SH + 32 * c + 8 * g));
+#pragma unroll
+      for (int i = 0; i < 4; ++i) lgv[i] = 4 * g + i < N ? acc[i] + bias[i] : 0.f;
+      float* dst = (p.logits && live && 4 * g < N) ? const_cast<float*>(p.logits) + (size_t)rw * p.ldl + 4 * g : sink32;
+      *reinterpret_cast<float4*>(dst) = make_float4(lgv[0], lgv[1], lgv[2], lgv[3]);
+    }
+    {  // softmax-CE of row r (as the bf16 kernel; e stays fp32)
+      float v[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[i] = 4 * g + i < N ? lgv[i] : -INFINITY;
+      float m = v[0];
+      int am = 4 * g;
+#pragma unroll
+      for (int i = 1; i < 4; ++i) {  // first max wins (cnn.c:510)
+        const bool take = v[i] > m;
+        m = take ? v[i] : m;
+        am = take ? 4 * g + i : am;
+      }
+      argmax4lanes(m, am);
+      float ex[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) ex[i] = 4 * g + i < N ? __expf(v[i] - m) : 0.f;
+      const float s = sum4lanes((ex[0] + ex[1]) + (ex[2] + ex[3]));
+      const float inv = 1.f / s;
+      float d[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) d[i] = ex[i] * inv - (4 * g + i == label ? 1.f : 0.f);
+      const float d2 = sum4lanes((d[0] * d[0] + d[1] * d[1]) + (d[2] * d[2] + d[3] * d[3]));
+      const int lq = label & 3;
+      const float vl = lq == 0 ? v[0] : lq == 1 ? v[1] : lq == 2 ? v[2] : v[3];
+      const bool first = live && g == 0;
+      loss += (first ? __logf(s) : 0.f) - ((live && (label >> 2) == g) ? vl - m : 0.f);
+      mse += first ? d2 / (float)N : 0.f;
+      correct += (first && am == label) ? 1.f : 0.f;
+      *((first && p.pred) ? p.pred + rw : reinterpret_cast<int32_t*>(sink32)) = am;
+      if (p.probs) {  // (eval only)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          *((live && 4 * g + i < N) ? p.probs + (size_t)rw * N + 4 * g + i : sink32) = ex[i] * inv;
+      }
+      const float sc = live ? p.scale : 0.f;
+      *reinterpret_cast<f32x4*>(Es + (16 * w + r) * 16 + 4 * g) = f32x4{d[0] * sc, d[1] * sc, d[2] * sc, d[3] * sc};
+    }
+
+    {  // dH^T tile t: C[16t + 4g + i][row r], K = 16 classes as four 16x16x4 steps
+      float eb[4];  // B[g][r] of step kk = E^T[class 4kk + g][row r]
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) eb[kk] = Es[(16 * w + r) * 16 + 4 * kk + g];
+      float* drp = row0 + r < M ? static_cast<float*>(hp.dh) + (size_t)(row0 + r) * hp.ldh : sink32;
+      const float* hrw = Hs + (16 * w + r) * SH + 4 * g;
+      const float* wtl = WT + r * 16 + 4 * g;
+      with_act(hp.act, [&](auto ak) {
+        constexpr int A = decltype(ak)::v;
+        auto tile_dh = [&](int t, auto last) {
+          const f32x4 a = *reinterpret_cast<const f32x4*>(wtl + 16 * 16 * t);  // A[r][g] of steps kk = 0..3
+          f32x4 c = z4;
+#pragma unroll
+          for (int kk = 0; kk < 4; ++kk) c = __builtin_amdgcn_mfma_f32_16x16x4f32(a[kk], eb[kk], c, 0, 0, 0);
+          const int kc = 16 * t + 4 * g;
+          const f32x4 y = *reinterpret_cast<const f32x4*>(hrw + 16 * t);
+          f32x4 o;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            o[i] = A == 1 ? (y[i] > 0.f ? c[i] : 0.f) : A == 2 ? c[i] * (1.f - y[i] * y[i]) : c[i];
+            if constexpr (decltype(last)::value) o[i] = kc + i < Kin ? o[i] : 0.f;
+          }
+          float* dst = drp + kc;
+          if constexpr (decltype(last)::value) dst = kc < K8 ? dst : sink32;
+          *reinterpret_cast<f32x4*>(dst) = o;
+        };
+#pragma unroll 1
+        for (int t = 0; t < NT - 1; ++t) tile_dh(t, std::false_type{});
+        tile_dh(NT - 1, std::true_type{});
+      });
+    }
+    __syncthreads();
+
+    // dW/db: C[n = 4g + i][k = 16t + r] += sum over the 128 rows, four rows per
+    // 16x16x4 step; tiles t = w, w + 8 (NT <= 14 here)
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt) {
+      const int t = w + kHmWaves * tt;
+      if (t < NT) {
+        f32x4 acc = dwacc[tt];
+#pragma unroll 8
+        for (int kk = 0; kk < kHeadRows / 4; ++kk) {
+          const float a = Es[(4 * kk + g) * 16 + r];
+          const float b = Hs[(4 * kk + g) * SH + 16 * t + r];
+          acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc, 0, 0, 0);
+        }
+        dwacc[tt] = acc;
+      }
+    }
+    __syncthreads();  // Hs / Es free for the next tile
+  }
   {
     const int r = lane & 15;
 #pragma unroll
@@ -972,6 +1207,25 @@ bool xent_head_supported(int N, int Kin, int ldh) {
 
 int xent_head_slabs(int M) { return cdiv(M, kHeadRows); }
 
+// workgroups of a persistent head kernel resident at once (occupancy at its
+// LDS size x CUs; cached per kernel and size)
+static int head_resident(const void* fn, int lds) {
+  static const void* c_fn[4] = {};
+  static int c_lds[4] = {}, c_fit[4] = {};
+  for (int i = 0; i < 4; ++i)
+    if (c_fn[i] == fn && c_lds[i] == lds) return c_fit[i];
+  int per_cu = 0, dev = 0, cus = 0;
+  MCC_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kHeadThreads, lds) == hipSuccess &&
+                hipGetDevice(&dev) == hipSuccess &&
+                hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess,
+            "xent_head: occupancy query failed");
+  const int fit = std::max(1, per_cu) * std::max(1, cus);
+  static int next = 0;
+  c_fn[next] = fn; c_lds[next] = lds; c_fit[next] = fit;
+  next = (next + 1) & 3;
+  return fit;
+}
+
 int xent_head(DType t, const XentHeadParams& p, hipStream_t s) {
   MCC_CHECK(p.x.M > 0 && xent_head_supported(p.x.N, p.Kin, p.ldh), "xent_head: needs N <= 16, Kin < 256, ldh % 8 == 0");
   MCC_CHECK((p.bias && !p.x.logits) ||
@@ -986,17 +1240,7 @@ int xent_head(DType t, const XentHeadParams& p, hipStream_t s) {
               "xent_head: packed weights need 16-byte rows");
     // persistent: as many workgroups as fit at once (A/B: MCC_AB=head_tile1, one tile each)
     const int lds = headm_lds(p.Kin), kch = head_kch(p.Kin);
-    static int fit_lds = -1, fit = 0;
-    if (fit_lds != lds) {
-      int per_cu = 0, dev = 0, cus = 0;
-      MCC_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, xent_head_mfma_kernel<true, 8>, kHeadThreads, lds) ==
-                        hipSuccess &&
-                    hipGetDevice(&dev) == hipSuccess &&
-                    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess,
-                "xent_head: occupancy query failed");
-      fit = std::max(1, per_cu) * std::max(1, cus);
-      fit_lds = lds;
-    }
+    const int fit = head_resident(reinterpret_cast<const void*>(xent_head_mfma_kernel<true, 8>), lds);
     const dim3 pg(ab_flag("head_tile1") ? grid.x : std::min(grid.x, (unsigned)fit));
     auto go = [&](auto kc) {
       constexpr int KC = decltype(kc)::value;
@@ -1012,6 +1256,26 @@ int xent_head(DType t, const XentHeadParams& p, hipStream_t s) {
       case 6: go(std::integral_constant<int, 6>{}); break;
       case 7: go(std::integral_constant<int, 7>{}); break;
       default: go(std::integral_constant<int, 8>{}); break;
+    }
+    return (int)pg.x;
+  }
+  if (t == DType::F32 && head_kch(p.Kin) <= 7 && !ab_flag("head32_valu")) {
+    const int lds = head32_lds(p.Kin);
+    const int fit = head_resident(reinterpret_cast<const void*>(xent_head_mfma32_kernel<true, 7>), lds);
+    const dim3 pg(ab_flag("head_tile1") ? grid.x : std::min(grid.x, (unsigned)fit));
+    auto go = [&](auto kc) {
+      constexpr int KC = decltype(kc)::value;
+      if (p.bias) hipLaunchKernelGGL((xent_head_mfma32_kernel<true, KC>), pg, block, lds, s, p);
+      else hipLaunchKernelGGL((xent_head_mfma32_kernel<false, KC>), pg, block, lds, s, p);
+    };
+    switch (head_kch(p.Kin)) {
+      case 1: go(std::integral_constant<int, 1>{}); break;
+      case 2: go(std::integral_constant<int, 2>{}); break;
+      case 3: go(std::integral_constant<int, 3>{}); break;
+      case 4: go(std::integral_constant<int, 4>{}); break;
+      case 5: go(std::integral_constant<int, 5>{}); break;
+      case 6: go(std::integral_constant<int, 6>{}); break;
+      default: go(std::integral_constant<int, 7>{}); break;
     }
     return (int)pg.x;
   }
