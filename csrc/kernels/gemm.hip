@@ -17,6 +17,7 @@
 // (16-byte row copies) and read with ds_read_b64_tr_b16, the CDNA4 hardware
 // transpose read, instead of being transposed element by element.
 #include "kernels.h"
+#include "mcc/ab.h"
 #include "mfma.h"
 
 #include <algorithm>
@@ -291,6 +292,50 @@ __global__ void __launch_bounds__(256) dw_reduce_kernel(DwReduceParams p) {
   *dst = p.beta != 0.f ? p.beta * *dst + acc : acc;
 }
 
+// The same sum for many outputs (FC weight gradients: the reference model's
+// FC2 has 40,200 over 896 slabs): a wave takes 64 CONSECUTIVE outputs, so
+// every load is one contiguous 256-byte run of one slab (the L-lane form
+// reads 64 slabs per instruction, one 4-byte word of each); the WV waves of a
+// workgroup split the slabs and meet in LDS in a fixed order.
+template <int WV>
+__global__ void __launch_bounds__(64 * WV) dw_reduce_cols_kernel(DwReduceParams p) {
+  __shared__ float part[WV][64];
+  const int kc = p.kfeat + 1;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t j = (int64_t)blockIdx.x * 64 + lane;
+  const bool ok = j < (int64_t)p.Nout * kc;
+  const int n = ok ? (int)(j / kc) : 0, k = ok ? (int)(j - (int64_t)n * kc) : 0;
+  const float* src = p.part + (size_t)n * p.ldp + k;
+  const size_t st = (size_t)p.partial_stride;
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  int s = w;
+  for (; s + 3 * WV < p.S; s += 4 * WV) {
+    a0 += src[(size_t)s * st];
+    a1 += src[(size_t)(s + WV) * st];
+    a2 += src[(size_t)(s + 2 * WV) * st];
+    a3 += src[(size_t)(s + 3 * WV) * st];
+  }
+  for (; s < p.S; s += WV) a0 += src[(size_t)s * st];
+  part[w][lane] = (a0 + a1) + (a2 + a3);
+  __syncthreads();
+  if (w != 0 || !ok) return;
+  float acc = part[0][lane];
+#pragma unroll
+  for (int v = 1; v < WV; ++v) acc += part[v][lane];
+  float* dst;
+  if (k < p.kfeat) {
+    int kk = k;
+    if (p.permC > 0) {
+      const int hw = k / p.permC, c = k - hw * p.permC;
+      kk = c * p.permHW + hw;
+    }
+    dst = p.gw + (size_t)n * p.kfeat + kk;
+  } else {
+    dst = p.gb + n;
+  }
+  *dst = p.beta != 0.f ? p.beta * *dst + acc : acc;
+}
+
 // Finishing pass of a split-K forward GEMM: out = epi(sum_s part[s] + bias).
 template <typename T>
 __global__ void __launch_bounds__(256) splitk_finish_kernel(GemmParams p, const float* __restrict__ part, int S) {
@@ -395,6 +440,10 @@ void gemm_splitk_fwd(DType t, const GemmParams& p0, float* scratch, int splitk, 
 
 void dw_reduce(const DwReduceParams& p, hipStream_t s) {
   const int64_t n = (int64_t)p.Nout * (p.kfeat + 1);
+  if (n >= 8192 && !ab_flag("dw_reduce_lanes")) {  // enough outputs to fill the chip 64 at a time
+    hipLaunchKernelGGL(dw_reduce_cols_kernel<4>, dim3((unsigned)((n + 63) / 64)), dim3(256), 0, s, p);
+    return;
+  }
   if (p.S >= 256) hipLaunchKernelGGL(dw_reduce_kernel<64>, dim3((unsigned)((64 * n + 255) / 256)), dim3(256), 0, s, p);
   else if (p.S >= 64) hipLaunchKernelGGL(dw_reduce_kernel<16>, dim3((unsigned)((16 * n + 255) / 256)), dim3(256), 0, s, p);
   else hipLaunchKernelGGL(dw_reduce_kernel<4>, dim3((unsigned)((4 * n + 255) / 256)), dim3(256), 0, s, p);
