@@ -192,19 +192,24 @@ __global__ void __launch_bounds__(kDT) __attribute__((amdgpu_waves_per_eu(4))) c
       // FMAs (924 us at B = 131072).  An opaque copy of the pointer per item
       // keeps them as scalar loads next to their use (549 us).  conv2's
       // weights live inside the channel loop and are not hoisted.
-      const float* wtv = wt;
+      // The copy is a constant-address-space pointer: laundered as a generic
+      // one it lost the __restrict__ no-clobber proof and the 150 weights
+      // became 38 flat_load_dwordx4 per item (vector memory, counted on both
+      // vmcnt and lgkmcnt) instead of scalar loads.
+      typedef __attribute__((address_space(4))) const float cfloat;
+      cfloat* wtv = (cfloat*)wt;
       if constexpr (CIN == 1) asm volatile("" : "+s"(wtv));  // (conv2: measured 793 -> 1511 us with it)
       for (int ci = 0; ci < CIN; ++ci) {
         f2 P[KS + 1][(KS + 1) / 2];
         d_patch<KS, CIN>(xs + m * t.IMG, t.TW, py, px, ci, P);
-        const float* wc = wtv + ci * KS * KS * COUT;  // wave-uniform: scalar loads
+        cfloat* wc = wtv + ci * KS * KS * COUT;  // wave-uniform: scalar loads
 #pragma unroll
         for (int kh = 0; kh < KS; ++kh) {
 #pragma unroll
           for (int kw = 0; kw < KS; ++kw) {
 #pragma unroll
             for (int c = 0; c < CP; ++c) {
-              const f2 wv = *reinterpret_cast<const f2*>(wc + (kh * KS + kw) * COUT + 2 * c);
+              const f2 wv = *reinterpret_cast<__attribute__((address_space(4))) const f2*>(wc + (kh * KS + kw) * COUT + 2 * c);
               acc[c][0] = pfma(wv, MCC_PS(P[kh], kw), acc[c][0]);
               acc[c][1] = pfma(wv, MCC_PS(P[kh], kw + 1), acc[c][1]);
               acc[c][2] = pfma(wv, MCC_PS(P[kh + 1], kw), acc[c][2]);
