@@ -84,14 +84,14 @@ def timed_run(args, spec, dtype, B, d_img, d_lab, dev, dev_idx, rank, world, mul
     # its step counter live on the GPU, so a graph replay draws a fresh batch
     K = mcc._C.kernels
     idx_buf = torch.empty(B, dtype=torch.int32, device=dev)
-    counter = torch.zeros(1, dtype=torch.int64, device=dev)
+    counter = torch.zeros(2, dtype=torch.int64, device=dev)  # (step, ticket of the fused sampler)
     seed = 0x5EED0000 + rank
 
     def step_launch():
         s = torch.cuda.current_stream(dev).cuda_stream
-        K.sample_indices(idx_buf.data_ptr(), B, 0, args.dataset, seed, counter.data_ptr(), s)
+        # indices of this step + the counter advance in one launch
+        K.sample_indices_advance(idx_buf.data_ptr(), B, 0, args.dataset, seed, counter.data_ptr(), s)
         tr.step(d_img, d_lab, idx_buf)
-        K.advance_counter(counter.data_ptr(), s)
 
     # host-side rank agreement (capture consensus, the barriers around the
     # timed loop, the MAX of the per-rank times) only where there are ranks

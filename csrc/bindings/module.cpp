@@ -589,6 +589,13 @@ PYBIND11_MODULE(_C, m) {
         py::arg("stream") = 0);
   k.def("advance_counter", [](uintptr_t step, uintptr_t s) { gpu::advance_counter(ptr<uint64_t>(step), stream_of(s)); },
         py::arg("step"), py::arg("stream") = 0);
+  // both in one launch: step -> int64[2] (counter, ticket; zero-initialised)
+  k.def("sample_indices_advance",
+        [](uintptr_t idx, int B, int64_t lo, int64_t hi, uint64_t seed, uintptr_t step, uintptr_t s) {
+          gpu::sample_indices_advance(ptr<int32_t>(idx), B, lo, hi, seed, ptr<uint64_t>(step), stream_of(s));
+        },
+        py::arg("idx"), py::arg("B"), py::arg("lo"), py::arg("hi"), py::arg("seed"), py::arg("step"),
+        py::arg("stream") = 0);
   k.def("sgd_update",
         [](uintptr_t p, uintptr_t g, uintptr_t v, int64_t n, float lr, float mu, float wd, uintptr_t s) {
           gpu::sgd_update(ptr<float>(p), ptr<const float>(g), ptr<float>(v), n, lr, mu, wd, stream_of(s));

@@ -686,6 +686,10 @@ void sample_indices(int32_t* idx, int B, int64_t lo, int64_t hi, uint64_t seed, 
 void seq_sample_indices(int32_t* idx, int B, int64_t offset, int64_t stride, int64_t n, const uint64_t* step,
                         hipStream_t s);
 void advance_counter(uint64_t* step, hipStream_t s);
+// sample_indices at *step, then ++*step, in ONE launch; step -> uint64[2]
+// (counter, ticket = 0): the same index stream as sample + advance
+void sample_indices_advance(int32_t* idx, int B, int64_t lo, int64_t hi, uint64_t seed, uint64_t* step,
+                            hipStream_t s);
 // contention probe: nwg workgroups holding lds_bytes of LDS each, spinning usec
 void cu_hold(int nwg, int lds_bytes, double usec, hipStream_t s);
 // idx[b] = start + b (sequential evaluation windows)

@@ -1160,6 +1160,29 @@ __global__ void sample_kernel(int32_t* idx, int B, int64_t lo, int64_t span, uin
 
 __global__ void advance_kernel(uint64_t* step) { *step += 1; }
 
+// sample_kernel + advance_kernel as one launch: step[0] is the counter,
+// step[1] a ticket.  Every workgroup reads the counter before it takes a
+// ticket; the workgroup that takes the last one advances the counter and
+// resets the ticket, so no workgroup can see the advanced value.  (Grid-
+// stride over the batch.)
+__global__ void __launch_bounds__(256) sample_advance_kernel(int32_t* idx, int B, int64_t lo, int64_t span,
+                                                             uint64_t seed, uint64_t* step) {
+  __shared__ uint64_t c;
+  if (threadIdx.x == 0) c = __hip_atomic_load(step, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  const uint64_t cv = c;
+  const uint64_t hs = mix64(seed ^ (cv * 0xD1B54A32D192ED03ull));
+  for (int b = blockIdx.x * blockDim.x + threadIdx.x; b < B; b += gridDim.x * blockDim.x)
+    idx[b] = (int32_t)(lo + (int64_t)(mix64(hs + (uint64_t)b) % (uint64_t)span));
+  if (threadIdx.x == 0) {
+    const uint64_t t = __hip_atomic_fetch_add(step + 1, 1ull, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (t == gridDim.x - 1) {
+      __hip_atomic_store(step + 1, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(step, cv + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
 // Contention probe (tools/probes/cu_contention.py): `nwg` workgroups of 256
 // threads that each hold `lds` bytes of LDS and spin for `ticks` wall-clock
 // ticks -- a stand-in for an RCCL kernel that occupies CUs while it waits for
@@ -1388,6 +1411,15 @@ void cu_hold(int nwg, int lds_bytes, double usec, hipStream_t s) {
             "cu_hold: device query failed");
   const uint64_t ticks = (uint64_t)(usec * 1e-3 * (khz > 0 ? khz : 100000));
   hipLaunchKernelGGL(cu_hold_kernel, dim3((unsigned)nwg), dim3(256), (size_t)lds_bytes, s, ticks, nullptr);
+}
+
+void sample_indices_advance(int32_t* idx, int B, int64_t lo, int64_t hi, uint64_t seed, uint64_t* step,
+                            hipStream_t s) {
+  MCC_CHECK(B > 0 && hi > lo, "sample_indices_advance: empty range");
+  // few workgroups: the tickets of one launch serialise on one address
+  // (640 workgroups took 16 us, twice sample + advance)
+  hipLaunchKernelGGL(sample_advance_kernel, dim3((unsigned)std::min(cdiv(B, 256), 64)), dim3(256), 0, s, idx, B, lo,
+                     hi - lo, seed, step);
 }
 
 void advance_counter(uint64_t* step, hipStream_t s) {

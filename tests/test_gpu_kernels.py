@@ -282,3 +282,38 @@ def test_fc1_splitk_forward_vgg_shape(cuda, M):
     # bf16 output rounding (2^-9 relative) dominates; a dropped split or K
     # slice would be O(1) on every channel
     assert err.max().item() < 1e-2, (err.max().item(), int(err.argmax()))
+
+
+@pytest.mark.gpu
+def test_sample_indices_advance_matches_two_launches(cuda):
+    """The fused sampler (sample_indices_advance: one launch, the last
+    workgroup advances the counter) draws the same index stream as
+    sample_indices + advance_counter, eagerly and replayed from a graph."""
+    K = mcc._C.kernels
+    B, lo, hi, seed = 50_000, 3, 60_003, 0x5EED0007
+    s = torch.cuda.current_stream().cuda_stream
+    c2 = torch.zeros(1, dtype=torch.int64, device=cuda)
+    ref = torch.empty(B, dtype=torch.int32, device=cuda)
+    want = []
+    for _ in range(6):
+        K.sample_indices(ref.data_ptr(), B, lo, hi, seed, c2.data_ptr(), s)
+        K.advance_counter(c2.data_ptr(), s)
+        want.append(ref.clone())
+    c1 = torch.zeros(2, dtype=torch.int64, device=cuda)
+    got = torch.empty(B, dtype=torch.int32, device=cuda)
+    out = []
+    for _ in range(3):
+        K.sample_indices_advance(got.data_ptr(), B, lo, hi, seed, c1.data_ptr(), s)
+        out.append(got.clone())
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        K.sample_indices_advance(got.data_ptr(), B, lo, hi, seed, c1.data_ptr(),
+                                 torch.cuda.current_stream().cuda_stream)
+    for _ in range(2):  # the capture did not run the kernel; replays do
+        g.replay()
+        out.append(got.clone())
+    torch.cuda.synchronize()
+    assert c1.tolist() == [5, 0]
+    for i, (a, b) in enumerate(zip(out, want)):
+        assert torch.equal(a, b), f"step {i}"
+    assert int(want[0].min()) >= lo and int(want[0].max()) < hi

@@ -1,11 +1,11 @@
 #!/usr/bin/env python3
 """Per-dispatch timeline (us, grid, kernel) of the last full step in a rocprofv3
-kernel trace; steps are delimited by the device sampler's sample_kernel."""
+kernel trace; steps are delimited by the device sampler (sample_kernel / sample_advance_kernel)."""
 import csv
 import sys
 
 
-def main(path, marker="sample_kernel"):
+def main(path, marker="sample"):
     rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
     idx = [i for i, r in enumerate(rows) if marker in r["Kernel_Name"]]
     start, end = idx[-2], idx[-1]
