@@ -15,8 +15,9 @@
 // write.  K moves in 32-deep stages (A rows then W rows, 24 KB) through a
 // 3-deep ring of LDS buffers filled by global->LDS DMA (16 B per lane,
 // wave-uniform destination): two stages in flight while one is multiplied,
-// one barrier per stage, and every iteration issues exactly 3 DMAs per wave
-// (past K: the zero page) so the wait is a fixed vmcnt(3).  73 KB of LDS:
+// one barrier per stage, and every iteration issues the same number of DMAs
+// per wave (past K: the zero page; weight pieces wholly past N: none, their
+// rows zero-filled once) so the wait is a fixed per-wave vmcnt.  73 KB of LDS:
 // two workgroups per CU, whose load / multiply phases interleave (a
 // persistent one-workgroup-per-CU variant with a 6-deep ring and deferred
 // epilogues measured 36 % slower: at 256 workgroups a CU still busy with the
@@ -80,7 +81,8 @@ __global__ void __launch_bounds__(kTT, NS == 3 ? 2 : 1) fc_tall_kernel(FcTallPar
   constexpr int EPS = 16 / (int)sizeof(T);  // elements per 16-byte segment
   typedef typename std::conditional<sizeof(T) == 2, bf16x8, f32x4>::type V;
   extern __shared__ __attribute__((aligned(16))) char tsm[];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // (scalar: the per-wave DMA branches below)
   const int r16 = lane & 15, g = lane >> 4;
   const int wm = wave & 3, wn = wave >> 2;
   // XCD-aware order: consecutive column tiles of one row block share its A
@@ -115,11 +117,30 @@ __global__ void __launch_bounds__(kTT, NS == 3 ? 2 : 1) fc_tall_kernel(FcTallPar
     }
   }
   const int nk = (p.K + EPR - 1) / EPR;
-  auto stage = [&](int kt) {  // always DM DMAs (past K: the zero page)
+  // Weight pieces whose 16 rows all lie past N (or past the tile: N = 200 on
+  // 224 / 256-row slots) are zero-filled once per ring slot and never
+  // fetched again (they were zero-page DMAs every stage: 3 of the 16 weight
+  // pieces of the reference FC1).  The count is fixed per wave, so each
+  // wave's stage wait stays an exact vmcnt.
+  bool dead[DM];
+  int cnt = 1;
+#pragma unroll
+  for (int i = 0; i < DM; ++i) {
+    const int rb = 16 * (wave + 8 * (i - 1));
+    dead[i] = i > 0 && (rb >= kTN || n0 + rb >= p.N);
+    cnt += (i > 0 && !dead[i]) ? 1 : 0;
+#pragma unroll
+    for (int sl = 0; sl < NS; ++sl)
+      if (dead[i])
+        *reinterpret_cast<f32x4*>(tsm + sl * Gm::STAGE + kTXBytes + (wave + 8 * (i - 1)) * 1024 + lane * 16) =
+            f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  auto stage = [&](int kt) {  // cnt DMAs (past K: the zero page)
     char* dst = tsm + (kt % NS) * Gm::STAGE;
     const int k0 = kt * EPR;
 #pragma unroll
     for (int i = 0; i < DM; ++i) {
+      if (dead[i]) continue;
 #ifdef MCC_TALL_BLOCKED
       const T* s = (src[i] && k0 + sk[i] < p.K) ? src[i] + (i == 0 ? (size_t)kt * kTM * EPR : (size_t)k0) : zero;
 #else
@@ -143,13 +164,15 @@ __global__ void __launch_bounds__(kTT, NS == 3 ? 2 : 1) fc_tall_kernel(FcTallPar
     // DM) = stage kt landed (in-order retirement); the barrier (an explicit
     // s_barrier: __syncthreads() would drain vmcnt) makes every wave's pieces
     // visible and frees the slot read in iteration kt - 1
-    constexpr int VM = (NS - 2) * DM;
-    static_assert(VM == 2 || VM == 3 || VM == 6 || VM == 9 || VM == 12, "the s_waitcnt below");
-    if constexpr (VM == 12) asm volatile("s_waitcnt vmcnt(12)\n\ts_barrier" ::: "memory");
-    else if constexpr (VM == 9) asm volatile("s_waitcnt vmcnt(9)\n\ts_barrier" ::: "memory");
-    else if constexpr (VM == 6) asm volatile("s_waitcnt vmcnt(6)\n\ts_barrier" ::: "memory");
-    else if constexpr (VM == 3) asm volatile("s_waitcnt vmcnt(3)\n\ts_barrier" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(2)\n\ts_barrier" ::: "memory");
+    static_assert(NS >= 3 && NS <= 4 && DM <= 3, "the s_waitcnt below");
+    const int vm = (NS - 2) * cnt;  // wave-uniform
+    if (vm >= 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else if (vm == 5) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+    else if (vm == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else if (vm == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+    else if (vm == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+    asm volatile("s_barrier" ::: "memory");
     stage(kt + NS - 1);
     const char* xb_ = tsm + (kt % NS) * Gm::STAGE;
     const char* wb_ = xb_ + kTXBytes;
