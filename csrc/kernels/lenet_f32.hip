@@ -205,6 +205,18 @@ constexpr int kD1W = (kD1Imgs * 196 + kD1T - 1) / kD1T;      // staged u8 words 
 constexpr int kD1Q = (kD1Imgs * 294 + kD1T - 1) / kD1T;      // staged dY quads per thread
 static_assert(40 * 6 * 26 * 4 <= kD1Lds, "reduction scratch fits in the staging LDS");
 
+// the 5 x 3 patch reads of one conv1-dW window as single ds_read_b64 (byte
+// offsets kh * kD1P * 4 + {0, 8, 16}); results valid after lds_wait()
+template <int KH>
+__device__ __forceinline__ void d1_rows(uint32_t a, f2 (&r)[5][3]) {
+  if constexpr (KH < 5) {
+    asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(r[KH][0]) : "v"(a), "n"(KH * kD1P * 4));
+    asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(r[KH][1]) : "v"(a), "n"(KH * kD1P * 4 + 8));
+    asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(r[KH][2]) : "v"(a), "n"(KH * kD1P * 4 + 16));
+    d1_rows<KH + 1>(a, r);
+  }
+}
+
 __global__ void __launch_bounds__(kD1T) lenet32_dw1_kernel(Conv1DirectParams p) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* xs = smem;
@@ -316,6 +328,24 @@ __global__ void __launch_bounds__(kD1T) lenet32_dw1_kernel(Conv1DirectParams p) 
           accb += dy;
           const f2 g = f2{dy, dy};
           const float* x = xs + m * kD1X + (code & 1) * kD1Copy + (2 * wy + ((code >> 1) & 1)) * kD1P + 2 * wx;
+#ifndef MCC_D1_COMPILER_READS
+          // 15 single ds_read_b64 in inline asm: left to the compiler, the
+          // adjacent 8-byte reads were merged into ds_read2_b32 / ds_read2_b64,
+          // whose banking is (a/4) mod 32 -- the second image copy's 32-bank
+          // offset then collides (SQ_LDS_BANK_CONFLICT 47 % of 93 % LDS-active
+          // cycles, 11 LDS cycles per instruction)
+          const uint32_t xa = (uint32_t)(uintptr_t)((const __attribute__((address_space(3))) float*)x);
+          f2 rd[5][3];
+          d1_rows<0>(xa, rd);
+          lds_wait();
+#pragma unroll
+          for (int kh = 0; kh < 5; ++kh) {
+            asm volatile("" : "+v"(rd[kh][0]), "+v"(rd[kh][1]), "+v"(rd[kh][2]));
+            acc[kh][0] = pfma(g, rd[kh][0], acc[kh][0]);
+            acc[kh][1] = pfma(g, rd[kh][1], acc[kh][1]);
+            acc[kh][2] = pfma(g, rd[kh][2], acc[kh][2]);  // .y: tap kw = 5 (unused)
+          }
+#else
 #pragma unroll
           for (int kh = 0; kh < 5; ++kh) {
             const f2 a = *reinterpret_cast<const f2*>(x + kh * kD1P);
@@ -325,6 +355,7 @@ __global__ void __launch_bounds__(kD1T) lenet32_dw1_kernel(Conv1DirectParams p) 
             acc[kh][1] = pfma(g, b, acc[kh][1]);
             acc[kh][2] = pfma(g, c, acc[kh][2]);  // .y: tap kw = 5 (unused)
           }
+#endif
         }
       }
     }
