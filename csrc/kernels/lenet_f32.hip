@@ -65,6 +65,22 @@ constexpr int kD2Red = 4 * 16 * 151 * 4;   // reduction scratch [wave][co][151] 
 // The next group's global loads are issued into registers before the current
 // group's windows are processed (a group's staging would otherwise expose the
 // HBM latency once per group: 4 images).
+// conv2 dW window slots: slot -> (window, second window or -1), windows
+// py * 5 + px; slots 2k and 2k + 1 hold vertical neighbours (row 4: two
+// columns apart)
+__device__ constexpr signed char kD2Win[16][2] = {{0, 13}, {5, 18}, {1, 14}, {6, 19}, {2, 20}, {7, 22},
+                                                  {3, 21}, {8, 23}, {4, 24}, {9, -1}, {10, -1}, {15, -1},
+                                                  {11, -1}, {16, -1}, {12, -1}, {17, -1}};
+// taps (kh, 0..4) of a window: the 8-byte halves (floats 4, 5 of each pixel)
+__device__ __forceinline__ void d2_row(uint32_t a, int kh, f2 (&r)[5]) {
+  const uint32_t b = a + (uint32_t)(kh * 14 * 8 * 4 + 16);
+  asm volatile("ds_read_b64 %0, %1 offset:0" : "=v"(r[0]) : "v"(b));
+  asm volatile("ds_read_b64 %0, %1 offset:32" : "=v"(r[1]) : "v"(b));
+  asm volatile("ds_read_b64 %0, %1 offset:64" : "=v"(r[2]) : "v"(b));
+  asm volatile("ds_read_b64 %0, %1 offset:96" : "=v"(r[3]) : "v"(b));
+  asm volatile("ds_read_b64 %0, %1 offset:128" : "=v"(r[4]) : "v"(b));
+}
+
 __global__ void __launch_bounds__(kD2T) __attribute__((amdgpu_waves_per_eu(2, 2))) lenet32_dw2_kernel(Conv1DirectParams p) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* y1s = smem;
@@ -77,10 +93,15 @@ __global__ void __launch_bounds__(kD2T) __attribute__((amdgpu_waves_per_eu(2, 2)
   // 8-float pixels -- conflict-free
   const int gi = kB128Group[lane], co = kB128Pos[lane];
   const int slot = wv * 4 + gi;  // 16 window slots per workgroup
-  // this lane's windows w = slot, slot + 16 (< 25) of an image: pixel offset of the window corner
-  const int w0 = slot, w1 = slot + 16;
+  // this lane's windows (kD2Win: all 25 once).  The 8-byte reads of a
+  // half-wave (ds_read_b64: lanes 0-31 = slots 4wv, 4wv + 1) pair windows
+  // whose corners are 32 banks apart (vertical neighbours, or two columns
+  // apart in row 4), so their 2 x 4 argmax pixels never share a bank; with
+  // slot = window (adjacent windows, 16 banks apart) two of the four pixel
+  // sets collided (SQ_LDS_BANK_CONFLICT 30 % of 91 % LDS-active cycles)
+  const int w0 = kD2Win[slot][0], w1 = kD2Win[slot][1];
   const int p0 = (2 * (w0 / 5) * 14 + 2 * (w0 % 5)) * 8;
-  const int p1 = w1 < 25 ? (2 * (w1 / 5) * 14 + 2 * (w1 % 5)) * 8 : p0;
+  const int p1 = w1 >= 0 ? (2 * (w1 / 5) * 14 + 2 * (w1 % 5)) * 8 : p0;
 
   for (int i = t * 4; i < kD2Imgs * kD2Y1; i += kD2T * 4) *reinterpret_cast<f32x4*>(y1s + i) = f32x4{0.f, 0.f, 0.f, 0.f};
 
@@ -144,7 +165,7 @@ __global__ void __launch_bounds__(kD2T) __attribute__((amdgpu_waves_per_eu(2, 2)
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const int w = j ? w1 : w0;
-        if (j == 1 && w1 >= 25) break;
+        if (j == 1 && w1 < 0) break;
         const int it = m * 25 + w;
         const float dy0 = dys[it * 16 + co];
         const int code = ars[it * 16 + co];
@@ -152,17 +173,25 @@ __global__ void __launch_bounds__(kD2T) __attribute__((amdgpu_waves_per_eu(2, 2)
         accb += dy;
         const f2 g = f2{dy, dy};
         const float* y = y1s + m * kD2Y1 + (j ? p1 : p0) + (((code >> 1) & 1) * 14 + (code & 1)) * 8;
+        const uint32_t ya = (uint32_t)(uintptr_t)((const __attribute__((address_space(3))) float*)y);
 #pragma unroll
-        for (int kh = 0; kh < 5; ++kh)
+        for (int kh = 0; kh < 5; ++kh) {
+          // the 8-byte halves as single ds_read_b64 (asm): left to the
+          // compiler they merge into ds_read2_b64, banked (a/4) mod 32 over
+          // 16 contiguous lanes, which undoes the pairing above
+          f2 v2[5];
+          d2_row(ya, kh, v2);
+          lds_wait();
 #pragma unroll
           for (int kw = 0; kw < 5; ++kw) {
+            asm volatile("" : "+v"(v2[kw]));
             const f32x4 v = *reinterpret_cast<const f32x4*>(y + (kh * 14 + kw) * 8);
-            const f2 v2 = *reinterpret_cast<const f2*>(y + (kh * 14 + kw) * 8 + 4);
             f2* a = acc[kh * 5 + kw];
             a[0] = pfma(g, f2{v[0], v[1]}, a[0]);
             a[1] = pfma(g, f2{v[2], v[3]}, a[1]);
-            a[2] = pfma(g, v2, a[2]);
+            a[2] = pfma(g, v2[kw], a[2]);
           }
+        }
       }
     }
   }
